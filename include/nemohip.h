@@ -1,0 +1,223 @@
+/*
+ * nemohip.h — C ABI of libnemohip, the MI355X (gfx950) engine behind Nemo's
+ * provenance-graph analysis.
+ *
+ * This is the drop-in boundary that replaces the Bolt connection + Neo4j 3.3.3
+ * engine underneath the Go `graphing` package of at15/nemo.  Every entry point
+ * below names the reference method (file:line, relative to the reference root)
+ * whose database round trips it replaces.  The Go side (a cgo stub, see
+ * INTEGRATION.md) keeps every string: it interns table names, labels, rule
+ * types and node IDs into the integer arrays below and rebuilds IDs, labels,
+ * `<code>` wrappers, corrections and DOT graphs from the integer results.
+ *
+ * Conventions
+ *   - Plain C, plain pointers and sizes; no HIP, torch or C++ types.
+ *   - Every function returns NEMO_OK (0) or a NEMO_ERR_* code; the message of
+ *     the last failure is nemo_last_error(ctx) (reference messages reused where
+ *     the reference has one, e.g. graphing/pre-post-prov.go:209).
+ *   - A context is bound to one HIP device and is not re-entrant (the
+ *     reference's Bolt connections are not thread-safe either:
+ *     vendor/github.com/johnnadratowski/golang-neo4j-bolt-driver/driver.go:33-36).
+ *   - Graph g of a corpus is run r's antecedent (pre) graph when g == 2r and its
+ *     consequent (post) graph when g == 2r+1 (the two loadProv calls of
+ *     graphing/pre-post-prov.go:255,269).
+ *   - Node indices in every array are local to their graph (0 .. V_g-1).
+ */
+#ifndef NEMOHIP_H
+#define NEMOHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NEMOHIP_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define NEMO_OK            0
+#define NEMO_ERR_INVALID   1  /* bad argument / malformed corpus               */
+#define NEMO_ERR_HIP       2  /* HIP runtime failure                           */
+#define NEMO_ERR_LOAD      3  /* loadProv validation (dangling/duplicate edge)  */
+#define NEMO_ERR_CYCLE     4  /* provenance graph is not acyclic               */
+#define NEMO_ERR_STATE     5  /* call out of order (e.g. simplify before load)  */
+#define NEMO_ERR_LIMIT     6  /* a size limit of this build was exceeded        */
+#define NEMO_ERR_NOTFOUND  7  /* unknown run iteration                          */
+#define NEMO_ERR_NOGPU     8  /* no usable HIP device                           */
+
+/* ---- packed node word (input) ------------------------------------------ *
+ * bit 31      : 1 = Rule node, 0 = Goal node   (Neo4j labels :Rule / :Goal,
+ *               graphing/pre-post-prov.go:28,91)
+ * bits 28..30 : rule type class (goals: 0)      (Rule.type, pre-post-prov.go:91)
+ * bits 0..23  : interned table id               (Goal.table / Rule.table)      */
+#define NEMO_NODE_RULE    0x80000000u
+#define NEMO_TYPE_SHIFT   28
+#define NEMO_TYPE_MASK    0x70000000u
+#define NEMO_TYPE_OTHER   0u  /* any type string other than the two below      */
+#define NEMO_TYPE_NEXT    1u  /* "next"  (preprocessing.go:71, corrections.go:213) */
+#define NEMO_TYPE_ASYNC   2u  /* "async" (extensions.go:64, diagrams.go:53)    */
+#define NEMO_TABLE_MASK   0x00FFFFFFu
+#define NEMO_MAX_TABLES   16384u /* table-id universe supported by this build   */
+
+#define NEMO_WORD(is_rule, type, table) \
+  (((is_rule) ? NEMO_NODE_RULE : 0u) | ((uint32_t)(type) << NEMO_TYPE_SHIFT) | ((uint32_t)(table) & NEMO_TABLE_MASK))
+
+/* ---- per-node result flags (output) ------------------------------------ */
+#define NEMO_F_HOLDS    0x01u /* condition_holds after markConditionHolds        */
+#define NEMO_F_KEPT     0x02u /* node survives cleanCopyProv (run 1000+i copy)   */
+#define NEMO_F_DELETED  0x04u /* removed by collapseNextChains' DETACH DELETE     */
+#define NEMO_F_HEAD     0x08u /* first rule of >= 1 accepted @next chain         */
+#define NEMO_F_TAIL     0x10u /* last rule of >= 1 accepted @next chain          */
+
+/* ---- corpus (input; replaces fi.Run/ProvData, faultinjectors/data-types.go:43-98) */
+typedef struct nemo_corpus {
+  uint32_t n_runs;           /* runs in this corpus (or this rank's shard)          */
+  uint32_t n_tables;         /* table ids are < n_tables (<= NEMO_MAX_TABLES)       */
+  uint32_t table_pre;        /* interned id of table "pre"  (UINT32_MAX if absent)  */
+  uint32_t table_post;       /* interned id of table "post" (UINT32_MAX if absent)  */
+  const uint32_t *iteration; /* [n_runs] Run.Iteration (data-types.go:82)          */
+  const uint8_t *owned;      /* [n_runs] 1 = counted in cross-run reductions;
+                                NULL = all owned (replicated run 0 on a shard: 0)   */
+  const uint64_t *node_off;  /* [2*n_runs+1] first node of graph g                  */
+  const uint64_t *edge_off;  /* [2*n_runs+1] first edge of graph g                  */
+  const uint32_t *node_word; /* [V] NEMO_WORD(...)                                  */
+  const uint32_t *label;     /* [V] interned label (exact interning, never a hash)  */
+  const uint32_t *id_rank;   /* [V] rank of the node's ID string inside its graph,
+                                or NULL when local index order == ID string order   */
+  const uint32_t *edge_src;  /* [E] local index of the DUETO edge's source          */
+  const uint32_t *edge_dst;  /* [E] local index of its target                       */
+} nemo_corpus;
+
+/* one accepted @next chain (graphing/preprocessing.go:108-138,249-305) */
+typedef struct nemo_chain {
+  uint32_t graph;  /* graph index g (2r or 2r+1)                                   */
+  uint32_t k;      /* acceptance index: the _<k> of run_<1000+i>_<C>_<t>_collapsed_<k> */
+  uint32_t head;   /* r1: local index, its table names the collapsed rule          */
+  uint32_t tail;   /* rk: local index                                              */
+  uint32_t len;    /* path length (relationships)                                  */
+} nemo_chain;
+
+/* one missing event of differential provenance (differential-provenance.go:82-146) */
+typedef struct nemo_missing {
+  uint32_t entry;  /* diff entry (index into the failed-run list)                  */
+  uint32_t rule;   /* local index of the rule in run 0's post graph               */
+} nemo_missing;
+
+/* ---- context --------------------------------------------------------------
+ * Replaces InitGraphDB / CloseDB (graphing/helpers.go:17-55, 58-86): no docker,
+ * no 10 s sleep, no Bolt; binds one HIP device.                             */
+typedef struct nemo_ctx nemo_ctx;
+int nemo_ctx_create(int device, nemo_ctx **out);
+void nemo_ctx_destroy(nemo_ctx *ctx);
+const char *nemo_last_error(const nemo_ctx *ctx);
+int nemo_abi_version(void);
+/* Launch every kernel on `stream` (a hipStream_t, NULL = the context's own). */
+int nemo_set_stream(nemo_ctx *ctx, void *stream);
+/* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
+int nemo_set_timing(nemo_ctx *ctx, int enable);
+
+/* ---- load (loadProv, graphing/pre-post-prov.go:25-213) ---------------------
+ * Copies the corpus to HBM, builds forward + reverse CSR and the topological
+ * levels of every graph on the device, and validates like loadProv does:
+ * dangling or duplicate DUETO edges and goal->goal / rule->rule edges fail with
+ * the reference's "inserted number of edges" message (pre-post-prov.go:208-210).
+ * Cycles fail with NEMO_ERR_CYCLE.  Host arrays may be freed on return.     */
+int nemo_load_corpus(nemo_ctx *ctx, const nemo_corpus *corpus);
+/* Re-run the device part of the load (CSR + topo) on the resident corpus.    */
+int nemo_rebuild(nemo_ctx *ctx);
+uint64_t nemo_num_nodes(const nemo_ctx *ctx);
+uint64_t nemo_num_edges(const nemo_ctx *ctx);
+
+/* ---- markConditionHolds for every graph (pre-post-prov.go:218-244,247-285) */
+int nemo_mark_holds(nemo_ctx *ctx);
+
+/* ---- SimplifyProv for every run (preprocessing.go:351-387):
+ * cleanCopyProv (:13-63) then collapseNextChains (:66-348), pre and post.   */
+int nemo_simplify(nemo_ctx *ctx);
+
+/* ---- prototypes (prototype.go:9-256) --------------------------------------
+ * Cross-run reduction vector (u32, device memory, nemo_reduce_len entries):
+ *   [0, T)        cnt[t]   = #owned success runs whose proto list holds t
+ *   [T, 2T)       first[t] = table bits of the first success run's list
+ *   2T            achvdCond (prototype.go:70)
+ *   2T+1          first list non-empty (prototype.go:80-103)
+ *   2T+2          #holding "pre" goals in raw pre graphs (extensions.go:25-49)
+ *   2T+3          #owned runs
+ * Every entry is a sum, so a multi-GPU job all-reduces it with ncclSum.     */
+size_t nemo_reduce_len(const nemo_ctx *ctx);
+int nemo_protos_partial(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
+                        uint32_t *d_reduce /* device, nemo_reduce_len() u32 */);
+/* Interprets a (reduced) vector: inter/union table ids, ascending, "post"
+ * excluded (prototype.go:106,120).  Returns counts through n_inter/n_union;
+ * `inter`/`uni` may be NULL to query sizes (capacity n_tables is enough).   */
+int nemo_protos_finalize(nemo_ctx *ctx, const uint32_t *d_reduce, uint32_t *achieved,
+                         uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union,
+                         uint64_t *pre_holds_count, uint32_t *n_runs_total);
+/* Single-process convenience: partial + finalize with the context's own buffer. */
+int nemo_prototypes(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
+                    uint32_t *achieved, uint32_t *inter, uint32_t *n_inter,
+                    uint32_t *uni, uint32_t *n_union);
+/* missingFrom (prototype.go:141-206): entries of `proto` (table ids, in the
+ * caller's order) absent from the table set of the failed run's simplified
+ * post graph (run 1000+f).  `out` receives them in proto order.            */
+int nemo_missing_from(nemo_ctx *ctx, uint32_t failed_iter, const uint32_t *proto, uint32_t n_proto,
+                      uint32_t *out, uint32_t *n_out);
+
+/* ---- differential provenance (differential-provenance.go:18-243) ----------
+ * Good = run-0 post goals whose label is absent from the post goals of the
+ * label source run; D = Fwd*(Good) ∩ Bwd*(Good); missing events = deepest
+ * leaf-parent rules of D.  mode NEMO_DIFF_REFERENCE reproduces the reference's
+ * in-place ###RUN### substitution (:43): every entry uses failed_iters[0] as
+ * label source.  NEMO_DIFF_PER_RUN uses each entry's own failed run.        */
+#define NEMO_DIFF_REFERENCE 0
+#define NEMO_DIFF_PER_RUN   1
+int nemo_diffprov(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, int mode);
+/* D node mask over run 0's post graph for entry e (1 byte per node).        */
+int nemo_fetch_diff_mask(nemo_ctx *ctx, uint32_t entry, uint8_t *out, uint64_t cap);
+/* Missing rules of every entry; goals = all D-children of each rule.        */
+int nemo_fetch_missing(nemo_ctx *ctx, nemo_missing *out, uint64_t cap, uint64_t *n_out);
+
+/* ---- corrections / extensions on run 0 (corrections.go:25-193, extensions.go:13-99)
+ * pre rows (a, g, r) of findPreTriggers, post rows (g, r) of findPostTriggers,
+ * async rules of GenerateExtensions (only meaningful when not all achieved).  */
+int nemo_triggers(nemo_ctx *ctx);
+int nemo_fetch_triggers(nemo_ctx *ctx, uint32_t *pre_rows /* 3 per row */, uint64_t pre_cap,
+                        uint64_t *n_pre, uint32_t *post_rows /* 2 per row */, uint64_t post_cap,
+                        uint64_t *n_post, uint32_t *async_rules, uint64_t async_cap, uint64_t *n_async);
+
+/* ---- results ---------------------------------------------------------------- */
+/* Per-node flags (NEMO_F_*) of graphs [g_lo, g_hi), concatenated.           */
+int nemo_fetch_node_flags(nemo_ctx *ctx, uint32_t g_lo, uint32_t g_hi, uint8_t *out, uint64_t cap);
+/* Accepted @next chains of every graph, ordered by (graph, k).              */
+int nemo_fetch_chains(nemo_ctx *ctx, nemo_chain *out, uint64_t cap, uint64_t *n_out);
+/* Per-run table bitsets, words = ceil(n_tables/32) u32 per run:
+ *   which = 0: proto list of the run (extractProtos, prototype.go:11-24)
+ *   which = 1: all rule tables of the simplified post graph (missingFrom)   */
+int nemo_fetch_run_tables(nemo_ctx *ctx, int which, uint32_t *out, uint64_t cap);
+
+/* ---- edge pulls (PullPrePostProv, pre-post-prov.go:288-459; Q24) -----------
+ * which = 0: raw graph, 1: simplified graph (run 1000+i: kept, not deleted,
+ * plus collapsed rules), 2: differential graph of diff entry `aux`.
+ * Collapsed rule k of graph g is reported as node index V_g + k.           */
+int nemo_pull_edges(nemo_ctx *ctx, int which, uint32_t aux);
+uint64_t nemo_pulled_count(const nemo_ctx *ctx, uint32_t graph);
+int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t graph, uint32_t *src, uint32_t *dst, uint64_t cap,
+                      uint64_t *n_out);
+
+/* ---- instrumentation ------------------------------------------------------ */
+typedef struct nemo_timing {
+  char name[32];      /* kernel name                                        */
+  uint64_t launches;  /* launches recorded since the last reset             */
+  double ms;          /* summed HIP-event time                              */
+  double bytes;       /* summed algorithmic bytes     */
+  double edges;       /* summed edges examined                              */
+} nemo_timing;
+int nemo_timings(nemo_ctx *ctx, nemo_timing *out, uint32_t cap, uint32_t *n_out);
+int nemo_reset_timings(nemo_ctx *ctx);
+int nemo_synchronize(nemo_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEMOHIP_H */
