@@ -1,0 +1,32 @@
+# libnemohip: gfx950 kernels + C ABI (include/nemohip.h).  Cross-compiles here
+# (no GPU needed); the .so travels to the GPU box with the gpurun snapshot.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -Wno-unused-value
+BUILD := build
+SRCS := $(wildcard nemo_amd/csrc/*.hip)
+OBJS := $(patsubst nemo_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
+HDRS := $(wildcard nemo_amd/csrc/*.h) include/nemohip.h
+LIB := nemo_amd/libnemohip.so
+
+all: $(LIB) oracle tools
+
+$(BUILD)/%.o: nemo_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+tools:
+	$(MAKE) -s -C tools
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+	$(MAKE) -s -C oracle clean
+	$(MAKE) -s -C tools clean
+
+.PHONY: all oracle tools clean

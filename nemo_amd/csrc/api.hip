@@ -1,0 +1,882 @@
+// api.hip — the C ABI of libnemohip (include/nemohip.h): context, device
+// memory layout of a loaded corpus, phase orchestration, result fetches and
+// per-kernel HIP-event timing.  No CPU fallback exists: every analysis result
+// comes from the gfx950 kernels in k_*.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "device.h"
+#include "internal.h"
+
+namespace {
+
+struct Agg {
+  uint64_t launches = 0;
+  double ms = 0, bytes = 0, edges = 0;
+};
+
+struct PendingEv {
+  std::string name;
+  hipEvent_t a, b;
+  double bytes, edges;
+};
+
+}  // namespace
+
+struct nemo_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::string err;
+  bool timing = false;
+  std::vector<PendingEv> pending;
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, Agg> agg;
+
+  // host view of the loaded corpus
+  bool loaded = false, marked = false, simplified = false, protos_done = false;
+  uint32_t n_runs = 0, G = 0, T = 0, W = 0, table_pre = 0, table_post = 0;
+  uint64_t V = 0, E = 0;
+  std::vector<uint32_t> iteration;
+  std::vector<uint8_t> owned;
+  std::vector<uint64_t> node_off, edge_off;
+  std::unordered_map<uint32_t, uint32_t> it2run;
+  int32_t run0 = -1;
+  bool has_rank = false;
+
+  DevCorpus dc{};
+  uint8_t *d_owned = nullptr, *d_is_success = nullptr;
+  std::vector<void *> allocs;
+  uint32_t *d_red = nullptr;
+
+  // diff
+  uint32_t n_entries = 0, diff_cap = 0;
+  uint32_t *d_r0lab = nullptr, *d_r0idx = nullptr, n_r0lab = 0;
+  uint32_t *d_dsrc = nullptr, *d_miss = nullptr, *d_nmiss = nullptr;
+  uint8_t *d_dbits = nullptr, *d_dmask = nullptr;
+  int32_t *d_ddepth = nullptr;
+  uint64_t miss_cap = 0;
+
+  // pulls
+  int pull_which = -1;
+  uint32_t pull_aux = 0, pull_slots = 0;
+  uint32_t *d_pcnt = nullptr, *d_psrc = nullptr, *d_pdst = nullptr;
+  uint64_t *d_poff = nullptr, pull_cap = 0;
+  std::vector<uint64_t> h_poff;
+
+  // triggers
+  bool trig_done = false;
+  uint32_t *d_tcounts = nullptr, *d_tpre = nullptr, *d_tpost = nullptr, *d_tasync = nullptr;
+  uint32_t tcounts[3] = {0, 0, 0};
+
+  // chain gather
+  uint32_t *d_chcnt = nullptr, *d_chout = nullptr;
+  uint64_t *d_choff = nullptr;
+};
+
+static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) return fail((c), NEMO_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_));     \
+  } while (0)
+
+template <class T>
+static int dalloc(nemo_ctx *c, T **p, size_t n) {
+  void *q = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc(&q, n * sizeof(T));
+  if (e != hipSuccess)
+    return fail(c, NEMO_ERR_HIP, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+  c->allocs.push_back(q);
+  *p = (T *)q;
+  return NEMO_OK;
+}
+
+static void dfree(nemo_ctx *c, void *p) {
+  if (!p) return;
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+  if (it != c->allocs.end()) c->allocs.erase(it);
+  hipFree(p);
+}
+
+static hipEvent_t get_event(nemo_ctx *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+template <class F>
+static int timed(nemo_ctx *c, const char *name, double bytes, double edges, F &&f) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->timing) {
+    a = get_event(c);
+    b = get_event(c);
+    hipEventRecord(a, c->stream);
+  }
+  f();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(c, NEMO_ERR_HIP, "launch %s: %s", name, hipGetErrorString(e));
+  if (c->timing) {
+    hipEventRecord(b, c->stream);
+    c->pending.push_back({name, a, b, bytes, edges});
+    if (c->pending.size() > 4096) {  // bound outstanding events
+      hipEventSynchronize(c->pending.back().b);
+      for (auto &p : c->pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        Agg &g = c->agg[p.name];
+        g.launches++;
+        g.ms += ms;
+        g.bytes += p.bytes;
+        g.edges += p.edges;
+        c->ev_pool.push_back(p.a);
+        c->ev_pool.push_back(p.b);
+      }
+      c->pending.clear();
+    }
+  }
+  return NEMO_OK;
+}
+
+static int run_index(nemo_ctx *c, uint32_t it, uint32_t *r) {
+  auto f = c->it2run.find(it);
+  if (f == c->it2run.end()) return fail(c, NEMO_ERR_NOTFOUND, "unknown run iteration %u", it);
+  *r = f->second;
+  return NEMO_OK;
+}
+
+template <int K>
+static void sort_rows(uint32_t *rows, uint64_t n) {
+  std::vector<std::array<uint32_t, K>> v(n);
+  for (uint64_t i = 0; i < n; i++)
+    for (int k = 0; k < K; k++) v[i][k] = rows[K * i + k];
+  std::sort(v.begin(), v.end());
+  for (uint64_t i = 0; i < n; i++)
+    for (int k = 0; k < K; k++) rows[K * i + k] = v[i][k];
+}
+
+extern "C" {
+
+int nemo_abi_version(void) { return NEMOHIP_ABI_VERSION; }
+
+int nemo_ctx_create(int device, nemo_ctx **out) {
+  if (!out) return NEMO_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return NEMO_ERR_NOGPU;
+  if (device < 0 || device >= n) return NEMO_ERR_INVALID;
+  nemo_ctx *c = new nemo_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return NEMO_ERR_HIP;
+  }
+  c->stream = c->own;
+  *out = c;
+  return NEMO_OK;
+}
+
+static void release_corpus(nemo_ctx *c) {
+  for (void *p : c->allocs) hipFree(p);
+  c->allocs.clear();
+  c->dc = DevCorpus{};
+  c->d_owned = c->d_is_success = nullptr;
+  c->d_red = nullptr;
+  c->d_r0lab = c->d_r0idx = c->d_dsrc = c->d_miss = c->d_nmiss = nullptr;
+  c->d_dbits = c->d_dmask = nullptr;
+  c->d_ddepth = nullptr;
+  c->n_entries = c->diff_cap = 0;
+  c->miss_cap = 0;
+  c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
+  c->d_poff = nullptr;
+  c->pull_cap = 0;
+  c->pull_which = -1;
+  c->d_tcounts = c->d_tpre = c->d_tpost = c->d_tasync = nullptr;
+  c->d_chcnt = c->d_chout = nullptr;
+  c->d_choff = nullptr;
+  c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
+}
+
+void nemo_ctx_destroy(nemo_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  release_corpus(c);
+  for (auto &p : c->pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char *nemo_last_error(const nemo_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int nemo_set_stream(nemo_ctx *c, void *stream) {
+  if (!c) return NEMO_ERR_INVALID;
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return NEMO_OK;
+}
+
+int nemo_set_timing(nemo_ctx *c, int enable) {
+  if (!c) return NEMO_ERR_INVALID;
+  c->timing = enable != 0;
+  return NEMO_OK;
+}
+
+uint64_t nemo_num_nodes(const nemo_ctx *c) { return c ? c->V : 0; }
+uint64_t nemo_num_edges(const nemo_ctx *c) { return c ? c->E : 0; }
+
+static int check_graph_errors(nemo_ctx *c) {
+  std::vector<uint32_t> err(c->G), created(c->G);
+  HIPCHK(c, hipMemcpyAsync(err.data(), c->dc.err, c->G * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(created.data(), c->dc.created, c->G * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t g = 0; g < c->G; g++) {
+    if (!err[g]) continue;
+    const uint32_t it = c->iteration[g / 2];
+    const uint64_t E = c->edge_off[g + 1] - c->edge_off[g];
+    if (err[g] == NEMO_ERR_LOAD)
+      return fail(c, NEMO_ERR_LOAD,
+                  "Run %u: inserted number of edges (%u) does not equal number of antecedent provenance edges (%llu)",
+                  it, created[g], (unsigned long long)E);
+    if (err[g] == NEMO_ERR_CYCLE) return fail(c, NEMO_ERR_CYCLE, "Run %u: provenance graph is not acyclic", it);
+    return fail(c, (int)err[g], "Run %u: edge references a node index out of range", it);
+  }
+  return NEMO_OK;
+}
+
+static int device_load(nemo_ctx *c) {
+  int rc;
+  HIPCHK(c, hipMemsetAsync(c->dc.err, 0, c->G * sizeof(uint32_t), c->stream));
+  const double V = (double)c->V, E = (double)c->E;
+  if ((rc = timed(c, "k_csr", 16 * E + 12 * V, E, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
+  if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
+  return NEMO_OK;
+}
+
+int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
+  if (!c || !in) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  release_corpus(c);
+  if (in->n_tables > NEMO_MAX_TABLES)
+    return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
+  if (!in->iteration || !in->node_off || !in->edge_off || (!in->node_word && in->n_runs))
+    return fail(c, NEMO_ERR_INVALID, "corpus arrays missing");
+  c->n_runs = in->n_runs;
+  c->G = 2 * in->n_runs;
+  c->T = in->n_tables;
+  c->W = (in->n_tables + 31) / 32;
+  c->table_pre = in->table_pre;
+  c->table_post = in->table_post;
+  c->iteration.assign(in->iteration, in->iteration + in->n_runs);
+  c->owned.assign(in->n_runs, 1);
+  if (in->owned)
+    for (uint32_t r = 0; r < in->n_runs; r++) c->owned[r] = in->owned[r] ? 1 : 0;
+  c->node_off.assign(in->node_off, in->node_off + c->G + 1);
+  c->edge_off.assign(in->edge_off, in->edge_off + c->G + 1);
+  c->V = c->node_off[c->G];
+  c->E = c->edge_off[c->G];
+  c->it2run.clear();
+  c->run0 = -1;
+  for (uint32_t r = 0; r < c->n_runs; r++) {
+    if (c->it2run.count(c->iteration[r]))
+      return fail(c, NEMO_ERR_INVALID, "duplicate run iteration %u", c->iteration[r]);
+    c->it2run[c->iteration[r]] = r;
+    if (c->iteration[r] == 0) c->run0 = (int32_t)r;
+  }
+  for (uint32_t g = 0; g < c->G; g++) {
+    if (c->node_off[g + 1] < c->node_off[g] || c->edge_off[g + 1] < c->edge_off[g])
+      return fail(c, NEMO_ERR_INVALID, "offsets not monotone at graph %u", g);
+    if (c->node_off[g + 1] - c->node_off[g] >= 0xFFFFFFF0ull || c->edge_off[g + 1] - c->edge_off[g] >= 0xFFFFFFF0ull)
+      return fail(c, NEMO_ERR_LIMIT, "graph %u exceeds 2^32 nodes/edges", g);
+  }
+  if (c->node_off[0] != 0 || c->edge_off[0] != 0) return fail(c, NEMO_ERR_INVALID, "offsets must start at 0");
+  c->has_rank = in->id_rank != nullptr;
+  const size_t V = c->V, E = c->E, G = c->G, R = c->n_runs;
+  DevCorpus &d = c->dc;
+  int rc = 0;
+  uint64_t *no, *eo;
+  uint32_t *word, *label, *rank = nullptr, *es, *ed;
+#define A(p, n) \
+  if ((rc = dalloc(c, &(p), (n)))) return rc
+  A(no, G + 1);
+  A(eo, G + 1);
+  A(word, V);
+  A(label, V);
+  if (c->has_rank) A(rank, V);
+  A(es, E);
+  A(ed, E);
+  A(d.fp, V + G);
+  A(d.rp, V + G);
+  A(d.fc, E);
+  A(d.rc, E);
+  A(d.topo, V);
+  A(d.lvl, V + G);
+  A(d.nlev, G);
+  A(d.flags, V);
+  A(d.sb, V);
+  A(d.s_a, V + G);
+  A(d.s_b, V + G);
+  A(d.s_c, V + G);
+  A(d.s_d, V);
+  A(d.s_e, V);
+  A(d.err, G);
+  A(d.created, G);
+  A(d.prehold, G);
+  A(d.chain, 5 * V);
+  A(d.chain_tmp, 5 * V);
+  A(d.nch, G);
+  A(d.tail_first, V);
+  A(d.chain_nt, V);
+  A(d.proto_bits, R * c->W);
+  A(d.graph_tables, R * c->W);
+  A(d.gate, R);
+  A(c->d_owned, R);
+  A(c->d_is_success, R);
+  A(c->d_red, 2 * (size_t)c->T + 4);
+#undef A
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(no, in->node_off, (G + 1) * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(eo, in->edge_off, (G + 1) * 8, hipMemcpyHostToDevice, s));
+  if (V) {
+    HIPCHK(c, hipMemcpyAsync(word, in->node_word, V * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(label, in->label, V * 4, hipMemcpyHostToDevice, s));
+    if (rank) HIPCHK(c, hipMemcpyAsync(rank, in->id_rank, V * 4, hipMemcpyHostToDevice, s));
+  }
+  if (E) {
+    HIPCHK(c, hipMemcpyAsync(es, in->edge_src, E * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(ed, in->edge_dst, E * 4, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_owned, c->owned.data(), R, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemsetAsync(d.nch, 0, G * 4, s));
+  HIPCHK(c, hipMemsetAsync(d.prehold, 0, G * 4, s));
+  d.G = c->G;
+  d.n_runs = c->n_runs;
+  d.n_tables = c->T;
+  d.words = c->W;
+  d.table_pre = c->table_pre;
+  d.table_post = c->table_post;
+  d.node_off = no;
+  d.edge_off = eo;
+  d.word = word;
+  d.label = label;
+  d.rank = rank;
+  d.esrc = es;
+  d.edst = ed;
+  // run 0's post goal labels, sorted, for the diff's failGoals lookup
+  if (c->run0 >= 0) {
+    const uint32_t g0 = 2 * c->run0 + 1;
+    std::vector<std::pair<uint32_t, uint32_t>> lab;
+    for (uint64_t v = c->node_off[g0]; v < c->node_off[g0 + 1]; v++)
+      if (!(in->node_word[v] & NEMO_NODE_RULE)) lab.push_back({in->label[v], (uint32_t)(v - c->node_off[g0])});
+    std::sort(lab.begin(), lab.end());
+    std::vector<uint32_t> l(lab.size()), ix(lab.size());
+    for (size_t i = 0; i < lab.size(); i++) {
+      l[i] = lab[i].first;
+      ix[i] = lab[i].second;
+    }
+    c->n_r0lab = (uint32_t)lab.size();
+    if ((rc = dalloc(c, &c->d_r0lab, l.size()))) return rc;
+    if ((rc = dalloc(c, &c->d_r0idx, l.size()))) return rc;
+    if (!l.empty()) {
+      HIPCHK(c, hipMemcpyAsync(c->d_r0lab, l.data(), l.size() * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(c, hipMemcpyAsync(c->d_r0idx, ix.data(), ix.size() * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(c, hipStreamSynchronize(s));  // host vectors go out of scope
+    }
+  }
+  if ((rc = device_load(c))) return rc;
+  if ((rc = check_graph_errors(c))) return rc;
+  c->loaded = true;
+  return NEMO_OK;
+}
+
+int nemo_rebuild(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = device_load(c);
+  if (rc) return rc;
+  c->marked = c->simplified = c->protos_done = c->trig_done = false;
+  return NEMO_OK;
+}
+
+int nemo_mark_holds(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_mark_holds before nemo_load_corpus");
+  HIPCHK(c, hipSetDevice(c->device));
+  const double V = (double)c->V, E = (double)c->E;
+  int rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, c->stream); });
+  if (rc) return rc;
+  c->marked = true;
+  c->simplified = c->protos_done = c->trig_done = false;
+  return NEMO_OK;
+}
+
+int nemo_simplify(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_simplify before nemo_mark_holds");
+  HIPCHK(c, hipSetDevice(c->device));
+  const double V = (double)c->V, E = (double)c->E;
+  int rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, c->stream); });
+  if (rc) return rc;
+  rc = timed(c, "k_chains", 9 * V, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
+  if (rc) return rc;
+  c->simplified = true;
+  c->protos_done = false;
+  return NEMO_OK;
+}
+
+size_t nemo_reduce_len(const nemo_ctx *c) { return c ? 2 * (size_t)c->T + 4 : 0; }
+
+int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *d_red) {
+  if (!c || !d_red) return NEMO_ERR_INVALID;
+  if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_protos_partial before nemo_simplify");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint8_t> succ(c->n_runs, 0);
+  uint32_t first = NEMO_NONE;
+  for (size_t i = 0; i < n_success; i++) {
+    auto f = c->it2run.find(success_iters[i]);
+    if (f == c->it2run.end()) continue;  // another rank's run
+    succ[f->second] = 1;
+    if (i == 0) first = f->second;
+  }
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->d_is_success, succ.data(), c->n_runs, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemsetAsync(d_red, 0, nemo_reduce_len(c) * 4, s));
+  const double V = (double)c->V, E = (double)c->E;
+  int rc = timed(c, "k_proto", 8 * E + 12 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
+  if (rc) return rc;
+  rc = timed(c, "k_reduce", (double)c->n_runs * (c->W * 8 + 8), 0,
+             [&] { nemo::launch_reduce(c->dc, c->d_is_success, c->d_owned, first, d_red, s); });
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(s));  // host vector `succ` and caller's collective
+  c->protos_done = true;
+  return NEMO_OK;
+}
+
+int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
+                         uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
+                         uint32_t *n_runs_total) {
+  if (!c || !d_red) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t T = c->T;
+  std::vector<uint32_t> red(2 * (size_t)T + 4);
+  HIPCHK(c, hipMemcpyAsync(red.data(), d_red, red.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint32_t ni = 0, nu = 0;
+  if (red[2 * T + 1]) {  // `longest` is only set inside the loop over list0 (prototype.go:80-103)
+    for (uint32_t t = 0; t < T; t++) {
+      if (t == c->table_post) continue;  // != condition (prototype.go:106,120)
+      if (red[T + t] && red[t] == red[2 * T]) {
+        if (inter) inter[ni] = t;
+        ni++;
+      }
+      if (red[t] > 0) {
+        if (uni) uni[nu] = t;
+        nu++;
+      }
+    }
+  }
+  if (achieved) *achieved = red[2 * T];
+  if (n_inter) *n_inter = ni;
+  if (n_union) *n_union = nu;
+  if (pre_holds) *pre_holds = red[2 * T + 2];
+  if (n_runs_total) *n_runs_total = red[2 * T + 3];
+  return NEMO_OK;
+}
+
+int nemo_prototypes(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *achieved,
+                    uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (n_success == 0)
+    return fail(c, NEMO_ERR_INVALID, "no successful runs: extractProtos indexes iterProv[0] (prototype.go:80)");
+  int rc = nemo_protos_partial(c, success_iters, n_success, c->d_red);
+  if (rc) return rc;
+  return nemo_protos_finalize(c, c->d_red, achieved, inter, n_inter, uni, n_union, nullptr, nullptr);
+}
+
+int nemo_fetch_run_tables(nemo_ctx *c, int which, uint32_t *out, uint64_t cap) {
+  if (!c || !out) return NEMO_ERR_INVALID;
+  if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "run tables before nemo_protos_partial");
+  const uint64_t n = (uint64_t)c->n_runs * c->W;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)n);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, which == 0 ? c->dc.proto_bits : c->dc.graph_tables, n * 4, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return NEMO_OK;
+}
+
+int nemo_missing_from(nemo_ctx *c, uint32_t failed_iter, const uint32_t *proto, uint32_t n_proto, uint32_t *out,
+                      uint32_t *n_out) {
+  if (!c || (!proto && n_proto)) return NEMO_ERR_INVALID;
+  if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "nemo_missing_from before prototypes");
+  uint32_t r;
+  int rc = run_index(c, failed_iter, &r);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint32_t> bits(c->W);
+  HIPCHK(c, hipMemcpyAsync(bits.data(), c->dc.graph_tables + (size_t)r * c->W, c->W * 4, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < n_proto; i++) {
+    const uint32_t t = proto[i];
+    const bool have = t < c->T && ((bits[t >> 5] >> (t & 31)) & 1u);
+    if (!have) {
+      if (out) out[n] = t;
+      n++;
+    }
+  }
+  if (n_out) *n_out = n;
+  return NEMO_OK;
+}
+
+int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode) {
+  if (!c || (!failed_iters && n_failed)) return NEMO_ERR_INVALID;
+  if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_diffprov before nemo_mark_holds");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->n_entries = 0;
+  if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
+  std::vector<uint32_t> src(n_failed);
+  for (size_t e = 0; e < n_failed; e++) {
+    uint32_t r;
+    const uint32_t it = mode == NEMO_DIFF_PER_RUN ? failed_iters[e] : failed_iters[0];
+    int rc = run_index(c, it, &r);
+    if (rc) return rc;
+    src[e] = 2 * r + 1;
+  }
+  const uint32_t g0 = 2 * c->run0 + 1;
+  const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
+  const uint64_t E0 = c->edge_off[g0 + 1] - c->edge_off[g0];
+  int rc;
+  if (n_failed > c->diff_cap) {
+    dfree(c, c->d_dsrc);
+    dfree(c, c->d_dbits);
+    dfree(c, c->d_dmask);
+    dfree(c, c->d_ddepth);
+    dfree(c, c->d_miss);
+    if ((rc = dalloc(c, &c->d_dsrc, n_failed))) return rc;
+    if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
+    c->diff_cap = (uint32_t)n_failed;
+  }
+  if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->d_dsrc, src.data(), n_failed * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemsetAsync(c->d_nmiss, 0, 4, s));
+  nemo::DiffArgs a;
+  a.g0 = g0;
+  a.src = c->d_dsrc;
+  a.r0lab = c->d_r0lab;
+  a.r0idx = c->d_r0idx;
+  a.n_r0lab = c->n_r0lab;
+  a.bits = c->d_dbits;
+  a.depth = c->d_ddepth;
+  a.mask = c->d_dmask;
+  a.missing = c->d_miss;
+  a.n_missing = c->d_nmiss;
+  double bytes = (double)n_failed * (3.0 * (4 * E0 + 9 * V0) + 6 * V0);
+  rc = timed(c, "k_diff", bytes, (double)n_failed * 4 * E0,
+             [&] { nemo::launch_diff(c->dc, a, (uint32_t)n_failed, s); });
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(s));  // `src` host vector
+  c->n_entries = (uint32_t)n_failed;
+  return NEMO_OK;
+}
+
+int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap) {
+  if (!c || !out) return NEMO_ERR_INVALID;
+  if (entry >= c->n_entries) return fail(c, NEMO_ERR_INVALID, "diff entry %u out of range", entry);
+  const uint32_t g0 = 2 * c->run0 + 1;
+  const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
+  if (cap < V0) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_dmask + (size_t)entry * V0, V0, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return NEMO_OK;
+}
+
+int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n_out) {
+  if (!c) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t n = 0;
+  if (c->n_entries) {
+    HIPCHK(c, hipMemcpyAsync(&n, c->d_nmiss, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (n_out) *n_out = n;
+  if (!out) return NEMO_OK;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  std::vector<uint32_t> rows(2 * (size_t)n);
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(rows.data(), c->d_miss, rows.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  std::vector<std::pair<uint32_t, uint32_t>> v(n);
+  for (uint32_t i = 0; i < n; i++) v[i] = {rows[2 * i], rows[2 * i + 1]};
+  std::sort(v.begin(), v.end());
+  for (uint32_t i = 0; i < n; i++) {
+    out[i].entry = v[i].first;
+    out[i].rule = v[i].second;
+  }
+  return NEMO_OK;
+}
+
+int nemo_triggers(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_triggers before nemo_mark_holds");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->tcounts[0] = c->tcounts[1] = c->tcounts[2] = 0;
+  c->trig_done = true;
+  if (c->run0 < 0) return NEMO_OK;
+  int rc;
+  if (!c->d_tcounts && (rc = dalloc(c, &c->d_tcounts, 3))) return rc;
+  nemo::TrigArgs a{};
+  a.g_pre = 2 * c->run0;
+  a.g_post = 2 * c->run0 + 1;
+  a.counts = c->d_tcounts;
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemsetAsync(c->d_tcounts, 0, 12, s));
+  rc = timed(c, "k_triggers", 0, 0, [&] { nemo::launch_triggers(c->dc, a, 0, s); });
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->tcounts, c->d_tcounts, 12, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  dfree(c, c->d_tpre);
+  dfree(c, c->d_tpost);
+  dfree(c, c->d_tasync);
+  if ((rc = dalloc(c, &c->d_tpre, 3 * (size_t)c->tcounts[0]))) return rc;
+  if ((rc = dalloc(c, &c->d_tpost, 2 * (size_t)c->tcounts[1]))) return rc;
+  if ((rc = dalloc(c, &c->d_tasync, (size_t)c->tcounts[2]))) return rc;
+  a.pre = c->d_tpre;
+  a.post = c->d_tpost;
+  a.async_rules = c->d_tasync;
+  HIPCHK(c, hipMemsetAsync(c->d_tcounts, 0, 12, s));
+  rc = timed(c, "k_triggers", 0, 0, [&] { nemo::launch_triggers(c->dc, a, 1, s); });
+  if (rc) return rc;
+  return NEMO_OK;
+}
+
+
+int nemo_fetch_triggers(nemo_ctx *c, uint32_t *pre, uint64_t pre_cap, uint64_t *n_pre, uint32_t *post,
+                        uint64_t post_cap, uint64_t *n_post, uint32_t *async_rules, uint64_t async_cap,
+                        uint64_t *n_async) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->trig_done) return fail(c, NEMO_ERR_STATE, "nemo_fetch_triggers before nemo_triggers");
+  if (n_pre) *n_pre = c->tcounts[0];
+  if (n_post) *n_post = c->tcounts[1];
+  if (n_async) *n_async = c->tcounts[2];
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (pre && c->tcounts[0]) {
+    if (pre_cap < c->tcounts[0]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+    HIPCHK(c, hipMemcpyAsync(pre, c->d_tpre, 12 * (size_t)c->tcounts[0], hipMemcpyDeviceToHost, s));
+  }
+  if (post && c->tcounts[1]) {
+    if (post_cap < c->tcounts[1]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+    HIPCHK(c, hipMemcpyAsync(post, c->d_tpost, 8 * (size_t)c->tcounts[1], hipMemcpyDeviceToHost, s));
+  }
+  if (async_rules && c->tcounts[2]) {
+    if (async_cap < c->tcounts[2]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+    HIPCHK(c, hipMemcpyAsync(async_rules, c->d_tasync, 4 * (size_t)c->tcounts[2], hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (pre) sort_rows<3>(pre, c->tcounts[0]);
+  if (post) sort_rows<2>(post, c->tcounts[1]);
+  if (async_rules) std::sort(async_rules, async_rules + c->tcounts[2]);
+  return NEMO_OK;
+}
+
+int nemo_fetch_node_flags(nemo_ctx *c, uint32_t g_lo, uint32_t g_hi, uint8_t *out, uint64_t cap) {
+  if (!c || !out || g_lo > g_hi || g_hi > c->G) return NEMO_ERR_INVALID;
+  if (!c->marked) return fail(c, NEMO_ERR_STATE, "no flags before nemo_mark_holds");
+  const uint64_t a = c->node_off[g_lo], b = c->node_off[g_hi];
+  if (cap < b - a) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (b > a) {
+    HIPCHK(c, hipMemcpyAsync(out, c->dc.flags + a, b - a, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return NEMO_OK;
+}
+
+int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_out) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->simplified) return fail(c, NEMO_ERR_STATE, "no chains before nemo_simplify");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint32_t> nch(c->G);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(nch.data(), c->dc.nch, c->G * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  uint64_t n = 0;
+  for (uint32_t g = 0; g < c->G; g++) n += nch[g];
+  if (n_out) *n_out = n;
+  if (!out) return NEMO_OK;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  std::vector<uint32_t> buf;
+  uint64_t k = 0;
+  for (uint32_t g = 0; g < c->G; g++) {
+    if (!nch[g]) continue;
+    buf.resize(5 * (size_t)nch[g]);
+    HIPCHK(c, hipMemcpyAsync(buf.data(), c->dc.chain + 5 * c->node_off[g], buf.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (uint32_t i = 0; i < nch[g]; i++, k++) {
+      out[k].graph = g;
+      out[k].k = i;
+      out[k].head = buf[5 * i];
+      out[k].tail = buf[5 * i + 1];
+      out[k].len = buf[5 * i + 2];
+    }
+  }
+  return NEMO_OK;
+}
+
+int nemo_pull_edges(nemo_ctx *c, int which, uint32_t aux) {
+  if (!c || which < 0 || which > 2) return NEMO_ERR_INVALID;
+  if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
+  if (which == 2 && aux >= c->n_entries) return fail(c, NEMO_ERR_INVALID, "diff entry %u out of range", aux);
+  if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  const uint32_t slots = which == 2 ? 1 : c->G;
+  if (!c->d_pcnt) {
+    if ((rc = dalloc(c, &c->d_pcnt, (size_t)c->G + 1))) return rc;
+    if ((rc = dalloc(c, &c->d_poff, (size_t)c->G + 2))) return rc;
+  }
+  nemo::PullArgs a{};
+  a.which = (uint32_t)which;
+  const uint32_t g0 = c->run0 >= 0 ? 2 * c->run0 + 1 : 0;
+  a.g0 = g0;
+  if (which == 2) {
+    const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
+    a.mask = c->d_dmask + (size_t)aux * V0;
+  }
+  a.cnt = c->d_pcnt;
+  a.off = c->d_poff;
+  hipStream_t s = c->stream;
+  const double V = (double)c->V, E = (double)c->E;
+  rc = timed(c, "k_pull_count", 4 * E + 13 * V, E, [&] { nemo::launch_pull_count(c->dc, a, slots, s); });
+  if (rc) return rc;
+  c->h_poff.resize(slots + 1);
+  HIPCHK(c, hipMemcpyAsync(c->h_poff.data(), c->d_poff, (slots + 1) * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  const uint64_t total = c->h_poff[slots];
+  if (total > c->pull_cap) {
+    dfree(c, c->d_psrc);
+    dfree(c, c->d_pdst);
+    c->d_psrc = c->d_pdst = nullptr;
+    if ((rc = dalloc(c, &c->d_psrc, total))) return rc;
+    if ((rc = dalloc(c, &c->d_pdst, total))) return rc;
+    c->pull_cap = total;
+  }
+  a.src = c->d_psrc;
+  a.dst = c->d_pdst;
+  rc = timed(c, "k_pull_write", 4 * E + 13 * V + 8.0 * total, E, [&] { nemo::launch_pull_write(c->dc, a, slots, s); });
+  if (rc) return rc;
+  c->pull_which = which;
+  c->pull_aux = aux;
+  c->pull_slots = slots;
+  return NEMO_OK;
+}
+
+uint64_t nemo_pulled_count(const nemo_ctx *c, uint32_t graph) {
+  if (!c || c->pull_which < 0) return 0;
+  const uint32_t slot = c->pull_which == 2 ? 0 : graph;
+  if (slot >= c->pull_slots) return 0;
+  return c->h_poff[slot + 1] - c->h_poff[slot];
+}
+
+int nemo_fetch_pulled(nemo_ctx *c, uint32_t graph, uint32_t *src, uint32_t *dst, uint64_t cap, uint64_t *n_out) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
+  const uint32_t slot = c->pull_which == 2 ? 0 : graph;
+  if (slot >= c->pull_slots) return fail(c, NEMO_ERR_INVALID, "graph %u out of range", graph);
+  const uint64_t a = c->h_poff[slot], n = c->h_poff[slot + 1] - a;
+  if (n_out) *n_out = n;
+  if (!src && !dst) return NEMO_OK;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n) {
+    if (src) HIPCHK(c, hipMemcpyAsync(src, c->d_psrc + a, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (dst) HIPCHK(c, hipMemcpyAsync(dst, c->d_pdst + a, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return NEMO_OK;
+}
+
+int nemo_synchronize(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return NEMO_OK;
+}
+
+int nemo_timings(nemo_ctx *c, nemo_timing *out, uint32_t cap, uint32_t *n_out) {
+  if (!c) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  for (auto &p : c->pending) {
+    HIPCHK(c, hipEventSynchronize(p.b));
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, p.a, p.b));
+    Agg &g = c->agg[p.name];
+    g.launches++;
+    g.ms += ms;
+    g.bytes += p.bytes;
+    g.edges += p.edges;
+    c->ev_pool.push_back(p.a);
+    c->ev_pool.push_back(p.b);
+  }
+  c->pending.clear();
+  uint32_t n = 0;
+  for (auto &kv : c->agg) {
+    if (out && n < cap) {
+      memset(&out[n], 0, sizeof out[n]);
+      strncpy(out[n].name, kv.first.c_str(), sizeof out[n].name - 1);
+      out[n].launches = kv.second.launches;
+      out[n].ms = kv.second.ms;
+      out[n].bytes = kv.second.bytes;
+      out[n].edges = kv.second.edges;
+    }
+    n++;
+  }
+  if (n_out) *n_out = n;
+  return NEMO_OK;
+}
+
+int nemo_reset_timings(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  uint32_t n;
+  int rc = nemo_timings(c, nullptr, 0, &n);
+  c->agg.clear();
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+// device.h — gfx950 device helpers shared by the libnemohip kernels.
+//
+// Execution model: one 256-thread workgroup (4 wave64s)
+// owns one provenance graph; per-node state lives in graph-local slices of
+// global arrays (L2-resident while the workgroup works on its graph), and
+// level-synchronous sweeps walk the graph's Kahn levels with one workgroup
+// barrier per level.  Frontier queues are filled with wave-aggregated appends
+// (ballot + mbcnt, one LDS atomic per wave).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nemohip.h"
+
+#define NEMO_BLOCK 256
+#define NEMO_WAVES (NEMO_BLOCK / 64)
+#define NEMO_NONE 0xFFFFFFFFu
+
+// scratch flag bits (second byte array `sb`)
+#define SB_ROOT 0x01u
+#define SB_HASRC 0x02u
+#define SB_R1 0x04u
+#define SB_G2 0x08u
+#define SB_RCH 0x10u
+// transient bits in the flags byte (cleared before a phase returns)
+#define FT_NP 0x20u   // goal: has a kept next-rule parent
+#define FT_NC 0x40u   // goal: has a kept next-rule child
+#define FT_SEEN 0x80u // chain greedy: node covered by an accepted chain
+
+__device__ __forceinline__ bool is_rule(uint32_t w) { return (w & NEMO_NODE_RULE) != 0u; }
+__device__ __forceinline__ uint32_t type_of(uint32_t w) { return (w & NEMO_TYPE_MASK) >> NEMO_TYPE_SHIFT; }
+__device__ __forceinline__ uint32_t table_of(uint32_t w) { return w & NEMO_TABLE_MASK; }
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave-aggregated append of `val` (where pred) to q[*tail++]; one LDS atomic per wave.
+__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t *q, uint32_t *tail) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return;
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  if (pred) q[base + mbcnt(m)] = val;
+}
+
+// Block-wide exclusive scan of one u32 per thread; `lds` holds NEMO_WAVES u32.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, uint32_t *lds) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  if (lane == 63) lds[w] = v;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NEMO_WAVES; i++) {
+    uint32_t s = lds[i];
+    off += (i < (int)w) ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + v - x;
+}
+
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Graph-local view.  Arrays indexed per node use base n0 (+g for the V+1-sized
+// ones), arrays indexed per edge use base e0.
+struct GraphView {
+  uint32_t g, V, E;
+  uint64_t n0, e0;
+  const uint32_t *word, *label, *rank;
+  const uint32_t *fp, *fc, *rp, *rc;  // local CSR (rows sorted)
+  const uint32_t *topo, *lvl;          // Kahn order, level offsets into topo
+  uint32_t nlev;
+  uint8_t *flags;
+
+  __device__ __forceinline__ uint32_t rank_of(uint32_t v) const { return rank ? rank[v] : v; }
+  __device__ __forceinline__ uint32_t indeg(uint32_t v) const { return rp[v + 1] - rp[v]; }
+  __device__ __forceinline__ uint32_t outdeg(uint32_t v) const { return fp[v + 1] - fp[v]; }
+};
+
+// Device-side arrays of a loaded corpus (all graphs concatenated).
+struct DevCorpus {
+  uint32_t G, n_runs, n_tables, words, table_pre, table_post;
+  const uint64_t *node_off, *edge_off;
+  const uint32_t *word, *label, *rank;  // rank may be null
+  const uint32_t *esrc, *edst;
+  uint32_t *fp, *fc, *rp, *rc;           // fp/rp: V+G entries (graph g at n0+g)
+  uint32_t *topo, *lvl, *nlev;           // lvl: V+G entries
+  uint8_t *flags, *sb;                   // V
+  uint32_t *s_a, *s_b, *s_c;             // V+G scratch
+  int32_t *s_d;                          // V scratch
+  unsigned long long *s_e;               // V scratch
+  uint32_t *err;                         // [G] NEMO_ERR_* of the graph (0 = fine)
+  uint32_t *created;                     // [G] loadProv relationships-created
+  uint32_t *prehold;                     // [G] #holding "pre" goals (pre graphs)
+  uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
+  uint32_t *chain_tmp;                   // [5*V]
+  uint32_t *nch;                         // [G]
+  uint32_t *tail_first;                  // [V] head of per-tail chain list
+  uint32_t *chain_nt;                    // [V] next chain with the same tail
+  uint32_t *proto_bits, *graph_tables;   // [n_runs*words]
+  uint8_t *gate;                         // [n_runs]
+
+  __device__ __forceinline__ GraphView view(uint32_t g) const {
+    GraphView v;
+    v.g = g;
+    v.n0 = node_off[g];
+    v.e0 = edge_off[g];
+    v.V = (uint32_t)(node_off[g + 1] - v.n0);
+    v.E = (uint32_t)(edge_off[g + 1] - v.e0);
+    v.word = word + v.n0;
+    v.label = label + v.n0;
+    v.rank = rank ? rank + v.n0 : nullptr;
+    v.fp = fp + v.n0 + g;
+    v.rp = rp + v.n0 + g;
+    v.fc = fc + v.e0;
+    v.rc = rc + v.e0;
+    v.topo = topo + v.n0;
+    v.lvl = lvl + v.n0 + g;
+    v.nlev = nlev[g];
+    v.flags = flags + v.n0;
+    return v;
+  }
+};

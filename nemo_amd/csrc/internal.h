@@ -1,0 +1,52 @@
+// internal.h — host/device interface between the C ABI (api.hip) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct DevCorpus;
+
+namespace nemo {
+
+struct DiffArgs {
+  uint32_t g0;              // run 0's post graph
+  const uint32_t *src;      // [entries] label-source graph per entry
+  const uint32_t *r0lab;    // sorted goal labels of g0
+  const uint32_t *r0idx;    // local node of each sorted label
+  uint32_t n_r0lab;
+  uint8_t *bits;            // [entries * V0] scratch
+  int32_t *depth;           // [entries * V0] scratch
+  uint8_t *mask;            // [entries * V0] D mask (output)
+  uint32_t *missing;        // [2 * cap] (entry, rule)
+  uint32_t *n_missing;      // counter
+};
+
+struct PullArgs {
+  uint32_t which;           // 0 raw, 1 simplified, 2 diff
+  uint32_t g0;              // graph of which == 2
+  const uint8_t *mask;      // which == 2: D mask of the entry
+  uint32_t *cnt;            // [slots]
+  uint64_t *off;            // [slots + 1]
+  uint32_t *src, *dst;      // output
+};
+
+struct TrigArgs {
+  uint32_t g_pre, g_post;
+  uint32_t *counts;         // [3] pre rows, post rows, async rules
+  uint32_t *pre, *post, *async_rules;
+};
+
+void launch_load(const DevCorpus &c, hipStream_t s);
+void launch_topo(const DevCorpus &c, hipStream_t s);
+void launch_mark(const DevCorpus &c, hipStream_t s);
+void launch_simplify(const DevCorpus &c, hipStream_t s);
+void launch_chains(const DevCorpus &c, hipStream_t s);
+void launch_proto(const DevCorpus &c, hipStream_t s);
+void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
+                   uint32_t *red, hipStream_t s);
+void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s);
+void launch_pull_count(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
+void launch_pull_write(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
+void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
+
+}  // namespace nemo

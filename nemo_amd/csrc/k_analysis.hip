@@ -1,0 +1,492 @@
+// k_analysis.hip — markConditionHolds, cleanCopyProv, collapseNextChains and
+// extractProtos as per-graph workgroup kernels (one graph per workgroup).
+#include "device.h"
+#include "internal.h"
+
+namespace nemo {
+
+// markConditionHolds (graphing/pre-post-prov.go:218-244): a goal g qualifies
+// iff it has a rule child, some (C goal)->(C rule)->g exists, and no such
+// pattern starts at a C goal that has a parent.  Tq = tables of qualifying
+// goals (LDS bitset); if Tq is non-empty every goal whose table is C or in Tq
+// holds.  Also counts holding "pre" goals for GenerateExtensions
+// (extensions.go:25-49).  Resets every other flag bit of the graph.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c) {
+  __shared__ uint32_t s_tq[NEMO_MAX_TABLES / 32];
+  __shared__ uint32_t s_any, s_pre;
+  const uint32_t g = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
+  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) s_tq[i] = 0;
+  if (threadIdx.x == 0) {
+    s_any = 0;
+    s_pre = 0;
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    const uint32_t w = gv.word[x];
+    if (is_rule(w) || gv.outdeg(x) == 0) continue;
+    bool pos = false, neg = false;
+    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
+      const uint32_t rcn = gv.rc[j];
+      if (table_of(gv.word[rcn]) != C) continue;
+      for (uint32_t i = gv.rp[rcn]; i < gv.rp[rcn + 1]; i++) {
+        const uint32_t t = gv.rc[i];
+        if (table_of(gv.word[t]) != C) continue;
+        pos = true;
+        neg |= gv.indeg(t) > 0;
+      }
+    }
+    if (pos && !neg) {
+      atomicOr(&s_tq[table_of(w) >> 5], 1u << (table_of(w) & 31));
+      s_any = 1;
+    }
+  }
+  __syncthreads();
+  const bool any = s_any != 0;
+  uint32_t pre = 0;
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    const uint32_t w = gv.word[x];
+    const uint32_t t = table_of(w);
+    const bool h = any && !is_rule(w) && (t == C || ((s_tq[t >> 5] >> (t & 31)) & 1u));
+    gv.flags[x] = h ? (uint8_t)NEMO_F_HOLDS : (uint8_t)0;
+    pre += (h && t == c.table_pre) ? 1u : 0u;
+  }
+  if (pre) atomicAdd(&s_pre, pre);
+  __syncthreads();
+  if (threadIdx.x == 0) c.prehold[g] = s_pre;
+}
+
+// cleanCopyProv (preprocessing.go:13-63) + the local part of
+// collapseNextChains (:66-348): KEPT = goal or rule with in>0 and out>0;
+// on the clean graph a goal with a next-rule parent and a next-rule child, or
+// a next rule with a next-rule grandparent or grandchild, lies on an @next
+// chain and is DETACH DELETEd; heads/tails are the chain ends.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c) {
+  const uint32_t g = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  uint8_t *f = gv.flags;
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    uint8_t fl = f[x] & NEMO_F_HOLDS;
+    if (!is_rule(gv.word[x]) || (gv.indeg(x) > 0 && gv.outdeg(x) > 0)) fl |= NEMO_F_KEPT;
+    f[x] = fl;
+  }
+  __syncthreads();
+#define ISNEXT(v) (is_rule(gv.word[v]) && type_of(gv.word[v]) == NEMO_TYPE_NEXT && (f[v] & NEMO_F_KEPT))
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    if (is_rule(gv.word[x])) continue;
+    uint8_t b = 0;
+    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++)
+      if (ISNEXT(gv.rc[j])) b |= FT_NP;
+    for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++)
+      if (ISNEXT(gv.fc[j])) b |= FT_NC;
+    f[x] |= b;
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    if (!ISNEXT(x)) continue;
+    bool gp = false, gc = false;
+    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) gp |= (f[gv.rc[j]] & FT_NP) != 0;
+    for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) gc |= (f[gv.fc[j]] & FT_NC) != 0;
+    uint8_t fl = f[x];
+    if (gp || gc) fl |= NEMO_F_DELETED;
+    if (!gp && gc) fl |= NEMO_F_HEAD;
+    if (gp && !gc) fl |= NEMO_F_TAIL;
+    f[x] = fl;
+  }
+#undef ISNEXT
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    if (is_rule(gv.word[x])) continue;
+    uint8_t fl = f[x];
+    if ((fl & FT_NP) && (fl & FT_NC)) fl |= NEMO_F_DELETED;
+    f[x] = fl & (uint8_t)~(FT_NP | FT_NC);
+  }
+}
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t *p, uint32_t x) {
+  uint32_t y = ld_relaxed(&p[x]);
+  while (y != x) {
+    x = y;
+    y = ld_relaxed(&p[x]);
+  }
+  return x;
+}
+
+// Greedy @next chain cover (preprocessing.go:70-138).  Per weakly connected
+// component of the chain subgraph H* the accepted sequence is "the first path
+// in (length desc, ID-rank sequence asc) order that contains an unseen node";
+// every iteration runs one down-sweep over H* (longest unseen-containing
+// suffix, du) and one walker thread per component.  The global acceptance
+// index k is the rank of (len desc, head rank asc, iteration asc).
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
+  __shared__ uint32_t s_n, s_flag, s_nch;
+  const uint32_t g = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  uint8_t *f = gv.flags;
+  uint32_t *hs = c.s_a + gv.n0 + g;      // H* in topological order
+  uint32_t *hl = c.s_b + gv.n0 + g;      // H* level offsets
+  uint32_t *par = c.s_c + gv.n0 + g;     // union-find parent
+  int32_t *down = c.s_d + gv.n0;         // longest chain suffix (any)
+  int32_t *du = (int32_t *)(c.tail_first + gv.n0);  // longest unseen-containing suffix (temp)
+  unsigned long long *best = c.s_e + gv.n0;
+  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  if (threadIdx.x == 0) {
+    s_n = 0;
+    s_nch = 0;
+    hl[0] = 0;
+  }
+  __syncthreads();
+  // compact H* level by level
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    const uint32_t a = gv.lvl[l], b = gv.lvl[l + 1];
+    for (uint32_t base = a; base < b; base += NEMO_BLOCK) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t v = 0;
+      bool p = false;
+      if (i < b) {
+        v = gv.topo[i];
+        p = (f[v] & NEMO_F_DELETED) != 0;
+      }
+      wave_append(p, v, hs, &s_n);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) hl[l + 1] = s_n;
+    __syncthreads();
+  }
+  const uint32_t nh = s_n;
+  if (nh == 0) {
+    if (threadIdx.x == 0) c.nch[g] = 0;
+    return;
+  }
+#define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
+  // down[v]: longest H* path from v to a next rule
+  for (uint32_t l = gv.nlev; l-- > 0;) {
+    for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = hs[i];
+      int32_t d = is_rule(gv.word[v]) ? 0 : -1;
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+        const uint32_t w = gv.fc[j];
+        if (INH(w)) d = max(d, down[w] + 1);
+      }
+      down[v] = d;
+      par[v] = v;
+      best[v] = 0ull;
+    }
+    __syncthreads();
+  }
+  // weakly connected components of H* (hook to the smaller root + compress)
+  for (;;) {
+    if (threadIdx.x == 0) s_flag = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+      const uint32_t v = hs[i];
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+        const uint32_t w = gv.fc[j];
+        if (!INH(w)) continue;
+        const uint32_t a = uf_find(par, v), b = uf_find(par, w);
+        if (a != b) {
+          atomicMin(&par[max(a, b)], min(a, b));
+          s_flag = 1;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+      const uint32_t v = hs[i];
+      atomicMin(&par[v], uf_find(par, v));
+    }
+    __syncthreads();
+    if (!s_flag) break;
+    __syncthreads();
+  }
+  for (uint32_t iter = 0;; iter++) {
+    // du sweep (bottom-up)
+    for (uint32_t l = gv.nlev; l-- > 0;) {
+      for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
+        const uint32_t v = hs[i];
+        int32_t d;
+        if (!(f[v] & FT_SEEN)) {
+          d = down[v];
+        } else {
+          d = -1;
+          for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+            const uint32_t w = gv.fc[j];
+            if (INH(w) && du[w] >= 0) d = max(d, du[w] + 1);
+          }
+        }
+        du[v] = d;
+      }
+      __syncthreads();
+    }
+    // per component: max du, then min rank (packed key)
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+      const uint32_t v = hs[i];
+      if (is_rule(gv.word[v]) && du[v] >= 2) {
+        const unsigned long long key = ((unsigned long long)(uint32_t)du[v] << 32) | (0xFFFFFFFFu - gv.rank_of(v));
+        atomicMax(&best[par[v]], key);
+      }
+    }
+    if (threadIdx.x == 0) s_flag = 0;
+    __syncthreads();
+    // one walker per component: the lexicographically first path of that length
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+      const uint32_t s = hs[i];
+      if (!is_rule(gv.word[s]) || du[s] < 2) continue;
+      const unsigned long long key = ((unsigned long long)(uint32_t)du[s] << 32) | (0xFFFFFFFFu - gv.rank_of(s));
+      if (best[par[s]] != key) continue;
+      int32_t rem = du[s];
+      bool u = !(f[s] & FT_SEEN);
+      f[s] |= FT_SEEN;
+      uint32_t v = s;
+      while (rem > 0) {
+        uint32_t bc = NEMO_NONE, br = NEMO_NONE;
+        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+          const uint32_t w = gv.fc[j];
+          if (!INH(w)) continue;
+          const int32_t val = u ? down[w] : du[w];
+          const uint32_t rw = gv.rank_of(w);
+          if (val == rem - 1 && (bc == NEMO_NONE || rw < br)) {
+            bc = w;
+            br = rw;
+          }
+        }
+        if (bc == NEMO_NONE) break;  // unreachable: du/down guarantee a child
+        v = bc;
+        u |= !(f[v] & FT_SEEN);
+        f[v] |= FT_SEEN;
+        rem--;
+      }
+      const uint32_t k = atomicAdd(&s_nch, 1u);
+      uint32_t *t = tmp + 5 * k;
+      t[0] = s;
+      t[1] = v;
+      t[2] = (uint32_t)du[s];
+      t[3] = gv.rank_of(s);
+      t[4] = iter;
+      s_flag = 1;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) best[hs[i]] = 0ull;
+    const bool more = s_flag != 0;
+    __syncthreads();
+    if (!more) break;
+  }
+  // acceptance order k = rank of (len desc, head rank asc, iteration asc)
+  const uint32_t n = s_nch;
+  uint32_t *out = c.chain + 5 * gv.n0;
+  for (uint32_t i = threadIdx.x; i < n; i += NEMO_BLOCK) {
+    const uint32_t li = tmp[5 * i + 2], ri = tmp[5 * i + 3], ii = tmp[5 * i + 4];
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t lj = tmp[5 * j + 2], rj = tmp[5 * j + 3], ij = tmp[5 * j + 4];
+      k += (lj > li) || (lj == li && (rj < ri || (rj == ri && ij < ii)));
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) out[5 * k + q] = tmp[5 * i + q];
+  }
+  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+    const uint32_t v = hs[i];
+    f[v] &= (uint8_t)~FT_SEEN;
+    c.tail_first[gv.n0 + v] = NEMO_NONE;
+  }
+#undef INH
+  __syncthreads();
+  // per-tail chain lists (order irrelevant: only OR-ed over)
+  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) {
+    const uint32_t t = out[5 * k + 1];
+    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
+  }
+  if (threadIdx.x == 0) c.nch[g] = n;
+}
+
+// extractProtos' per-run query (prototype.go:11-24) and missingFrom's table
+// set (:143-147) on the simplified post graph, without materialising it:
+// collapsed rule k is reached through its head (preds(r1) = goal parents of
+// the head) and leads to the goal children of its tail.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
+  __shared__ uint32_t s_s[NEMO_MAX_TABLES / 32];
+  __shared__ uint32_t s_t[NEMO_MAX_TABLES / 32];
+  __shared__ uint32_t s_gate;
+  const uint32_t r = blockIdx.x;
+  const uint32_t g = 2 * r + 1;
+  if (c.err[g] || c.err[g - 1]) return;
+  const GraphView gv = c.view(g);
+  const GraphView pre = c.view(g - 1);
+  const uint8_t *f = gv.flags;
+  uint8_t *sb = c.sb + gv.n0;
+  const uint32_t *ch = c.chain + 5 * gv.n0;
+  const uint32_t *tf = c.tail_first + gv.n0, *nt = c.chain_nt + gv.n0;
+  const uint32_t nch = c.nch[g];
+  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) {
+    s_s[i] = 0;
+    s_t[i] = 0;
+  }
+  if (threadIdx.x == 0) s_gate = 0;
+  __syncthreads();
+  // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
+  for (uint32_t x = threadIdx.x; x < pre.V; x += NEMO_BLOCK) {
+    const uint8_t fl = pre.flags[x];
+    if (!is_rule(pre.word[x]) && (fl & NEMO_F_HOLDS) && !(fl & NEMO_F_DELETED)) s_gate = 1;
+  }
+#define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
+#define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+#define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    const uint32_t w = gv.word[x];
+    uint8_t b = 0;
+    if (is_rule(w)) {
+      if (REG(x) || (f[x] & NEMO_F_HEAD)) ADD(s_t, table_of(w));
+    } else if (!DEL(x)) {
+      bool root = true, hasrc = false;
+      for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
+        const uint32_t p = gv.rc[j];
+        if (REG(p) || (f[p] & NEMO_F_TAIL)) root = false;
+      }
+      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) {
+        const uint32_t q = gv.fc[j];
+        if (REG(q) || (f[q] & NEMO_F_HEAD)) hasrc = true;
+      }
+      b = (root ? SB_ROOT : 0) | (hasrc ? SB_HASRC : 0);
+    }
+    sb[x] = b;
+  }
+  __syncthreads();
+  // R1: rule children of roots (regular rules, and collapsed rules via their head)
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    const uint32_t w = gv.word[x];
+    if (!is_rule(w) || !(REG(x) || (f[x] & NEMO_F_HEAD))) continue;
+    bool r1 = false;
+    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
+      const uint32_t p = gv.rc[j];
+      if (!DEL(p) && (sb[p] & SB_ROOT)) r1 = true;
+    }
+    if (!r1) continue;
+    sb[x] |= SB_R1;
+    if (REG(x)) {
+      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) {
+        const uint32_t q = gv.fc[j];
+        if (!DEL(q) && (sb[q] & SB_HASRC)) {
+          ADD(s_s, table_of(w));
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // G2: goal children of R1 rules; collapsed R1 rules that have a goal child with a rule child
+  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+    if (is_rule(gv.word[x]) || DEL(x)) continue;
+    bool g2 = false;
+    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1] && !g2; j++) {
+      const uint32_t p = gv.rc[j];
+      if (REG(p)) {
+        g2 = (sb[p] & SB_R1) != 0;
+      } else if (f[p] & NEMO_F_TAIL) {
+        for (uint32_t k = tf[p]; k != NEMO_NONE; k = nt[k])
+          if (sb[ch[5 * k]] & SB_R1) g2 = true;
+      }
+    }
+    if (g2) sb[x] |= SB_G2;
+  }
+  for (uint32_t k = threadIdx.x; k < nch; k += NEMO_BLOCK) {
+    const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
+    if (!(sb[h] & SB_R1)) continue;
+    for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) {
+      const uint32_t q = gv.fc[j];
+      if (!DEL(q) && (sb[q] & SB_HASRC)) {
+        ADD(s_s, table_of(gv.word[h]));
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // rules reachable from G2 (forward level sweep over graph')
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t x = gv.topo[i];
+      const uint32_t w = gv.word[x];
+      bool rch = false;
+      if (!is_rule(w)) {
+        if (DEL(x)) continue;
+        for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1] && !rch; j++) {
+          const uint32_t p = gv.rc[j];
+          if (REG(p)) {
+            rch = (sb[p] & SB_RCH) != 0;
+          } else if (f[p] & NEMO_F_TAIL) {
+            for (uint32_t k = tf[p]; k != NEMO_NONE; k = nt[k])
+              if (sb[ch[5 * k]] & SB_RCH) rch = true;
+          }
+        }
+      } else if (REG(x) || (f[x] & NEMO_F_HEAD)) {
+        for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
+          const uint32_t p = gv.rc[j];
+          if (!DEL(p) && (sb[p] & (SB_G2 | SB_RCH))) rch = true;
+        }
+        if (rch) ADD(s_s, table_of(w));
+      }
+      if (rch) sb[x] |= SB_RCH;
+    }
+    __syncthreads();
+  }
+#undef DEL
+#undef REG
+#undef ADD
+  const bool gate = s_gate != 0;
+  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) {
+    c.proto_bits[(size_t)r * c.words + i] = gate ? s_s[i] : 0u;
+    c.graph_tables[(size_t)r * c.words + i] = s_t[i];
+  }
+  if (threadIdx.x == 0) c.gate[r] = gate ? 1 : 0;
+}
+
+// Cross-run reduction vector (nemo_reduce_len): per-table counts over owned
+// success runs with a non-empty list, the first success run's list, achvdCond
+// (prototype.go:29-130) and the holding-"pre"-goal count (extensions.go:25-49).
+__global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_t *is_success, const uint8_t *owned,
+                                                        uint32_t first_run, uint32_t *red) {
+  const uint32_t T = c.n_tables, W = c.words;
+  for (uint32_t r = blockIdx.x * NEMO_BLOCK + threadIdx.x; r < c.n_runs; r += gridDim.x * NEMO_BLOCK) {
+    const bool own = owned == nullptr || owned[r];
+    if (!own) continue;
+    atomicAdd(&red[2 * T + 3], 1u);
+    if (c.prehold[2 * r]) atomicAdd(&red[2 * T + 2], c.prehold[2 * r]);
+    const uint32_t *b = c.proto_bits + (size_t)r * W;
+    bool nonempty = false;
+    for (uint32_t i = 0; i < W; i++) nonempty |= b[i] != 0u;
+    if (r == first_run) {
+      red[2 * T + 1] = nonempty ? 1u : 0u;
+      for (uint32_t i = 0; i < W; i++)
+        for (uint32_t m = b[i]; m; m &= m - 1) red[T + 32 * i + __builtin_ctz(m)] = 1u;
+    }
+    if (!is_success[r] || !nonempty) continue;
+    atomicAdd(&red[2 * T], 1u);
+    for (uint32_t i = 0; i < W; i++)
+      for (uint32_t m = b[i]; m; m &= m - 1) atomicAdd(&red[32 * i + __builtin_ctz(m)], 1u);
+  }
+}
+
+void launch_mark(const DevCorpus &c, hipStream_t s) {
+  hipLaunchKernelGGL(k_mark, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+}
+void launch_simplify(const DevCorpus &c, hipStream_t s) {
+  hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+}
+void launch_chains(const DevCorpus &c, hipStream_t s) {
+  hipLaunchKernelGGL(k_chains, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+}
+void launch_proto(const DevCorpus &c, hipStream_t s) {
+  hipLaunchKernelGGL(k_proto, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);
+}
+void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
+                   uint32_t *red, hipStream_t s) {
+  uint32_t blocks = (c.n_runs + NEMO_BLOCK - 1) / NEMO_BLOCK;
+  if (blocks == 0) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_reduce, dim3(blocks), dim3(NEMO_BLOCK), 0, s, c, is_success, owned, first_run, red);
+}
+
+}  // namespace nemo

@@ -1,0 +1,317 @@
+// k_diff.hip — differential provenance (differential-provenance.go:18-146),
+// edge pulls (pre-post-prov.go:288-459, Q24) and the run-0 trigger patterns of
+// corrections.go:30-34,121-125 / extensions.go:63-67.
+#include "device.h"
+#include "internal.h"
+
+namespace nemo {
+
+#define DB_F 0x01u
+#define DB_B 0x02u
+#define DB_PRESENT 0x04u
+#define DB_LEAF 0x08u
+#define DB_D 0x10u
+#define DB_LP 0x20u
+
+// One workgroup per diff entry, all over run 0's post graph g0:
+//   Good = goals of g0 whose label is absent from the source run's post goals
+//   D    = Fwd*(Good) ∩ Bwd*(Good)                       (:22-32, APOC export)
+//   missing = D rules with a D-leaf child at maximal depth (:82-98)
+__global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
+  __shared__ int32_t s_max;
+  const uint32_t e = blockIdx.x;
+  const GraphView gv = c.view(a.g0);
+  const GraphView src = c.view(a.src[e]);
+  const uint32_t V = gv.V;
+  uint8_t *bits = a.bits + (size_t)e * V;
+  int32_t *depth = a.depth + (size_t)e * V;
+  uint8_t *mask = a.mask + (size_t)e * V;
+  if (threadIdx.x == 0) s_max = -1;
+  for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) bits[v] = 0;
+  __syncthreads();
+  // failGoals = collect(failed.label) (:23-24), looked up in run 0's sorted goal labels
+  for (uint32_t x = threadIdx.x; x < src.V; x += NEMO_BLOCK) {
+    if (is_rule(src.word[x])) continue;
+    const uint32_t lab = src.label[x];
+    uint32_t lo = 0, hi = a.n_r0lab;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.r0lab[mid] < lab) lo = mid + 1;
+      else hi = mid;
+    }
+    for (uint32_t i = lo; i < a.n_r0lab && a.r0lab[i] == lab; i++) bits[a.r0idx[i]] = DB_PRESENT;
+  }
+  __syncthreads();
+#define GOOD(v) (!is_rule(gv.word[v]) && !(bits[v] & DB_PRESENT))
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      bool fw = GOOD(v);
+      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1] && !fw; j++) fw = (bits[gv.rc[j]] & DB_F) != 0;
+      if (fw) bits[v] |= DB_F;
+    }
+    __syncthreads();
+  }
+  for (uint32_t l = gv.nlev; l-- > 0;) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      bool bw = GOOD(v);
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1] && !bw; j++) bw = (bits[gv.fc[j]] & DB_B) != 0;
+      uint8_t b = bits[v];
+      if (bw) b |= DB_B;
+      if ((b & DB_F) && bw) b |= DB_D;
+      bits[v] = b;
+    }
+    __syncthreads();
+  }
+#undef GOOD
+  // longest path from a D root (Kahn-level DP restricted to D)
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      const uint8_t b = bits[v];
+      mask[v] = (b & DB_D) ? 1 : 0;
+      if (!(b & DB_D)) continue;
+      int32_t d = 0;
+      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) {
+        const uint32_t p = gv.rc[j];
+        if (bits[p] & DB_D) d = max(d, depth[p] + 1);
+      }
+      depth[v] = d;
+      if (!is_rule(gv.word[v])) {
+        bool leaf = true;
+        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++)
+          if (bits[gv.fc[j]] & DB_D) leaf = false;
+        if (leaf) bits[v] = b | DB_LEAF;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t r = threadIdx.x; r < V; r += NEMO_BLOCK) {
+    if (!(bits[r] & DB_D) || !is_rule(gv.word[r])) continue;
+    bool lp = false;
+    for (uint32_t j = gv.fp[r]; j < gv.fp[r + 1]; j++) {
+      const uint32_t x = gv.fc[j];
+      if ((bits[x] & (DB_D | DB_LEAF)) == (DB_D | DB_LEAF)) lp = true;
+    }
+    if (lp) {
+      bits[r] |= DB_LP;
+      atomicMax(&s_max, depth[r] + 1);
+    }
+  }
+  __syncthreads();
+  const int32_t mx = s_max;
+  for (uint32_t r = threadIdx.x; r < V; r += NEMO_BLOCK) {
+    if ((bits[r] & DB_LP) && depth[r] + 1 == mx) {
+      const uint32_t k = atomicAdd(a.n_missing, 1u);
+      a.missing[2 * k] = e;
+      a.missing[2 * k + 1] = r;
+    }
+  }
+}
+
+// ---- edge pulls: which 0 = raw, 1 = simplified (graph'), 2 = diff entry ---------
+__device__ __forceinline__ bool pull_alive(uint32_t which, const uint8_t *f, const uint8_t *m, uint32_t v) {
+  if (which == 0) return true;
+  if (which == 1) return (f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT;
+  return m[v] != 0;
+}
+
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pull_count(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_cnt;
+  const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
+  const uint32_t slot = blockIdx.x;
+  if (c.err[g]) {
+    if (threadIdx.x == 0) a.cnt[slot] = 0;
+    return;
+  }
+  const GraphView gv = c.view(g);
+  const uint8_t *m = a.mask;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  uint32_t n = 0;
+  for (uint32_t u = threadIdx.x; u < gv.V; u += NEMO_BLOCK) {
+    if (!pull_alive(a.which, gv.flags, m, u)) continue;
+    for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
+  }
+  if (a.which == 1) {
+    const uint32_t *ch = c.chain + 5 * gv.n0;
+    for (uint32_t k = threadIdx.x; k < c.nch[g]; k += NEMO_BLOCK) {
+      const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
+      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
+      for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
+    }
+  }
+  atomicAdd(&s_cnt, n);
+  __syncthreads();
+  if (threadIdx.x == 0) a.cnt[slot] = s_cnt;
+}
+
+// exclusive scan of cnt[0..n) into off[0..n], one workgroup
+__global__ __launch_bounds__(NEMO_BLOCK) void k_scan64(const uint32_t *cnt, uint64_t *off, uint32_t n) {
+  __shared__ unsigned long long s_part[NEMO_BLOCK];
+  unsigned long long carry = 0;
+  for (uint32_t base = 0; base < n; base += NEMO_BLOCK) {
+    const uint32_t i = base + threadIdx.x;
+    const unsigned long long x = i < n ? cnt[i] : 0ull;
+    s_part[threadIdx.x] = x;
+    __syncthreads();
+    for (uint32_t d = 1; d < NEMO_BLOCK; d <<= 1) {
+      unsigned long long y = threadIdx.x >= d ? s_part[threadIdx.x - d] : 0ull;
+      __syncthreads();
+      s_part[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (i < n) off[i] = carry + s_part[threadIdx.x] - x;
+    const unsigned long long tot = s_part[NEMO_BLOCK - 1];
+    __syncthreads();
+    carry += tot;
+  }
+  if (threadIdx.x == 0) off[n] = carry;
+}
+
+// Ordered write: rows in node order, each row in CSR order, then collapsed
+// edges by k (pred->V+k for the head's goal parents, V+k->succ for the tail's
+// goal children).  Wave/block prefix sums place every edge.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pull_write(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_lds[NEMO_WAVES];
+  const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
+  const uint32_t slot = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  const uint8_t *m = a.mask;
+  uint64_t pos = a.off[slot];
+  for (uint32_t base = 0; base < gv.V; base += NEMO_BLOCK) {
+    const uint32_t u = base + threadIdx.x;
+    uint32_t n = 0;
+    const bool au = u < gv.V && pull_alive(a.which, gv.flags, m, u);
+    if (au)
+      for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
+    uint32_t tot;
+    uint64_t o = pos + block_exscan(n, &tot, s_lds);
+    if (au)
+      for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) {
+        const uint32_t v = gv.fc[j];
+        if (!pull_alive(a.which, gv.flags, m, v)) continue;
+        a.src[o] = u;
+        a.dst[o] = v;
+        o++;
+      }
+    pos += tot;
+  }
+  if (a.which != 1) return;
+  const uint32_t *ch = c.chain + 5 * gv.n0;
+  const uint32_t nch = c.nch[g];
+  for (uint32_t base = 0; base < nch; base += NEMO_BLOCK) {
+    const uint32_t k = base + threadIdx.x;
+    uint32_t n = 0, h = 0, t = 0;
+    if (k < nch) {
+      h = ch[5 * k];
+      t = ch[5 * k + 1];
+      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
+      for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
+    }
+    uint32_t tot;
+    uint64_t o = pos + block_exscan(n, &tot, s_lds);
+    if (k < nch) {
+      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) {
+        const uint32_t p = gv.rc[j];
+        if (!pull_alive(1, gv.flags, m, p)) continue;
+        a.src[o] = p;
+        a.dst[o] = gv.V + k;
+        o++;
+      }
+      for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) {
+        const uint32_t q = gv.fc[j];
+        if (!pull_alive(1, gv.flags, m, q)) continue;
+        a.src[o] = gv.V + k;
+        a.dst[o] = q;
+        o++;
+      }
+    }
+    pos += tot;
+  }
+}
+
+// ---- run-0 trigger patterns ------------------------------------------------------
+// phase 0 counts, phase 1 writes (capacities sized from the counts).
+__global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a, int phase) {
+  const GraphView gp = c.view(a.g_pre), gq = c.view(a.g_post);
+#define HOLDS(gg, v) (((gg).flags[v] & NEMO_F_HOLDS) != 0)
+  if (blockIdx.x == 0) {
+    // findPreTriggers (corrections.go:30-34): (a:Rule)->(g:Goal{holds:false})->(r:Rule), (h{holds})->(a)
+    for (uint32_t x = threadIdx.x; x < gp.V; x += NEMO_BLOCK) {
+      if (is_rule(gp.word[x]) || HOLDS(gp, x)) continue;
+      for (uint32_t j = gp.rp[x]; j < gp.rp[x + 1]; j++) {
+        const uint32_t ar = gp.rc[j];
+        bool hp = false;
+        for (uint32_t i = gp.rp[ar]; i < gp.rp[ar + 1]; i++) hp |= HOLDS(gp, gp.rc[i]);
+        if (!hp) continue;
+        const uint32_t n = gp.outdeg(x);
+        if (!n) continue;
+        const uint32_t k = atomicAdd(&a.counts[0], n);
+        if (phase == 1)
+          for (uint32_t i = 0; i < n; i++) {
+            a.pre[3 * (k + i)] = ar;
+            a.pre[3 * (k + i) + 1] = x;
+            a.pre[3 * (k + i) + 2] = gp.fc[gp.fp[x] + i];
+          }
+      }
+    }
+  } else if (blockIdx.x == 1) {
+    // findPostTriggers (corrections.go:121-125)
+    for (uint32_t x = threadIdx.x; x < gq.V; x += NEMO_BLOCK) {
+      if (is_rule(gq.word[x]) || !HOLDS(gq, x) || gq.indeg(x) == 0) continue;
+      for (uint32_t j = gq.fp[x]; j < gq.fp[x + 1]; j++) {
+        const uint32_t r = gq.fc[j];
+        bool ok = false;
+        for (uint32_t i = gq.fp[r]; i < gq.fp[r + 1]; i++) {
+          const uint32_t y = gq.fc[i];
+          ok |= !HOLDS(gq, y) && gq.outdeg(y) > 0;
+        }
+        if (!ok) continue;
+        const uint32_t k = atomicAdd(&a.counts[1], 1u);
+        if (phase == 1) {
+          a.post[2 * k] = x;
+          a.post[2 * k + 1] = r;
+        }
+      }
+    }
+  } else {
+    // GenerateExtensions' async rules (extensions.go:63-67)
+    for (uint32_t r = threadIdx.x; r < gp.V; r += NEMO_BLOCK) {
+      const uint32_t w = gp.word[r];
+      if (!is_rule(w) || type_of(w) != NEMO_TYPE_ASYNC) continue;
+      bool hp = false, np = false, down = false;
+      for (uint32_t j = gp.rp[r]; j < gp.rp[r + 1]; j++) {
+        if (HOLDS(gp, gp.rc[j])) hp = true;
+        else np = true;
+      }
+      for (uint32_t j = gp.fp[r]; j < gp.fp[r + 1]; j++) {
+        const uint32_t y = gp.fc[j];
+        down |= !HOLDS(gp, y) && gp.outdeg(y) > 0;
+      }
+      if ((hp && down) || np) {
+        const uint32_t k = atomicAdd(&a.counts[2], 1u);
+        if (phase == 1) a.async_rules[k] = r;
+      }
+    }
+  }
+#undef HOLDS
+}
+
+void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s) {
+  hipLaunchKernelGGL(k_diff, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
+}
+void launch_pull_count(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
+  hipLaunchKernelGGL(k_pull_count, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
+  hipLaunchKernelGGL(k_scan64, dim3(1), dim3(NEMO_BLOCK), 0, s, a.cnt, a.off, slots);
+}
+void launch_pull_write(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
+  hipLaunchKernelGGL(k_pull_write, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
+}
+void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
+  hipLaunchKernelGGL(k_triggers, dim3(3), dim3(NEMO_BLOCK), 0, s, c, a, phase);
+}
+
+}  // namespace nemo

@@ -1,0 +1,85 @@
+"""GPU parity: libnemohip (gfx950 kernels, called through the C ABI) vs the CPU oracle.
+
+Integer/index/bit work throughout, so the bar is bit-exact on every output
+(flags, chains incl. acceptance order k, table bitsets, inter/union, diff
+masks, missing events, trigger rows, simplified-graph edge multisets).
+"""
+import numpy as np
+import pytest
+
+from nemo_amd import engine as E
+from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE, corpus_from_graphs
+from oracle import oracle as O
+from tests.compare import assert_same
+from tests.small import random_corpus
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def _check(eng, corpus, mode=DIFF_REFERENCE, pulls=True):
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, diff_mode=mode)
+    res = E.analyze(corpus, s, f, diff_mode=mode, engine=eng, pulls=pulls)
+    assert_same(corpus, res, orc, len(f), check_pulls=pulls)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_small(eng, seed):
+    corpus, _ = random_corpus(seed, max_nodes=16)
+    _check(eng, corpus)
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_small_per_run_diff(eng, seed):
+    corpus, _ = random_corpus(1000 + seed, n_runs=4, max_nodes=16)
+    _check(eng, corpus, mode=DIFF_PER_RUN)
+
+
+def test_batched_many_graphs(eng):
+    # many tiny corpora concatenated into one corpus: one workgroup per graph
+    graphs = []
+    import random
+    from tests.small import random_prov
+    rng = random.Random(7)
+    for it in range(300):
+        st = "success" if it == 0 or rng.random() < 0.8 else "failure"
+        graphs.append((it, st, random_prov(rng, "pre", 24, p_next=0.7), random_prov(rng, "post", 24, p_next=0.7)))
+    _check(eng, corpus_from_graphs(graphs))
+
+
+def test_empty_graphs(eng):
+    empty = {"goals": [], "rules": [], "edges": []}
+    corpus = corpus_from_graphs([(0, "success", empty, empty), (1, "failure", empty, empty)])
+    _check(eng, corpus)
+
+
+def test_load_error_duplicate_and_nonbipartite(eng):
+    g = {"goals": [{"id": "goal0", "label": "a(1)", "table": "a", "time": "1"},
+                   {"id": "goal1", "label": "b(1)", "table": "b", "time": "1"}],
+         "rules": [], "edges": []}
+    corpus = corpus_from_graphs([(0, "success", g, g)])
+    # inject a goal->goal edge behind the host layer's back: the device load must refuse it
+    import numpy as np
+    corpus.edge_src = np.array([0], np.uint32)
+    corpus.edge_dst = np.array([1], np.uint32)
+    corpus.edge_off = np.array([0, 1, 1], np.uint64)
+    with pytest.raises(E.NemoError) as ei:
+        eng.load(corpus)
+    assert "inserted number of edges (0) does not equal number of antecedent provenance edges (1)" in str(ei.value)
+
+
+def test_cycle_refused(eng):
+    g = {"goals": [{"id": "goal0", "label": "a(1)", "table": "a", "time": "1"}],
+         "rules": [{"id": "rule0", "label": "a", "table": "a", "type": "next"}],
+         "edges": [{"from": "goal0", "to": "rule0"}, {"from": "rule0", "to": "goal0"}]}
+    corpus = corpus_from_graphs([(0, "success", g, g)])
+    with pytest.raises(E.NemoError) as ei:
+        eng.load(corpus)
+    assert ei.value.code == 4
