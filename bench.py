@@ -1,0 +1,233 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json's metric on its single-GPU config (C3), run-sharded over N GPUs.
+
+Metric: fault-injection runs analyzed per second (whole job, all ranks) plus
+edges traversed per second and the dominant kernel's fraction of the MI355X
+HBM roofline.  Workload: a synthetic Molly-shaped corpus of
+10k runs x (pre, post) provenance graphs of ~5k nodes per GPU (weak scaling:
+every rank owns its own 10k runs; run 0 is replicated on every rank as the
+good run of the differential provenance).
+
+One step = the whole hot path over the rank's corpus, inputs resident in HBM:
+  loadProv's device half (CSR + Kahn levels + validations)   nemo_rebuild
+  markConditionHolds (all graphs)                            nemo_mark_holds
+  SimplifyProv: cleanCopyProv + collapseNextChains           nemo_simplify
+  CreatePrototypes: extractProtos partial -> RCCL all-reduce (N>1) -> finalize,
+                    missingFrom for every failed run (table sets D2H)
+  CreateNaiveDiffProv for every failed run (per-run label sets)  nemo_diffprov
+  GenerateCorrections/Extensions trigger patterns (rank owning run 0)
+  PullPrePostProv + Q24 edge pulls (device compaction of simplified + diff graphs)
+  D2H of every compact result (node flags, chains, D masks, missing events)
+
+Launched as `python bench.py` (N=1) or under torch.distributed.run for N>1
+(RANK/LOCAL_RANK/WORLD_SIZE from the env, backend nccl = RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+METRIC = "fault-injection runs analyzed/sec (whole node) + edges traversed/sec vs HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--runs-per-gpu", type=int, default=10000)
+    ap.add_argument("--nodes", type=int, default=5000, help="target nodes per provenance graph")
+    ap.add_argument("--eot", type=int, default=10)
+    ap.add_argument("--diff-mode", choices=["per_run", "reference"], default="per_run")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    n_gpus = world
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE
+    from nemo_amd.engine import Engine
+    from tools import synth
+
+    R = args.runs_per_gpu
+    t0 = time.time()
+    corpus, info = synth.generate(R, target_nodes=args.nodes, eot=args.eot, run_base=rank * R,
+                                  prepend_run0=True, threads=min(16, os.cpu_count() or 1))
+    gen_s = time.time() - t0
+    owned = corpus.owned if corpus.owned is not None else np.ones(corpus.n_runs, np.uint8)
+    status_ok = np.array([s == "success" for s in corpus.status])
+    its = corpus.iteration
+    # global GetSuccessRunsIters(): run 0 is the fault-free first run, so it leads the list
+    success = [0] + [int(it) for it, ok, o in zip(its, status_ok, owned) if ok and o and it != 0]
+    failed = [int(it) for it, ok, o in zip(its, status_ok, owned) if (not ok) and o]
+    has_run0 = bool(owned[corpus.run_index(0)]) if 0 in set(its.tolist()) else False
+    mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
+
+    eng = Engine(local)
+    stream = torch.cuda.current_stream()
+    eng.set_stream(stream.cuda_stream)
+    eng.load(corpus)
+    d_red = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda")
+    T = corpus.n_tables
+    W = (T + 31) // 32
+    g0 = 2 * corpus.run_index(0) + 1
+    V0 = corpus.graph_size(g0)
+
+    def step():
+        eng.rebuild()
+        eng.mark()
+        eng.simplify()
+        eng.protos_partial(success, d_red.data_ptr())
+        if world > 1:
+            dist.all_reduce(d_red)
+        protos = eng.protos_finalize(d_red.data_ptr())
+        tabs = eng.run_tables(1)
+        inter = np.asarray(protos["inter"], np.int64)
+        uni = np.asarray(protos["union"], np.int64)
+        fidx = np.array([corpus.run_index(f) for f in failed], np.int64)
+        if len(fidx):
+            have_i = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
+            have_u = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
+        eng.diffprov(failed, mode)
+        if has_run0:
+            eng.triggers()
+            eng.trigger_rows()
+        eng.pull(1)
+        eng.pull(2)
+        flags = eng.flags()
+        chains = eng.chains()
+        masks = eng.diff_masks(len(failed)) if failed else None
+        miss = eng.missing()
+        return flags, chains, masks, miss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    eng.reset_timings()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    tim = eng.timings()
+    eng.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    owned_runs = int(owned.sum())
+    total_runs = owned_runs * world if world > 1 else owned_runs
+    if world > 1:
+        t = torch.tensor([owned_runs], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        total_runs = int(t.item())
+    runs_per_s = total_runs * args.steps / elapsed
+    kern_ms = sum(v["ms"] for v in tim.values())
+    edges = sum(v["edges"] for v in tim.values())
+    if world > 1:
+        t = torch.tensor([edges, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        edges, kern_ms_sum = float(t[0].item()), float(t[1].item())
+    # edges/s: edges examined by all traversal kernels of all ranks over the wall time
+    edges_per_s = edges / elapsed
+    dom = max(tim.items(), key=lambda kv: kv[1]["ms"])
+    dname, d = dom
+    per_launch_bytes = d["bytes"] / d["launches"]
+    avg_ms = d["ms"] / d["launches"]
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{dname}.json")
+    if os.path.exists(pmc):
+        try:
+            pj = json.load(open(pmc))
+            if pj.get("workload_nodes") == int(corpus.node_off[-1]):
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        reps, t_cpu = 0, 0.0
+        while t_cpu < args.cpu_seconds:
+            tc = time.perf_counter()
+            O.analyze(corpus, success, failed, diff_mode=mode, threads=threads, skip_pulls=True)
+            t_cpu += time.perf_counter() - tc
+            reps += 1
+        cpu = {"value": round(owned_runs * reps / t_cpu, 2), "unit": "runs/s", "cores": threads, "kind": "port",
+               "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on the same {owned_runs}-run "
+                         f"C3 corpus, {reps} full pass(es) in {t_cpu:.1f}s; same phases except the D2H/edge-list "
+                         f"materialisation"}
+    out = {
+        "metric": METRIC,
+        "value": round(runs_per_s, 2),
+        "unit": "runs/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance graphs "
+                               "of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated",
+                   "runs_per_gpu": R, "nodes_per_graph": args.nodes, "eot": args.eot,
+                   "nodes_total_rank0": int(corpus.node_off[-1]), "edges_total_rank0": int(corpus.edge_off[-1]),
+                   "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,
+                   "parallelism": f"run-sharded x{n_gpus}, RCCL all-reduce of the prototype vector"},
+        "edges_traversed_per_s": round(edges_per_s, 1),
+        "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(avg_ms, 4)},
+        "cpu_baseline": cpu,
+        "kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
+                        "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
+                    for k, v in sorted(tim.items(), key=lambda kv: -kv[1]["ms"])},
+        "gen_seconds_rank0": round(gen_s, 2),
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

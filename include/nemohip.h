@@ -114,6 +114,11 @@ const char *nemo_last_error(const nemo_ctx *ctx);
 int nemo_abi_version(void);
 /* Launch every kernel on `stream` (a hipStream_t, NULL = the context's own). */
 int nemo_set_stream(nemo_ctx *ctx, void *stream);
+/* Tuning / test knobs (-1 = default): "chains_lds_max" = largest chain
+ * subgraph (nodes) the first @next-chain tier stages in LDS; larger graphs go
+ * to the component tier, where "chains_comp_max" = largest component run in
+ * LDS by one wave (larger ones take the workgroup-wide global-memory path). */
+int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);
 
@@ -154,6 +159,10 @@ int nemo_protos_partial(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_s
 int nemo_protos_finalize(nemo_ctx *ctx, const uint32_t *d_reduce, uint32_t *achieved,
                          uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union,
                          uint64_t *pre_holds_count, uint32_t *n_runs_total);
+/* Host-only interpretation of a (reduced) vector held in HOST memory; needs no
+ * context or device (nemo_protos_finalize = D2H + this). */
+int nemo_reduce_interpret(const uint32_t *h_reduce, uint32_t n_tables, uint32_t table_post, uint32_t *achieved,
+                          uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union);
 /* Single-process convenience: partial + finalize with the context's own buffer. */
 int nemo_prototypes(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
                     uint32_t *achieved, uint32_t *inter, uint32_t *n_inter,
@@ -175,6 +184,8 @@ int nemo_missing_from(nemo_ctx *ctx, uint32_t failed_iter, const uint32_t *proto
 int nemo_diffprov(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, int mode);
 /* D node mask over run 0's post graph for entry e (1 byte per node).        */
 int nemo_fetch_diff_mask(nemo_ctx *ctx, uint32_t entry, uint8_t *out, uint64_t cap);
+/* D masks of every entry, entry-major (n_entries * V0 bytes).               */
+int nemo_fetch_diff_masks(nemo_ctx *ctx, uint8_t *out, uint64_t cap);
 /* Missing rules of every entry; goals = all D-children of each rule.        */
 int nemo_fetch_missing(nemo_ctx *ctx, nemo_missing *out, uint64_t cap, uint64_t *n_out);
 
@@ -197,12 +208,14 @@ int nemo_fetch_chains(nemo_ctx *ctx, nemo_chain *out, uint64_t cap, uint64_t *n_
 int nemo_fetch_run_tables(nemo_ctx *ctx, int which, uint32_t *out, uint64_t cap);
 
 /* ---- edge pulls (PullPrePostProv, pre-post-prov.go:288-459; Q24) -----------
- * which = 0: raw graph, 1: simplified graph (run 1000+i: kept, not deleted,
- * plus collapsed rules), 2: differential graph of diff entry `aux`.
- * Collapsed rule k of graph g is reported as node index V_g + k.           */
-int nemo_pull_edges(nemo_ctx *ctx, int which, uint32_t aux);
-uint64_t nemo_pulled_count(const nemo_ctx *ctx, uint32_t graph);
-int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t graph, uint32_t *src, uint32_t *dst, uint64_t cap,
+ * which = 0: raw graphs, 1: simplified graphs (run 1000+i: kept, not deleted,
+ * plus collapsed rules), 2: differential graphs of every diff entry.  The
+ * compacted edge lists stay in HBM; `slot` below is the graph index (which
+ * 0/1) or the diff entry (which 2).  Collapsed rule k of graph g is reported
+ * as node index V_g + k.                                                   */
+int nemo_pull_edges(nemo_ctx *ctx, int which);
+uint64_t nemo_pulled_count(const nemo_ctx *ctx, uint32_t slot);
+int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap,
                       uint64_t *n_out);
 
 /* ---- instrumentation ------------------------------------------------------ */
@@ -216,6 +229,9 @@ typedef struct nemo_timing {
 int nemo_timings(nemo_ctx *ctx, nemo_timing *out, uint32_t cap, uint32_t *n_out);
 int nemo_reset_timings(nemo_ctx *ctx);
 int nemo_synchronize(nemo_ctx *ctx);
+/* Inspection hook for tests: copy bytes of a named internal device array
+ * ("topo", "lvl", "nlev", "fp", "fc", "rp", "rc", "flags", "dbits", "dmask"). */
+int nemo_debug_copy(nemo_ctx *ctx, const char *name, void *out, uint64_t offset, uint64_t bytes);
 
 #ifdef __cplusplus
 }

@@ -51,6 +51,7 @@ struct nemo_ctx {
   std::unordered_map<uint32_t, uint32_t> it2run;
   int32_t run0 = -1;
   bool has_rank = false;
+  uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu;
 
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
@@ -67,7 +68,7 @@ struct nemo_ctx {
 
   // pulls
   int pull_which = -1;
-  uint32_t pull_aux = 0, pull_slots = 0;
+  uint32_t pull_slots = 0, pull_slot_cap = 0;
   uint32_t *d_pcnt = nullptr, *d_psrc = nullptr, *d_pdst = nullptr;
   uint64_t *d_poff = nullptr, pull_cap = 0;
   std::vector<uint64_t> h_poff;
@@ -78,8 +79,8 @@ struct nemo_ctx {
   uint32_t tcounts[3] = {0, 0, 0};
 
   // chain gather
-  uint32_t *d_chcnt = nullptr, *d_chout = nullptr;
-  uint64_t *d_choff = nullptr;
+  uint32_t *d_chout = nullptr;
+  uint64_t *d_choff = nullptr, chout_cap = 0;
 };
 
 static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
@@ -213,10 +214,12 @@ static void release_corpus(nemo_ctx *c) {
   c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
   c->d_poff = nullptr;
   c->pull_cap = 0;
+  c->pull_slot_cap = 0;
   c->pull_which = -1;
   c->d_tcounts = c->d_tpre = c->d_tpost = c->d_tasync = nullptr;
-  c->d_chcnt = c->d_chout = nullptr;
+  c->d_chout = nullptr;
   c->d_choff = nullptr;
+  c->chout_cap = 0;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
 }
 
@@ -240,6 +243,21 @@ int nemo_set_stream(nemo_ctx *c, void *stream) {
   if (!c) return NEMO_ERR_INVALID;
   c->stream = stream ? (hipStream_t)stream : c->own;
   return NEMO_OK;
+}
+
+int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
+  if (!c || !name) return NEMO_ERR_INVALID;
+  if (!strcmp(name, "chains_lds_max")) {
+    c->hcap_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
+    c->dc.hcap_limit = c->hcap_limit;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "chains_comp_max")) {
+    c->comp_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
+    c->dc.comp_limit = c->comp_limit;
+    return NEMO_OK;
+  }
+  return fail(c, NEMO_ERR_INVALID, "unknown option %s", name);
 }
 
 int nemo_set_timing(nemo_ctx *c, int enable) {
@@ -346,6 +364,8 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.s_c, V + G);
   A(d.s_d, V);
   A(d.s_e, V);
+  A(d.s_f, V + G);
+  A(d.s_g, V + G);
   A(d.err, G);
   A(d.created, G);
   A(d.prehold, G);
@@ -377,6 +397,8 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipMemsetAsync(d.nch, 0, G * 4, s));
   HIPCHK(c, hipMemsetAsync(d.prehold, 0, G * 4, s));
   d.G = c->G;
+  d.hcap_limit = c->hcap_limit;
+  d.comp_limit = c->comp_limit;
   d.n_runs = c->n_runs;
   d.n_tables = c->T;
   d.words = c->W;
@@ -480,20 +502,14 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   return NEMO_OK;
 }
 
-int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
-                         uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
-                         uint32_t *n_runs_total) {
-  if (!c || !d_red) return NEMO_ERR_INVALID;
-  HIPCHK(c, hipSetDevice(c->device));
-  const uint32_t T = c->T;
-  std::vector<uint32_t> red(2 * (size_t)T + 4);
-  HIPCHK(c, hipMemcpyAsync(red.data(), d_red, red.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+int nemo_reduce_interpret(const uint32_t *red, uint32_t T, uint32_t table_post, uint32_t *achieved, uint32_t *inter,
+                          uint32_t *n_inter, uint32_t *uni, uint32_t *n_union) {
+  if (!red) return NEMO_ERR_INVALID;
   uint32_t ni = 0, nu = 0;
   if (red[2 * T + 1]) {  // `longest` is only set inside the loop over list0 (prototype.go:80-103)
     for (uint32_t t = 0; t < T; t++) {
-      if (t == c->table_post) continue;  // != condition (prototype.go:106,120)
-      if (red[T + t] && red[t] == red[2 * T]) {
+      if (t == table_post) continue;  // != condition (prototype.go:106,120)
+      if (red[T + t] && red[t] == red[2 * T]) {  // foundIn == achvdCond (prototype.go:106)
         if (inter) inter[ni] = t;
         ni++;
       }
@@ -506,9 +522,21 @@ int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved,
   if (achieved) *achieved = red[2 * T];
   if (n_inter) *n_inter = ni;
   if (n_union) *n_union = nu;
+  return NEMO_OK;
+}
+
+int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
+                         uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
+                         uint32_t *n_runs_total) {
+  if (!c || !d_red) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t T = c->T;
+  std::vector<uint32_t> red(2 * (size_t)T + 4);
+  HIPCHK(c, hipMemcpyAsync(red.data(), d_red, red.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (pre_holds) *pre_holds = red[2 * T + 2];
   if (n_runs_total) *n_runs_total = red[2 * T + 3];
-  return NEMO_OK;
+  return nemo_reduce_interpret(red.data(), T, c->table_post, achieved, inter, n_inter, uni, n_union);
 }
 
 int nemo_prototypes(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *achieved,
@@ -625,6 +653,18 @@ int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap
   return NEMO_OK;
 }
 
+int nemo_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap) {
+  if (!c || !out) return NEMO_ERR_INVALID;
+  if (!c->n_entries) return NEMO_OK;
+  const uint32_t g0 = 2 * c->run0 + 1;
+  const uint64_t n = (uint64_t)c->n_entries * (c->node_off[g0 + 1] - c->node_off[g0]);
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_dmask, n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return NEMO_OK;
+}
+
 int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n_out) {
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
@@ -732,60 +772,67 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
   if (!c) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "no chains before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<uint32_t> nch(c->G);
+  int rc;
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(nch.data(), c->dc.nch, c->G * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
+  if (!c->d_choff && (rc = dalloc(c, &c->d_choff, (size_t)c->G + 1))) return rc;
+  rc = timed(c, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
+  if (rc) return rc;
   uint64_t n = 0;
-  for (uint32_t g = 0; g < c->G; g++) n += nch[g];
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_choff + c->G, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   if (n_out) *n_out = n;
   if (!out) return NEMO_OK;
   if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  std::vector<uint32_t> buf;
-  uint64_t k = 0;
-  for (uint32_t g = 0; g < c->G; g++) {
-    if (!nch[g]) continue;
-    buf.resize(5 * (size_t)nch[g]);
-    HIPCHK(c, hipMemcpyAsync(buf.data(), c->dc.chain + 5 * c->node_off[g], buf.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    for (uint32_t i = 0; i < nch[g]; i++, k++) {
-      out[k].graph = g;
-      out[k].k = i;
-      out[k].head = buf[5 * i];
-      out[k].tail = buf[5 * i + 1];
-      out[k].len = buf[5 * i + 2];
-    }
+  if (n > c->chout_cap) {
+    dfree(c, c->d_chout);
+    c->d_chout = nullptr;
+    if ((rc = dalloc(c, &c->d_chout, 5 * n))) return rc;
+    c->chout_cap = n;
   }
+  rc = timed(c, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, c->d_chout, s); });
+  if (rc) return rc;
+  static_assert(sizeof(nemo_chain) == 20, "nemo_chain layout");
+  if (n) HIPCHK(c, hipMemcpyAsync(out, c->d_chout, n * 20, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   return NEMO_OK;
 }
 
-int nemo_pull_edges(nemo_ctx *c, int which, uint32_t aux) {
+int nemo_pull_edges(nemo_ctx *c, int which) {
   if (!c || which < 0 || which > 2) return NEMO_ERR_INVALID;
-  if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
-  if (which == 2 && aux >= c->n_entries) return fail(c, NEMO_ERR_INVALID, "diff entry %u out of range", aux);
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
+  if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
-  const uint32_t slots = which == 2 ? 1 : c->G;
-  if (!c->d_pcnt) {
-    if ((rc = dalloc(c, &c->d_pcnt, (size_t)c->G + 1))) return rc;
-    if ((rc = dalloc(c, &c->d_poff, (size_t)c->G + 2))) return rc;
+  const uint32_t slots = which == 2 ? c->n_entries : c->G;
+  if (slots + 1 > c->pull_slot_cap) {
+    dfree(c, c->d_pcnt);
+    dfree(c, c->d_poff);
+    if ((rc = dalloc(c, &c->d_pcnt, (size_t)slots + 1))) return rc;
+    if ((rc = dalloc(c, &c->d_poff, (size_t)slots + 2))) return rc;
+    c->pull_slot_cap = slots + 1;
   }
+  c->pull_which = which;
+  c->pull_slots = slots;
+  c->h_poff.assign(slots + 1, 0);
+  if (slots == 0) return NEMO_OK;
   nemo::PullArgs a{};
   a.which = (uint32_t)which;
   const uint32_t g0 = c->run0 >= 0 ? 2 * c->run0 + 1 : 0;
   a.g0 = g0;
   if (which == 2) {
-    const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
-    a.mask = c->d_dmask + (size_t)aux * V0;
+    a.mask = c->d_dmask;
+    a.mask_stride = c->node_off[g0 + 1] - c->node_off[g0];
   }
   a.cnt = c->d_pcnt;
   a.off = c->d_poff;
   hipStream_t s = c->stream;
-  const double V = (double)c->V, E = (double)c->E;
+  double V = (double)c->V, E = (double)c->E;
+  if (which == 2) {
+    V = (double)slots * (double)a.mask_stride;
+    E = (double)slots * (double)(c->edge_off[g0 + 1] - c->edge_off[g0]);
+  }
   rc = timed(c, "k_pull_count", 4 * E + 13 * V, E, [&] { nemo::launch_pull_count(c->dc, a, slots, s); });
   if (rc) return rc;
-  c->h_poff.resize(slots + 1);
   HIPCHK(c, hipMemcpyAsync(c->h_poff.data(), c->d_poff, (slots + 1) * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   const uint64_t total = c->h_poff[slots];
@@ -799,26 +846,20 @@ int nemo_pull_edges(nemo_ctx *c, int which, uint32_t aux) {
   }
   a.src = c->d_psrc;
   a.dst = c->d_pdst;
-  rc = timed(c, "k_pull_write", 4 * E + 13 * V + 8.0 * total, E, [&] { nemo::launch_pull_write(c->dc, a, slots, s); });
-  if (rc) return rc;
-  c->pull_which = which;
-  c->pull_aux = aux;
-  c->pull_slots = slots;
-  return NEMO_OK;
+  rc = timed(c, "k_pull_write", 4 * E + 13 * V + 8.0 * (double)total, E,
+             [&] { nemo::launch_pull_write(c->dc, a, slots, s); });
+  return rc;
 }
 
-uint64_t nemo_pulled_count(const nemo_ctx *c, uint32_t graph) {
-  if (!c || c->pull_which < 0) return 0;
-  const uint32_t slot = c->pull_which == 2 ? 0 : graph;
-  if (slot >= c->pull_slots) return 0;
+uint64_t nemo_pulled_count(const nemo_ctx *c, uint32_t slot) {
+  if (!c || c->pull_which < 0 || slot >= c->pull_slots) return 0;
   return c->h_poff[slot + 1] - c->h_poff[slot];
 }
 
-int nemo_fetch_pulled(nemo_ctx *c, uint32_t graph, uint32_t *src, uint32_t *dst, uint64_t cap, uint64_t *n_out) {
+int nemo_fetch_pulled(nemo_ctx *c, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap, uint64_t *n_out) {
   if (!c) return NEMO_ERR_INVALID;
   if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
-  const uint32_t slot = c->pull_which == 2 ? 0 : graph;
-  if (slot >= c->pull_slots) return fail(c, NEMO_ERR_INVALID, "graph %u out of range", graph);
+  if (slot >= c->pull_slots) return fail(c, NEMO_ERR_INVALID, "slot %u out of range", slot);
   const uint64_t a = c->h_poff[slot], n = c->h_poff[slot + 1] - a;
   if (n_out) *n_out = n;
   if (!src && !dst) return NEMO_OK;
@@ -829,6 +870,30 @@ int nemo_fetch_pulled(nemo_ctx *c, uint32_t graph, uint32_t *src, uint32_t *dst,
     if (dst) HIPCHK(c, hipMemcpyAsync(dst, c->d_pdst + a, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return NEMO_OK;
+}
+
+// Debug/inspection: copy `bytes` bytes at byte `offset` of an internal device array.
+int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, uint64_t bytes) {
+  if (!c || !name || !out) return NEMO_ERR_INVALID;
+  const void *base = nullptr;
+  const std::string n(name);
+  if (n == "topo") base = c->dc.topo;
+  else if (n == "lvl") base = c->dc.lvl;
+  else if (n == "nlev") base = c->dc.nlev;
+  else if (n == "fp") base = c->dc.fp;
+  else if (n == "fc") base = c->dc.fc;
+  else if (n == "rp") base = c->dc.rp;
+  else if (n == "rc") base = c->dc.rc;
+  else if (n == "flags") base = c->dc.flags;
+  else if (n == "dbits") base = c->d_dbits;
+  else if (n == "dmask") base = c->d_dmask;
+  else if (n == "r0lab") base = c->d_r0lab;
+  else if (n == "r0idx") base = c->d_r0idx;
+  if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return NEMO_OK;
 }
 

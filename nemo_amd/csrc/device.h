@@ -72,8 +72,61 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
   return off + v - x;
 }
 
+// In-place exclusive scan of a[0..n) by one workgroup; returns the total.
+__device__ __forceinline__ uint32_t block_scan_inplace(uint32_t *a, uint32_t n, uint32_t *lds) {
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n; base += NEMO_BLOCK * 4) {
+    const uint32_t i0 = base + threadIdx.x * 4;
+    uint32_t x[4], s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      x[k] = (i0 + k < n) ? a[i0 + k] : 0u;
+      s += x[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_exscan(s, &tot, lds) + carry;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i0 + k < n) a[i0 + k] = ex;
+      ex += x[k];
+    }
+    carry += tot;
+  }
+  __syncthreads();  // the writes above land after block_exscan's last barrier
+  return carry;
+}
+
 __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Intra-wave LDS hand-off: lanes of one wave run in lockstep and DS ops of a
+// wave complete in order, so ordering the compiler is all that is needed.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_exscan(uint32_t x, uint32_t *total) {
+  const uint32_t lane = lane_id();
+  uint32_t v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  *total = __shfl(v, 63);
+  return v - x;
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long y = __shfl_xor(v, d);
+    v = y > v ? y : v;
+  }
+  return v;
 }
 
 // Graph-local view.  Arrays indexed per node use base n0 (+g for the V+1-sized
@@ -95,6 +148,8 @@ struct GraphView {
 // Device-side arrays of a loaded corpus (all graphs concatenated).
 struct DevCorpus {
   uint32_t G, n_runs, n_tables, words, table_pre, table_post;
+  uint32_t hcap_limit;                   // largest chain subgraph H* k_chains stages in LDS (test knob)
+  uint32_t comp_limit;                   // largest H* component k_chains_big stages in LDS (test knob)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
   const uint32_t *esrc, *edst;
@@ -104,6 +159,7 @@ struct DevCorpus {
   uint32_t *s_a, *s_b, *s_c;             // V+G scratch
   int32_t *s_d;                          // V scratch
   unsigned long long *s_e;               // V scratch
+  uint32_t *s_f, *s_g;                   // V+G scratch
   uint32_t *err;                         // [G] NEMO_ERR_* of the graph (0 = fine)
   uint32_t *created;                     // [G] loadProv relationships-created
   uint32_t *prehold;                     // [G] #holding "pre" goals (pre graphs)

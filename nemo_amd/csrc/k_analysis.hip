@@ -106,203 +106,6 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c) {
   }
 }
 
-__device__ __forceinline__ uint32_t uf_find(uint32_t *p, uint32_t x) {
-  uint32_t y = ld_relaxed(&p[x]);
-  while (y != x) {
-    x = y;
-    y = ld_relaxed(&p[x]);
-  }
-  return x;
-}
-
-// Greedy @next chain cover (preprocessing.go:70-138).  Per weakly connected
-// component of the chain subgraph H* the accepted sequence is "the first path
-// in (length desc, ID-rank sequence asc) order that contains an unseen node";
-// every iteration runs one down-sweep over H* (longest unseen-containing
-// suffix, du) and one walker thread per component.  The global acceptance
-// index k is the rank of (len desc, head rank asc, iteration asc).
-__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
-  __shared__ uint32_t s_n, s_flag, s_nch;
-  const uint32_t g = blockIdx.x;
-  if (c.err[g]) return;
-  const GraphView gv = c.view(g);
-  uint8_t *f = gv.flags;
-  uint32_t *hs = c.s_a + gv.n0 + g;      // H* in topological order
-  uint32_t *hl = c.s_b + gv.n0 + g;      // H* level offsets
-  uint32_t *par = c.s_c + gv.n0 + g;     // union-find parent
-  int32_t *down = c.s_d + gv.n0;         // longest chain suffix (any)
-  int32_t *du = (int32_t *)(c.tail_first + gv.n0);  // longest unseen-containing suffix (temp)
-  unsigned long long *best = c.s_e + gv.n0;
-  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
-  if (threadIdx.x == 0) {
-    s_n = 0;
-    s_nch = 0;
-    hl[0] = 0;
-  }
-  __syncthreads();
-  // compact H* level by level
-  for (uint32_t l = 0; l < gv.nlev; l++) {
-    const uint32_t a = gv.lvl[l], b = gv.lvl[l + 1];
-    for (uint32_t base = a; base < b; base += NEMO_BLOCK) {
-      const uint32_t i = base + threadIdx.x;
-      uint32_t v = 0;
-      bool p = false;
-      if (i < b) {
-        v = gv.topo[i];
-        p = (f[v] & NEMO_F_DELETED) != 0;
-      }
-      wave_append(p, v, hs, &s_n);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) hl[l + 1] = s_n;
-    __syncthreads();
-  }
-  const uint32_t nh = s_n;
-  if (nh == 0) {
-    if (threadIdx.x == 0) c.nch[g] = 0;
-    return;
-  }
-#define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
-  // down[v]: longest H* path from v to a next rule
-  for (uint32_t l = gv.nlev; l-- > 0;) {
-    for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
-      const uint32_t v = hs[i];
-      int32_t d = is_rule(gv.word[v]) ? 0 : -1;
-      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
-        const uint32_t w = gv.fc[j];
-        if (INH(w)) d = max(d, down[w] + 1);
-      }
-      down[v] = d;
-      par[v] = v;
-      best[v] = 0ull;
-    }
-    __syncthreads();
-  }
-  // weakly connected components of H* (hook to the smaller root + compress)
-  for (;;) {
-    if (threadIdx.x == 0) s_flag = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-      const uint32_t v = hs[i];
-      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
-        const uint32_t w = gv.fc[j];
-        if (!INH(w)) continue;
-        const uint32_t a = uf_find(par, v), b = uf_find(par, w);
-        if (a != b) {
-          atomicMin(&par[max(a, b)], min(a, b));
-          s_flag = 1;
-        }
-      }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-      const uint32_t v = hs[i];
-      atomicMin(&par[v], uf_find(par, v));
-    }
-    __syncthreads();
-    if (!s_flag) break;
-    __syncthreads();
-  }
-  for (uint32_t iter = 0;; iter++) {
-    // du sweep (bottom-up)
-    for (uint32_t l = gv.nlev; l-- > 0;) {
-      for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
-        const uint32_t v = hs[i];
-        int32_t d;
-        if (!(f[v] & FT_SEEN)) {
-          d = down[v];
-        } else {
-          d = -1;
-          for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
-            const uint32_t w = gv.fc[j];
-            if (INH(w) && du[w] >= 0) d = max(d, du[w] + 1);
-          }
-        }
-        du[v] = d;
-      }
-      __syncthreads();
-    }
-    // per component: max du, then min rank (packed key)
-    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-      const uint32_t v = hs[i];
-      if (is_rule(gv.word[v]) && du[v] >= 2) {
-        const unsigned long long key = ((unsigned long long)(uint32_t)du[v] << 32) | (0xFFFFFFFFu - gv.rank_of(v));
-        atomicMax(&best[par[v]], key);
-      }
-    }
-    if (threadIdx.x == 0) s_flag = 0;
-    __syncthreads();
-    // one walker per component: the lexicographically first path of that length
-    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-      const uint32_t s = hs[i];
-      if (!is_rule(gv.word[s]) || du[s] < 2) continue;
-      const unsigned long long key = ((unsigned long long)(uint32_t)du[s] << 32) | (0xFFFFFFFFu - gv.rank_of(s));
-      if (best[par[s]] != key) continue;
-      int32_t rem = du[s];
-      bool u = !(f[s] & FT_SEEN);
-      f[s] |= FT_SEEN;
-      uint32_t v = s;
-      while (rem > 0) {
-        uint32_t bc = NEMO_NONE, br = NEMO_NONE;
-        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
-          const uint32_t w = gv.fc[j];
-          if (!INH(w)) continue;
-          const int32_t val = u ? down[w] : du[w];
-          const uint32_t rw = gv.rank_of(w);
-          if (val == rem - 1 && (bc == NEMO_NONE || rw < br)) {
-            bc = w;
-            br = rw;
-          }
-        }
-        if (bc == NEMO_NONE) break;  // unreachable: du/down guarantee a child
-        v = bc;
-        u |= !(f[v] & FT_SEEN);
-        f[v] |= FT_SEEN;
-        rem--;
-      }
-      const uint32_t k = atomicAdd(&s_nch, 1u);
-      uint32_t *t = tmp + 5 * k;
-      t[0] = s;
-      t[1] = v;
-      t[2] = (uint32_t)du[s];
-      t[3] = gv.rank_of(s);
-      t[4] = iter;
-      s_flag = 1;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) best[hs[i]] = 0ull;
-    const bool more = s_flag != 0;
-    __syncthreads();
-    if (!more) break;
-  }
-  // acceptance order k = rank of (len desc, head rank asc, iteration asc)
-  const uint32_t n = s_nch;
-  uint32_t *out = c.chain + 5 * gv.n0;
-  for (uint32_t i = threadIdx.x; i < n; i += NEMO_BLOCK) {
-    const uint32_t li = tmp[5 * i + 2], ri = tmp[5 * i + 3], ii = tmp[5 * i + 4];
-    uint32_t k = 0;
-    for (uint32_t j = 0; j < n; j++) {
-      const uint32_t lj = tmp[5 * j + 2], rj = tmp[5 * j + 3], ij = tmp[5 * j + 4];
-      k += (lj > li) || (lj == li && (rj < ri || (rj == ri && ij < ii)));
-    }
-#pragma unroll
-    for (int q = 0; q < 5; q++) out[5 * k + q] = tmp[5 * i + q];
-  }
-  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-    const uint32_t v = hs[i];
-    f[v] &= (uint8_t)~FT_SEEN;
-    c.tail_first[gv.n0 + v] = NEMO_NONE;
-  }
-#undef INH
-  __syncthreads();
-  // per-tail chain lists (order irrelevant: only OR-ed over)
-  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) {
-    const uint32_t t = out[5 * k + 1];
-    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
-  }
-  if (threadIdx.x == 0) c.nch[g] = n;
-}
-
 // extractProtos' per-run query (prototype.go:11-24) and missingFrom's table
 // set (:143-147) on the simplified post graph, without materialising it:
 // collapsed rule k is reached through its head (preds(r1) = goal parents of
@@ -446,14 +249,22 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
 // Cross-run reduction vector (nemo_reduce_len): per-table counts over owned
 // success runs with a non-empty list, the first success run's list, achvdCond
 // (prototype.go:29-130) and the holding-"pre"-goal count (extensions.go:25-49).
+// Counts are summed per workgroup in LDS, then one global atomic per table.
+#define RED_LDS_TABLES 4096
 __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_t *is_success, const uint8_t *owned,
                                                         uint32_t first_run, uint32_t *red) {
+  __shared__ uint32_t s_cnt[RED_LDS_TABLES];
+  __shared__ uint32_t s_misc[3];
   const uint32_t T = c.n_tables, W = c.words;
+  const bool lds = T <= RED_LDS_TABLES;
+  for (uint32_t t = threadIdx.x; t < T && lds; t += NEMO_BLOCK) s_cnt[t] = 0;
+  if (threadIdx.x < 3) s_misc[threadIdx.x] = 0;
+  __syncthreads();
   for (uint32_t r = blockIdx.x * NEMO_BLOCK + threadIdx.x; r < c.n_runs; r += gridDim.x * NEMO_BLOCK) {
     const bool own = owned == nullptr || owned[r];
     if (!own) continue;
-    atomicAdd(&red[2 * T + 3], 1u);
-    if (c.prehold[2 * r]) atomicAdd(&red[2 * T + 2], c.prehold[2 * r]);
+    atomicAdd(&s_misc[0], 1u);
+    if (c.prehold[2 * r]) atomicAdd(&s_misc[1], c.prehold[2 * r]);
     const uint32_t *b = c.proto_bits + (size_t)r * W;
     bool nonempty = false;
     for (uint32_t i = 0; i < W; i++) nonempty |= b[i] != 0u;
@@ -463,9 +274,21 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_
         for (uint32_t m = b[i]; m; m &= m - 1) red[T + 32 * i + __builtin_ctz(m)] = 1u;
     }
     if (!is_success[r] || !nonempty) continue;
-    atomicAdd(&red[2 * T], 1u);
+    atomicAdd(&s_misc[2], 1u);
     for (uint32_t i = 0; i < W; i++)
-      for (uint32_t m = b[i]; m; m &= m - 1) atomicAdd(&red[32 * i + __builtin_ctz(m)], 1u);
+      for (uint32_t m = b[i]; m; m &= m - 1) {
+        const uint32_t t = 32 * i + __builtin_ctz(m);
+        if (lds) atomicAdd(&s_cnt[t], 1u);
+        else atomicAdd(&red[t], 1u);
+      }
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < T && lds; t += NEMO_BLOCK)
+    if (s_cnt[t]) atomicAdd(&red[t], s_cnt[t]);
+  if (threadIdx.x == 0) {
+    if (s_misc[0]) atomicAdd(&red[2 * T + 3], s_misc[0]);
+    if (s_misc[1]) atomicAdd(&red[2 * T + 2], s_misc[1]);
+    if (s_misc[2]) atomicAdd(&red[2 * T], s_misc[2]);
   }
 }
 
@@ -474,9 +297,6 @@ void launch_mark(const DevCorpus &c, hipStream_t s) {
 }
 void launch_simplify(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
-}
-void launch_chains(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_chains, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_proto(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_proto, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);

@@ -1,0 +1,744 @@
+// k_chains.hip — the greedy @next chain cover of collapseNextChains
+// (graphing/preprocessing.go:70-138) on the clean copy, one graph per
+// workgroup.
+//
+// Q13 lists every path r1(next)-[*1..]->(g)-[*1..]->r2(next) over goals and
+// next rules, ORDER BY len DESC; the Go loop accepts a path iff it holds a node
+// no accepted path holds.  Neo4j's tie order is unspecified; ties are broken by
+// the lexicographic sequence of node-ID ranks.  Acceptance only interacts
+// inside a weakly connected component of the chain subgraph H* (the nodes
+// k_simplify_flags marks DELETED), and inside a component the next accepted
+// path is "the first path in that order containing an unseen node":
+//   du(v) = longest H* path from v to a next rule that contains an unseen
+//           node (down(v) if v is unseen),
+//   start = the min-rank next rule with the component's maximal du,
+//   walk  = at every step the min-rank child that can still complete the length.
+// k_chains (first tier) does not iterate at all: a path is accepted iff it is
+// first(v), the first path in sorted order through some node v (when first(v)
+// comes up, v is unseen; an accepted path's fresh node has no earlier path).
+// first(v) = best_prefix(v) ++ best_suffix(v): the lexicographically least
+// longest path from a head to v (ranked per prefix length) and the least
+// longest path from v to a tail (min-rank child with down = down-1).  The
+// witnesses of a path are contiguous on it, so its representative is the
+// witness whose best parent does not continue into it: up(v)==0 or
+// nxt(bp(v)) != v.  The whole chain subgraph H* of a graph is staged in LDS.
+// Graphs whose H* exceeds the LDS tile go to k_chains_big: per weakly
+// connected component, the greedy iterated literally ("next accepted = first
+// path holding an unseen node"), one wave per component in LDS, or a
+// workgroup-wide sweep over global memory for the largest components.  Both
+// tiers produce the same acceptance index k = rank of (len desc, lex asc).
+#include "device.h"
+#include "internal.h"
+
+namespace nemo {
+
+#define CM 256  // nodes of a component staged in LDS
+#define CE 768  // intra-component edges staged in LDS
+
+struct CompLDS {
+  uint32_t node[CM];  // graph-local node ids, topological (level, id) order
+  uint32_t rank[CM];
+  uint32_t key[CM];   // level
+  uint16_t coff[CM + 1];
+  uint16_t child[CE];
+  uint16_t seg[CM + 1];
+  int16_t down[CM];
+  int16_t du[CM];
+  uint8_t flag[CM];   // 1 = rule, 2 = unseen
+};
+
+#define CF_RULE 1u
+#define CF_UNSEEN 2u
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t *p, uint32_t x) {
+  uint32_t y = ld_relaxed(&p[x]);
+  while (y != x) {
+    x = y;
+    y = ld_relaxed(&p[x]);
+  }
+  return x;
+}
+
+// One wave: the whole greedy of one component held in LDS.  Returns false if
+// the component does not fit (caller leaves it to the fallback).
+__device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *nodes, uint32_t m,
+                               const uint32_t *lev, uint32_t *cidx, uint32_t *tmp, uint32_t *nch) {
+  const uint32_t lane = lane_id();
+  const uint8_t *f = gv.flags;
+  // topological order inside the component: sort by (level, node id)
+  for (uint32_t i = lane; i < m; i += 64) {
+    const uint32_t v = nodes[i];
+    L.key[i] = lev[v];
+    L.rank[i] = v;
+  }
+  wsync();
+  for (uint32_t i = lane; i < m; i += 64) {
+    const uint32_t ki = L.key[i], vi = L.rank[i];
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < m; j++) {
+      const uint32_t kj = L.key[j], vj = L.rank[j];
+      pos += (kj < ki) || (kj == ki && vj < vi);
+    }
+    L.node[pos] = vi;
+  }
+  wsync();
+  for (uint32_t i = lane; i < m; i += 64) {
+    const uint32_t v = L.node[i];
+    cidx[v] = i;
+    L.key[i] = lev[v];
+    L.rank[i] = gv.rank_of(v);
+    L.flag[i] = (uint8_t)((is_rule(gv.word[v]) ? CF_RULE : 0u) | CF_UNSEEN);
+  }
+  __threadfence_block();
+  wsync();
+  // level segments
+  uint32_t nseg = 0;
+  for (uint32_t base = 0; base < m; base += 64) {
+    const uint32_t i = base + lane;
+    const bool st = i < m && (i == 0 || L.key[i] != L.key[i - 1]);
+    const uint64_t b = __ballot(st);
+    if (st) L.seg[nseg + mbcnt(b)] = (uint16_t)i;
+    nseg += (uint32_t)__popcll(b);
+  }
+  if (lane == 0) L.seg[nseg] = (uint16_t)m;
+  // intra-component adjacency (children in H*)
+  uint32_t ne = 0;
+  for (uint32_t base = 0; base < m; base += 64) {
+    const uint32_t i = base + lane;
+    uint32_t n = 0, v = 0;
+    if (i < m) {
+      v = L.node[i];
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) n += (f[gv.fc[j]] & NEMO_F_DELETED) != 0;
+    }
+    uint32_t tot;
+    const uint32_t off = ne + wave_exscan(n, &tot);
+    if (i < m) L.coff[i] = (uint16_t)off;
+    if (ne + tot <= CE && i < m) {
+      uint32_t k = off;
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+        const uint32_t w = gv.fc[j];
+        if (f[w] & NEMO_F_DELETED) L.child[k++] = (uint16_t)cidx[w];
+      }
+    }
+    ne += tot;
+  }
+  if (ne > CE) return false;
+  if (lane == 0) L.coff[m] = (uint16_t)ne;
+  wsync();
+  // down(i): longest H* path from i to a next rule
+  for (uint32_t s = nseg; s-- > 0;) {
+    for (uint32_t i = L.seg[s] + lane; i < L.seg[s + 1]; i += 64) {
+      int32_t d = (L.flag[i] & CF_RULE) ? 0 : -1;
+      for (uint32_t j = L.coff[i]; j < L.coff[i + 1]; j++) d = max(d, (int32_t)L.down[L.child[j]] + 1);
+      L.down[i] = (int16_t)d;
+    }
+    wsync();
+  }
+  for (uint32_t iter = 0;; iter++) {
+    for (uint32_t s = nseg; s-- > 0;) {
+      for (uint32_t i = L.seg[s] + lane; i < L.seg[s + 1]; i += 64) {
+        int32_t d;
+        if (L.flag[i] & CF_UNSEEN) {
+          d = L.down[i];
+        } else {
+          d = -1;
+          for (uint32_t j = L.coff[i]; j < L.coff[i + 1]; j++) {
+            const int32_t x = L.du[L.child[j]];
+            if (x >= 0) d = max(d, x + 1);
+          }
+        }
+        L.du[i] = (int16_t)d;
+      }
+      wsync();
+    }
+    unsigned long long mine = 0;
+    uint32_t mi = 0;
+    for (uint32_t i = lane; i < m; i += 64) {
+      if (!(L.flag[i] & CF_RULE) || L.du[i] < 2) continue;
+      const unsigned long long k = ((unsigned long long)(uint32_t)L.du[i] << 32) | (0xFFFFFFFFu - L.rank[i]);
+      if (k > mine) {
+        mine = k;
+        mi = i;
+      }
+    }
+    const unsigned long long best = wave_max_u64(mine);
+    if (best == 0) break;
+    if (mine == best) {  // exactly one lane: ranks are unique
+      uint32_t v = mi;
+      int32_t rem = L.du[mi];
+      bool u = (L.flag[mi] & CF_UNSEEN) != 0;
+      L.flag[mi] &= (uint8_t)~CF_UNSEEN;
+      while (rem > 0) {
+        uint32_t bc = 0xFFFFu, br = NEMO_NONE;
+        for (uint32_t j = L.coff[v]; j < L.coff[v + 1]; j++) {
+          const uint32_t w = L.child[j];
+          const int32_t val = u ? L.down[w] : L.du[w];
+          if (val == rem - 1 && L.rank[w] < br) {
+            bc = w;
+            br = L.rank[w];
+          }
+        }
+        if (bc == 0xFFFFu) break;  // unreachable by construction
+        v = bc;
+        u |= (L.flag[v] & CF_UNSEEN) != 0;
+        L.flag[v] &= (uint8_t)~CF_UNSEEN;
+        rem--;
+      }
+      const uint32_t k = atomicAdd(nch, 1u);
+      uint32_t *t = tmp + 5 * k;
+      t[0] = L.node[mi];
+      t[1] = L.node[v];
+      t[2] = (uint32_t)L.du[mi];
+      t[3] = L.rank[mi];
+      t[4] = iter;
+    }
+    wsync();
+  }
+  // covered: the fallback (if any) must treat these nodes as seen
+  for (uint32_t i = lane; i < m; i += 64) gv.flags[L.node[i]] |= FT_SEEN;
+  return true;
+}
+
+
+// ---- first tier: first(v) over an LDS-resident chain subgraph ------------------
+#define HCAP 2048  // H* nodes staged in LDS
+#define ECAP 2048  // H* edges staged in LDS (each direction)
+#define NIL16 0xFFFFu
+#define UCAP 1024  // distinct prefix lengths (longest chain path + 2)
+
+struct ChainsLDS {
+  uint16_t crank[HCAP];  // rank of the node's ID among H* nodes
+  int16_t up[HCAP], down[HCAP];
+  uint16_t nxt[HCAP], bp[HCAP], head[HCAP], tail[HCAP], po[HCAP], pnew[HCAP];
+  uint16_t ub[HCAP];
+  uint32_t uoff[UCAP], cur[UCAP];
+  uint16_t seg[HCAP + 1];
+  uint8_t isrule[HCAP];
+  union {
+    struct {
+      uint16_t pcoff[HCAP + 1], par[ECAP];  // live until the prefix ranks are done
+      uint16_t ccoff[HCAP + 1], child[ECAP];
+    } adj;
+    struct {
+      uint16_t pad[HCAP + 2 + ECAP];       // keeps bk 4-byte aligned, past par[]
+      uint32_t bk[HCAP];                   // bucket keys (po(bp) << 16 | crank), over ccoff/child
+    } rk;
+    unsigned long long kk[HCAP];           // bitonic sort of ranks; later the chain sort keys
+  } u;
+};
+
+// Is the path represented by witness a before the one represented by b?
+// (Both have the same length and head; see the file comment.)
+__device__ __forceinline__ bool path_before(const ChainsLDS &L, uint32_t a, uint32_t b) {
+  if (L.up[a] <= L.up[b]) {
+    uint32_t x = b;
+    while (L.up[x] > L.up[a]) x = L.bp[x];
+    return x == a ? true : L.po[a] < L.po[x];
+  }
+  uint32_t x = a;
+  while (L.up[x] > L.up[b]) x = L.bp[x];
+  return x == b ? false : L.po[x] < L.po[b];
+}
+
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
+  __shared__ ChainsLDS L;
+  __shared__ uint32_t s_lds[NEMO_WAVES];
+  __shared__ uint32_t s_nch, s_maxup, s_fail;
+  const uint32_t g = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  const uint8_t *f = gv.flags;
+  uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
+  uint32_t *hidx = c.s_f + gv.n0 + g;  // graph-local node -> compact index
+  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t cap = min((uint32_t)HCAP, c.hcap_limit);
+#define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
+  // ordered compaction of H* in Kahn order (chunks of 4 positions per thread);
+  // pc[p] = #H* nodes before topo position p gives every level's segment
+  uint32_t *pc = c.s_b + gv.n0 + g;
+  uint32_t n = 0;
+  for (uint32_t base = 0; base < gv.V; base += 4 * NEMO_BLOCK) {
+    const uint32_t i0 = base + 4 * tid;
+    uint32_t v[4], cnt = 0;
+    bool p[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      v[q] = i0 + q < gv.V ? gv.topo[i0 + q] : 0u;
+      p[q] = i0 + q < gv.V && INH(v[q]);
+      cnt += p[q];
+    }
+    uint32_t tot;
+    uint32_t off = n + block_exscan(cnt, &tot, s_lds);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (i0 + q < gv.V) pc[i0 + q] = off;
+      if (p[q]) {
+        if (off < cap) hs[off] = v[q];
+        off++;
+      }
+    }
+    n += tot;
+  }
+  if (n == 0) {
+    if (tid == 0) c.nch[g] = 0;
+    return;
+  }
+  if (n > cap) {  // too large for the LDS tier: k_chains_big takes the graph
+    if (tid == 0) c.nch[g] = NEMO_NONE;
+    return;
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t ns = gv.nlev;
+  if (ns > HCAP) {
+    if (tid == 0) c.nch[g] = NEMO_NONE;
+    return;
+  }
+  for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) L.seg[l] = (uint16_t)(l == ns ? n : pc[gv.lvl[l]]);
+  if (tid == 0) {
+    s_nch = 0;
+    s_maxup = 0;
+    s_fail = 0;
+  }
+  // compact ID ranks: bitonic sort of (rank, index) pairs in LDS
+  uint32_t N2 = 1;
+  while (N2 < n) N2 <<= 1;
+  for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
+    if (i < n) {
+      const uint32_t v = hs[i];
+      hidx[v] = i;
+      L.isrule[i] = is_rule(gv.word[v]) ? 1 : 0;
+      L.u.kk[i] = ((unsigned long long)gv.rank_of(v) << 16) | i;
+    } else {
+      L.u.kk[i] = ~0ull;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t k = 2; k <= N2; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long x = L.u.kk[i], y = L.u.kk[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            L.u.kk[i] = y;
+            L.u.kk[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t q = tid; q < n; q += NEMO_BLOCK) L.crank[L.u.kk[q] & 0xFFFFu] = (uint16_t)q;
+  __syncthreads();
+  // compact child / parent lists
+  uint32_t ce = 0, pe = 0;
+  for (uint32_t base = 0; base < n; base += NEMO_BLOCK) {
+    const uint32_t i = base + tid;
+    uint32_t nc = 0, np = 0, v = 0;
+    if (i < n) {
+      v = hs[i];
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) nc += INH(gv.fc[j]);
+      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) np += INH(gv.rc[j]);
+    }
+    uint32_t tc, tp;
+    const uint32_t oc = ce + block_exscan(nc, &tc, s_lds);
+    const uint32_t op = pe + block_exscan(np, &tp, s_lds);
+    if (i < n) {
+      L.u.adj.ccoff[i] = (uint16_t)min(oc, (uint32_t)ECAP);
+      L.u.adj.pcoff[i] = (uint16_t)min(op, (uint32_t)ECAP);
+      if (oc + nc <= ECAP) {
+        uint32_t k = oc;
+        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+          const uint32_t w = gv.fc[j];
+          if (INH(w)) L.u.adj.child[k++] = (uint16_t)hidx[w];
+        }
+      }
+      if (op + np <= ECAP) {
+        uint32_t k = op;
+        for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) {
+          const uint32_t w = gv.rc[j];
+          if (INH(w)) L.u.adj.par[k++] = (uint16_t)hidx[w];
+        }
+      }
+    }
+    ce += tc;
+    pe += tp;
+  }
+  if (ce > ECAP || pe > ECAP) {
+    if (tid == 0) c.nch[g] = NEMO_NONE;
+    return;
+  }
+  if (tid == 0) {
+    L.u.adj.ccoff[n] = (uint16_t)ce;
+    L.u.adj.pcoff[n] = (uint16_t)pe;
+  }
+  __syncthreads();
+  // up: longest H* path from a next rule ending here; down/nxt/tail: the
+  // lexicographically least longest continuation to a next rule
+  for (uint32_t s = 0; s < ns; s++) {
+    for (uint32_t i = L.seg[s] + tid; i < L.seg[s + 1]; i += NEMO_BLOCK) {
+      int32_t d = L.isrule[i] ? 0 : -1;
+      for (uint32_t j = L.u.adj.pcoff[i]; j < L.u.adj.pcoff[i + 1]; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
+      L.up[i] = (int16_t)d;
+      atomicMax(&s_maxup, (uint32_t)max(d, 0));
+    }
+    __syncthreads();
+  }
+  for (uint32_t s = ns; s-- > 0;) {
+    for (uint32_t i = L.seg[s] + tid; i < L.seg[s + 1]; i += NEMO_BLOCK) {
+      int32_t d = L.isrule[i] ? 0 : -1;
+      for (uint32_t j = L.u.adj.ccoff[i]; j < L.u.adj.ccoff[i + 1]; j++)
+        d = max(d, (int32_t)L.down[L.u.adj.child[j]] + 1);
+      uint32_t bc = NIL16, br = NEMO_NONE;
+      if (d > 0)
+        for (uint32_t j = L.u.adj.ccoff[i]; j < L.u.adj.ccoff[i + 1]; j++) {
+          const uint32_t w = L.u.adj.child[j];
+          if (L.down[w] == d - 1 && L.crank[w] < br) {
+            bc = w;
+            br = L.crank[w];
+          }
+        }
+      L.down[i] = (int16_t)d;
+      L.nxt[i] = (uint16_t)bc;
+      L.tail[i] = (uint16_t)(d > 0 ? L.tail[bc] : i);
+      if (d < 0 || (d > 0 && bc == NIL16)) s_fail = 1;  // impossible on a chain subgraph
+    }
+    __syncthreads();
+  }
+  // bucket by up value (counting sort in LDS)
+  const uint32_t maxup = s_maxup;
+  if (maxup + 2 > UCAP) {
+    if (tid == 0) c.nch[g] = NEMO_NONE;
+    return;
+  }
+  for (uint32_t k = tid; k <= maxup + 1; k += NEMO_BLOCK) L.cur[k] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) atomicAdd(&L.cur[L.up[i]], 1u);
+  __syncthreads();
+  block_scan_inplace(L.cur, maxup + 2, s_lds);
+  for (uint32_t k = tid; k <= maxup + 1; k += NEMO_BLOCK) L.uoff[k] = L.cur[k];
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) L.ub[atomicAdd(&L.cur[L.up[i]], 1u)] = (uint16_t)i;
+  __syncthreads();
+  // prefix ranks: po(v) = rank of best_prefix(v) among the prefixes of its length
+  for (uint32_t k = 0; k <= maxup; k++) {
+    const uint32_t a = L.uoff[k], b = L.uoff[k + 1];
+    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+      const uint32_t i = L.ub[j];
+      uint32_t bpi = NIL16, bpo = NEMO_NONE;
+      if (k > 0)
+        for (uint32_t q = L.u.adj.pcoff[i]; q < L.u.adj.pcoff[i + 1]; q++) {
+          const uint32_t p = L.u.adj.par[q];
+          if ((uint32_t)L.up[p] == k - 1 && L.po[p] < bpo) {
+            bpi = p;
+            bpo = L.po[p];
+          }
+        }
+      L.bp[i] = (uint16_t)bpi;
+      L.head[i] = (uint16_t)(k == 0 ? i : L.head[bpi]);
+    }
+    __syncthreads();
+    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+      const uint32_t i = L.ub[j];
+      L.u.rk.bk[j - a] = ((k ? (uint32_t)L.po[L.bp[i]] : 0u) << 16) | L.crank[i];
+    }
+    __syncthreads();
+    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+      const uint32_t me = L.u.rk.bk[j - a];
+      uint32_t pos = 0;
+      for (uint32_t q = 0; q < b - a; q++) pos += L.u.rk.bk[q] < me;
+      L.pnew[L.ub[j]] = (uint16_t)pos;
+    }
+    __syncthreads();
+    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) L.po[L.ub[j]] = L.pnew[L.ub[j]];
+    __syncthreads();
+  }
+  // one representative per accepted path
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+    const bool rep = L.up[i] == 0 || L.nxt[L.bp[i]] != i;
+    if (!rep) continue;
+    const uint32_t k = atomicAdd(&s_nch, 1u);
+    uint32_t *t = tmp + 5 * k;
+    t[0] = L.head[i];
+    t[1] = L.tail[i];
+    t[2] = (uint32_t)(L.up[i] + L.down[i]);
+    t[3] = L.crank[L.head[i]];
+    t[4] = i;
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t nch = s_nch;
+  for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
+    const uint32_t len = tmp[5 * q + 2], hr = tmp[5 * q + 3], rep = tmp[5 * q + 4];
+    L.u.kk[q] = ((unsigned long long)(0xFFFFu - len) << 48) | ((unsigned long long)hr << 16) | rep;
+  }
+  __syncthreads();
+  uint32_t *out = c.chain + 5 * gv.n0;
+  for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
+    const unsigned long long me = L.u.kk[q];
+    uint32_t pos = 0;
+    for (uint32_t r = 0; r < nch; r++) {
+      const unsigned long long o = L.u.kk[r];
+      if ((o >> 16) != (me >> 16)) pos += o < me;
+      else if (o != me) pos += path_before(L, (uint32_t)(o & 0xFFFF), (uint32_t)(me & 0xFFFF));
+    }
+    uint32_t *w = out + 5 * pos;
+    w[0] = hs[tmp[5 * q]];
+    w[1] = hs[tmp[5 * q + 1]];
+    w[2] = tmp[5 * q + 2];
+    w[3] = gv.rank_of(w[0]);
+    w[4] = 0;
+  }
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) c.tail_first[gv.n0 + hs[i]] = NEMO_NONE;
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t k = tid; k < nch; k += NEMO_BLOCK) {
+    const uint32_t t = out[5 * k + 1];
+    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
+  }
+  if (tid == 0) {
+    c.nch[g] = nch;
+    if (s_fail) c.err[g] = NEMO_ERR_INVALID;
+  }
+#undef INH
+}
+
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
+  __shared__ CompLDS s_comp[NEMO_WAVES];
+  __shared__ uint32_t s_lds[NEMO_WAVES];
+  __shared__ uint32_t s_n, s_flag, s_nch, s_ncomp, s_big;
+  const uint32_t g = blockIdx.x;
+  if (c.err[g] || c.nch[g] != NEMO_NONE) return;  // handled by k_chains (LDS tier)
+  const GraphView gv = c.view(g);
+  uint8_t *f = gv.flags;
+  uint32_t *hs = c.s_a + gv.n0 + g;                   // H* in topological order
+  uint32_t *hl = c.s_b + gv.n0 + g;                   // H* level offsets
+  uint32_t *par = c.s_c + gv.n0 + g;                  // union-find parent
+  uint32_t *lev = (uint32_t *)(c.s_d + gv.n0);        // Kahn level of H* nodes
+  uint32_t *ccomp = c.s_f + gv.n0 + g;                // component id
+  uint32_t *cnodes = c.s_g + gv.n0 + g;               // nodes bucketed by component
+  uint32_t *coff = (uint32_t *)(c.s_e + gv.n0);       // [ncomp+1] bucket offsets, then cursors
+  uint32_t *roots = c.chain + 5 * gv.n0;              // temp until the final sort
+  uint32_t *cidx = c.chain_nt + gv.n0;                // graph-local -> component-local
+  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  const uint32_t wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_n = 0;
+    s_nch = 0;
+    s_ncomp = 0;
+    s_big = 0;
+    hl[0] = 0;
+  }
+  __syncthreads();
+#define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    const uint32_t a = gv.lvl[l], b = gv.lvl[l + 1];
+    for (uint32_t base = a; base < b; base += NEMO_BLOCK) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t v = 0;
+      bool p = false;
+      if (i < b) {
+        v = gv.topo[i];
+        p = INH(v);
+        if (p) {
+          lev[v] = l;
+          par[v] = v;
+        }
+      }
+      wave_append(p, v, hs, &s_n);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) hl[l + 1] = s_n;
+    __syncthreads();
+  }
+  const uint32_t nh = s_n;
+  if (nh == 0) {
+    if (threadIdx.x == 0) c.nch[g] = 0;
+    return;
+  }
+  // weakly connected components of H* (hook to the smaller root + compress)
+  for (;;) {
+    if (threadIdx.x == 0) s_flag = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+      const uint32_t v = hs[i];
+      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+        const uint32_t w = gv.fc[j];
+        if (!INH(w)) continue;
+        const uint32_t a = uf_find(par, v), b = uf_find(par, w);
+        if (a != b) {
+          atomicMin(&par[max(a, b)], min(a, b));
+          s_flag = 1;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) atomicMin(&par[hs[i]], uf_find(par, hs[i]));
+    __syncthreads();
+    if (!s_flag) break;
+    __syncthreads();
+  }
+  // bucket H* by component
+  for (uint32_t base = 0; base < nh; base += NEMO_BLOCK) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nh ? hs[i] : 0;
+    wave_append(i < nh && par[v] == v, v, roots, &s_ncomp);
+  }
+  __syncthreads();
+  const uint32_t ncomp = s_ncomp;
+  for (uint32_t k = threadIdx.x; k < ncomp; k += NEMO_BLOCK) {
+    ccomp[roots[k]] = k;
+    coff[k] = 0;
+  }
+  if (threadIdx.x == 0) coff[ncomp] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+    const uint32_t v = hs[i];
+    const uint32_t k = ccomp[par[v]];
+    if (par[v] != v) ccomp[v] = k;
+    atomicAdd(&coff[k], 1u);
+  }
+  __syncthreads();
+  block_scan_inplace(coff, ncomp + 1, s_lds);
+  uint32_t *cur = coff + ncomp + 1;
+  for (uint32_t k = threadIdx.x; k < ncomp; k += NEMO_BLOCK) cur[k] = coff[k];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+    const uint32_t v = hs[i];
+    cnodes[atomicAdd(&cur[ccomp[v]], 1u)] = v;
+  }
+  __syncthreads();
+  // one wave per component, LDS-resident
+  for (uint32_t k = wave; k < ncomp; k += NEMO_WAVES) {
+    const uint32_t a = coff[k], m = coff[k + 1] - a;
+    bool ok = false;
+    if (m <= CM && m <= c.comp_limit) ok = wave_component(gv, s_comp[wave], cnodes + a, m, lev, cidx, tmp, &s_nch);
+    if (!ok && lane_id() == 0) s_big = 1;
+  }
+  __syncthreads();
+  if (s_big) {
+    // fallback for components beyond the LDS tile: workgroup-wide sweeps over
+    // global memory; LDS-handled components are all FT_SEEN already.
+    int32_t *down = c.s_d + gv.n0;
+    int32_t *du = (int32_t *)(c.tail_first + gv.n0);
+    unsigned long long *best = c.s_e + gv.n0;
+    for (uint32_t l = gv.nlev; l-- > 0;) {
+      for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
+        const uint32_t v = hs[i];
+        int32_t d = is_rule(gv.word[v]) ? 0 : -1;
+        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+          const uint32_t w = gv.fc[j];
+          if (INH(w)) d = max(d, down[w] + 1);
+        }
+        down[v] = d;
+        best[v] = 0ull;
+      }
+      __syncthreads();
+    }
+    for (uint32_t iter = 0;; iter++) {
+      for (uint32_t l = gv.nlev; l-- > 0;) {
+        for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
+          const uint32_t v = hs[i];
+          int32_t d;
+          if (!(f[v] & FT_SEEN)) {
+            d = down[v];
+          } else {
+            d = -1;
+            for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+              const uint32_t w = gv.fc[j];
+              if (INH(w) && du[w] >= 0) d = max(d, du[w] + 1);
+            }
+          }
+          du[v] = d;
+        }
+        __syncthreads();
+      }
+      for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+        const uint32_t v = hs[i];
+        if (is_rule(gv.word[v]) && du[v] >= 2) {
+          const unsigned long long key = ((unsigned long long)(uint32_t)du[v] << 32) | (0xFFFFFFFFu - gv.rank_of(v));
+          atomicMax(&best[par[v]], key);
+        }
+      }
+      if (threadIdx.x == 0) s_flag = 0;
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+        const uint32_t s = hs[i];
+        if (!is_rule(gv.word[s]) || du[s] < 2) continue;
+        const unsigned long long key = ((unsigned long long)(uint32_t)du[s] << 32) | (0xFFFFFFFFu - gv.rank_of(s));
+        if (best[par[s]] != key) continue;
+        int32_t rem = du[s];
+        bool u = !(f[s] & FT_SEEN);
+        f[s] |= FT_SEEN;
+        uint32_t v = s;
+        while (rem > 0) {
+          uint32_t bc = NEMO_NONE, br = NEMO_NONE;
+          for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
+            const uint32_t w = gv.fc[j];
+            if (!INH(w)) continue;
+            const int32_t val = u ? down[w] : du[w];
+            const uint32_t rw = gv.rank_of(w);
+            if (val == rem - 1 && (bc == NEMO_NONE || rw < br)) {
+              bc = w;
+              br = rw;
+            }
+          }
+          if (bc == NEMO_NONE) break;
+          v = bc;
+          u |= !(f[v] & FT_SEEN);
+          f[v] |= FT_SEEN;
+          rem--;
+        }
+        const uint32_t k = atomicAdd(&s_nch, 1u);
+        uint32_t *t = tmp + 5 * k;
+        t[0] = s;
+        t[1] = v;
+        t[2] = (uint32_t)du[s];
+        t[3] = gv.rank_of(s);
+        t[4] = iter;
+        s_flag = 1;
+      }
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) best[hs[i]] = 0ull;
+      const bool more = s_flag != 0;
+      __syncthreads();
+      if (!more) break;
+    }
+  }
+  // acceptance order k = rank of (len desc, head rank asc, iteration asc)
+  const uint32_t n = s_nch;
+  uint32_t *out = c.chain + 5 * gv.n0;
+  for (uint32_t i = threadIdx.x; i < n; i += NEMO_BLOCK) {
+    const uint32_t li = tmp[5 * i + 2], ri = tmp[5 * i + 3], ii = tmp[5 * i + 4];
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t lj = tmp[5 * j + 2], rj = tmp[5 * j + 3], ij = tmp[5 * j + 4];
+      k += (lj > li) || (lj == li && (rj < ri || (rj == ri && ij < ii)));
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) out[5 * k + q] = tmp[5 * i + q];
+  }
+  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
+    const uint32_t v = hs[i];
+    f[v] &= (uint8_t)~FT_SEEN;
+    c.tail_first[gv.n0 + v] = NEMO_NONE;
+  }
+#undef INH
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) {
+    const uint32_t t = out[5 * k + 1];
+    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
+  }
+  if (threadIdx.x == 0) c.nch[g] = n;
+}
+
+void launch_chains(const DevCorpus &c, hipStream_t s) {
+  hipLaunchKernelGGL(k_chains, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_chains_big, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+}
+
+}  // namespace nemo

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull_count(DevCorpus c, PullArgs
     return;
   }
   const GraphView gv = c.view(g);
-  const uint8_t *m = a.mask;
+  const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   uint32_t n = 0;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull_write(DevCorpus c, PullArgs
   const uint32_t slot = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
-  const uint8_t *m = a.mask;
+  const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   uint64_t pos = a.off[slot];
   for (uint32_t base = 0; base < gv.V; base += NEMO_BLOCK) {
     const uint32_t u = base + threadIdx.x;
@@ -298,6 +298,26 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a
     }
   }
 #undef HOLDS
+}
+
+// gather every graph's sorted chains into one array (graph, k, head, tail, len)
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chain_gather(DevCorpus c, const uint64_t *off, uint32_t *out) {
+  const uint32_t g = blockIdx.x;
+  const uint32_t n = c.nch[g];
+  const uint32_t *ch = c.chain + 5 * c.node_off[g];
+  uint32_t *o = out + 5 * off[g];
+  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) {
+    o[5 * k] = g;
+    o[5 * k + 1] = k;
+    o[5 * k + 2] = ch[5 * k];
+    o[5 * k + 3] = ch[5 * k + 1];
+    o[5 * k + 4] = ch[5 * k + 2];
+  }
+}
+
+void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan64, dim3(1), dim3(NEMO_BLOCK), 0, s, c.nch, off, c.G);
+  if (out) hipLaunchKernelGGL(k_chain_gather, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);
 }
 
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s) {

@@ -5,29 +5,6 @@
 
 namespace nemo {
 
-// In-place exclusive scan of a[0..n) by one workgroup; returns the total.
-__device__ uint32_t block_scan_inplace(uint32_t *a, uint32_t n, uint32_t *lds) {
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < n; base += NEMO_BLOCK * 4) {
-    const uint32_t i0 = base + threadIdx.x * 4;
-    uint32_t x[4], s = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      x[k] = (i0 + k < n) ? a[i0 + k] : 0u;
-      s += x[k];
-    }
-    uint32_t tot;
-    uint32_t ex = block_exscan(s, &tot, lds) + carry;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (i0 + k < n) a[i0 + k] = ex;
-      ex += x[k];
-    }
-    carry += tot;
-  }
-  return carry;
-}
-
 __device__ void sort_row(uint32_t *r, uint32_t n) {
   if (n <= 32) {
     for (uint32_t i = 1; i < n; i++) {
@@ -171,9 +148,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
     }
     __syncthreads();
     nl++;
-    lo = hi;
+    lo = hi;  // level nl-1 is topo[lvl[nl-1] .. lo)
     hi = s_tail;
-    if (threadIdx.x == 0) lvl[nl] = hi;
+    if (threadIdx.x == 0) lvl[nl] = lo;
     __syncthreads();
   }
   if (threadIdx.x == 0) {

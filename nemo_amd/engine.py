@@ -57,6 +57,7 @@ def lib():
             "nemo_last_error": ([vp], ctypes.c_char_p),
             "nemo_set_stream": ([vp, vp], i32),
             "nemo_set_timing": ([vp, i32], i32),
+            "nemo_set_option": ([vp, ctypes.c_char_p, ctypes.c_int64], i32),
             "nemo_load_corpus": ([vp, vp], i32),
             "nemo_rebuild": ([vp], i32),
             "nemo_num_nodes": ([vp], u64),
@@ -71,17 +72,20 @@ def lib():
             "nemo_diffprov": ([vp, vp, sz, i32], i32),
             "nemo_fetch_diff_mask": ([vp, u32, vp, u64], i32),
             "nemo_fetch_missing": ([vp, vp, u64, P(u64)], i32),
+            "nemo_fetch_diff_masks": ([vp, vp, u64], i32),
             "nemo_triggers": ([vp], i32),
             "nemo_fetch_triggers": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
             "nemo_fetch_node_flags": ([vp, u32, u32, vp, u64], i32),
             "nemo_fetch_chains": ([vp, vp, u64, P(u64)], i32),
             "nemo_fetch_run_tables": ([vp, i32, vp, u64], i32),
-            "nemo_pull_edges": ([vp, i32, u32], i32),
+            "nemo_pull_edges": ([vp, i32], i32),
+            "nemo_reduce_interpret": ([vp, u32, u32, P(u32), vp, P(u32), vp, P(u32)], i32),
             "nemo_pulled_count": ([vp, u32], u64),
             "nemo_fetch_pulled": ([vp, u32, vp, vp, u64, P(u64)], i32),
             "nemo_timings": ([vp, vp, u32, P(u32)], i32),
             "nemo_reset_timings": ([vp], i32),
             "nemo_synchronize": ([vp], i32),
+            "nemo_debug_copy": ([vp, ctypes.c_char_p, vp, u64, u64], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -125,6 +129,9 @@ class Engine:
     # ---- phases -------------------------------------------------------------------
     def set_stream(self, stream_handle: int) -> None:
         self._chk(self.L.nemo_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def set_option(self, name: str, value: int) -> None:
+        self._chk(self.L.nemo_set_option(self.h, name.encode(), int(value)))
 
     def set_timing(self, on: bool = True) -> None:
         self._chk(self.L.nemo_set_timing(self.h, int(on)))
@@ -186,8 +193,8 @@ class Engine:
     def triggers(self) -> None:
         self._chk(self.L.nemo_triggers(self.h))
 
-    def pull(self, which: int, aux: int = 0) -> None:
-        self._chk(self.L.nemo_pull_edges(self.h, which, aux))
+    def pull(self, which: int) -> None:
+        self._chk(self.L.nemo_pull_edges(self.h, which))
 
     def synchronize(self) -> None:
         self._chk(self.L.nemo_synchronize(self.h))
@@ -224,6 +231,13 @@ class Engine:
         self._chk(self.L.nemo_fetch_diff_mask(self.h, entry, _p(out), V0))
         return out[:V0]
 
+    def diff_masks(self, n_entries: int) -> np.ndarray:
+        c = self.corpus
+        V0 = c.graph_size(2 * c.run_index(0) + 1)
+        out = np.zeros(max(n_entries * V0, 1), np.uint8)
+        self._chk(self.L.nemo_fetch_diff_masks(self.h, _p(out), n_entries * V0))
+        return out[:n_entries * V0].reshape(n_entries, V0)
+
     def missing(self) -> np.ndarray:
         n = ctypes.c_uint64()
         self._chk(self.L.nemo_fetch_missing(self.h, None, 0, ctypes.byref(n)))
@@ -242,13 +256,18 @@ class Engine:
                                              ctypes.byref(npost), _p(asy), nasync.value, ctypes.byref(nasync)))
         return (pre[:3 * npre.value].reshape(-1, 3), post[:2 * npost.value].reshape(-1, 2), asy[:nasync.value])
 
-    def pulled(self, graph: int):
+    def pulled(self, slot: int):
         n = ctypes.c_uint64()
-        self._chk(self.L.nemo_fetch_pulled(self.h, graph, None, None, 0, ctypes.byref(n)))
+        self._chk(self.L.nemo_fetch_pulled(self.h, slot, None, None, 0, ctypes.byref(n)))
         s = np.zeros(n.value + 1, np.uint32)
         d = np.zeros(n.value + 1, np.uint32)
-        self._chk(self.L.nemo_fetch_pulled(self.h, graph, _p(s), _p(d), n.value, ctypes.byref(n)))
+        self._chk(self.L.nemo_fetch_pulled(self.h, slot, _p(s), _p(d), n.value, ctypes.byref(n)))
         return s[:n.value], d[:n.value]
+
+    def debug_copy(self, name: str, offset: int, nbytes: int) -> np.ndarray:
+        out = np.zeros(max(nbytes, 1), np.uint8)
+        self._chk(self.L.nemo_debug_copy(self.h, name.encode(), _p(out), offset, nbytes))
+        return out[:nbytes]
 
     def timings(self) -> Dict[str, dict]:
         n = ctypes.c_uint32()
@@ -260,6 +279,19 @@ class Engine:
 
     def reset_timings(self) -> None:
         self._chk(self.L.nemo_reset_timings(self.h))
+
+
+def reduce_interpret(vec: np.ndarray, n_tables: int, table_post: int):
+    """nemo_reduce_interpret: inter/union/achvdCond from a (reduced) host vector; no device needed."""
+    v = np.ascontiguousarray(vec, dtype=np.uint32)
+    inter = np.zeros(n_tables + 1, np.uint32)
+    uni = np.zeros(n_tables + 1, np.uint32)
+    a, ni, nu = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    rc = lib().nemo_reduce_interpret(v.ctypes.data, n_tables, table_post, ctypes.byref(a), inter.ctypes.data,
+                                     ctypes.byref(ni), uni.ctypes.data, ctypes.byref(nu))
+    if rc != 0:
+        raise NemoError(rc, "nemo_reduce_interpret")
+    return a.value, inter[:ni.value].tolist(), uni[:nu.value].tolist()
 
 
 @dataclass

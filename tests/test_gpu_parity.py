@@ -83,3 +83,54 @@ def test_cycle_refused(eng):
     with pytest.raises(E.NemoError) as ei:
         eng.load(corpus)
     assert ei.value.code == 4
+
+
+def test_diff_edge_pulls(eng):
+    corpus, _ = random_corpus(4242, n_runs=5, max_nodes=20)
+    f = corpus.failed_iters()
+    if not f:
+        pytest.skip("no failed run")
+    E.analyze(corpus, corpus.success_iters(), f, diff_mode=DIFF_PER_RUN, engine=eng, pulls=False)
+    eng.pull(2)
+    g0 = 2 * corpus.run_index(0) + 1
+    e0, e1 = int(corpus.edge_off[g0]), int(corpus.edge_off[g0 + 1])
+    src, dst = corpus.edge_src[e0:e1], corpus.edge_dst[e0:e1]
+    for e in range(len(f)):
+        m = eng.diff_mask(e)
+        want = sorted((int(a), int(b)) for a, b in zip(src, dst) if m[a] and m[b])
+        s, d = eng.pulled(e)
+        assert sorted(zip(s.tolist(), d.tolist())) == want
+
+
+@pytest.mark.parametrize("lds_max,comp_max", [(-1, -1), (0, -1), (0, 0), (0, 8), (12, 5), (30, -1)])
+def test_chain_paths_lds_and_fallback(eng, lds_max, comp_max):
+    # exercise the LDS wave path, the workgroup fallback, and mixtures of both
+    import random
+    from tests.small import random_prov
+    rng = random.Random(99)
+    graphs = []
+    for it in range(40):
+        st = "success" if it == 0 or rng.random() < 0.8 else "failure"
+        graphs.append((it, st, random_prov(rng, "pre", 40, p_edge=0.2, p_next=0.9),
+                       random_prov(rng, "post", 40, p_edge=0.2, p_next=0.9)))
+    corpus = corpus_from_graphs(graphs)
+    eng.set_option("chains_lds_max", lds_max)
+    eng.set_option("chains_comp_max", comp_max)
+    try:
+        _check(eng, corpus)
+    finally:
+        eng.set_option("chains_lds_max", -1)
+        eng.set_option("chains_comp_max", -1)
+
+
+@pytest.mark.parametrize("lds_max,comp_max,nval", [(-1, -1, 8), (0, -1, 8), (0, 0, 8), (-1, -1, 2), (0, -1, 2)])
+def test_synthetic_corpus(eng, lds_max, comp_max, nval):
+    from tools import synth
+    corpus, _ = synth.generate(40, target_nodes=3000, nval=nval)
+    eng.set_option("chains_lds_max", lds_max)
+    eng.set_option("chains_comp_max", comp_max)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+    finally:
+        eng.set_option("chains_lds_max", -1)
+        eng.set_option("chains_comp_max", -1)
