@@ -18,6 +18,12 @@ $(BUILD)/%.o: nemo_amd/csrc/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
 
+# diagnostic build with in-kernel phase stamps (never shipped as libnemohip.so)
+stamps: $(SRCS) $(HDRS)
+	@mkdir -p $(BUILD)/stamps
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -DNEMO_STAMPS -c -o $(BUILD)/stamps/$$(basename $$f .hip).o $$f || exit 1; done
+	$(HIPCC) $(HIPFLAGS) -shared -o nemo_amd/libnemohip_stamps.so $(BUILD)/stamps/*.o
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -29,4 +35,4 @@ clean:
 	$(MAKE) -s -C oracle clean
 	$(MAKE) -s -C tools clean
 
-.PHONY: all oracle tools clean
+.PHONY: all oracle tools clean stamps

@@ -380,6 +380,10 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(c->d_owned, R);
   A(c->d_is_success, R);
   A(c->d_red, 2 * (size_t)c->T + 4);
+#ifdef NEMO_STAMPS
+  A(d.stamps, 16 * G);
+  HIPCHK(c, hipMemsetAsync(d.stamps, 0, 16 * G * 8, c->stream));
+#endif
 #undef A
   hipStream_t s = c->stream;
   HIPCHK(c, hipMemcpyAsync(no, in->node_off, (G + 1) * 8, hipMemcpyHostToDevice, s));
@@ -890,6 +894,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "dmask") base = c->d_dmask;
   else if (n == "r0lab") base = c->d_r0lab;
   else if (n == "r0idx") base = c->d_r0idx;
+  else if (n == "stamps") base = c->dc.stamps;
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));

@@ -170,6 +170,7 @@ struct DevCorpus {
   uint32_t *chain_nt;                    // [V] next chain with the same tail
   uint32_t *proto_bits, *graph_tables;   // [n_runs*words]
   uint8_t *gate;                         // [n_runs]
+  unsigned long long *stamps;            // diagnostic builds only: [16*G] phase stamps
 
   __device__ __forceinline__ GraphView view(uint32_t g) const {
     GraphView v;

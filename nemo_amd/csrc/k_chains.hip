@@ -47,6 +47,22 @@ struct CompLDS {
   uint8_t flag[CM];   // 1 = rule, 2 = unseen
 };
 
+#ifdef NEMO_STAMPS
+// diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product build)
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && c.stamps) {                                                   \
+      unsigned long long t_;                                                              \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+      c.stamps[16 * (size_t)blockIdx.x + (k)] = t_;                                       \
+    }                                                                                     \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 #define CF_RULE 1u
 #define CF_UNSEEN 2u
 
@@ -253,6 +269,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
   const uint32_t tid = threadIdx.x;
   const uint32_t cap = min((uint32_t)HCAP, c.hcap_limit);
+  STAMP(0);
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
   // ordered compaction of H* in Kahn order (chunks of 4 positions per thread);
   // pc[p] = #H* nodes before topo position p gives every level's segment
@@ -301,6 +318,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     s_maxup = 0;
     s_fail = 0;
   }
+  STAMP(1);
   // compact ID ranks: bitonic sort of (rank, index) pairs in LDS
   uint32_t N2 = 1;
   while (N2 < n) N2 <<= 1;
@@ -334,6 +352,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   }
   for (uint32_t q = tid; q < n; q += NEMO_BLOCK) L.crank[L.u.kk[q] & 0xFFFFu] = (uint16_t)q;
   __syncthreads();
+  STAMP(2);
   // compact child / parent lists
   uint32_t ce = 0, pe = 0;
   for (uint32_t base = 0; base < n; base += NEMO_BLOCK) {
@@ -377,6 +396,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     L.u.adj.pcoff[n] = (uint16_t)pe;
   }
   __syncthreads();
+  STAMP(3);
   // up: longest H* path from a next rule ending here; down/nxt/tail: the
   // lexicographically least longest continuation to a next rule
   for (uint32_t s = 0; s < ns; s++) {
@@ -409,6 +429,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     }
     __syncthreads();
   }
+  STAMP(4);
   // bucket by up value (counting sort in LDS)
   const uint32_t maxup = s_maxup;
   if (maxup + 2 > UCAP) {
@@ -457,6 +478,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) L.po[L.ub[j]] = L.pnew[L.ub[j]];
     __syncthreads();
   }
+  STAMP(5);
   // one representative per accepted path
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
     const bool rep = L.up[i] == 0 || L.nxt[L.bp[i]] != i;
@@ -477,6 +499,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     L.u.kk[q] = ((unsigned long long)(0xFFFFu - len) << 48) | ((unsigned long long)hr << 16) | rep;
   }
   __syncthreads();
+  STAMP(6);
   uint32_t *out = c.chain + 5 * gv.n0;
   for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
     const unsigned long long me = L.u.kk[q];
@@ -500,6 +523,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     const uint32_t t = out[5 * k + 1];
     c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
   }
+  STAMP(7);
   if (tid == 0) {
     c.nch[g] = nch;
     if (s_fail) c.err[g] = NEMO_ERR_INVALID;

@@ -41,51 +41,70 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 // CSR (forward + reverse) of every graph; rows sorted so that a merged
 // duplicate DUETO edge is adjacent.  relationships-created counts edges that
 // are neither duplicates nor goal->goal / rule->rule (pre-post-prov.go:150-210).
+// Graphs with V < CSR_LDS count degrees, scan and hand out cursors in LDS;
+// larger ones do the same with global atomics.
+#define CSR_LDS 8192
 __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
+  __shared__ uint32_t s_cnt[CSR_LDS];
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_bad, s_created;
   const uint32_t g = blockIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0, *rc = c.rc + e0;
-  uint32_t *cf = c.s_a + n0 + g, *cr = c.s_b + n0 + g;
   const uint32_t *es = c.esrc + e0, *ed = c.edst + e0, *word = c.word + n0;
   if (threadIdx.x == 0) {
     s_bad = 0;
     s_created = 0;
   }
-  for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) {
-    fp[v] = 0;
-    rp[v] = 0;
-  }
-  __syncthreads();
-  for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
-    const uint32_t s = es[e], d = ed[e];
-    if (s >= V || d >= V) {
-      atomicOr(&s_bad, 1u);
-      continue;
-    }
-    atomicAdd(&fp[s], 1u);
-    atomicAdd(&rp[d], 1u);
-  }
+  for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK)
+    if (es[e] >= V || ed[e] >= V) s_bad = 1;
   __syncthreads();
   if (s_bad) {
     if (threadIdx.x == 0) c.err[g] = NEMO_ERR_INVALID;
     return;
   }
-  block_scan_inplace(fp, V + 1, s_lds);
-  block_scan_inplace(rp, V + 1, s_lds);
-  for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) {
-    cf[v] = fp[v];
-    cr[v] = rp[v];
+  if (V < CSR_LDS) {
+    for (int dir = 0; dir < 2; dir++) {
+      const uint32_t *key = dir ? ed : es, *val = dir ? es : ed;
+      uint32_t *ptr = dir ? rp : fp, *col = dir ? rc : fc;
+      for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) s_cnt[v] = 0;
+      __syncthreads();
+      for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) atomicAdd(&s_cnt[key[e]], 1u);
+      __syncthreads();
+      block_scan_inplace(s_cnt, V + 1, s_lds);
+      for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) ptr[v] = s_cnt[v];
+      __syncthreads();
+      for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) col[atomicAdd(&s_cnt[key[e]], 1u)] = val[e];
+      __syncthreads();
+    }
+  } else {
+    uint32_t *cf = c.s_a + n0 + g, *cr = c.s_b + n0 + g;
+    for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) {
+      fp[v] = 0;
+      rp[v] = 0;
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
+      atomicAdd(&fp[es[e]], 1u);
+      atomicAdd(&rp[ed[e]], 1u);
+    }
+    __syncthreads();
+    block_scan_inplace(fp, V + 1, s_lds);
+    block_scan_inplace(rp, V + 1, s_lds);
+    for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) {
+      cf[v] = fp[v];
+      cr[v] = rp[v];
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
+      const uint32_t s = es[e], d = ed[e];
+      fc[atomicAdd(&cf[s], 1u)] = d;
+      rc[atomicAdd(&cr[d], 1u)] = s;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
-    const uint32_t s = es[e], d = ed[e];
-    fc[atomicAdd(&cf[s], 1u)] = d;
-    rc[atomicAdd(&cr[d], 1u)] = s;
-  }
-  __syncthreads();
+  __threadfence_block();
   uint32_t created = 0;
   for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) {
     const uint32_t a = fp[v], b = fp[v + 1];

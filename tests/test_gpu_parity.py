@@ -134,3 +134,11 @@ def test_synthetic_corpus(eng, lds_max, comp_max, nval):
     finally:
         eng.set_option("chains_lds_max", -1)
         eng.set_option("chains_comp_max", -1)
+
+
+def test_large_graphs_global_paths(eng):
+    # V >= 8192 takes the global-memory CSR build; |H*| > 2048 takes k_chains_big
+    from tools import synth
+    corpus, _ = synth.generate(6, target_nodes=14000)
+    assert max(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 8192
+    _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
