@@ -225,7 +225,7 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 struct ChainsLDS {
   uint16_t crank[HCAP];  // rank of the node's ID among H* nodes
   int16_t up[HCAP], down[HCAP];
-  uint16_t nxt[HCAP], bp[HCAP], head[HCAP], tail[HCAP], po[HCAP], pnew[HCAP];
+  uint16_t nxt[HCAP], bp[HCAP], head[HCAP], tail[HCAP], po[HCAP];
   uint16_t ub[HCAP];
   uint32_t uoff[UCAP], cur[UCAP];
   uint16_t seg[HCAP + 1];
@@ -242,19 +242,6 @@ struct ChainsLDS {
     unsigned long long kk[HCAP];           // bitonic sort of ranks; later the chain sort keys
   } u;
 };
-
-// Is the path represented by witness a before the one represented by b?
-// (Both have the same length and head; see the file comment.)
-__device__ __forceinline__ bool path_before(const ChainsLDS &L, uint32_t a, uint32_t b) {
-  if (L.up[a] <= L.up[b]) {
-    uint32_t x = b;
-    while (L.up[x] > L.up[a]) x = L.bp[x];
-    return x == a ? true : L.po[a] < L.po[x];
-  }
-  uint32_t x = a;
-  while (L.up[x] > L.up[b]) x = L.bp[x];
-  return x == b ? false : L.po[x] < L.po[b];
-}
 
 __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __shared__ ChainsLDS L;
@@ -319,38 +306,58 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     s_fail = 0;
   }
   STAMP(1);
-  // compact ID ranks: bitonic sort of (rank, index) pairs in LDS
-  uint32_t N2 = 1;
-  while (N2 < n) N2 <<= 1;
-  for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
-    if (i < n) {
-      const uint32_t v = hs[i];
-      hidx[v] = i;
-      L.isrule[i] = is_rule(gv.word[v]) ? 1 : 0;
-      L.u.kk[i] = ((unsigned long long)gv.rank_of(v) << 16) | i;
-    } else {
-      L.u.kk[i] = ~0ull;
-    }
+  // compact ID ranks: crank(v) = #H* nodes of smaller ID rank.  Small graphs
+  // set one bit per H* node in a rank bitmap and take prefix popcounts; larger
+  // ones sort (rank, index) pairs with an LDS bitonic network.
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+    const uint32_t v = hs[i];
+    hidx[v] = i;
+    L.isrule[i] = is_rule(gv.word[v]) ? 1 : 0;
   }
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t k = 2; k <= N2; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long x = L.u.kk[i], y = L.u.kk[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            L.u.kk[i] = y;
-            L.u.kk[ixj] = x;
+  if (gv.V <= 32768) {
+    uint32_t *bm = (uint32_t *)L.u.kk;            // [1024] rank bitmap
+    uint32_t *pre = bm + 1024;                    // [1025] prefix popcounts
+    const uint32_t nw = (gv.V + 31) >> 5;
+    for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) bm[w] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+      const uint32_t r = gv.rank_of(hs[i]);
+      atomicOr(&bm[r >> 5], 1u << (r & 31));
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) pre[w] = __popc(bm[w]);
+    __syncthreads();
+    block_scan_inplace(pre, nw, s_lds);
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+      const uint32_t r = gv.rank_of(hs[i]);
+      L.crank[i] = (uint16_t)(pre[r >> 5] + __popc(bm[r >> 5] & ((1u << (r & 31)) - 1u)));
+    }
+    __syncthreads();
+  } else {
+    uint32_t N2 = 1;
+    while (N2 < n) N2 <<= 1;
+    for (uint32_t i = tid; i < N2; i += NEMO_BLOCK)
+      L.u.kk[i] = i < n ? (((unsigned long long)gv.rank_of(hs[i]) << 16) | i) : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= N2; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
+          const uint32_t ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long x = L.u.kk[i], y = L.u.kk[ixj];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) {
+              L.u.kk[i] = y;
+              L.u.kk[ixj] = x;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
+    for (uint32_t q = tid; q < n; q += NEMO_BLOCK) L.crank[L.u.kk[q] & 0xFFFFu] = (uint16_t)q;
   }
-  for (uint32_t q = tid; q < n; q += NEMO_BLOCK) L.crank[L.u.kk[q] & 0xFFFFu] = (uint16_t)q;
+  __threadfence_block();
   __syncthreads();
   STAMP(2);
   // compact child / parent lists
@@ -400,33 +407,47 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   // up: longest H* path from a next rule ending here; down/nxt/tail: the
   // lexicographically least longest continuation to a next rule
   for (uint32_t s = 0; s < ns; s++) {
-    for (uint32_t i = L.seg[s] + tid; i < L.seg[s + 1]; i += NEMO_BLOCK) {
+    const uint32_t e = L.seg[s + 1];
+    for (uint32_t i = L.seg[s] + tid; i < e; i += NEMO_BLOCK) {
       int32_t d = L.isrule[i] ? 0 : -1;
-      for (uint32_t j = L.u.adj.pcoff[i]; j < L.u.adj.pcoff[i + 1]; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
+      const uint32_t j1 = L.u.adj.pcoff[i + 1];
+      for (uint32_t j = L.u.adj.pcoff[i]; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
       L.up[i] = (int16_t)d;
-      atomicMax(&s_maxup, (uint32_t)max(d, 0));
     }
     __syncthreads();
   }
   for (uint32_t s = ns; s-- > 0;) {
-    for (uint32_t i = L.seg[s] + tid; i < L.seg[s + 1]; i += NEMO_BLOCK) {
-      int32_t d = L.isrule[i] ? 0 : -1;
-      for (uint32_t j = L.u.adj.ccoff[i]; j < L.u.adj.ccoff[i + 1]; j++)
-        d = max(d, (int32_t)L.down[L.u.adj.child[j]] + 1);
+    const uint32_t e = L.seg[s + 1];
+    for (uint32_t i = L.seg[s] + tid; i < e; i += NEMO_BLOCK) {
+      // one pass: the deepest child, ties to the smallest ID rank
+      int32_t best = -1;
       uint32_t bc = NIL16, br = NEMO_NONE;
-      if (d > 0)
-        for (uint32_t j = L.u.adj.ccoff[i]; j < L.u.adj.ccoff[i + 1]; j++) {
-          const uint32_t w = L.u.adj.child[j];
-          if (L.down[w] == d - 1 && L.crank[w] < br) {
-            bc = w;
-            br = L.crank[w];
-          }
+      const uint32_t j1 = L.u.adj.ccoff[i + 1];
+      for (uint32_t j = L.u.adj.ccoff[i]; j < j1; j++) {
+        const uint32_t w = L.u.adj.child[j];
+        const int32_t dw = L.down[w];
+        const uint32_t rw = L.crank[w];
+        if (dw > best || (dw == best && rw < br)) {
+          best = dw;
+          bc = w;
+          br = rw;
         }
+      }
+      int32_t d = best >= 0 ? best + 1 : (L.isrule[i] ? 0 : -1);
+      if (L.isrule[i] && d < 0) d = 0;
+      if (d > 0 && best < 0) bc = NIL16;
       L.down[i] = (int16_t)d;
-      L.nxt[i] = (uint16_t)bc;
+      L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
       L.tail[i] = (uint16_t)(d > 0 ? L.tail[bc] : i);
-      if (d < 0 || (d > 0 && bc == NIL16)) s_fail = 1;  // impossible on a chain subgraph
+      if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
     }
+    __syncthreads();
+  }
+  {
+    uint32_t m = 0;
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) m = max(m, (uint32_t)max((int32_t)L.up[i], 0));
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+    if (lane_id() == 0) atomicMax(&s_maxup, m);
     __syncthreads();
   }
   STAMP(4);
@@ -445,37 +466,36 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __syncthreads();
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) L.ub[atomicAdd(&L.cur[L.up[i]], 1u)] = (uint16_t)i;
   __syncthreads();
-  // prefix ranks: po(v) = rank of best_prefix(v) among the prefixes of its length
+  // prefix ranks: po(v) = rank of best_prefix(v) among the prefixes of its
+  // length; key = (po(bp(v)), crank(v)) is unique inside a level
   for (uint32_t k = 0; k <= maxup; k++) {
     const uint32_t a = L.uoff[k], b = L.uoff[k + 1];
     for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
       const uint32_t i = L.ub[j];
       uint32_t bpi = NIL16, bpo = NEMO_NONE;
-      if (k > 0)
-        for (uint32_t q = L.u.adj.pcoff[i]; q < L.u.adj.pcoff[i + 1]; q++) {
+      if (k > 0) {
+        const uint32_t q1 = L.u.adj.pcoff[i + 1];
+        for (uint32_t q = L.u.adj.pcoff[i]; q < q1; q++) {
           const uint32_t p = L.u.adj.par[q];
           if ((uint32_t)L.up[p] == k - 1 && L.po[p] < bpo) {
             bpi = p;
             bpo = L.po[p];
           }
         }
+      }
       L.bp[i] = (uint16_t)bpi;
       L.head[i] = (uint16_t)(k == 0 ? i : L.head[bpi]);
+      L.u.rk.bk[j - a] = ((k ? bpo : 0u) << 16) | L.crank[i];
     }
     __syncthreads();
-    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
-      const uint32_t i = L.ub[j];
-      L.u.rk.bk[j - a] = ((k ? (uint32_t)L.po[L.bp[i]] : 0u) << 16) | L.crank[i];
-    }
-    __syncthreads();
+    const uint32_t m = b - a;
     for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
       const uint32_t me = L.u.rk.bk[j - a];
       uint32_t pos = 0;
-      for (uint32_t q = 0; q < b - a; q++) pos += L.u.rk.bk[q] < me;
-      L.pnew[L.ub[j]] = (uint16_t)pos;
+#pragma unroll 8
+      for (uint32_t q = 0; q < m; q++) pos += L.u.rk.bk[q] < me;
+      L.po[L.ub[j]] = (uint16_t)pos;
     }
-    __syncthreads();
-    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) L.po[L.ub[j]] = L.pnew[L.ub[j]];
     __syncthreads();
   }
   STAMP(5);
@@ -494,21 +514,75 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __threadfence_block();
   __syncthreads();
   const uint32_t nch = s_nch;
-  for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
-    const uint32_t len = tmp[5 * q + 2], hr = tmp[5 * q + 3], rep = tmp[5 * q + 4];
-    L.u.kk[q] = ((unsigned long long)(0xFFFFu - len) << 48) | ((unsigned long long)hr << 16) | rep;
-  }
-  __syncthreads();
   STAMP(6);
-  uint32_t *out = c.chain + 5 * gv.n0;
-  for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
-    const unsigned long long me = L.u.kk[q];
-    uint32_t pos = 0;
-    for (uint32_t r = 0; r < nch; r++) {
-      const unsigned long long o = L.u.kk[r];
-      if ((o >> 16) != (me >> 16)) pos += o < me;
-      else if (o != me) pos += path_before(L, (uint32_t)(o & 0xFFFF), (uint32_t)(me & 0xFFFF));
+  // Acceptance order.  For equal lengths, the lexicographic order of accepted
+  // paths is the preorder of their representatives in the best-prefix forest
+  // (bp pointers; roots = heads; children in ID-rank order, which is po order
+  // inside a level): an ancestor's path comes first, otherwise the first
+  // divergence decides.  S = subtree sizes (bottom-up), pre = preorder
+  // (top-down, exclusive scans of sizes in po order).
+  {
+    uint32_t *S = (uint32_t *)L.u.kk;  // subtree size, then "first child position" of a parent
+    uint32_t *A = S + HCAP;            // sizes of one level in po order -> exclusive scan
+    uint16_t *pre = L.head;            // head[] is dead once the records are written
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) S[i] = 1;
+    __syncthreads();
+    for (uint32_t k = maxup; k >= 1; k--) {
+      for (uint32_t j = L.uoff[k] + tid; j < L.uoff[k + 1]; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j];
+        atomicAdd(&S[L.bp[i]], S[i]);
+      }
+      __syncthreads();
     }
+    for (uint32_t k = 0; k <= maxup; k++) {
+      const uint32_t a = L.uoff[k], m = L.uoff[k + 1] - a;
+      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j];
+        A[L.po[i]] = S[i];
+        if (k > 0) atomicMin(&S[L.bp[i]], (uint32_t)L.po[i]);
+      }
+      __syncthreads();
+      block_scan_inplace(A, m, s_lds);
+      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j];
+        const uint32_t pos = L.po[i];
+        pre[i] = (uint16_t)(k == 0 ? A[pos] : pre[L.bp[i]] + 1u + A[pos] - A[S[L.bp[i]]]);
+      }
+      __syncthreads();
+      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) S[L.ub[j]] = NEMO_NONE;
+      __syncthreads();
+    }
+    // tie-free keys (len desc, preorder asc), bitonic sort in LDS
+    uint32_t N2 = 1;
+    while (N2 < nch) N2 <<= 1;
+    for (uint32_t q = tid; q < N2; q += NEMO_BLOCK) {
+      unsigned long long key = ~0ull;
+      if (q < nch) {
+        const uint32_t len = tmp[5 * q + 2], rep = tmp[5 * q + 4];
+        key = ((unsigned long long)(((0xFFFFu - len) << 16) | pre[rep]) << 32) | q;
+      }
+      L.u.kk[q] = key;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= N2; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
+          const uint32_t ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long x = L.u.kk[i], y = L.u.kk[ixj];
+            if ((x > y) == ((i & k) == 0)) {
+              L.u.kk[i] = y;
+              L.u.kk[ixj] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  uint32_t *out = c.chain + 5 * gv.n0;
+  for (uint32_t pos = tid; pos < nch; pos += NEMO_BLOCK) {
+    const uint32_t q = (uint32_t)(L.u.kk[pos] & 0xFFFFFFFFu);
     uint32_t *w = out + 5 * pos;
     w[0] = hs[tmp[5 * q]];
     w[1] = hs[tmp[5 * q + 1]];
@@ -516,6 +590,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     w[3] = gv.rank_of(w[0]);
     w[4] = 0;
   }
+#ifdef NEMO_STAMPS
+  __syncthreads();
+#endif
+  STAMP(8);
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) c.tail_first[gv.n0 + hs[i]] = NEMO_NONE;
   __threadfence_block();
   __syncthreads();
@@ -523,7 +601,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     const uint32_t t = out[5 * k + 1];
     c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
   }
-  STAMP(7);
+  STAMP(9);
   if (tid == 0) {
     c.nch[g] = nch;
     if (s_fail) c.err[g] = NEMO_ERR_INVALID;

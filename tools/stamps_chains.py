@@ -10,10 +10,17 @@ eng = E.Engine(0)
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 G = corpus.n_graphs
 st = eng.debug_copy("stamps", 0, 16 * 8 * G).view(np.uint64).reshape(G, 16).astype(np.int64)
-names = ["compact", "ranks", "adjacency", "up/down", "prefix ranks", "reps", "sort+lists"]
-d = np.diff(st[:, :8], axis=1)
-ok = (st[:, 7] > 0)
+idx = [0, 1, 2, 3, 4, 5, 6, 8, 9]
+names = ["compact", "ranks", "adjacency", "up/down", "prefix ranks", "reps", "sort", "tail lists"]
+d = np.diff(st[:, idx], axis=1)
+ok = (st[:, 9] > 0)
 d = d[ok]
 print("graphs", ok.sum(), "total cycles per graph: median", np.median(d.sum(1)), "p90", np.percentile(d.sum(1), 90))
 for i, nm in enumerate(names):
     print(f"{nm:14s} median {np.median(d[:, i]):10.0f}  mean {d[:, i].mean():10.0f}  share {d[:, i].sum() / d.sum():.3f}")
+nch = []
+ch = eng.chains()
+import collections
+cnt = collections.Counter(int(g) for g in ch[:, 0])
+keys = collections.Counter((int(r[0]), int(r[2]), int(r[4])) for r in ch)
+print("chains per graph mean", len(ch) / G, "max", max(cnt.values()), "records with (len, head) ties:", sum(v for v in keys.values() if v > 1), "of", len(ch))
