@@ -309,9 +309,20 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   // compact ID ranks: crank(v) = #H* nodes of smaller ID rank.  Small graphs
   // set one bit per H* node in a rank bitmap and take prefix popcounts; larger
   // ones sort (rank, index) pairs with an LDS bitonic network.
+  // graph-local node -> compact index (NONE outside H*): in LDS over the
+  // not-yet-used up..ub arrays when the graph is small enough, else global
+  uint16_t *hmap = (uint16_t *)L.up;
+  const bool lmap = gv.V <= 8u * HCAP;
+  if (lmap) {
+    for (uint32_t v = tid; v < gv.V; v += NEMO_BLOCK) hmap[v] = 0xFFFFu;
+    __syncthreads();
+  }
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
     const uint32_t v = hs[i];
-    hidx[v] = i;
+    if (lmap)
+      hmap[v] = (uint16_t)i;
+    else
+      hidx[v] = i;
     L.isrule[i] = is_rule(gv.word[v]) ? 1 : 0;
   }
   if (gv.V <= 32768) {
@@ -361,14 +372,25 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __syncthreads();
   STAMP(2);
   // compact child / parent lists
+  auto hx = [&](uint32_t w) -> uint32_t {
+    if (lmap) {
+      const uint32_t h = hmap[w];
+      return h == 0xFFFFu ? NEMO_NONE : h;
+    }
+    return INH(w) ? hidx[w] : NEMO_NONE;
+  };
   uint32_t ce = 0, pe = 0;
   for (uint32_t base = 0; base < n; base += NEMO_BLOCK) {
     const uint32_t i = base + tid;
-    uint32_t nc = 0, np = 0, v = 0;
+    uint32_t nc = 0, np = 0, fb = 0, fe = 0, rb = 0, re = 0;
     if (i < n) {
-      v = hs[i];
-      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) nc += INH(gv.fc[j]);
-      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) np += INH(gv.rc[j]);
+      const uint32_t v = hs[i];
+      fb = gv.fp[v];
+      fe = gv.fp[v + 1];
+      rb = gv.rp[v];
+      re = gv.rp[v + 1];
+      for (uint32_t j = fb; j < fe; j++) nc += hx(gv.fc[j]) != NEMO_NONE;
+      for (uint32_t j = rb; j < re; j++) np += hx(gv.rc[j]) != NEMO_NONE;
     }
     uint32_t tc, tp;
     const uint32_t oc = ce + block_exscan(nc, &tc, s_lds);
@@ -378,16 +400,16 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       L.u.adj.pcoff[i] = (uint16_t)min(op, (uint32_t)ECAP);
       if (oc + nc <= ECAP) {
         uint32_t k = oc;
-        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) {
-          const uint32_t w = gv.fc[j];
-          if (INH(w)) L.u.adj.child[k++] = (uint16_t)hidx[w];
+        for (uint32_t j = fb; j < fe; j++) {
+          const uint32_t h = hx(gv.fc[j]);
+          if (h != NEMO_NONE) L.u.adj.child[k++] = (uint16_t)h;
         }
       }
       if (op + np <= ECAP) {
         uint32_t k = op;
-        for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) {
-          const uint32_t w = gv.rc[j];
-          if (INH(w)) L.u.adj.par[k++] = (uint16_t)hidx[w];
+        for (uint32_t j = rb; j < re; j++) {
+          const uint32_t h = hx(gv.rc[j]);
+          if (h != NEMO_NONE) L.u.adj.par[k++] = (uint16_t)h;
         }
       }
     }
