@@ -17,7 +17,9 @@ One step = the whole hot path over the rank's corpus, inputs resident in HBM:
   CreateNaiveDiffProv for every failed run (per-run label sets)  nemo_diffprov
   GenerateCorrections/Extensions trigger patterns (rank owning run 0)
   PullPrePostProv + Q24 edge pulls (device compaction of simplified + diff graphs)
-  D2H of every compact result (node flags, chains, D masks, missing events)
+  D2H of every host-facing result: node flags + chain (head, tail) pairs (pinned,
+    async on a copy stream from right after SimplifyProv), D masks, missing events,
+    table sets, trigger rows
 
 Launched as `python bench.py` (N=1) or under torch.distributed.run for N>1
 (RANK/LOCAL_RANK/WORLD_SIZE from the env, backend nccl = RCCL).
@@ -101,6 +103,7 @@ def main():
         eng.rebuild()
         eng.mark()
         eng.simplify()
+        eng.stage_simplified()  # flags + chain pairs -> pinned host, overlapping the rest
         eng.protos_partial(success, d_red.data_ptr())
         if world > 1:
             dist.all_reduce(d_red)
@@ -118,11 +121,10 @@ def main():
             eng.trigger_rows()
         eng.pull(1)
         eng.pull(2)
-        flags = eng.flags()
-        chains = eng.chains()
         masks = eng.diff_masks(len(failed)) if failed else None
         miss = eng.missing()
-        return flags, chains, masks, miss
+        flags, chain_off, chain_ht = eng.simplified_view()
+        return flags, chain_off, chain_ht, masks, miss
 
     for _ in range(args.warmup):
         step()

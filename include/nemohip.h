@@ -202,6 +202,19 @@ int nemo_fetch_triggers(nemo_ctx *ctx, uint32_t *pre_rows /* 3 per row */, uint6
 int nemo_fetch_node_flags(nemo_ctx *ctx, uint32_t g_lo, uint32_t g_hi, uint8_t *out, uint64_t cap);
 /* Accepted @next chains of every graph, ordered by (graph, k).              */
 int nemo_fetch_chains(nemo_ctx *ctx, nemo_chain *out, uint64_t cap, uint64_t *n_out);
+/* Asynchronous hand-over of the simplification (SimplifyProv,
+ * preprocessing.go:351-387) to the host: gathers every graph's accepted chains
+ * as dense (head, tail) pairs (graph-local node indices; graph g's chain k at
+ * chain_off[g] + k) and copies them with all node flags into library-owned
+ * pinned memory on a second stream, overlapping whatever the caller launches
+ * next.  Flags + pairs determine the simplified graphs exactly (collapsed rule
+ * k of graph g: preds(head) -> V_g + k -> succs(tail)).                      */
+int nemo_stage_simplified(nemo_ctx *ctx);
+/* Waits for the staged copies and returns views into the pinned buffers
+ * (flags[V], chain_off[G+1], chain_ht[2*n]); valid until the next
+ * nemo_stage_simplified or nemo_ctx_destroy.  Any out-pointer may be NULL.   */
+int nemo_simplified_view(nemo_ctx *ctx, const uint8_t **flags, const uint64_t **chain_off,
+                         const uint32_t **chain_ht, uint64_t *n_chains);
 /* Per-run table bitsets, words = ceil(n_tables/32) u32 per run:
  *   which = 0: proto list of the run (extractProtos, prototype.go:11-24)
  *   which = 1: all rule tables of the simplified post graph (missingFrom)   */

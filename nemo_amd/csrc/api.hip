@@ -81,6 +81,18 @@ struct nemo_ctx {
   // chain gather
   uint32_t *d_chout = nullptr;
   uint64_t *d_choff = nullptr, chout_cap = 0;
+
+  // staged simplification results: pinned host copies made on `copy`
+  hipStream_t copy = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
+  bool staged = false;
+  uint64_t staged_n = 0;
+  uint32_t *d_chht = nullptr;
+  uint64_t d_chht_cap = 0;
+  uint8_t *h_flags = nullptr;
+  uint64_t *h_choff = nullptr;
+  uint32_t *h_chht = nullptr;
+  uint64_t h_flags_cap = 0, h_choff_cap = 0, h_chht_cap = 0;
 };
 
 static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
@@ -111,6 +123,17 @@ static int dalloc(nemo_ctx *c, T **p, size_t n) {
   return NEMO_OK;
 }
 
+template <class T>
+static int hgrow(nemo_ctx *c, T **p, uint64_t *cap, uint64_t n) {
+  if (n <= *cap && *p) return NEMO_OK;
+  if (*p) HIPCHK(c, hipHostFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  HIPCHK(c, hipHostMalloc((void **)p, (n ? n : 1) * sizeof(T), hipHostMallocDefault));
+  *cap = n;
+  return NEMO_OK;
+}
+
 static void dfree(nemo_ctx *c, void *p) {
   if (!p) return;
   auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
@@ -127,6 +150,12 @@ static hipEvent_t get_event(nemo_ctx *c) {
   hipEvent_t e = nullptr;
   hipEventCreate(&e);
   return e;
+}
+
+// Kernels that rewrite node flags must not overtake a staged copy still in flight.
+static int guard_staged(nemo_ctx *c) {
+  if (c->staged) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
+  return NEMO_OK;
 }
 
 template <class F>
@@ -220,6 +249,9 @@ static void release_corpus(nemo_ctx *c) {
   c->d_chout = nullptr;
   c->d_choff = nullptr;
   c->chout_cap = 0;
+  c->d_chht = nullptr;
+  c->d_chht_cap = 0;
+  c->staged = false;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
 }
 
@@ -227,12 +259,22 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  if (c->copy) hipStreamSynchronize(c->copy);
   release_corpus(c);
   for (auto &p : c->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
   }
   for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
+  if (c->copy) {
+    hipStreamSynchronize(c->copy);
+    hipStreamDestroy(c->copy);
+  }
+  if (c->ev_ready) hipEventDestroy(c->ev_ready);
+  if (c->ev_copied) hipEventDestroy(c->ev_copied);
+  if (c->h_flags) hipHostFree(c->h_flags);
+  if (c->h_choff) hipHostFree(c->h_choff);
+  if (c->h_chht) hipHostFree(c->h_chht);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -301,6 +343,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   if (!c || !in) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->copy) HIPCHK(c, hipStreamSynchronize(c->copy));
   release_corpus(c);
   if (in->n_tables > NEMO_MAX_TABLES)
     return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
@@ -446,7 +489,9 @@ int nemo_rebuild(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   HIPCHK(c, hipSetDevice(c->device));
-  int rc = device_load(c);
+  int rc = guard_staged(c);
+  if (rc) return rc;
+  rc = device_load(c);
   if (rc) return rc;
   c->marked = c->simplified = c->protos_done = c->trig_done = false;
   return NEMO_OK;
@@ -457,7 +502,9 @@ int nemo_mark_holds(nemo_ctx *c) {
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_mark_holds before nemo_load_corpus");
   HIPCHK(c, hipSetDevice(c->device));
   const double V = (double)c->V, E = (double)c->E;
-  int rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, c->stream); });
+  int rc = guard_staged(c);
+  if (rc) return rc;
+  rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, c->stream); });
   if (rc) return rc;
   c->marked = true;
   c->simplified = c->protos_done = c->trig_done = false;
@@ -469,7 +516,9 @@ int nemo_simplify(nemo_ctx *c) {
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_simplify before nemo_mark_holds");
   HIPCHK(c, hipSetDevice(c->device));
   const double V = (double)c->V, E = (double)c->E;
-  int rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, c->stream); });
+  int rc = guard_staged(c);
+  if (rc) return rc;
+  rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, c->stream); });
   if (rc) return rc;
   rc = timed(c, "k_chains", 9 * V, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
   if (rc) return rc;
@@ -798,6 +847,61 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
   static_assert(sizeof(nemo_chain) == 20, "nemo_chain layout");
   if (n) HIPCHK(c, hipMemcpyAsync(out, c->d_chout, n * 20, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
+  return NEMO_OK;
+}
+
+int nemo_stage_simplified(nemo_ctx *c) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_stage_simplified before nemo_simplify");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  hipStream_t s = c->stream;
+  if (!c->copy) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));
+  }
+  if (c->staged) HIPCHK(c, hipEventSynchronize(c->ev_copied));  // host buffers are reused
+  c->staged = false;
+  if (!c->d_choff && (rc = dalloc(c, &c->d_choff, (size_t)c->G + 1))) return rc;
+  rc = timed(c, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
+  if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_choff, &c->h_choff_cap, (uint64_t)c->G + 1))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  const uint64_t n = c->h_choff[c->G];
+  if (2 * n > c->d_chht_cap) {
+    dfree(c, c->d_chht);
+    c->d_chht = nullptr;
+    c->d_chht_cap = 0;
+    if ((rc = dalloc(c, &c->d_chht, 2 * n + 2 * (n >> 3)))) return rc;
+    c->d_chht_cap = 2 * n + 2 * (n >> 3);
+  }
+  rc = timed(c, "k_chain_pairs", 8.0 * (double)n + 8.0 * c->G, 0,
+             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, s); });
+  if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, c->V))) return rc;
+  if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, 2 * n))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev_ready, s));
+  HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_ready, 0));
+  if (c->V) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->dc.flags, c->V, hipMemcpyDeviceToHost, c->copy));
+  if (n) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, 2 * n * 4, hipMemcpyDeviceToHost, c->copy));
+  HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
+  c->staged = true;
+  c->staged_n = n;
+  return NEMO_OK;
+}
+
+int nemo_simplified_view(nemo_ctx *c, const uint8_t **flags, const uint64_t **chain_off, const uint32_t **chain_ht,
+                         uint64_t *n_chains) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (!c->staged) return fail(c, NEMO_ERR_STATE, "nothing staged: call nemo_stage_simplified");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventSynchronize(c->ev_copied));
+  if (flags) *flags = c->h_flags;
+  if (chain_off) *chain_off = c->h_choff;
+  if (chain_ht) *chain_ht = c->h_chht;
+  if (n_chains) *n_chains = c->staged_n;
   return NEMO_OK;
 }
 

@@ -48,6 +48,7 @@ void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t 
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s);
 void launch_pull_count(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
 void launch_pull_write(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
+void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
 

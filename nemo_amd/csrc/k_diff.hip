@@ -315,6 +315,21 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chain_gather(DevCorpus c, const 
   }
 }
 
+// Dense (head, tail) pairs of every graph's accepted chains, graph g's chain k
+// at off[g] + k: with the node flags this is the whole simplified graph
+// (preprocessing.go:249-340 materialises exactly head.preds -> c -> tail.succs).
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chain_pairs(DevCorpus c, const uint64_t *off, uint32_t *out) {
+  const uint32_t g = blockIdx.x;
+  const uint32_t n = c.nch[g];
+  const uint32_t *ch = c.chain + 5 * c.node_off[g];
+  uint2 *o = reinterpret_cast<uint2 *>(out) + off[g];
+  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) o[k] = make_uint2(ch[5 * k], ch[5 * k + 1]);
+}
+
+void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_pairs, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);
+}
+
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s) {
   hipLaunchKernelGGL(k_scan64, dim3(1), dim3(NEMO_BLOCK), 0, s, c.nch, off, c.G);
   if (out) hipLaunchKernelGGL(k_chain_gather, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);

@@ -77,6 +77,8 @@ def lib():
             "nemo_fetch_triggers": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
             "nemo_fetch_node_flags": ([vp, u32, u32, vp, u64], i32),
             "nemo_fetch_chains": ([vp, vp, u64, P(u64)], i32),
+            "nemo_stage_simplified": ([vp], i32),
+            "nemo_simplified_view": ([vp, P(vp), P(vp), P(vp), P(u64)], i32),
             "nemo_fetch_run_tables": ([vp, i32, vp, u64], i32),
             "nemo_pull_edges": ([vp, i32], i32),
             "nemo_reduce_interpret": ([vp, u32, u32, P(u32), vp, P(u32), vp, P(u32)], i32),
@@ -207,6 +209,30 @@ class Engine:
         out = np.zeros(max(n, 1), np.uint8)
         self._chk(self.L.nemo_fetch_node_flags(self.h, g_lo, g_hi, _p(out), n))
         return out[:n]
+
+    def stage_simplified(self) -> None:
+        """nemo_stage_simplified: async D2H of flags + chain (head, tail) pairs."""
+        self._chk(self.L.nemo_stage_simplified(self.h))
+
+    def simplified_view(self):
+        """Zero-copy views of the staged results: (flags[V] u8, chain_off[G+1] u64,
+        chain_ht[n, 2] u32), valid until the next stage_simplified()."""
+        vp = ctypes.c_void_p
+        f, o, h, n = vp(), vp(), vp(), ctypes.c_uint64()
+        self._chk(self.L.nemo_simplified_view(self.h, ctypes.byref(f), ctypes.byref(o), ctypes.byref(h),
+                                              ctypes.byref(n)))
+        c = self.corpus
+        V, G = int(c.node_off[-1]), c.n_graphs
+
+        def view(ptr, ctype, count, dtype):
+            if count == 0 or not ptr.value:
+                return np.zeros(0, dtype)
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctype)), shape=(count,))
+
+        flags = view(f, ctypes.c_uint8, V, np.uint8)
+        off = view(o, ctypes.c_uint64, G + 1, np.uint64)
+        ht = view(h, ctypes.c_uint32, 2 * n.value, np.uint32).reshape(-1, 2)
+        return flags, off, ht
 
     def chains(self) -> np.ndarray:
         n = ctypes.c_uint64()

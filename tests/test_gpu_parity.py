@@ -142,3 +142,28 @@ def test_large_graphs_global_paths(eng):
     corpus, _ = synth.generate(6, target_nodes=14000)
     assert max(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 8192
     _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+
+
+def test_staged_simplified_views(eng):
+    # nemo_stage_simplified: pinned async hand-over of flags + chain (head, tail)
+    # pairs, overlapping later kernels; restaging reuses the pinned buffers
+    from tools import synth
+    corpus, _ = synth.generate(30, target_nodes=2000)
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, skip_pulls=True)
+    eng.load(corpus)
+    for _ in range(2):
+        eng.rebuild()
+        eng.mark()
+        eng.simplify()
+        eng.stage_simplified()
+        eng.prototypes(s)  # launched while the copies are in flight
+        eng.diffprov(f, DIFF_PER_RUN)
+        flags, off, ht = eng.simplified_view()
+        assert np.array_equal(flags, orc.flags)
+        G = corpus.n_graphs
+        assert len(off) == G + 1 and int(off[-1]) == len(ht) == len(orc.chains)
+        g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
+        k = np.arange(len(ht)) - off[g].astype(np.int64)
+        got = np.stack([g, k, ht[:, 0], ht[:, 1]], 1)
+        assert np.array_equal(got, orc.chains[:, :4].astype(np.int64))
