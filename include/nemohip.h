@@ -117,7 +117,10 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
 /* Tuning / test knobs (-1 = default): "chains_lds_max" = largest chain
  * subgraph (nodes) the first @next-chain tier stages in LDS; larger graphs go
  * to the component tier, where "chains_comp_max" = largest component run in
- * LDS by one wave (larger ones take the workgroup-wide global-memory path). */
+ * LDS by one wave (larger ones take the workgroup-wide global-memory path);
+ * "build_lds_max" = largest graph (nodes) whose CSR + Kahn levels are built
+ * in LDS by k_build (also capped at 6144 nodes / 8192 edges); applies from the
+ * next nemo_load_corpus / nemo_rebuild.                                      */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);

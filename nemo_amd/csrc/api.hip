@@ -51,7 +51,7 @@ struct nemo_ctx {
   std::unordered_map<uint32_t, uint32_t> it2run;
   int32_t run0 = -1;
   bool has_rank = false;
-  uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu;
+  uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu, build_limit = 0xFFFFFFFFu;
 
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
@@ -294,6 +294,11 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->dc.hcap_limit = c->hcap_limit;
     return NEMO_OK;
   }
+  if (!strcmp(name, "build_lds_max")) {
+    c->build_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
+    c->dc.build_limit = c->build_limit;
+    return NEMO_OK;
+  }
   if (!strcmp(name, "chains_comp_max")) {
     c->comp_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.comp_limit = c->comp_limit;
@@ -333,7 +338,19 @@ static int check_graph_errors(nemo_ctx *c) {
 static int device_load(nemo_ctx *c) {
   int rc;
   HIPCHK(c, hipMemsetAsync(c->dc.err, 0, c->G * sizeof(uint32_t), c->stream));
-  const double V = (double)c->V, E = (double)c->E;
+  // graphs within k_build's LDS caps (k_load.hip BLD_V/BLD_E) vs the global tier
+  double Vb = 0, Eb = 0;
+  for (uint32_t g = 0; g < c->G; g++) {
+    const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+    if (v <= 6144 && e <= 8192 && v <= c->build_limit) {
+      Vb += (double)v;
+      Eb += (double)e;
+    }
+  }
+  const double V = (double)c->V - Vb, E = (double)c->E - Eb;
+  // k_build: read edges twice + words; write both CSRs, topo, levels
+  if ((rc = timed(c, "k_build", 20 * Eb + 32 * Vb, 2 * Eb, [&] { nemo::launch_build(c->dc, c->stream); })))
+    return rc;
   if ((rc = timed(c, "k_csr", 16 * E + 12 * V, E, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
   return NEMO_OK;
@@ -445,6 +462,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipMemsetAsync(d.prehold, 0, G * 4, s));
   d.G = c->G;
   d.hcap_limit = c->hcap_limit;
+  d.build_limit = c->build_limit;
   d.comp_limit = c->comp_limit;
   d.n_runs = c->n_runs;
   d.n_tables = c->T;

@@ -150,6 +150,7 @@ struct DevCorpus {
   uint32_t G, n_runs, n_tables, words, table_pre, table_post;
   uint32_t hcap_limit;                   // largest chain subgraph H* k_chains stages in LDS (test knob)
   uint32_t comp_limit;                   // largest H* component k_chains_big stages in LDS (test knob)
+  uint32_t build_limit;                  // largest graph k_build handles in LDS (test knob)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
   const uint32_t *esrc, *edst;
@@ -193,3 +194,19 @@ struct DevCorpus {
     return v;
   }
 };
+
+#ifdef NEMO_STAMPS
+// diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product build)
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && c.stamps) {                                                   \
+      unsigned long long t_;                                                              \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+      c.stamps[16 * (size_t)blockIdx.x + (k)] = t_;                                       \
+    }                                                                                     \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif

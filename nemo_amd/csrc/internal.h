@@ -37,6 +37,7 @@ struct TrigArgs {
   uint32_t *pre, *post, *async_rules;
 };
 
+void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
 void launch_topo(const DevCorpus &c, hipStream_t s);
 void launch_mark(const DevCorpus &c, hipStream_t s);

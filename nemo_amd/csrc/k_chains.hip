@@ -47,21 +47,6 @@ struct CompLDS {
   uint8_t flag[CM];   // 1 = rule, 2 = unseen
 };
 
-#ifdef NEMO_STAMPS
-// diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product build)
-#define STAMP(k)                                                                          \
-  do {                                                                                    \
-    if (threadIdx.x == 0 && c.stamps) {                                                   \
-      unsigned long long t_;                                                              \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
-      c.stamps[16 * (size_t)blockIdx.x + (k)] = t_;                                       \
-    }                                                                                     \
-  } while (0)
-#else
-#define STAMP(k) \
-  do {           \
-  } while (0)
-#endif
 
 #define CF_RULE 1u
 #define CF_UNSEEN 2u
