@@ -205,16 +205,17 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define HCAP 2048  // H* nodes staged in LDS
 #define ECAP 2048  // H* edges staged in LDS (each direction)
 #define NIL16 0xFFFFu
-#define UCAP 1024  // distinct prefix lengths (longest chain path + 2)
+#define UCAP 512   // distinct prefix lengths (longest chain path + 2)
 
 struct ChainsLDS {
   uint16_t crank[HCAP];  // rank of the node's ID among H* nodes
   int16_t up[HCAP], down[HCAP];
-  uint16_t nxt[HCAP], bp[HCAP], head[HCAP], tail[HCAP], po[HCAP];
+  uint16_t nxt[HCAP], bp[HCAP], po[HCAP];
   uint16_t ub[HCAP];
-  uint32_t uoff[UCAP], cur[UCAP];
+  uint32_t cur[UCAP];
+  uint16_t uoff[UCAP];
   uint16_t seg[HCAP + 1];
-  uint8_t isrule[HCAP];
+  uint32_t isrule[HCAP / 32];  // bitmap
   union {
     struct {
       uint16_t pcoff[HCAP + 1], par[ECAP];  // live until the prefix ranks are done
@@ -242,7 +243,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   const uint32_t tid = threadIdx.x;
   const uint32_t cap = min((uint32_t)HCAP, c.hcap_limit);
   STAMP(0);
+  for (uint32_t w = tid; w < HCAP / 32; w += NEMO_BLOCK) L.isrule[w] = 0;
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
+#define RULE(i) ((L.isrule[(i) >> 5] >> ((i) & 31)) & 1u)
   // ordered compaction of H* in Kahn order (chunks of 4 positions per thread);
   // pc[p] = #H* nodes before topo position p gives every level's segment
   uint32_t *pc = c.s_b + gv.n0 + g;
@@ -296,8 +299,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   // ones sort (rank, index) pairs with an LDS bitonic network.
   // graph-local node -> compact index (NONE outside H*): in LDS over the
   // not-yet-used up..ub arrays when the graph is small enough, else global
-  uint16_t *hmap = (uint16_t *)L.up;
-  const bool lmap = gv.V <= 8u * HCAP;
+  uint16_t *hmap = (uint16_t *)L.up;  // spans up, down, nxt, bp, po, ub
+  const bool lmap = gv.V <= 6u * HCAP;
   if (lmap) {
     for (uint32_t v = tid; v < gv.V; v += NEMO_BLOCK) hmap[v] = 0xFFFFu;
     __syncthreads();
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       hmap[v] = (uint16_t)i;
     else
       hidx[v] = i;
-    L.isrule[i] = is_rule(gv.word[v]) ? 1 : 0;
+    if (is_rule(gv.word[v])) atomicOr(&L.isrule[i >> 5], 1u << (i & 31));
   }
   if (gv.V <= 32768) {
     uint32_t *bm = (uint32_t *)L.u.kk;            // [1024] rank bitmap
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   for (uint32_t s = 0; s < ns; s++) {
     const uint32_t e = L.seg[s + 1];
     for (uint32_t i = L.seg[s] + tid; i < e; i += NEMO_BLOCK) {
-      int32_t d = L.isrule[i] ? 0 : -1;
+      int32_t d = RULE(i) ? 0 : -1;
       const uint32_t j1 = L.u.adj.pcoff[i + 1];
       for (uint32_t j = L.u.adj.pcoff[i]; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
       L.up[i] = (int16_t)d;
@@ -440,12 +443,11 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
           br = rw;
         }
       }
-      int32_t d = best >= 0 ? best + 1 : (L.isrule[i] ? 0 : -1);
-      if (L.isrule[i] && d < 0) d = 0;
+      int32_t d = best >= 0 ? best + 1 : (RULE(i) ? 0 : -1);
+      if (RULE(i) && d < 0) d = 0;
       if (d > 0 && best < 0) bc = NIL16;
       L.down[i] = (int16_t)d;
       L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
-      L.tail[i] = (uint16_t)(d > 0 ? L.tail[bc] : i);
       if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
     }
     __syncthreads();
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) atomicAdd(&L.cur[L.up[i]], 1u);
   __syncthreads();
   block_scan_inplace(L.cur, maxup + 2, s_lds);
-  for (uint32_t k = tid; k <= maxup + 1; k += NEMO_BLOCK) L.uoff[k] = L.cur[k];
+  for (uint32_t k = tid; k <= maxup + 1; k += NEMO_BLOCK) L.uoff[k] = (uint16_t)L.cur[k];
   __syncthreads();
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) L.ub[atomicAdd(&L.cur[L.up[i]], 1u)] = (uint16_t)i;
   __syncthreads();
@@ -491,7 +493,6 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
         }
       }
       L.bp[i] = (uint16_t)bpi;
-      L.head[i] = (uint16_t)(k == 0 ? i : L.head[bpi]);
       L.u.rk.bk[j - a] = ((k ? bpo : 0u) << 16) | L.crank[i];
     }
     __syncthreads();
@@ -510,13 +511,16 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
     const bool rep = L.up[i] == 0 || L.nxt[L.bp[i]] != i;
     if (!rep) continue;
+    uint32_t h = i, t = i;  // head: root of the bp chain; tail: end of the nxt chain
+    while (L.up[h] > 0) h = L.bp[h];
+    while (L.nxt[t] != NIL16) t = L.nxt[t];
     const uint32_t k = atomicAdd(&s_nch, 1u);
-    uint32_t *t = tmp + 5 * k;
-    t[0] = L.head[i];
-    t[1] = L.tail[i];
-    t[2] = (uint32_t)(L.up[i] + L.down[i]);
-    t[3] = L.crank[L.head[i]];
-    t[4] = i;
+    uint32_t *r = tmp + 5 * k;
+    r[0] = h;
+    r[1] = t;
+    r[2] = (uint32_t)(L.up[i] + L.down[i]);
+    r[3] = L.crank[h];
+    r[4] = i;
   }
   __threadfence_block();
   __syncthreads();
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   {
     uint32_t *S = (uint32_t *)L.u.kk;  // subtree size, then "first child position" of a parent
     uint32_t *A = S + HCAP;            // sizes of one level in po order -> exclusive scan
-    uint16_t *pre = L.head;            // head[] is dead once the records are written
+    uint16_t *pre = L.nxt;             // nxt[] is dead once the records are written
     for (uint32_t i = tid; i < n; i += NEMO_BLOCK) S[i] = 1;
     __syncthreads();
     for (uint32_t k = maxup; k >= 1; k--) {
@@ -614,6 +618,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     if (s_fail) c.err[g] = NEMO_ERR_INVALID;
   }
 #undef INH
+#undef RULE
 }
 
 __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
