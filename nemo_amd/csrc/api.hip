@@ -52,6 +52,7 @@ struct nemo_ctx {
   int32_t run0 = -1;
   bool has_rank = false;
   uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu, build_limit = 0xFFFFFFFFu;
+  uint32_t lds_limit = 0xFFFFFFFFu;  // test knob: largest V of the LDS graph tier (0 = off)
 
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
@@ -94,6 +95,8 @@ struct nemo_ctx {
   uint32_t *h_chht = nullptr;
   uint64_t h_flags_cap = 0, h_choff_cap = 0, h_chht_cap = 0;
 };
+
+static void set_lds_tier(nemo_ctx *c);
 
 static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
   char buf[512];
@@ -299,6 +302,11 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->dc.build_limit = c->build_limit;
     return NEMO_OK;
   }
+  if (!strcmp(name, "graph_lds_max")) {
+    c->lds_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
+    if (c->loaded) set_lds_tier(c);
+    return NEMO_OK;
+  }
   if (!strcmp(name, "chains_comp_max")) {
     c->comp_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.comp_limit = c->comp_limit;
@@ -315,6 +323,31 @@ int nemo_set_timing(nemo_ctx *c, int enable) {
 
 uint64_t nemo_num_nodes(const nemo_ctx *c) { return c ? c->V : 0; }
 uint64_t nemo_num_edges(const nemo_ctx *c) { return c ? c->E : 0; }
+
+// LDS graph tier caps (device.h): the largest graphs, smallest first, whose
+// staged form fits LDS_TIER_BUDGET, i.e. two workgroups per CU.
+#define LDS_TIER_BUDGET (78u * 1024u)
+static void set_lds_tier(nemo_ctx *c) {
+  std::vector<std::pair<uint32_t, uint32_t>> ve;
+  ve.reserve(c->G);
+  for (uint32_t g = 0; g < c->G; g++) {
+    const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+    if (v <= std::min<uint64_t>(16384, c->lds_limit) && e <= 65535) ve.push_back({(uint32_t)v, (uint32_t)e});
+  }
+  std::sort(ve.begin(), ve.end());
+  uint32_t cv = 0, ce = 0, emax = 0;
+  for (auto &x : ve) {
+    emax = std::max(emax, x.second);
+    const uint32_t l = std::min(x.first, 512u);
+    if (lds_tier_bytes(x.first, emax, l, c->W) > LDS_TIER_BUDGET) break;
+    cv = x.first;
+    ce = emax;
+  }
+  c->dc.lds_v = cv;
+  c->dc.lds_e = ce;
+  c->dc.lds_l = std::min(cv, 512u);
+  c->dc.lds_bytes = cv ? lds_tier_bytes(cv, ce, c->dc.lds_l, c->W) : 0;
+}
 
 static int check_graph_errors(nemo_ctx *c) {
   std::vector<uint32_t> err(c->G), created(c->G);
@@ -429,6 +462,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.err, G);
   A(d.created, G);
   A(d.prehold, G);
+  A(d.holdany, G);
   A(d.chain, 5 * V);
   A(d.chain_tmp, 5 * V);
   A(d.nch, G);
@@ -464,6 +498,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   d.hcap_limit = c->hcap_limit;
   d.build_limit = c->build_limit;
   d.comp_limit = c->comp_limit;
+  set_lds_tier(c);
   d.n_runs = c->n_runs;
   d.n_tables = c->T;
   d.words = c->W;

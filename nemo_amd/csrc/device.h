@@ -151,6 +151,8 @@ struct DevCorpus {
   uint32_t hcap_limit;                   // largest chain subgraph H* k_chains stages in LDS (test knob)
   uint32_t comp_limit;                   // largest H* component k_chains_big stages in LDS (test knob)
   uint32_t build_limit;                  // largest graph k_build handles in LDS (test knob)
+  uint32_t lds_v, lds_e, lds_l;          // LDS graph tier caps (V, E, Kahn levels); 0 = tier off
+  uint32_t lds_bytes;                    // dynamic LDS of the tier's kernels
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
   const uint32_t *esrc, *edst;
@@ -164,6 +166,7 @@ struct DevCorpus {
   uint32_t *err;                         // [G] NEMO_ERR_* of the graph (0 = fine)
   uint32_t *created;                     // [G] loadProv relationships-created
   uint32_t *prehold;                     // [G] #holding "pre" goals (pre graphs)
+  uint32_t *holdany;                     // [G] 1 iff a holding goal survives simplification
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
   uint32_t *chain_tmp;                   // [5*V]
   uint32_t *nch;                         // [G]
@@ -194,6 +197,139 @@ struct DevCorpus {
     return v;
   }
 };
+
+// ---- LDS graph tier ------------------------------------------------------------
+// A graph with V <= lds_v, E <= lds_e and nlev <= lds_l is staged into LDS as
+// u16 CSR rows (both directions), u16 Kahn order and level offsets, a u16 node
+// word (bit 15 rule, bit 14 @next rule, low 14 bits table) and two bytes of
+// node state; the kernel then walks it without touching HBM.  The host sizes
+// the caps from the corpus so that two workgroups fit a CU.  Graphs outside
+// the caps run the global-memory kernels.
+#define NW_RULE 0x8000u
+#define NW_NEXT 0x4000u
+#define NW_TABLE 0x3FFFu
+__host__ __device__ __forceinline__ uint32_t lds_align(uint32_t b) { return (b + 15u) & ~15u; }
+// accepted @next chains of a tier graph held in LDS (head + per-tail list link)
+__host__ __device__ __forceinline__ uint32_t lds_chain_cap(uint32_t v) { return v / 4u < 32766u ? v / 4u : 32766u; }
+__host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t e, uint32_t l, uint32_t words) {
+  return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + 2u * lds_align(2u * v) + lds_align(2u * (l + 1u)) +
+         2u * lds_align(v) + lds_align(8u * words) + 2u * lds_align(2u * lds_chain_cap(v));
+}
+
+__device__ __forceinline__ bool lds_fits(const DevCorpus &c, uint32_t V, uint32_t E, uint32_t nlev) {
+  return c.lds_bytes != 0u && V <= c.lds_v && E <= c.lds_e && nlev <= c.lds_l;
+}
+
+struct LdsGraph {
+  uint16_t *rp, *rc, *fp, *fc, *topo, *lv, *nw;
+  uint16_t *chd, *cnx;  // chain head, next chain with the same tail (0x7FFF ends)
+  uint8_t *a, *b;       // two bytes of per-node state
+  uint32_t *words;      // 2 * c.words u32 of table bitsets
+};
+
+// Carve the tier's dynamic LDS for a graph of V nodes / E edges / L levels.
+__device__ __forceinline__ LdsGraph lds_carve(void *base, uint32_t V, uint32_t E, uint32_t L, uint32_t words) {
+  uint8_t *p = (uint8_t *)base;
+  LdsGraph g;
+  g.chd = (uint16_t *)p;
+  p += lds_align(2u * lds_chain_cap(V));
+  g.cnx = (uint16_t *)p;
+  p += lds_align(2u * lds_chain_cap(V));
+  g.words = (uint32_t *)p;
+  p += lds_align(8u * words);
+  g.rp = (uint16_t *)p;
+  p += lds_align(2u * (V + 1u));
+  g.fp = (uint16_t *)p;
+  p += lds_align(2u * (V + 1u));
+  g.rc = (uint16_t *)p;
+  p += lds_align(2u * E);
+  g.fc = (uint16_t *)p;
+  p += lds_align(2u * E);
+  g.topo = (uint16_t *)p;
+  p += lds_align(2u * V);
+  g.nw = (uint16_t *)p;
+  p += lds_align(2u * V);
+  g.lv = (uint16_t *)p;
+  p += lds_align(2u * (L + 1u));
+  g.a = p;
+  p += lds_align(V);
+  g.b = p;
+  return g;
+}
+
+// Batched HBM -> LDS staging.  Every source is read in 16-B aligned chunks
+// (a chunk may start before the slice or end after it: slices live inside
+// page-granular allocations and the extra lanes are dropped), and each thread
+// keeps STAGE_DEPTH chunks in flight, so a whole ~5k-node graph arrives in a
+// handful of HBM round trips instead of one per loop iteration.
+enum StageKind : uint32_t { ST_U16 = 0, ST_U8 = 1, ST_WORD = 2 };
+struct StageDesc {
+  const void *src;
+  void *dst;
+  uint32_t n;     // elements
+  uint32_t kind;  // ST_U16: u32 -> u16; ST_U8: u8 -> u8; ST_WORD: node word -> NW_* u16
+};
+#define STAGE_DEPTH 8
+
+__device__ __forceinline__ uint16_t nw_of(uint32_t w) {
+  return (uint16_t)((is_rule(w) ? NW_RULE : 0u) | ((is_rule(w) && type_of(w) == NEMO_TYPE_NEXT) ? NW_NEXT : 0u) |
+                    (table_of(w) & NW_TABLE));
+}
+
+// Every descriptor index below is a compile-time constant after unrolling, so
+// the descriptors stay in registers (a dynamically indexed local array would
+// live in scratch memory).
+template <int ND, int BLOCK = NEMO_BLOCK>
+__device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
+  uint32_t first[ND + 1], skip[ND];
+  first[0] = 0;
+#pragma unroll
+  for (int i = 0; i < ND; i++) {
+    const uint32_t es = d[i].kind == ST_U8 ? 1u : 4u;
+    const uint32_t a = (uint32_t)((uintptr_t)d[i].src & 15u) / es;  // elements before the slice in its chunk
+    const uint32_t per = 16u / es;
+    skip[i] = a;
+    first[i + 1] = first[i] + (d[i].n ? (d[i].n + a + per - 1) / per : 0u);
+  }
+  const uint32_t total = first[ND];
+  for (uint32_t base = 0; base < total; base += STAGE_DEPTH * BLOCK) {
+    uint4 v[STAGE_DEPTH];
+#pragma unroll
+    for (int q = 0; q < STAGE_DEPTH; q++) {
+      const uint32_t k = base + q * BLOCK + threadIdx.x;
+      const uint8_t *p = nullptr;
+#pragma unroll
+      for (int i = 0; i < ND; i++)
+        if (k >= first[i] && k < first[i + 1])
+          p = (const uint8_t *)((uintptr_t)d[i].src & ~(uintptr_t)15) + 16u * (k - first[i]);
+      v[q] = p ? *(const uint4 *)p : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < STAGE_DEPTH; q++) {
+      const uint32_t k = base + q * BLOCK + threadIdx.x;
+      const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+      for (int i = 0; i < ND; i++) {
+        if (!(k >= first[i] && k < first[i + 1])) continue;
+        const int32_t n = (int32_t)d[i].n;
+        if (d[i].kind == ST_U8) {
+          const int32_t e0 = 16 * (int32_t)(k - first[i]) - (int32_t)skip[i];
+          uint8_t *o = (uint8_t *)d[i].dst;
+#pragma unroll
+          for (int b = 0; b < 16; b++)
+            if (e0 + b >= 0 && e0 + b < n) o[e0 + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        } else {
+          const int32_t e0 = 4 * (int32_t)(k - first[i]) - (int32_t)skip[i];
+          uint16_t *o = (uint16_t *)d[i].dst;
+          const bool word = d[i].kind == ST_WORD;
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (e0 + b >= 0 && e0 + b < n) o[e0 + b] = word ? nw_of(w[b]) : (uint16_t)w[b];
+        }
+      }
+    }
+  }
+}
 
 #ifdef NEMO_STAMPS
 // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product build)

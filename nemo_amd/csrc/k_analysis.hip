@@ -64,6 +64,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c) {
 // a next rule with a next-rule grandparent or grandchild, lies on an @next
 // chain and is DETACH DELETEd; heads/tails are the chain ends.
 __global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c) {
+  __shared__ uint32_t s_hold;
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
@@ -98,12 +99,26 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c) {
   }
 #undef ISNEXT
   __syncthreads();
+  bool hold = false;
   for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
     if (is_rule(gv.word[x])) continue;
     uint8_t fl = f[x];
     if ((fl & FT_NP) && (fl & FT_NC)) fl |= NEMO_F_DELETED;
     f[x] = fl & (uint8_t)~(FT_NP | FT_NC);
+    hold |= (fl & (NEMO_F_HOLDS | NEMO_F_DELETED)) == NEMO_F_HOLDS;
   }
+  // extractProtos' gate (prototype.go:13): a holding goal of the simplified graph
+  if (threadIdx.x == 0) s_hold = 0;
+  __syncthreads();
+  if (__any(hold) && lane_id() == 0) s_hold = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) c.holdany[g] = s_hold;
+}
+
+// k_proto_lds takes the graphs within the LDS tier (and its chain cap)
+#define LCH_END 0x7FFFu
+__device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphView &gv) {
+  return lds_fits(c, gv.V, gv.E, gv.nlev) && c.nch[gv.g] <= lds_chain_cap(gv.V);
 }
 
 // extractProtos' per-run query (prototype.go:11-24) and missingFrom's table
@@ -118,6 +133,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   const uint32_t g = 2 * r + 1;
   if (c.err[g] || c.err[g - 1]) return;
   const GraphView gv = c.view(g);
+  if (proto_lds_fits(c, gv)) return;  // k_proto_lds's graph
   const GraphView pre = c.view(g - 1);
   const uint8_t *f = gv.flags;
   uint8_t *sb = c.sb + gv.n0;
@@ -246,6 +262,174 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   if (threadIdx.x == 0) c.gate[r] = gate ? 1 : 0;
 }
 
+// k_proto's LDS tier: the same phases over the post graph staged in LDS
+// (device.h LdsGraph).  Node byte a = flags, byte b = SB_* bits with bit 7 =
+// rule.  Tables are added in coalesced passes over the node words, so the
+// level sweep never leaves LDS; chain lists stay in HBM (read at tails only).
+#define PROTO_BLOCK 512
+__global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  const uint32_t r = blockIdx.x;
+  const uint32_t g = 2 * r + 1;
+  if (c.err[g] || c.err[g - 1]) return;
+  const GraphView gv = c.view(g);
+  if (!proto_lds_fits(c, gv)) return;
+  const uint32_t V = gv.V, W = c.words, tid = threadIdx.x;
+  STAMP(0);
+  LdsGraph L = lds_carve(dyn, V, gv.E, gv.nlev, W);
+  uint32_t *s_s = L.words, *s_t = L.words + W;
+  const uint32_t *ch = c.chain + 5 * gv.n0;
+  const uint32_t *tf = c.tail_first + gv.n0, *nt = c.chain_nt + gv.n0;
+  const uint32_t nch = c.nch[g];
+  for (uint32_t i = tid; i < 2 * W; i += PROTO_BLOCK) L.words[i] = 0;
+  {
+    const StageDesc d[9] = {{gv.rp, L.rp, V + 1, ST_U16},  {gv.fp, L.fp, V + 1, ST_U16},
+                            {gv.rc, L.rc, gv.E, ST_U16},   {gv.fc, L.fc, gv.E, ST_U16},
+                            {gv.topo, L.topo, V, ST_U16},  {gv.lvl, L.lv, gv.nlev + 1, ST_U16},
+                            {gv.word, L.nw, V, ST_WORD},   {gv.flags, L.a, V, ST_U8},
+                            {nt, L.cnx, nch, ST_U16}};
+    stage_lds<9, PROTO_BLOCK>(d);
+  }
+  __syncthreads();
+  STAMP(1);
+  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
+    L.chd[k] = (uint16_t)ch[5 * k];
+    const uint32_t nx = L.cnx[k];
+    L.cnx[k] = (uint16_t)(nx < nch ? nx : LCH_END);
+  }
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) L.b[x] = 0;
+  // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
+  const bool gt = c.holdany[g - 1] != 0;
+  __syncthreads();
+  // a tail's node word carries the first chain of its list (tails are read only through the list)
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK)
+    if (L.a[x] & NEMO_F_TAIL) {
+      const uint32_t k = tf[x];
+      L.nw[x] = (uint16_t)(NW_RULE | (k == NEMO_NONE ? LCH_END : k));
+    }
+  __syncthreads();
+  STAMP(2);
+  const uint8_t *f = L.a;
+  uint8_t *sb = L.b;
+#define LRULE(v) ((L.nw[v] & NW_RULE) != 0)
+#define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
+#define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+#define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
+#define TAIL_ANY(p, bit, out)                                                                  \
+  for (uint32_t k_ = L.nw[p] & LCH_END, n_ = 0; k_ < nch && n_ < nch && !(out); k_ = L.cnx[k_], n_++) \
+    if (sb[L.chd[k_]] & (bit)) out = true;
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (LRULE(x)) {
+      if (REG(x) || (f[x] & NEMO_F_HEAD)) ADD(s_t, L.nw[x] & NW_TABLE);
+    } else if (!DEL(x)) {
+      bool root = true, hasrc = false;
+      for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) {
+        const uint32_t p = L.rc[j];
+        if (REG(p) || (f[p] & NEMO_F_TAIL)) root = false;
+      }
+      for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
+        const uint32_t q = L.fc[j];
+        if (REG(q) || (f[q] & NEMO_F_HEAD)) hasrc = true;
+      }
+      sb[x] = (root ? SB_ROOT : 0) | (hasrc ? SB_HASRC : 0);
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  // R1: rule children of roots (regular rules, and collapsed rules via their head)
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (!LRULE(x) || !(REG(x) || (f[x] & NEMO_F_HEAD))) continue;
+    bool r1 = false;
+    for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) {
+      const uint32_t p = L.rc[j];
+      if (!DEL(p) && (sb[p] & SB_ROOT)) r1 = true;
+    }
+    if (!r1) continue;
+    sb[x] |= SB_R1;
+    if (REG(x)) {
+      for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
+        const uint32_t q = L.fc[j];
+        if (!DEL(q) && (sb[q] & SB_HASRC)) {
+          ADD(s_s, L.nw[x] & NW_TABLE);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(4);
+  // G2: goal children of R1 rules; collapsed R1 rules that have a goal child with a rule child
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (LRULE(x) || DEL(x)) continue;
+    bool g2 = false;
+    for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !g2; j++) {
+      const uint32_t p = L.rc[j];
+      if (REG(p)) {
+        g2 = (sb[p] & SB_R1) != 0;
+      } else if (f[p] & NEMO_F_TAIL) {
+        TAIL_ANY(p, SB_R1, g2);
+      }
+    }
+    if (g2) sb[x] |= SB_G2;
+  }
+  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
+    const uint32_t h = L.chd[k];
+    if (!(sb[h] & SB_R1)) continue;
+    const uint32_t t = ch[5 * k + 1];
+    for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) {
+      const uint32_t q = L.fc[j];
+      if (!DEL(q) && (sb[q] & SB_HASRC)) {
+        ADD(s_s, L.nw[h] & NW_TABLE);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(5);
+  // rules reachable from G2 (forward level sweep over graph'), all in LDS
+  for (uint32_t l = 0; l < gv.nlev; l++) {
+    const uint32_t e = L.lv[l + 1];
+    for (uint32_t i = L.lv[l] + tid; i < e; i += PROTO_BLOCK) {
+      const uint32_t x = L.topo[i];
+      bool rch = false;
+      if (!LRULE(x)) {
+        if (DEL(x)) continue;
+        for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !rch; j++) {
+          const uint32_t p = L.rc[j];
+          if (REG(p)) {
+            rch = (sb[p] & SB_RCH) != 0;
+          } else if (f[p] & NEMO_F_TAIL) {
+            TAIL_ANY(p, SB_RCH, rch);
+          }
+        }
+      } else if (REG(x) || (f[x] & NEMO_F_HEAD)) {
+        for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !rch; j++) {
+          const uint32_t p = L.rc[j];
+          if (!DEL(p) && (sb[p] & (SB_G2 | SB_RCH))) rch = true;
+        }
+      }
+      if (rch) sb[x] |= SB_RCH;
+    }
+    __syncthreads();
+  }
+  STAMP(6);
+  // tables of the reached rules
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK)
+    if (LRULE(x) && !(f[x] & NEMO_F_TAIL) && (sb[x] & SB_RCH)) ADD(s_s, L.nw[x] & NW_TABLE);
+#undef TAIL_ANY
+#undef LRULE
+#undef DEL
+#undef REG
+#undef ADD
+  __syncthreads();
+  for (uint32_t i = tid; i < W; i += PROTO_BLOCK) {
+    c.proto_bits[(size_t)r * W + i] = gt ? s_s[i] : 0u;
+    c.graph_tables[(size_t)r * W + i] = s_t[i];
+  }
+  if (tid == 0) c.gate[r] = gt ? 1 : 0;
+  STAMP(7);
+}
+
 // Cross-run reduction vector (nemo_reduce_len): per-table counts over owned
 // success runs with a non-empty list, the first success run's list, achvdCond
 // (prototype.go:29-130) and the holding-"pre"-goal count (extensions.go:25-49).
@@ -299,6 +483,10 @@ void launch_simplify(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_proto(const DevCorpus &c, hipStream_t s) {
+  if (c.lds_bytes) {
+    hipFuncSetAttribute((const void *)k_proto_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
+    hipLaunchKernelGGL(k_proto_lds, dim3(c.n_runs), dim3(PROTO_BLOCK), c.lds_bytes, s, c);
+  }
   hipLaunchKernelGGL(k_proto, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,

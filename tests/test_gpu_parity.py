@@ -207,3 +207,15 @@ def test_build_tiers_identical_device_arrays(eng):
         for l0, l1 in zip(off[:-1], off[1:]):
             assert sorted(a[n0 + l0:n0 + l1]) == sorted(b[n0 + l0:n0 + l1])
         assert int(off[-1]) == n1 - n0
+
+
+@pytest.mark.parametrize("lds_max", [0, 1500, 2600])
+def test_graph_lds_tier(eng, lds_max):
+    # kernels' LDS graph tier (graphs staged as u16 CSR) vs their global tier, and mixtures
+    from tools import synth
+    corpus, _ = synth.generate(30, target_nodes=2500)
+    eng.set_option("graph_lds_max", lds_max)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+    finally:
+        eng.set_option("graph_lds_max", -1)
