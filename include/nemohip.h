@@ -230,7 +230,7 @@ int nemo_fetch_run_tables(nemo_ctx *ctx, int which, uint32_t *out, uint64_t cap)
  * 0/1) or the diff entry (which 2).  Collapsed rule k of graph g is reported
  * as node index V_g + k.                                                   */
 int nemo_pull_edges(nemo_ctx *ctx, int which);
-uint64_t nemo_pulled_count(const nemo_ctx *ctx, uint32_t slot);
+uint64_t nemo_pulled_count(nemo_ctx *ctx, uint32_t slot);
 int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap,
                       uint64_t *n_out);
 

@@ -67,12 +67,21 @@ struct nemo_ctx {
   int32_t *d_ddepth = nullptr;
   uint64_t miss_cap = 0;
 
-  // pulls
+  // pulls: per-slot (offset, count) and the region cursor come back to pinned
+  // memory asynchronously; the first fetch waits for them
   int pull_which = -1;
   uint32_t pull_slots = 0, pull_slot_cap = 0;
   uint32_t *d_pcnt = nullptr, *d_psrc = nullptr, *d_pdst = nullptr;
   uint64_t *d_poff = nullptr, pull_cap = 0;
-  std::vector<uint64_t> h_poff;
+  unsigned long long *d_pcur = nullptr;
+  uint32_t *h_pcnt = nullptr;
+  uint64_t *h_poff = nullptr;
+  unsigned long long *h_pcur = nullptr;
+  uint32_t h_pslot_cap = 0;
+  hipEvent_t ev_pull = nullptr;
+  bool pull_synced = true;
+  uint64_t pull_hint[3] = {0, 0, 0};
+  nemo::PullArgs pull_args{};
 
   // triggers
   bool trig_done = false;
@@ -245,6 +254,9 @@ static void release_corpus(nemo_ctx *c) {
   c->miss_cap = 0;
   c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
   c->d_poff = nullptr;
+  c->d_pcur = nullptr;
+  c->pull_synced = true;
+  c->pull_hint[0] = c->pull_hint[1] = c->pull_hint[2] = 0;
   c->pull_cap = 0;
   c->pull_slot_cap = 0;
   c->pull_which = -1;
@@ -278,6 +290,10 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->h_flags) hipHostFree(c->h_flags);
   if (c->h_choff) hipHostFree(c->h_choff);
   if (c->h_chht) hipHostFree(c->h_chht);
+  if (c->h_pcnt) hipHostFree(c->h_pcnt);
+  if (c->h_poff) hipHostFree(c->h_poff);
+  if (c->h_pcur) hipHostFree(c->h_pcur);
+  if (c->ev_pull) hipEventDestroy(c->ev_pull);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -958,74 +974,134 @@ int nemo_simplified_view(nemo_ctx *c, const uint8_t **flags, const uint64_t **ch
   return NEMO_OK;
 }
 
+static int pull_launch(nemo_ctx *c) {
+  nemo::PullArgs &a = c->pull_args;
+  a.src = c->d_psrc;
+  a.dst = c->d_pdst;
+  a.cap = c->pull_cap;
+  const uint32_t slots = c->pull_slots;
+  hipStream_t s = c->stream;
+  double V = (double)c->V, E = (double)c->E;
+  if (a.which == 2) {
+    V = (double)slots * (double)a.mask_stride;
+    E = (double)slots * (double)(c->edge_off[a.g0 + 1] - c->edge_off[a.g0]);
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_pcur, 0, sizeof(unsigned long long), s));
+  // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
+  int rc = timed(c, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_poff, c->d_poff, slots * 8ull, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(c->h_pcnt, c->d_pcnt, slots * 4ull, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(c->h_pcur, c->d_pcur, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipEventRecord(c->ev_pull, s));
+  c->pull_synced = false;
+  return NEMO_OK;
+}
+
+static int pull_grow(nemo_ctx *c, uint64_t total) {
+  if (total <= c->pull_cap) return NEMO_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(c, c->d_psrc);
+  dfree(c, c->d_pdst);
+  c->d_psrc = c->d_pdst = nullptr;
+  c->pull_cap = 0;
+  int rc;
+  if ((rc = dalloc(c, &c->d_psrc, total))) return rc;
+  if ((rc = dalloc(c, &c->d_pdst, total))) return rc;
+  c->pull_cap = total;
+  return NEMO_OK;
+}
+
+// Wait for the last pull's slot table; re-run it once if its regions overran the capacity.
+static int pull_sync(nemo_ctx *c) {
+  if (c->pull_synced) return NEMO_OK;
+  HIPCHK(c, hipEventSynchronize(c->ev_pull));
+  const uint64_t total = *c->h_pcur;
+  if (total > c->pull_cap) {
+    int rc = pull_grow(c, total);
+    if (!rc) rc = pull_launch(c);
+    if (rc) return rc;
+    HIPCHK(c, hipEventSynchronize(c->ev_pull));
+  }
+  c->pull_hint[c->pull_which] = total;
+  c->pull_synced = true;
+  return NEMO_OK;
+}
+
 int nemo_pull_edges(nemo_ctx *c, int which) {
   if (!c || which < 0 || which > 2) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if (!c->pull_synced) HIPCHK(c, hipEventSynchronize(c->ev_pull));  // pinned slot table still in flight
+  c->pull_synced = true;
   const uint32_t slots = which == 2 ? c->n_entries : c->G;
+  if (!c->ev_pull) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pull, hipEventDisableTiming));
+  if (!c->h_pcur) HIPCHK(c, hipHostMalloc((void **)&c->h_pcur, sizeof(unsigned long long)));
+  if (!c->d_pcur && (rc = dalloc(c, &c->d_pcur, 1))) return rc;
   if (slots + 1 > c->pull_slot_cap) {
     dfree(c, c->d_pcnt);
     dfree(c, c->d_poff);
+    c->d_pcnt = nullptr;
+    c->d_poff = nullptr;
     if ((rc = dalloc(c, &c->d_pcnt, (size_t)slots + 1))) return rc;
-    if ((rc = dalloc(c, &c->d_poff, (size_t)slots + 2))) return rc;
+    if ((rc = dalloc(c, &c->d_poff, (size_t)slots + 1))) return rc;
     c->pull_slot_cap = slots + 1;
+  }
+  if (slots + 1 > c->h_pslot_cap) {
+    if (c->h_pcnt) hipHostFree(c->h_pcnt);
+    if (c->h_poff) hipHostFree(c->h_poff);
+    c->h_pcnt = nullptr;
+    c->h_poff = nullptr;
+    c->h_pslot_cap = 0;
+    HIPCHK(c, hipHostMalloc((void **)&c->h_pcnt, (slots + 1) * 4ull));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_poff, (slots + 1) * 8ull));
+    c->h_pslot_cap = slots + 1;
   }
   c->pull_which = which;
   c->pull_slots = slots;
-  c->h_poff.assign(slots + 1, 0);
   if (slots == 0) return NEMO_OK;
   nemo::PullArgs a{};
   a.which = (uint32_t)which;
   const uint32_t g0 = c->run0 >= 0 ? 2 * c->run0 + 1 : 0;
   a.g0 = g0;
+  uint64_t cap;
   if (which == 2) {
     a.mask = c->d_dmask;
     a.mask_stride = c->node_off[g0 + 1] - c->node_off[g0];
+    cap = (uint64_t)slots * (c->edge_off[g0 + 1] - c->edge_off[g0]);  // D is an induced subgraph of g0
+  } else if (which == 0) {
+    cap = c->E;  // every edge
+  } else {
+    // kept edges (<= E) + collapsed edges; a pull past the estimate re-runs on fetch
+    cap = std::max<uint64_t>(2 * c->E + 1024, c->pull_hint[1] + c->pull_hint[1] / 4);
   }
   a.cnt = c->d_pcnt;
   a.off = c->d_poff;
-  hipStream_t s = c->stream;
-  double V = (double)c->V, E = (double)c->E;
-  if (which == 2) {
-    V = (double)slots * (double)a.mask_stride;
-    E = (double)slots * (double)(c->edge_off[g0 + 1] - c->edge_off[g0]);
-  }
-  rc = timed(c, "k_pull_count", 4 * E + 13 * V, E, [&] { nemo::launch_pull_count(c->dc, a, slots, s); });
-  if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_poff.data(), c->d_poff, (slots + 1) * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  const uint64_t total = c->h_poff[slots];
-  if (total > c->pull_cap) {
-    dfree(c, c->d_psrc);
-    dfree(c, c->d_pdst);
-    c->d_psrc = c->d_pdst = nullptr;
-    if ((rc = dalloc(c, &c->d_psrc, total))) return rc;
-    if ((rc = dalloc(c, &c->d_pdst, total))) return rc;
-    c->pull_cap = total;
-  }
-  a.src = c->d_psrc;
-  a.dst = c->d_pdst;
-  rc = timed(c, "k_pull_write", 4 * E + 13 * V + 8.0 * (double)total, E,
-             [&] { nemo::launch_pull_write(c->dc, a, slots, s); });
-  return rc;
+  a.cursor = c->d_pcur;
+  c->pull_args = a;
+  if ((rc = pull_grow(c, std::max<uint64_t>(cap, 1)))) return rc;
+  return pull_launch(c);
 }
 
-uint64_t nemo_pulled_count(const nemo_ctx *c, uint32_t slot) {
+uint64_t nemo_pulled_count(nemo_ctx *c, uint32_t slot) {
   if (!c || c->pull_which < 0 || slot >= c->pull_slots) return 0;
-  return c->h_poff[slot + 1] - c->h_poff[slot];
+  if (pull_sync(c)) return 0;
+  return c->h_pcnt[slot];
 }
 
 int nemo_fetch_pulled(nemo_ctx *c, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap, uint64_t *n_out) {
   if (!c) return NEMO_ERR_INVALID;
   if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
   if (slot >= c->pull_slots) return fail(c, NEMO_ERR_INVALID, "slot %u out of range", slot);
-  const uint64_t a = c->h_poff[slot], n = c->h_poff[slot + 1] - a;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = pull_sync(c);
+  if (rc) return rc;
+  const uint64_t a = c->h_poff[slot], n = c->h_pcnt[slot];
   if (n_out) *n_out = n;
   if (!src && !dst) return NEMO_OK;
   if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  HIPCHK(c, hipSetDevice(c->device));
   if (n) {
     if (src) HIPCHK(c, hipMemcpyAsync(src, c->d_psrc + a, n * 4, hipMemcpyDeviceToHost, c->stream));
     if (dst) HIPCHK(c, hipMemcpyAsync(dst, c->d_pdst + a, n * 4, hipMemcpyDeviceToHost, c->stream));

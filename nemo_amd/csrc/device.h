@@ -73,7 +73,8 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
 }
 
 // In-place exclusive scan of a[0..n) by one workgroup; returns the total.
-__device__ __forceinline__ uint32_t block_scan_inplace(uint32_t *a, uint32_t n, uint32_t *lds) {
+template <typename T>
+__device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_t *lds) {
   uint32_t carry = 0;
   for (uint32_t base = 0; base < n; base += NEMO_BLOCK * 4) {
     const uint32_t i0 = base + threadIdx.x * 4;
@@ -87,7 +88,7 @@ __device__ __forceinline__ uint32_t block_scan_inplace(uint32_t *a, uint32_t n, 
     uint32_t ex = block_exscan(s, &tot, lds) + carry;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      if (i0 + k < n) a[i0 + k] = ex;
+      if (i0 + k < n) a[i0 + k] = (T)ex;
       ex += x[k];
     }
     carry += tot;

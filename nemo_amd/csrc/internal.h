@@ -26,8 +26,10 @@ struct PullArgs {
   uint32_t g0;              // graph of which == 2
   const uint8_t *mask;      // which == 2: D masks of the entries
   uint64_t mask_stride;     // bytes between two entries' masks
-  uint32_t *cnt;            // [slots]
-  uint64_t *off;            // [slots + 1]
+  uint32_t *cnt;            // [slots] edges of the slot
+  uint64_t *off;            // [slots] first edge of the slot in src/dst
+  unsigned long long *cursor;  // region allocator (zeroed before the launch)
+  uint64_t cap;             // capacity of src/dst
   uint32_t *src, *dst;      // output
 };
 
@@ -47,8 +49,7 @@ void launch_proto(const DevCorpus &c, hipStream_t s);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s);
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s);
-void launch_pull_count(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
-void launch_pull_write(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
+void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
 void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);

@@ -206,6 +206,8 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define ECAP 2048  // H* edges staged in LDS (each direction)
 #define NIL16 0xFFFFu
 #define UCAP 512   // distinct prefix lengths (longest chain path + 2)
+#define CF_ROWS 12  // topo positions per thread per compaction round (fast front)
+#define CF_EPT 32   // input edges per thread per adjacency round (fast front)
 
 struct ChainsLDS {
   uint16_t crank[HCAP];  // rank of the node's ID among H* nodes
@@ -216,10 +218,10 @@ struct ChainsLDS {
   uint16_t uoff[UCAP];
   uint16_t seg[HCAP + 1];
   uint32_t isrule[HCAP / 32];  // bitmap
-  union {
+  union __align__(16) {
     struct {
-      uint16_t pcoff[HCAP + 1], par[ECAP];  // live until the prefix ranks are done
-      uint16_t ccoff[HCAP + 1], child[ECAP];
+      uint16_t pcoff[HCAP + 2], par[ECAP];  // live until the prefix ranks are done
+      uint16_t ccoff[HCAP + 2], child[ECAP];  // (+2: ccoff 4-byte aligned for packed u16 atomics)
     } adj;
     struct {
       uint16_t pad[HCAP + 2 + ECAP];       // keeps bk 4-byte aligned, past par[]
@@ -233,6 +235,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __shared__ ChainsLDS L;
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_nch, s_maxup, s_fail;
+  __shared__ uint32_t s_wc[CF_ROWS * NEMO_WAVES];
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
@@ -246,10 +249,185 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   for (uint32_t w = tid; w < HCAP / 32; w += NEMO_BLOCK) L.isrule[w] = 0;
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
 #define RULE(i) ((L.isrule[(i) >> 5] >> ((i) & 31)) & 1u)
+  const uint32_t ns = gv.nlev;
+  uint32_t n = 0;
+  if (gv.V <= 6u * HCAP && ns + 1 < UCAP) {
+    // Fast front (graphs whose node map fits LDS).  Every HBM access of the
+    // compaction is issued in two rounds per CF_ROWS x 256 topo positions (the
+    // Kahn order, then the flag/word/rank gathers); positions are compacted
+    // in (row, wave, lane) order = topo order with ballots and per-row wave
+    // counts; each H* node's level goes into a histogram whose scan is the
+    // level segmentation; ranks via the rank bitmap; the H* adjacency comes
+    // from the coalesced input edge list with packed-u16 LDS counters.
+    uint32_t *bm = (uint32_t *)L.u.kk;  // [1024] rank bitmap
+    uint32_t *pre = bm + 1024;          // [1025] prefix popcounts
+    uint16_t *lvs = L.uoff;             // level starts (topo positions)
+    uint32_t *hist = L.cur;             // H* nodes per level -> segment starts
+    uint16_t *hmap = (uint16_t *)L.up;  // graph-local node -> compact index (spans up..ub)
+    const uint32_t nw = (gv.V + 31) >> 5;
+    const uint32_t wave = tid >> 6, lane = lane_id();
+    for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) bm[w] = 0;
+    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) {
+      hist[l] = 0;
+      lvs[l] = (uint16_t)gv.lvl[l];
+    }
+    for (uint32_t v = tid; v < gv.V; v += NEMO_BLOCK) hmap[v] = 0xFFFFu;
+    if (tid == 0) {
+      s_nch = 0;
+      s_maxup = 0;
+      s_fail = 0;
+    }
+    __syncthreads();
+    for (uint32_t sbase = 0; sbase < gv.V; sbase += CF_ROWS * NEMO_BLOCK) {
+      uint32_t v[CF_ROWS], wd[CF_ROWS], r[CF_ROWS];
+      uint8_t fl[CF_ROWS];
+#pragma unroll
+      for (int q = 0; q < CF_ROWS; q++) {
+        const uint32_t p = sbase + q * NEMO_BLOCK + tid;
+        v[q] = p < gv.V ? gv.topo[p] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < CF_ROWS; q++) {
+        const bool in = sbase + q * NEMO_BLOCK + tid < gv.V;
+        fl[q] = in ? f[v[q]] : (uint8_t)0;
+        wd[q] = in ? gv.word[v[q]] : 0u;
+        r[q] = in ? gv.rank_of(v[q]) : 0u;
+      }
+      uint32_t hm = 0;
+#pragma unroll
+      for (int q = 0; q < CF_ROWS; q++) {
+        hm |= ((fl[q] & NEMO_F_DELETED) ? 1u : 0u) << q;
+        const uint64_t b = __ballot((hm >> q) & 1u);
+        if (lane == 0) s_wc[q * NEMO_WAVES + wave] = (uint32_t)__popcll(b);
+      }
+      __syncthreads();
+      uint32_t run = n;
+#pragma unroll
+      for (int q = 0; q < CF_ROWS; q++) {
+        uint32_t before = 0, row = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < NEMO_WAVES; w2++) {
+          const uint32_t x = s_wc[q * NEMO_WAVES + w2];
+          row += x;
+          before += w2 < (int)wave ? x : 0u;
+        }
+        const bool h = (hm >> q) & 1u;
+        const uint64_t b = __ballot(h);
+        if (h) {
+          const uint32_t i = run + before + mbcnt(b);
+          if (i < cap) {
+            const uint32_t p = sbase + q * NEMO_BLOCK + tid;
+            hs[i] = v[q];
+            hmap[v[q]] = (uint16_t)i;
+            if (is_rule(wd[q])) atomicOr(&L.isrule[i >> 5], 1u << (i & 31));
+            atomicOr(&bm[r[q] >> 5], 1u << (r[q] & 31));
+            L.crank[i] = (uint16_t)r[q];  // the ID rank until the prefix popcounts exist
+            uint32_t lo = 0, hi = ns;     // level: lvs[lo] <= p < lvs[lo + 1]
+            while (lo + 1 < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (lvs[mid] <= p) lo = mid;
+              else hi = mid;
+            }
+            atomicAdd(&hist[lo], 1u);
+          }
+        }
+        run += row;
+      }
+      n = run;
+      __syncthreads();  // s_wc is reused
+    }
+    if (n == 0) {
+      if (tid == 0) c.nch[g] = 0;
+      return;
+    }
+    if (n > cap) {  // too large for the LDS tier: k_chains_big takes the graph
+      if (tid == 0) c.nch[g] = NEMO_NONE;
+      return;
+    }
+    __threadfence_block();
+    STAMP(1);
+    block_scan_inplace(hist, ns + 1, s_lds);
+    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) L.seg[l] = (uint16_t)hist[l];
+    for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) pre[w] = __popc(bm[w]);
+    __syncthreads();
+    block_scan_inplace(pre, nw, s_lds);
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+      const uint32_t rr = L.crank[i];
+      L.crank[i] = (uint16_t)(pre[rr >> 5] + __popc(bm[rr >> 5] & ((1u << (rr & 31)) - 1u)));
+    }
+    __syncthreads();
+    STAMP(2);
+    // H* adjacency from the edge list: count, scan, scatter (row order is
+    // irrelevant below: every consumer takes a max/min over the row)
+    uint32_t *cc32 = (uint32_t *)L.u.adj.ccoff, *pc32 = (uint32_t *)L.u.adj.pcoff;
+    for (uint32_t w = tid; w < (HCAP + 2) / 2; w += NEMO_BLOCK) {
+      cc32[w] = 0;
+      pc32[w] = 0;
+    }
+    __syncthreads();
+    const uint32_t *es = c.esrc + gv.e0, *ed = c.edst + gv.e0;
+    for (int pass = 0; pass < 2; pass++) {
+      for (uint32_t ebase = 0; ebase < gv.E; ebase += CF_EPT * NEMO_BLOCK) {
+        uint32_t sd[CF_EPT];
+#pragma unroll
+        for (int q = 0; q < CF_EPT; q++) {
+          const uint32_t e = ebase + q * NEMO_BLOCK + tid;
+          sd[q] = e < gv.E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int q = 0; q < CF_EPT; q++) {
+          if (sd[q] == 0xFFFFFFFFu) continue;
+          const uint32_t a = hmap[sd[q] >> 16], b = hmap[sd[q] & 0xFFFFu];
+          if (a == 0xFFFFu || b == 0xFFFFu) continue;
+          const uint32_t sa = 16u * (a & 1u), sb = 16u * (b & 1u);
+          if (pass == 0) {
+            atomicAdd(&cc32[a >> 1], 1u << sa);
+            atomicAdd(&pc32[b >> 1], 1u << sb);
+          } else {
+            L.u.adj.child[(atomicAdd(&cc32[a >> 1], 1u << sa) >> sa) & 0xFFFFu] = (uint16_t)b;
+            L.u.adj.par[(atomicAdd(&pc32[b >> 1], 1u << sb) >> sb) & 0xFFFFu] = (uint16_t)a;
+          }
+        }
+      }
+      __syncthreads();
+      if (pass == 0) {
+        const uint32_t tc = block_scan_inplace(L.u.adj.ccoff, n + 1, s_lds);
+        const uint32_t tp = block_scan_inplace(L.u.adj.pcoff, n + 1, s_lds);
+        if (tc > ECAP || tp > ECAP) {
+          if (tid == 0) c.nch[g] = NEMO_NONE;
+          return;
+        }
+      }
+    }
+    // the cursors now hold row ends: shift them into row starts
+    {
+      uint32_t ce[(HCAP + NEMO_BLOCK - 1) / NEMO_BLOCK], pe[(HCAP + NEMO_BLOCK - 1) / NEMO_BLOCK];
+#pragma unroll
+      for (int q = 0; q < (HCAP + NEMO_BLOCK - 1) / NEMO_BLOCK; q++) {
+        const uint32_t i = q * NEMO_BLOCK + tid;
+        ce[q] = i < n ? L.u.adj.ccoff[i] : 0u;
+        pe[q] = i < n ? L.u.adj.pcoff[i] : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < (HCAP + NEMO_BLOCK - 1) / NEMO_BLOCK; q++) {
+        const uint32_t i = q * NEMO_BLOCK + tid;
+        if (i < n) {
+          L.u.adj.ccoff[i + 1] = (uint16_t)ce[q];
+          L.u.adj.pcoff[i + 1] = (uint16_t)pe[q];
+        }
+      }
+      if (tid == 0) {
+        L.u.adj.ccoff[0] = 0;
+        L.u.adj.pcoff[0] = 0;
+      }
+      __syncthreads();
+    }
+    STAMP(3);
+  } else {
   // ordered compaction of H* in Kahn order (chunks of 4 positions per thread);
   // pc[p] = #H* nodes before topo position p gives every level's segment
   uint32_t *pc = c.s_b + gv.n0 + g;
-  uint32_t n = 0;
   for (uint32_t base = 0; base < gv.V; base += 4 * NEMO_BLOCK) {
     const uint32_t i0 = base + 4 * tid;
     uint32_t v[4], cnt = 0;
@@ -282,7 +460,6 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   }
   __threadfence_block();
   __syncthreads();
-  const uint32_t ns = gv.nlev;
   if (ns > HCAP) {
     if (tid == 0) c.nch[g] = NEMO_NONE;
     return;
@@ -414,41 +591,49 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   }
   __syncthreads();
   STAMP(3);
+  }
   // up: longest H* path from a next rule ending here; down/nxt/tail: the
   // lexicographically least longest continuation to a next rule
+  // both sweeps in one loop, one barrier per level: waves 0-1 walk the levels
+  // forward (up), waves 2-3 backward (down); they touch disjoint arrays, so
+  // their dependent LDS chains overlap instead of adding up
+  constexpr uint32_t HALF = NEMO_BLOCK / 2;
+  const bool upper = tid < HALF;
+  const uint32_t ht = upper ? tid : tid - HALF;
   for (uint32_t s = 0; s < ns; s++) {
-    const uint32_t e = L.seg[s + 1];
-    for (uint32_t i = L.seg[s] + tid; i < e; i += NEMO_BLOCK) {
-      int32_t d = RULE(i) ? 0 : -1;
-      const uint32_t j1 = L.u.adj.pcoff[i + 1];
-      for (uint32_t j = L.u.adj.pcoff[i]; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
-      L.up[i] = (int16_t)d;
-    }
-    __syncthreads();
-  }
-  for (uint32_t s = ns; s-- > 0;) {
-    const uint32_t e = L.seg[s + 1];
-    for (uint32_t i = L.seg[s] + tid; i < e; i += NEMO_BLOCK) {
-      // one pass: the deepest child, ties to the smallest ID rank
-      int32_t best = -1;
-      uint32_t bc = NIL16, br = NEMO_NONE;
-      const uint32_t j1 = L.u.adj.ccoff[i + 1];
-      for (uint32_t j = L.u.adj.ccoff[i]; j < j1; j++) {
-        const uint32_t w = L.u.adj.child[j];
-        const int32_t dw = L.down[w];
-        const uint32_t rw = L.crank[w];
-        if (dw > best || (dw == best && rw < br)) {
-          best = dw;
-          bc = w;
-          br = rw;
-        }
+    if (upper) {
+      const uint32_t e = L.seg[s + 1];
+      for (uint32_t i = L.seg[s] + ht; i < e; i += HALF) {
+        int32_t d = RULE(i) ? 0 : -1;
+        const uint32_t j1 = L.u.adj.pcoff[i + 1];
+        for (uint32_t j = L.u.adj.pcoff[i]; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
+        L.up[i] = (int16_t)d;
       }
-      int32_t d = best >= 0 ? best + 1 : (RULE(i) ? 0 : -1);
-      if (RULE(i) && d < 0) d = 0;
-      if (d > 0 && best < 0) bc = NIL16;
-      L.down[i] = (int16_t)d;
-      L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
-      if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
+    } else {
+      const uint32_t sd = ns - 1 - s;
+      const uint32_t e = L.seg[sd + 1];
+      for (uint32_t i = L.seg[sd] + ht; i < e; i += HALF) {
+        // one pass: the deepest child, ties to the smallest ID rank
+        int32_t best = -1;
+        uint32_t bc = NIL16, br = NEMO_NONE;
+        const uint32_t j1 = L.u.adj.ccoff[i + 1];
+        for (uint32_t j = L.u.adj.ccoff[i]; j < j1; j++) {
+          const uint32_t w = L.u.adj.child[j];
+          const int32_t dw = L.down[w];
+          const uint32_t rw = L.crank[w];
+          if (dw > best || (dw == best && rw < br)) {
+            best = dw;
+            bc = w;
+            br = rw;
+          }
+        }
+        int32_t d = best >= 0 ? best + 1 : (RULE(i) ? 0 : -1);
+        if (RULE(i) && d < 0) d = 0;
+        if (d > 0 && best < 0) bc = NIL16;
+        L.down[i] = (int16_t)d;
+        L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
+        if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
+      }
     }
     __syncthreads();
   }
@@ -563,37 +748,36 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) S[L.ub[j]] = NEMO_NONE;
       __syncthreads();
     }
-    // tie-free keys (len desc, preorder asc), bitonic sort in LDS
-    uint32_t N2 = 1;
-    while (N2 < nch) N2 <<= 1;
-    for (uint32_t q = tid; q < N2; q += NEMO_BLOCK) {
-      unsigned long long key = ~0ull;
+    // tie-free keys (len desc, preorder asc): every key is unique, so a
+    // chain's position is the number of smaller keys (broadcast LDS reads,
+    // four keys per read)
+    uint32_t *key = (uint32_t *)L.u.kk;
+    uint32_t *ord = key + ((nch + 3) & ~3u);
+    for (uint32_t q = tid; q < ((nch + 3) & ~3u); q += NEMO_BLOCK) {
+      uint32_t k = 0xFFFFFFFFu;
       if (q < nch) {
         const uint32_t len = tmp[5 * q + 2], rep = tmp[5 * q + 4];
-        key = ((unsigned long long)(((0xFFFFu - len) << 16) | pre[rep]) << 32) | q;
+        k = ((0xFFFFu - len) << 16) | pre[rep];
       }
-      L.u.kk[q] = key;
+      key[q] = k;
     }
     __syncthreads();
-    for (uint32_t k = 2; k <= N2; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = tid; i < N2; i += NEMO_BLOCK) {
-          const uint32_t ixj = i ^ j;
-          if (ixj > i) {
-            const unsigned long long x = L.u.kk[i], y = L.u.kk[ixj];
-            if ((x > y) == ((i & k) == 0)) {
-              L.u.kk[i] = y;
-              L.u.kk[ixj] = x;
-            }
-          }
-        }
-        __syncthreads();
+    const uint4 *k4 = (const uint4 *)key;
+    for (uint32_t q = tid; q < nch; q += NEMO_BLOCK) {
+      const uint32_t me = key[q];
+      uint32_t pos = 0;
+      for (uint32_t j = 0; j < (nch + 3) / 4; j++) {
+        const uint4 x = k4[j];
+        pos += (x.x < me) + (x.y < me) + (x.z < me) + (x.w < me);
       }
+      ord[pos] = q;
     }
+    __syncthreads();
   }
   uint32_t *out = c.chain + 5 * gv.n0;
+  const uint32_t *ord = (const uint32_t *)L.u.kk + ((nch + 3) & ~3u);
   for (uint32_t pos = tid; pos < nch; pos += NEMO_BLOCK) {
-    const uint32_t q = (uint32_t)(L.u.kk[pos] & 0xFFFFFFFFu);
+    const uint32_t q = ord[pos];
     uint32_t *w = out + 5 * pos;
     w[0] = hs[tmp[5 * q]];
     w[1] = hs[tmp[5 * q + 1]];

@@ -117,36 +117,6 @@ __device__ __forceinline__ bool pull_alive(uint32_t which, const uint8_t *f, con
   return m[v] != 0;
 }
 
-__global__ __launch_bounds__(NEMO_BLOCK) void k_pull_count(DevCorpus c, PullArgs a) {
-  __shared__ uint32_t s_cnt;
-  const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
-  const uint32_t slot = blockIdx.x;
-  if (c.err[g]) {
-    if (threadIdx.x == 0) a.cnt[slot] = 0;
-    return;
-  }
-  const GraphView gv = c.view(g);
-  const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-  uint32_t n = 0;
-  for (uint32_t u = threadIdx.x; u < gv.V; u += NEMO_BLOCK) {
-    if (!pull_alive(a.which, gv.flags, m, u)) continue;
-    for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
-  }
-  if (a.which == 1) {
-    const uint32_t *ch = c.chain + 5 * gv.n0;
-    for (uint32_t k = threadIdx.x; k < c.nch[g]; k += NEMO_BLOCK) {
-      const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
-      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
-      for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
-    }
-  }
-  atomicAdd(&s_cnt, n);
-  __syncthreads();
-  if (threadIdx.x == 0) a.cnt[slot] = s_cnt;
-}
-
 // exclusive scan of cnt[0..n) into off[0..n], one workgroup
 __global__ __launch_bounds__(NEMO_BLOCK) void k_scan64(const uint32_t *cnt, uint64_t *off, uint32_t n) {
   __shared__ unsigned long long s_part[NEMO_BLOCK];
@@ -170,17 +140,54 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_scan64(const uint32_t *cnt, uint
   if (threadIdx.x == 0) off[n] = carry;
 }
 
-// Ordered write: rows in node order, each row in CSR order, then collapsed
-// edges by k (pred->V+k for the head's goal parents, V+k->succ for the tail's
-// goal children).  Wave/block prefix sums place every edge.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_pull_write(DevCorpus c, PullArgs a) {
+// One pass per slot (graph, or diff entry over run 0's post graph): count the
+// slot's edges, claim a contiguous region with one global atomic (slots land
+// in any order; each slot's edges stay in reference order), then write rows
+// in node order, each row in CSR order, then collapsed edges by k
+// (pred->V+k for the head's goal parents, V+k->succ for the tail's goal
+// children).  A region past a.cap is not written: the host re-runs the pull
+// with the capacity the cursor reports.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
   __shared__ uint32_t s_lds[NEMO_WAVES];
+  __shared__ uint32_t s_cnt;
+  __shared__ unsigned long long s_base;
   const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
   const uint32_t slot = blockIdx.x;
-  if (c.err[g]) return;
+  if (c.err[g]) {
+    if (threadIdx.x == 0) {
+      a.cnt[slot] = 0;
+      a.off[slot] = 0;
+    }
+    return;
+  }
   const GraphView gv = c.view(g);
   const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
-  uint64_t pos = a.off[slot];
+  const uint32_t *ch = c.chain + 5 * gv.n0;
+  const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  uint32_t n = 0;
+  for (uint32_t u = threadIdx.x; u < gv.V; u += NEMO_BLOCK) {
+    if (!pull_alive(a.which, gv.flags, m, u)) continue;
+    for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
+  }
+  for (uint32_t k = threadIdx.x; k < nch; k += NEMO_BLOCK) {
+    const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
+    for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
+    for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
+  }
+  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
+  if (lane_id() == 0 && n) atomicAdd(&s_cnt, n);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)s_cnt);
+    s_base = base;
+    a.off[slot] = base;
+    a.cnt[slot] = s_cnt;
+  }
+  __syncthreads();
+  uint64_t pos = s_base;
+  if (pos + s_cnt > a.cap) return;
   for (uint32_t base = 0; base < gv.V; base += NEMO_BLOCK) {
     const uint32_t u = base + threadIdx.x;
     uint32_t n = 0;
@@ -199,9 +206,6 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull_write(DevCorpus c, PullArgs
       }
     pos += tot;
   }
-  if (a.which != 1) return;
-  const uint32_t *ch = c.chain + 5 * gv.n0;
-  const uint32_t nch = c.nch[g];
   for (uint32_t base = 0; base < nch; base += NEMO_BLOCK) {
     const uint32_t k = base + threadIdx.x;
     uint32_t n = 0, h = 0, t = 0;
@@ -338,12 +342,8 @@ void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipSt
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s) {
   hipLaunchKernelGGL(k_diff, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
-void launch_pull_count(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
-  hipLaunchKernelGGL(k_pull_count, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
-  hipLaunchKernelGGL(k_scan64, dim3(1), dim3(NEMO_BLOCK), 0, s, a.cnt, a.off, slots);
-}
-void launch_pull_write(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
-  hipLaunchKernelGGL(k_pull_write, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
+void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
+  hipLaunchKernelGGL(k_pull, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
   hipLaunchKernelGGL(k_triggers, dim3(3), dim3(NEMO_BLOCK), 0, s, c, a, phase);
