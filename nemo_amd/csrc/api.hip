@@ -465,6 +465,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.rc, E);
   A(d.topo, V);
   A(d.lvl, V + G);
+  A(d.nlv, V);
   A(d.nlev, G);
   A(d.flags, V);
   A(d.sb, V);
@@ -1117,6 +1118,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   const std::string n(name);
   if (n == "topo") base = c->dc.topo;
   else if (n == "lvl") base = c->dc.lvl;
+  else if (n == "nlv") base = c->dc.nlv;
   else if (n == "nlev") base = c->dc.nlev;
   else if (n == "fp") base = c->dc.fp;
   else if (n == "fc") base = c->dc.fc;

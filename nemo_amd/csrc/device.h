@@ -159,6 +159,7 @@ struct DevCorpus {
   const uint32_t *esrc, *edst;
   uint32_t *fp, *fc, *rp, *rc;           // fp/rp: V+G entries (graph g at n0+g)
   uint32_t *topo, *lvl, *nlev;           // lvl: V+G entries
+  uint32_t *nlv;                         // [V] Kahn level of every node
   uint8_t *flags, *sb;                   // V
   uint32_t *s_a, *s_b, *s_c;             // V+G scratch
   int32_t *s_d;                          // V scratch

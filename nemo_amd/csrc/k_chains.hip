@@ -206,7 +206,7 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define ECAP 2048  // H* edges staged in LDS (each direction)
 #define NIL16 0xFFFFu
 #define UCAP 512   // distinct prefix lengths (longest chain path + 2)
-#define CF_ROWS 12  // topo positions per thread per compaction round (fast front)
+#define CF_ROWS 20  // topo positions per thread per compaction round (fast front)
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
 
 struct ChainsLDS {
@@ -224,8 +224,8 @@ struct ChainsLDS {
       uint16_t ccoff[HCAP + 2], child[ECAP];  // (+2: ccoff 4-byte aligned for packed u16 atomics)
     } adj;
     struct {
-      uint16_t pad[HCAP + 2 + ECAP];       // keeps bk 4-byte aligned, past par[]
-      uint32_t bk[HCAP];                   // bucket keys (po(bp) << 16 | crank), over ccoff/child
+      uint16_t pad[HCAP + 2 + ECAP + 6];   // keeps bk 16-byte aligned, past par[]
+      uint32_t bk[HCAP + 4];               // level keys, or group counters + members; over ccoff/child
     } rk;
     unsigned long long kk[HCAP];           // bitonic sort of ranks; later the chain sort keys
   } u;
@@ -235,7 +235,6 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __shared__ ChainsLDS L;
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_nch, s_maxup, s_fail;
-  __shared__ uint32_t s_wc[CF_ROWS * NEMO_WAVES];
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
@@ -261,16 +260,11 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     // from the coalesced input edge list with packed-u16 LDS counters.
     uint32_t *bm = (uint32_t *)L.u.kk;  // [1024] rank bitmap
     uint32_t *pre = bm + 1024;          // [1025] prefix popcounts
-    uint16_t *lvs = L.uoff;             // level starts (topo positions)
     uint32_t *hist = L.cur;             // H* nodes per level -> segment starts
     uint16_t *hmap = (uint16_t *)L.up;  // graph-local node -> compact index (spans up..ub)
     const uint32_t nw = (gv.V + 31) >> 5;
-    const uint32_t wave = tid >> 6, lane = lane_id();
     for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) bm[w] = 0;
-    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) {
-      hist[l] = 0;
-      lvs[l] = (uint16_t)gv.lvl[l];
-    }
+    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) hist[l] = 0;
     for (uint32_t v = tid; v < gv.V; v += NEMO_BLOCK) hmap[v] = 0xFFFFu;
     if (tid == 0) {
       s_nch = 0;
@@ -278,64 +272,40 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       s_fail = 0;
     }
     __syncthreads();
-    for (uint32_t sbase = 0; sbase < gv.V; sbase += CF_ROWS * NEMO_BLOCK) {
-      uint32_t v[CF_ROWS], wd[CF_ROWS], r[CF_ROWS];
+    STAMP(10);
+    // H* in level order (any order inside a level: every later tie-break is by
+    // ID rank).  Node-order reads are coalesced: flags, level, word, rank.
+    const uint32_t *nlv = c.nlv + gv.n0;
+    uint32_t lev[CF_ROWS], rk[CF_ROWS], hm = 0, rl = 0;
+    auto rows = [&](uint32_t sbase) {
       uint8_t fl[CF_ROWS];
+      uint32_t wd[CF_ROWS];
 #pragma unroll
       for (int q = 0; q < CF_ROWS; q++) {
-        const uint32_t p = sbase + q * NEMO_BLOCK + tid;
-        v[q] = p < gv.V ? gv.topo[p] : 0u;
+        const uint32_t x = sbase + q * NEMO_BLOCK + tid;
+        const bool in = x < gv.V;
+        fl[q] = in ? f[x] : (uint8_t)0;
+        lev[q] = in ? nlv[x] : 0u;
+        wd[q] = in ? gv.word[x] : 0u;
+        rk[q] = in ? gv.rank_of(x) : 0u;
       }
-#pragma unroll
-      for (int q = 0; q < CF_ROWS; q++) {
-        const bool in = sbase + q * NEMO_BLOCK + tid < gv.V;
-        fl[q] = in ? f[v[q]] : (uint8_t)0;
-        wd[q] = in ? gv.word[v[q]] : 0u;
-        r[q] = in ? gv.rank_of(v[q]) : 0u;
-      }
-      uint32_t hm = 0;
+      hm = rl = 0;
 #pragma unroll
       for (int q = 0; q < CF_ROWS; q++) {
         hm |= ((fl[q] & NEMO_F_DELETED) ? 1u : 0u) << q;
-        const uint64_t b = __ballot((hm >> q) & 1u);
-        if (lane == 0) s_wc[q * NEMO_WAVES + wave] = (uint32_t)__popcll(b);
+        rl |= (is_rule(wd[q]) ? 1u : 0u) << q;
       }
-      __syncthreads();
-      uint32_t run = n;
+    };
+    const bool one = gv.V <= CF_ROWS * NEMO_BLOCK;  // one round: the rows stay in registers
+    for (uint32_t sbase = 0; sbase < gv.V; sbase += CF_ROWS * NEMO_BLOCK) {
+      rows(sbase);
 #pragma unroll
-      for (int q = 0; q < CF_ROWS; q++) {
-        uint32_t before = 0, row = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < NEMO_WAVES; w2++) {
-          const uint32_t x = s_wc[q * NEMO_WAVES + w2];
-          row += x;
-          before += w2 < (int)wave ? x : 0u;
-        }
-        const bool h = (hm >> q) & 1u;
-        const uint64_t b = __ballot(h);
-        if (h) {
-          const uint32_t i = run + before + mbcnt(b);
-          if (i < cap) {
-            const uint32_t p = sbase + q * NEMO_BLOCK + tid;
-            hs[i] = v[q];
-            hmap[v[q]] = (uint16_t)i;
-            if (is_rule(wd[q])) atomicOr(&L.isrule[i >> 5], 1u << (i & 31));
-            atomicOr(&bm[r[q] >> 5], 1u << (r[q] & 31));
-            L.crank[i] = (uint16_t)r[q];  // the ID rank until the prefix popcounts exist
-            uint32_t lo = 0, hi = ns;     // level: lvs[lo] <= p < lvs[lo + 1]
-            while (lo + 1 < hi) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (lvs[mid] <= p) lo = mid;
-              else hi = mid;
-            }
-            atomicAdd(&hist[lo], 1u);
-          }
-        }
-        run += row;
-      }
-      n = run;
-      __syncthreads();  // s_wc is reused
+      for (int q = 0; q < CF_ROWS; q++)
+        if ((hm >> q) & 1u) atomicAdd(&hist[lev[q]], 1u);
     }
+    __syncthreads();
+    STAMP(11);
+    n = block_scan_inplace(hist, ns + 1, s_lds);  // level starts; hist[ns] = n
     if (n == 0) {
       if (tid == 0) c.nch[g] = 0;
       return;
@@ -344,10 +314,25 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       if (tid == 0) c.nch[g] = NEMO_NONE;
       return;
     }
+    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) L.seg[l] = (uint16_t)hist[l];
+    __syncthreads();
+    for (uint32_t sbase = 0; sbase < gv.V; sbase += CF_ROWS * NEMO_BLOCK) {
+      if (!one) rows(sbase);
+#pragma unroll
+      for (int q = 0; q < CF_ROWS; q++) {
+        if (!((hm >> q) & 1u)) continue;
+        const uint32_t x = sbase + q * NEMO_BLOCK + tid;
+        const uint32_t i = atomicAdd(&hist[lev[q]], 1u);
+        hs[i] = x;
+        hmap[x] = (uint16_t)i;
+        if ((rl >> q) & 1u) atomicOr(&L.isrule[i >> 5], 1u << (i & 31));
+        atomicOr(&bm[rk[q] >> 5], 1u << (rk[q] & 31));
+        L.crank[i] = (uint16_t)rk[q];  // the ID rank until the prefix popcounts exist
+      }
+    }
+    __syncthreads();
     __threadfence_block();
     STAMP(1);
-    block_scan_inplace(hist, ns + 1, s_lds);
-    for (uint32_t l = tid; l <= ns; l += NEMO_BLOCK) L.seg[l] = (uint16_t)hist[l];
     for (uint32_t w = tid; w < nw; w += NEMO_BLOCK) pre[w] = __popc(bm[w]);
     __syncthreads();
     block_scan_inplace(pre, nw, s_lds);
@@ -661,13 +646,73 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   for (uint32_t i = tid; i < n; i += NEMO_BLOCK) L.ub[atomicAdd(&L.cur[L.up[i]], 1u)] = (uint16_t)i;
   __syncthreads();
   // prefix ranks: po(v) = rank of best_prefix(v) among the prefixes of its
-  // length; key = (po(bp(v)), crank(v)) is unique inside a level
+  // length; key = (po(bp(v)), crank(v)) is unique inside a level.  The best
+  // parent is fixed up front where only one parent has up == up(v) - 1 (the
+  // usual case), so a level only waits on its parents' po.  fpos(v) = the po
+  // of v's first sibling (keys below (po(bp(v)), 0)) feeds the preorder.
+  constexpr uint32_t MULTI16 = 0xFFFEu;
+  uint16_t *fpos = L.seg;  // seg[] is dead after the sweeps
+  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+    const int32_t k = L.up[i];
+    uint32_t cand = NIL16, cnt = 0;
+    if (k > 0) {
+      const uint32_t q1 = L.u.adj.pcoff[i + 1];
+      for (uint32_t q = L.u.adj.pcoff[i]; q < q1; q++) {
+        const uint32_t p = L.u.adj.par[q];
+        if (L.up[p] == k - 1) {
+          cnt++;
+          cand = p;
+        }
+      }
+    }
+    L.bp[i] = (uint16_t)(cnt > 1 ? MULTI16 : cand);
+  }
+  __syncthreads();
+  // Per level: roots rank by ID (bitmap + prefix popcounts); small levels
+  // count keys directly (broadcast reads); large levels group nodes by
+  // po(bp) (histogram + scan = group bases, cursors scatter the members) and
+  // rank inside the few-member groups.
   for (uint32_t k = 0; k <= maxup; k++) {
     const uint32_t a = L.uoff[k], b = L.uoff[k + 1];
+    const uint32_t m = b - a, m4 = (m + 3) & ~3u;
+    if (k == 0) {
+      uint32_t *bmr = L.cur, *pcr = L.cur + HCAP / 32;  // cur[] is dead after the bucketing
+      for (uint32_t w = tid; w < HCAP / 32; w += NEMO_BLOCK) bmr[w] = 0;
+      __syncthreads();
+      for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+        const uint32_t cr = L.crank[L.ub[j]];
+        atomicOr(&bmr[cr >> 5], 1u << (cr & 31));
+      }
+      __syncthreads();
+      if (tid < 64) {
+        uint32_t tot;
+        pcr[tid] = wave_exscan(tid < HCAP / 32 ? __popc(bmr[tid]) : 0u, &tot);
+      }
+      __syncthreads();
+      for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j], cr = L.crank[i];
+        L.po[i] = (uint16_t)(pcr[cr >> 5] + __popc(bmr[cr >> 5] & ((1u << (cr & 31)) - 1u)));
+        fpos[i] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    const bool grouped = m > 96;
+    const uint32_t mp = a - L.uoff[k - 1];  // size of level k-1: po(bp) < mp
+    uint32_t *cnt = L.u.rk.bk, *grp = L.u.rk.bk + mp + 1;
+    if (grouped) {
+      for (uint32_t w = tid; w <= mp; w += NEMO_BLOCK) cnt[w] = 0;
+      __syncthreads();
+    }
     for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
       const uint32_t i = L.ub[j];
-      uint32_t bpi = NIL16, bpo = NEMO_NONE;
-      if (k > 0) {
+      uint32_t bpo;
+      const uint32_t cand = L.bp[i];
+      if (cand != MULTI16) {
+        bpo = L.po[cand];
+      } else {
+        uint32_t bpi = NIL16;
+        bpo = NEMO_NONE;
         const uint32_t q1 = L.u.adj.pcoff[i + 1];
         for (uint32_t q = L.u.adj.pcoff[i]; q < q1; q++) {
           const uint32_t p = L.u.adj.par[q];
@@ -676,18 +721,45 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
             bpo = L.po[p];
           }
         }
+        L.bp[i] = (uint16_t)bpi;
       }
-      L.bp[i] = (uint16_t)bpi;
-      L.u.rk.bk[j - a] = ((k ? bpo : 0u) << 16) | L.crank[i];
+      if (grouped) atomicAdd(&cnt[bpo], 1u);
+      else L.u.rk.bk[j - a] = (bpo << 16) | L.crank[i];
     }
+    if (!grouped)
+      for (uint32_t j = m + tid; j < m4; j += NEMO_BLOCK) L.u.rk.bk[j] = 0xFFFFFFFFu;
     __syncthreads();
-    const uint32_t m = b - a;
-    for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
-      const uint32_t me = L.u.rk.bk[j - a];
-      uint32_t pos = 0;
+    if (!grouped) {
+      const uint4 *bk4 = (const uint4 *)L.u.rk.bk;
+      for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+        const uint32_t me = L.u.rk.bk[j - a], lo = me & 0xFFFF0000u;
+        uint32_t pos = 0, fp = 0;
 #pragma unroll 8
-      for (uint32_t q = 0; q < m; q++) pos += L.u.rk.bk[q] < me;
-      L.po[L.ub[j]] = (uint16_t)pos;
+        for (uint32_t q = 0; q < m4 / 4; q++) {
+          const uint4 x = bk4[q];
+          pos += (x.x < me) + (x.y < me) + (x.z < me) + (x.w < me);
+          fp += (x.x < lo) + (x.y < lo) + (x.z < lo) + (x.w < lo);
+        }
+        const uint32_t i = L.ub[j];
+        L.po[i] = (uint16_t)pos;
+        fpos[i] = (uint16_t)fp;
+      }
+    } else {
+      block_scan_inplace(cnt, mp + 1, s_lds);  // group bases
+      for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j];
+        const uint32_t slot = atomicAdd(&cnt[L.po[L.bp[i]]], 1u);
+        grp[slot] = ((uint32_t)L.crank[i] << 16) | i;
+      }
+      __syncthreads();  // cnt[g] = end of group g = base of group g + 1
+      for (uint32_t j = a + tid; j < b; j += NEMO_BLOCK) {
+        const uint32_t i = L.ub[j], bpo = L.po[L.bp[i]], cr = L.crank[i];
+        const uint32_t base = bpo ? cnt[bpo - 1] : 0u, end = cnt[bpo];
+        uint32_t r = 0;
+        for (uint32_t q = base; q < end; q++) r += (grp[q] >> 16) < cr;
+        L.po[i] = (uint16_t)(base + r);
+        fpos[i] = (uint16_t)base;
+      }
     }
     __syncthreads();
   }
@@ -718,9 +790,12 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   // divergence decides.  S = subtree sizes (bottom-up), pre = preorder
   // (top-down, exclusive scans of sizes in po order).
   {
-    uint32_t *S = (uint32_t *)L.u.kk;  // subtree size, then "first child position" of a parent
-    uint32_t *A = S + HCAP;            // sizes of one level in po order -> exclusive scan
-    uint16_t *pre = L.nxt;             // nxt[] is dead once the records are written
+    // pre(v) = up(v) + sum over v and its bp ancestors a of off(a), where
+    // off(a) = total size of a's earlier siblings = A[first sibling .. a) over
+    // the sizes laid out in (level, po) order; the ancestor sums come from
+    // pointer jumping (log2(maxup) rounds instead of one pass per level).
+    uint32_t *S = (uint32_t *)L.u.kk;  // subtree sizes
+    uint32_t *A = S + HCAP;            // sizes in (level, po) order -> exclusive scan
     for (uint32_t i = tid; i < n; i += NEMO_BLOCK) S[i] = 1;
     __syncthreads();
     for (uint32_t k = maxup; k >= 1; k--) {
@@ -730,24 +805,39 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
       }
       __syncthreads();
     }
-    for (uint32_t k = 0; k <= maxup; k++) {
-      const uint32_t a = L.uoff[k], m = L.uoff[k + 1] - a;
-      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) {
-        const uint32_t i = L.ub[j];
-        A[L.po[i]] = S[i];
-        if (k > 0) atomicMin(&S[L.bp[i]], (uint32_t)L.po[i]);
-      }
-      __syncthreads();
-      block_scan_inplace(A, m, s_lds);
-      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) {
-        const uint32_t i = L.ub[j];
-        const uint32_t pos = L.po[i];
-        pre[i] = (uint16_t)(k == 0 ? A[pos] : pre[L.bp[i]] + 1u + A[pos] - A[S[L.bp[i]]]);
-      }
-      __syncthreads();
-      for (uint32_t j = a + tid; j < a + m; j += NEMO_BLOCK) S[L.ub[j]] = NEMO_NONE;
-      __syncthreads();
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) A[L.uoff[L.up[i]] + L.po[i]] = S[i];
+    __syncthreads();
+    block_scan_inplace(A, n, s_lds);
+    uint16_t *va = L.nxt, *vb = L.crank;                            // dead once the records are written
+    uint16_t *pa = (uint16_t *)L.u.kk, *pb = pa + HCAP;              // over S (dead once A is built)
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+      const uint32_t k = L.up[i], base = L.uoff[k];
+      va[i] = (uint16_t)(A[base + L.po[i]] - A[base + fpos[i]]);
+      pa[i] = (uint16_t)(k ? L.bp[i] : NIL16);
     }
+    __syncthreads();
+    for (uint32_t r = 1; r <= maxup; r <<= 1) {
+      for (uint32_t i = tid; i < n; i += NEMO_BLOCK) {
+        const uint32_t p = pa[i];
+        if (p != NIL16) {
+          vb[i] = (uint16_t)(va[i] + va[p]);
+          pb[i] = pa[p];
+        } else {
+          vb[i] = va[i];
+          pb[i] = (uint16_t)NIL16;
+        }
+      }
+      __syncthreads();
+      uint16_t *t = va;
+      va = vb;
+      vb = t;
+      t = pa;
+      pa = pb;
+      pb = t;
+    }
+    uint16_t *pre = va;
+    for (uint32_t i = tid; i < n; i += NEMO_BLOCK) pre[i] = (uint16_t)(pre[i] + L.up[i]);
+    __syncthreads();
     // tie-free keys (len desc, preorder asc): every key is unique, so a
     // chain's position is the number of smaller keys (broadcast LDS reads,
     // four keys per read)

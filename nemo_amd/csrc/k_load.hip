@@ -193,6 +193,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
     const uint32_t v = base + tid;
     const bool src = v < V && ((L.cnt[v >> 1] >> (16 * (v & 1))) & 0xFFFFu) == 0u;
     lds_append16(src, v, q16, &s_tail);
+    if (src) c.nlv[n0 + v] = 0;
   }
   __syncthreads();
   STAMP(14);
@@ -217,6 +218,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
           p = ((atomicSub(&L.cnt[ch >> 1], 1u << sh) >> sh) & 0xFFFFu) == 1u;
         }
         lds_append16(p, ch, q16, &s_tail);
+        if (p) c.nlv[n0 + ch] = nl + 1;
       }
     }
     __syncthreads();
@@ -342,6 +344,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
   for (uint32_t base = 0; base < V; base += NEMO_BLOCK) {
     const uint32_t v = base + threadIdx.x;
     wave_append(v < V && cnt[v] == 0u, v, topo, &s_tail);
+    if (v < V && cnt[v] == 0u) c.nlv[n0 + v] = 0;
   }
   __syncthreads();
   uint32_t lo = 0, hi = s_tail, nl = 0;
@@ -364,6 +367,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
           p = atomicSub(&cnt[ch], 1u) == 1u;
         }
         wave_append(p, ch, topo, &s_tail);
+        if (p) c.nlv[n0 + ch] = nl + 1;
       }
     }
     __syncthreads();

@@ -24,3 +24,6 @@ import collections
 cnt = collections.Counter(int(g) for g in ch[:, 0])
 keys = collections.Counter((int(r[0]), int(r[2]), int(r[4])) for r in ch)
 print("chains per graph mean", len(ch) / G, "max", max(cnt.values()), "records with (len, head) ties:", sum(v for v in keys.values() if v > 1), "of", len(ch))
+# level statistics of H* (maxup = longest chain prefix) from the chain records
+lens = ch[:, 4] if ch.shape[1] > 4 else None
+print("chain length: mean", float(np.mean(ch[:, 4])), "max", int(np.max(ch[:, 4])))
