@@ -53,6 +53,8 @@ struct nemo_ctx {
   bool has_rank = false;
   uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu, build_limit = 0xFFFFFFFFu;
   uint32_t lds_limit = 0xFFFFFFFFu;  // test knob: largest V of the LDS graph tier (0 = off)
+  double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
+  bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
@@ -106,6 +108,7 @@ struct nemo_ctx {
 };
 
 static void set_lds_tier(nemo_ctx *c);
+static int ensure_marked(nemo_ctx *c);
 
 static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
   char buf[512];
@@ -268,6 +271,7 @@ static void release_corpus(nemo_ctx *c) {
   c->d_chht_cap = 0;
   c->staged = false;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
+  c->mark_pending = false;
 }
 
 void nemo_ctx_destroy(nemo_ctx *c) {
@@ -319,6 +323,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     return NEMO_OK;
   }
   if (!strcmp(name, "graph_lds_max")) {
+    if (c->loaded) {
+      HIPCHK(c, hipSetDevice(c->device));
+      if (int rm = ensure_marked(c)) return rm;  // the deferred set depends on the tier caps
+    }
     c->lds_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     if (c->loaded) set_lds_tier(c);
     return NEMO_OK;
@@ -363,6 +371,14 @@ static void set_lds_tier(nemo_ctx *c) {
   c->dc.lds_e = ce;
   c->dc.lds_l = std::min(cv, 512u);
   c->dc.lds_bytes = cv ? lds_tier_bytes(cv, ce, c->dc.lds_l, c->W) : 0;
+  c->tierV = c->tierE = 0;
+  for (uint32_t g = 0; g < c->G && cv; g++) {
+    const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+    if (v <= cv && e <= ce) {
+      c->tierV += (double)v;
+      c->tierE += (double)e;
+    }
+  }
 }
 
 static int check_graph_errors(nemo_ctx *c) {
@@ -564,6 +580,19 @@ int nemo_rebuild(nemo_ctx *c) {
   rc = device_load(c);
   if (rc) return rc;
   c->marked = c->simplified = c->protos_done = c->trig_done = false;
+  c->mark_pending = false;
+  return NEMO_OK;
+}
+
+// markConditionHolds is deferred for the LDS-tier graphs: nemo_simplify runs
+// it fused with the simplification (k_marksimp).  Anything that reads the
+// holds flags before that materialises it first (ensure_marked).
+static int ensure_marked(nemo_ctx *c) {
+  if (!c->mark_pending) return NEMO_OK;
+  const double V = c->tierV, E = c->tierE;
+  int rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, false, c->stream); });
+  if (rc) return rc;
+  c->mark_pending = false;
   return NEMO_OK;
 }
 
@@ -571,11 +600,13 @@ int nemo_mark_holds(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_mark_holds before nemo_load_corpus");
   HIPCHK(c, hipSetDevice(c->device));
-  const double V = (double)c->V, E = (double)c->E;
+  const double V = (double)c->V - c->tierV, E = (double)c->E - c->tierE;
   int rc = guard_staged(c);
   if (rc) return rc;
-  rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, c->stream); });
+  const bool defer = c->dc.lds_bytes != 0;
+  rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, defer, c->stream); });
   if (rc) return rc;
+  c->mark_pending = defer;
   c->marked = true;
   c->simplified = c->protos_done = c->trig_done = false;
   return NEMO_OK;
@@ -585,11 +616,21 @@ int nemo_simplify(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_simplify before nemo_mark_holds");
   HIPCHK(c, hipSetDevice(c->device));
-  const double V = (double)c->V, E = (double)c->E;
   int rc = guard_staged(c);
   if (rc) return rc;
-  rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, c->stream); });
-  if (rc) return rc;
+  if (c->mark_pending) {
+    const double V = c->tierV, E = c->tierE, Vg = (double)c->V - V, Eg = (double)c->E - E;
+    rc = timed(c, "k_marksimp", 8 * E + 13 * V, 4 * E, [&] { nemo::launch_marksimp(c->dc, c->stream); });
+    if (rc) return rc;
+    rc = timed(c, "k_simplify", 8 * Eg + 14 * Vg, 2 * Eg, [&] { nemo::launch_simplify(c->dc, true, c->stream); });
+    if (rc) return rc;
+    c->mark_pending = false;
+  } else {
+    const double V = (double)c->V, E = (double)c->E;
+    rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, false, c->stream); });
+    if (rc) return rc;
+  }
+  const double V = (double)c->V;
   rc = timed(c, "k_chains", 9 * V, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
   if (rc) return rc;
   c->simplified = true;
@@ -712,6 +753,7 @@ int nemo_missing_from(nemo_ctx *c, uint32_t failed_iter, const uint32_t *proto, 
 int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode) {
   if (!c || (!failed_iters && n_failed)) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_diffprov before nemo_mark_holds");
+  if (int rm = ensure_marked(c)) return rm;
   HIPCHK(c, hipSetDevice(c->device));
   c->n_entries = 0;
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
@@ -817,6 +859,7 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
 int nemo_triggers(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_triggers before nemo_mark_holds");
+  if (int rm = ensure_marked(c)) return rm;
   HIPCHK(c, hipSetDevice(c->device));
   c->tcounts[0] = c->tcounts[1] = c->tcounts[2] = 0;
   c->trig_done = true;
@@ -884,6 +927,7 @@ int nemo_fetch_node_flags(nemo_ctx *c, uint32_t g_lo, uint32_t g_hi, uint8_t *ou
   const uint64_t a = c->node_off[g_lo], b = c->node_off[g_hi];
   if (cap < b - a) return fail(c, NEMO_ERR_INVALID, "capacity too small");
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rm = ensure_marked(c)) return rm;
   if (b > a) {
     HIPCHK(c, hipMemcpyAsync(out, c->dc.flags + a, b - a, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -42,8 +42,9 @@ struct TrigArgs {
 void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
 void launch_topo(const DevCorpus &c, hipStream_t s);
-void launch_mark(const DevCorpus &c, hipStream_t s);
-void launch_simplify(const DevCorpus &c, hipStream_t s);
+void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s);
+void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s);
+void launch_marksimp(const DevCorpus &c, hipStream_t s);
 void launch_chains(const DevCorpus &c, hipStream_t s);
 void launch_proto(const DevCorpus &c, hipStream_t s);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,

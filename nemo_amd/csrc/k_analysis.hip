@@ -11,12 +11,13 @@ namespace nemo {
 // goals (LDS bitset); if Tq is non-empty every goal whose table is C or in Tq
 // holds.  Also counts holding "pre" goals for GenerateExtensions
 // (extensions.go:25-49).  Resets every other flag bit of the graph.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c) {
+__global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c, int skip_tier) {
   __shared__ uint32_t s_tq[NEMO_MAX_TABLES / 32];
   __shared__ uint32_t s_any, s_pre;
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
+  if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
   for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) s_tq[i] = 0;
   if (threadIdx.x == 0) {
@@ -63,11 +64,12 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c) {
 // on the clean graph a goal with a next-rule parent and a next-rule child, or
 // a next rule with a next-rule grandparent or grandchild, lies on an @next
 // chain and is DETACH DELETEd; heads/tails are the chain ends.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c) {
+__global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c, int skip_tier) {
   __shared__ uint32_t s_hold;
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
+  if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   uint8_t *f = gv.flags;
   for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
     uint8_t fl = f[x] & NEMO_F_HOLDS;
@@ -430,6 +432,122 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   STAMP(7);
 }
 
+
+// markConditionHolds + cleanCopyProv + the local part of collapseNextChains
+// fused over the LDS graph tier: the same rules as k_mark then
+// k_simplify_flags, every neighbour access in LDS, the flags written once.
+__global__ __launch_bounds__(PROTO_BLOCK) void k_marksimp(DevCorpus c) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  __shared__ uint32_t s_any, s_pre, s_hold;
+  const uint32_t g = blockIdx.x;
+  if (c.err[g]) return;
+  const GraphView gv = c.view(g);
+  if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
+  const uint32_t V = gv.V, W = c.words, tid = threadIdx.x;
+  LdsGraph L = lds_carve(dyn, V, gv.E, gv.nlev, W);
+  uint32_t *tq = L.words;
+  uint8_t *fl = L.a;
+  for (uint32_t i = tid; i < W; i += PROTO_BLOCK) tq[i] = 0;
+  if (tid == 0) {
+    s_any = 0;
+    s_pre = 0;
+    s_hold = 0;
+  }
+  {
+    const StageDesc d[5] = {{gv.rp, L.rp, V + 1, ST_U16}, {gv.fp, L.fp, V + 1, ST_U16}, {gv.rc, L.rc, gv.E, ST_U16},
+                            {gv.fc, L.fc, gv.E, ST_U16},  {gv.word, L.nw, V, ST_WORD}};
+    stage_lds<5, PROTO_BLOCK>(d);
+  }
+  __syncthreads();
+  const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
+#define NTAB(v) (L.nw[v] & NW_TABLE)
+#define NRULE(v) ((L.nw[v] & NW_RULE) != 0)
+#define INDEG(v) ((uint32_t)L.rp[(v) + 1] - L.rp[v])
+#define OUTDEG(v) ((uint32_t)L.fp[(v) + 1] - L.fp[v])
+  // markConditionHolds (pre-post-prov.go:218-244): qualifying tables
+  bool any = false;
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (NRULE(x) || OUTDEG(x) == 0) continue;
+    bool pos = false, neg = false;
+    for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) {
+      const uint32_t rcn = L.rc[j];
+      if (NTAB(rcn) != C) continue;
+      for (uint32_t i = L.rp[rcn]; i < L.rp[rcn + 1]; i++) {
+        const uint32_t t = L.rc[i];
+        if (NTAB(t) != C) continue;
+        pos = true;
+        neg |= INDEG(t) > 0;
+      }
+    }
+    if (pos && !neg) {
+      atomicOr(&tq[NTAB(x) >> 5], 1u << (NTAB(x) & 31));
+      any = true;
+    }
+  }
+  if (__any(any) && lane_id() == 0) s_any = 1;
+  __syncthreads();
+  // holds + cleanCopyProv's KEPT (preprocessing.go:13-63)
+  const bool anyq = s_any != 0;
+  uint32_t pre = 0;
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    const uint32_t t = NTAB(x);
+    const bool rule = NRULE(x);
+    const bool h = anyq && !rule && (t == C || ((tq[t >> 5] >> (t & 31)) & 1u));
+    uint8_t f = h ? (uint8_t)NEMO_F_HOLDS : (uint8_t)0;
+    if (!rule || (INDEG(x) > 0 && OUTDEG(x) > 0)) f |= NEMO_F_KEPT;
+    fl[x] = f;
+    pre += (h && t == c.table_pre) ? 1u : 0u;
+  }
+  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);
+  if (lane_id() == 0 && pre) atomicAdd(&s_pre, pre);
+  __syncthreads();
+  // collapseNextChains' local rules (preprocessing.go:66-348), as k_simplify_flags
+#define ISNEXT(v) ((L.nw[v] & NW_NEXT) && (fl[v] & NEMO_F_KEPT))
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (NRULE(x)) continue;
+    uint8_t b = 0;
+    for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++)
+      if (ISNEXT(L.rc[j])) b |= FT_NP;
+    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
+      if (ISNEXT(L.fc[j])) b |= FT_NC;
+    fl[x] |= b;
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (!ISNEXT(x)) continue;
+    bool gp = false, gc = false;
+    for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) gp |= (fl[L.rc[j]] & FT_NP) != 0;
+    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) gc |= (fl[L.fc[j]] & FT_NC) != 0;
+    uint8_t f = fl[x];
+    if (gp || gc) f |= NEMO_F_DELETED;
+    if (!gp && gc) f |= NEMO_F_HEAD;
+    if (gp && !gc) f |= NEMO_F_TAIL;
+    fl[x] = f;
+  }
+#undef ISNEXT
+  __syncthreads();
+  bool hold = false;
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    uint8_t f = fl[x];
+    if (!NRULE(x)) {
+      if ((f & FT_NP) && (f & FT_NC)) f |= NEMO_F_DELETED;
+      f &= (uint8_t)~(FT_NP | FT_NC);
+      hold |= (f & (NEMO_F_HOLDS | NEMO_F_DELETED)) == NEMO_F_HOLDS;
+    }
+    gv.flags[x] = f;
+  }
+#undef NTAB
+#undef NRULE
+#undef INDEG
+#undef OUTDEG
+  if (__any(hold) && lane_id() == 0) s_hold = 1;
+  __syncthreads();
+  if (tid == 0) {
+    c.prehold[g] = s_pre;
+    c.holdany[g] = s_hold;
+  }
+}
+
 // Cross-run reduction vector (nemo_reduce_len): per-table counts over owned
 // success runs with a non-empty list, the first success run's list, achvdCond
 // (prototype.go:29-130) and the holding-"pre"-goal count (extensions.go:25-49).
@@ -476,11 +594,16 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_
   }
 }
 
-void launch_mark(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_mark, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+  hipLaunchKernelGGL(k_mark, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
 }
-void launch_simplify(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+  hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
+}
+void launch_marksimp(const DevCorpus &c, hipStream_t s) {
+  if (!c.lds_bytes) return;
+  hipFuncSetAttribute((const void *)k_marksimp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
+  hipLaunchKernelGGL(k_marksimp, dim3(c.G), dim3(PROTO_BLOCK), c.lds_bytes, s, c);
 }
 void launch_proto(const DevCorpus &c, hipStream_t s) {
   if (c.lds_bytes) {

@@ -219,3 +219,23 @@ def test_graph_lds_tier(eng, lds_max):
         _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
     finally:
         eng.set_option("graph_lds_max", -1)
+
+
+@pytest.mark.parametrize("lds_max", [-1, 0])
+def test_holds_before_simplify(eng, lds_max):
+    # markConditionHolds is deferred for LDS-tier graphs (fused into nemo_simplify);
+    # reading the flags in between materialises exactly the holds bits
+    from nemo_amd.corpus import F_HOLDS
+    from tools import synth
+    corpus, _ = synth.generate(12, target_nodes=1500)
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, skip_pulls=True)
+    eng.set_option("graph_lds_max", lds_max)
+    try:
+        eng.load(corpus)
+        eng.mark()
+        assert np.array_equal(eng.flags(), orc.flags & F_HOLDS)
+        eng.simplify()
+        assert np.array_equal(eng.flags(), orc.flags)
+    finally:
+        eng.set_option("graph_lds_max", -1)
