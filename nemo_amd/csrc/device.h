@@ -49,8 +49,10 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t *q
   if (pred) q[base + mbcnt(m)] = val;
 }
 
-// Block-wide exclusive scan of one u32 per thread; `lds` holds NEMO_WAVES u32.
+// Block-wide exclusive scan of one u32 per thread; `lds` holds B/64 u32.
+template <int B = NEMO_BLOCK>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, uint32_t *lds) {
+  constexpr int NW = B / 64;
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   uint32_t v = x;
 #pragma unroll
@@ -62,7 +64,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < NEMO_WAVES; i++) {
+  for (int i = 0; i < NW; i++) {
     uint32_t s = lds[i];
     off += (i < (int)w) ? s : 0u;
     tot += s;
@@ -72,11 +74,11 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
   return off + v - x;
 }
 
-// In-place exclusive scan of a[0..n) by one workgroup; returns the total.
-template <typename T>
+// In-place exclusive scan of a[0..n) by one workgroup of B threads; returns the total.
+template <int B = NEMO_BLOCK, typename T>
 __device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_t *lds) {
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < n; base += NEMO_BLOCK * 4) {
+  for (uint32_t base = 0; base < n; base += B * 4) {
     const uint32_t i0 = base + threadIdx.x * 4;
     uint32_t x[4], s = 0;
 #pragma unroll
@@ -85,7 +87,7 @@ __device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_
       s += x[k];
     }
     uint32_t tot;
-    uint32_t ex = block_exscan(s, &tot, lds) + carry;
+    uint32_t ex = block_exscan<B>(s, &tot, lds) + carry;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (i0 + k < n) a[i0 + k] = (T)ex;

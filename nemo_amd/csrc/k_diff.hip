@@ -161,6 +161,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
     return;
   }
   const GraphView gv = c.view(g);
+  if (a.which != 2 && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph
   const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
@@ -235,6 +236,105 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
     }
     pos += tot;
   }
+}
+
+
+// k_pull over the LDS graph tier (raw / simplified graphs): the graph's rows
+// and flags staged in LDS, per-node output offsets from one block scan, the
+// same order as k_pull.
+#define PULL_BLOCK 512
+__global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  __shared__ uint32_t s_lds[PULL_BLOCK / 64];
+  __shared__ uint32_t s_cnt;
+  __shared__ unsigned long long s_base;
+  const uint32_t g = blockIdx.x, tid = threadIdx.x;
+  if (c.err[g]) return;  // k_pull writes the empty slot
+  const GraphView gv = c.view(g);
+  if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
+  const uint32_t V = gv.V;
+  LdsGraph L = lds_carve(dyn, V, gv.E, gv.nlev, c.words);
+  {
+    const StageDesc d[5] = {{gv.rp, L.rp, V + 1, ST_U16}, {gv.fp, L.fp, V + 1, ST_U16}, {gv.rc, L.rc, gv.E, ST_U16},
+                            {gv.fc, L.fc, gv.E, ST_U16},  {gv.flags, L.a, V, ST_U8}};
+    stage_lds<5, PULL_BLOCK>(d);
+  }
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  const uint32_t which = a.which;
+  const uint8_t *fl = L.a;
+#define ALIVE(v) (which == 0 || (fl[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+  uint16_t *cnt = L.topo;  // per-node edge counts -> output offsets
+  for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
+    uint32_t n = 0;
+    if (ALIVE(u))
+      for (uint32_t j = L.fp[u]; j < L.fp[u + 1]; j++) n += ALIVE(L.fc[j]);
+    cnt[u] = (uint16_t)n;
+  }
+  const uint32_t *ch = c.chain + 5 * gv.n0;
+  const uint32_t nch = which == 1 ? c.nch[g] : 0u;
+  uint32_t nc = 0;
+  for (uint32_t k = tid; k < nch; k += PULL_BLOCK) {
+    const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
+    for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) nc += ALIVE(L.rc[j]);
+    for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) nc += ALIVE(L.fc[j]);
+  }
+  for (int d = 32; d >= 1; d >>= 1) nc += __shfl_xor(nc, d);
+  if (lane_id() == 0 && nc) atomicAdd(&s_cnt, nc);
+  __syncthreads();
+  const uint32_t nn = block_scan_inplace<PULL_BLOCK>(cnt, V, s_lds);
+  if (tid == 0) {
+    const uint32_t tot = nn + s_cnt;
+    const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)tot);
+    s_base = base;
+    a.off[g] = base;
+    a.cnt[g] = tot;
+  }
+  __syncthreads();
+  const uint64_t base = s_base;
+  if (base + nn + s_cnt > a.cap) return;
+  for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
+    if (!ALIVE(u)) continue;
+    uint64_t o = base + cnt[u];
+    for (uint32_t j = L.fp[u]; j < L.fp[u + 1]; j++) {
+      const uint32_t v = L.fc[j];
+      if (!ALIVE(v)) continue;
+      a.src[o] = u;
+      a.dst[o] = v;
+      o++;
+    }
+  }
+  uint64_t pos = base + nn;
+  for (uint32_t kb = 0; kb < nch; kb += PULL_BLOCK) {
+    const uint32_t k = kb + tid;
+    uint32_t n = 0, h = 0, t = 0;
+    if (k < nch) {
+      h = ch[5 * k];
+      t = ch[5 * k + 1];
+      for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) n += ALIVE(L.rc[j]);
+      for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) n += ALIVE(L.fc[j]);
+    }
+    uint32_t tot;
+    uint64_t o = pos + block_exscan<PULL_BLOCK>(n, &tot, s_lds);
+    if (k < nch) {
+      for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) {
+        const uint32_t p = L.rc[j];
+        if (!ALIVE(p)) continue;
+        a.src[o] = p;
+        a.dst[o] = V + k;
+        o++;
+      }
+      for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) {
+        const uint32_t q = L.fc[j];
+        if (!ALIVE(q)) continue;
+        a.src[o] = V + k;
+        a.dst[o] = q;
+        o++;
+      }
+    }
+    pos += tot;
+  }
+#undef ALIVE
 }
 
 // ---- run-0 trigger patterns ------------------------------------------------------
@@ -343,6 +443,10 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipS
   hipLaunchKernelGGL(k_diff, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
+  if (a.which != 2 && c.lds_bytes) {
+    hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
+    hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), c.lds_bytes, s, c, a);
+  }
   hipLaunchKernelGGL(k_pull, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
