@@ -108,6 +108,7 @@ struct nemo_ctx {
 };
 
 static void set_lds_tier(nemo_ctx *c);
+static void set_build_tier(nemo_ctx *c);
 static int ensure_marked(nemo_ctx *c);
 
 static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
@@ -319,7 +320,7 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "build_lds_max")) {
     c->build_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
-    c->dc.build_limit = c->build_limit;
+    if (c->loaded) set_build_tier(c);
     return NEMO_OK;
   }
   if (!strcmp(name, "graph_lds_max")) {
@@ -381,6 +382,29 @@ static void set_lds_tier(nemo_ctx *c) {
   }
 }
 
+// k_build's LDS caps: the largest graphs, smallest first, whose build image
+// (k_load.hip build_tier_bytes) keeps four workgroups on a CU.
+#define BUILD_TIER_BUDGET (40u * 1024u - 64u)
+static void set_build_tier(nemo_ctx *c) {
+  std::vector<std::pair<uint32_t, uint32_t>> ve;
+  ve.reserve(c->G);
+  for (uint32_t g = 0; g < c->G; g++) {
+    const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+    if (v <= std::min<uint64_t>(16384, c->build_limit) && e <= 32u * NEMO_BLOCK) ve.push_back({(uint32_t)v, (uint32_t)e});
+  }
+  std::sort(ve.begin(), ve.end());
+  uint32_t cv = 0, ce = 0, emax = 0;
+  for (auto &x : ve) {
+    emax = std::max(emax, x.second);
+    if (nemo::build_tier_bytes(x.first, emax) > BUILD_TIER_BUDGET) break;
+    cv = x.first;
+    ce = emax;
+  }
+  c->dc.bld_v = cv;
+  c->dc.bld_e = ce;
+  c->dc.bld_bytes = cv ? nemo::build_tier_bytes(cv, ce) : 0;
+}
+
 static int check_graph_errors(nemo_ctx *c) {
   std::vector<uint32_t> err(c->G), created(c->G);
   HIPCHK(c, hipMemcpyAsync(err.data(), c->dc.err, c->G * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
@@ -403,11 +427,11 @@ static int check_graph_errors(nemo_ctx *c) {
 static int device_load(nemo_ctx *c) {
   int rc;
   HIPCHK(c, hipMemsetAsync(c->dc.err, 0, c->G * sizeof(uint32_t), c->stream));
-  // graphs within k_build's LDS caps (k_load.hip BLD_V/BLD_E) vs the global tier
+  // graphs within k_build's LDS caps vs the global tier
   double Vb = 0, Eb = 0;
-  for (uint32_t g = 0; g < c->G; g++) {
+  for (uint32_t g = 0; g < c->G && c->dc.bld_bytes; g++) {
     const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
-    if (v <= 6144 && e <= 8192 && v <= c->build_limit) {
+    if (v <= c->dc.bld_v && e <= c->dc.bld_e) {
       Vb += (double)v;
       Eb += (double)e;
     }
@@ -496,6 +520,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.created, G);
   A(d.prehold, G);
   A(d.holdany, G);
+  A(d.redo, G);
   A(d.chain, 5 * V);
   A(d.chain_tmp, 5 * V);
   A(d.nch, G);
@@ -529,7 +554,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipMemsetAsync(d.prehold, 0, G * 4, s));
   d.G = c->G;
   d.hcap_limit = c->hcap_limit;
-  d.build_limit = c->build_limit;
+  set_build_tier(c);
   d.comp_limit = c->comp_limit;
   set_lds_tier(c);
   d.n_runs = c->n_runs;

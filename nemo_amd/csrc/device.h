@@ -153,7 +153,7 @@ struct DevCorpus {
   uint32_t G, n_runs, n_tables, words, table_pre, table_post;
   uint32_t hcap_limit;                   // largest chain subgraph H* k_chains stages in LDS (test knob)
   uint32_t comp_limit;                   // largest H* component k_chains_big stages in LDS (test knob)
-  uint32_t build_limit;                  // largest graph k_build handles in LDS (test knob)
+  uint32_t bld_v, bld_e, bld_bytes;      // k_build's LDS caps and image size (0 = tier off)
   uint32_t lds_v, lds_e, lds_l;          // LDS graph tier caps (V, E, Kahn levels); 0 = tier off
   uint32_t lds_bytes;                    // dynamic LDS of the tier's kernels
   const uint64_t *node_off, *edge_off;
@@ -171,6 +171,7 @@ struct DevCorpus {
   uint32_t *created;                     // [G] loadProv relationships-created
   uint32_t *prehold;                     // [G] #holding "pre" goals (pre graphs)
   uint32_t *holdany;                     // [G] 1 iff a holding goal survives simplification
+  uint8_t *redo;                         // [G] k_build left the graph to the global tier
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
   uint32_t *chain_tmp;                   // [5*V]
   uint32_t *nch;                         // [G]

@@ -39,6 +39,7 @@ struct TrigArgs {
   uint32_t *pre, *post, *async_rules;
 };
 
+__host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e);
 void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
 void launch_topo(const DevCorpus &c, hipStream_t s);

@@ -38,18 +38,20 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
   }
 }
 
-// Fused LDS tier of loadProv's device half for graphs with V <= BLD_V and
-// E <= BLD_E (the bulk of a Molly corpus): reverse CSR, forward CSR and Kahn
-// levels built in LDS (u16 columns, in-degrees packed two per u32), each
-// output written once, coalesced.  Same outputs and validations as k_csr +
-// k_topo, which take the graphs that do not fit.
-#define BLD_V 6144
-#define BLD_E 8192
-struct BuildLDS {
-  uint32_t ptr[BLD_V + 1];  // counts -> offsets -> cursors (= row ends)
-  uint16_t col[BLD_E];      // one direction's rows at a time
-  uint32_t cnt[BLD_V / 2];  // in-degrees, u16 pairs
-};
+// Fused LDS tier of loadProv's device half for the bulk of a Molly corpus:
+// reverse CSR, forward CSR and Kahn levels built in LDS, each output written
+// once, coalesced.  The LDS image is sized per corpus (DevCorpus::bld_*): u16
+// row pointers (counted and cursored with packed-u16 atomics), u16 columns,
+// u8 in-degree counters (packed-u8 atomics) and a u16 level queue, so four
+// workgroups share a CU.  A graph with an in-degree above 255 is flagged
+// (redo) and rebuilt by k_csr + k_topo, which also take the graphs beyond
+// the caps; both tiers produce the same outputs and validations.
+#define BLD_EPT 32  // edges per thread held in registers (bld_e <= BLD_EPT * NEMO_BLOCK)
+
+__host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
+  return lds_align(4u * ((v + 31u) / 32u)) + lds_align(2u * (v + 2u)) + lds_align(2u * e) + lds_align(v) +
+         lds_align(2u * v);
+}
 
 // wave_append into an LDS u16 queue
 __device__ __forceinline__ void lds_append16(bool pred, uint32_t val, uint16_t *q, uint32_t *tail) {
@@ -63,27 +65,37 @@ __device__ __forceinline__ void lds_append16(bool pred, uint32_t val, uint16_t *
 }
 
 __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint32_t E) {
-  return V <= BLD_V && E <= BLD_E && V <= c.build_limit;
+  return c.bld_bytes != 0u && V <= c.bld_v && E <= c.bld_e;
 }
 
 __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
-  constexpr int EPT = BLD_E / NEMO_BLOCK;  // edges per thread, held in registers
-  __shared__ BuildLDS L;
-  __shared__ uint32_t s_rule[BLD_V / 32];  // is_rule bitmap
+  extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_bad, s_created, s_tail;
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   if (!build_fits(c, V, E)) return;
+  uint8_t *p = dyn;
+  uint32_t *s_rule = (uint32_t *)p;  // is_rule bitmap
+  p += lds_align(4u * ((V + 31u) / 32u));
+  uint16_t *ptr = (uint16_t *)p;  // counts -> row starts -> cursors (= row ends); u32-packed pairs
+  uint32_t *ptr32 = (uint32_t *)p;
+  p += lds_align(2u * (V + 2u));
+  uint16_t *col = (uint16_t *)p;  // one direction's rows at a time
+  p += lds_align(2u * E);
+  uint8_t *cnt8 = p;  // in-degrees, u32-packed quads
+  uint32_t *cnt32 = (uint32_t *)p;
+  p += lds_align(V);
+  uint16_t *q16 = (uint16_t *)p;  // Kahn order
   const uint32_t *es = c.esrc + e0, *ed = c.edst + e0, *word = c.word + n0;
   STAMP(10);
   // every load of the graph's input issued back to back: edge e = tid + q*BLOCK
   // as (src << 16 | dst), and the rule bits of the node words
-  uint32_t sd[EPT];
+  uint32_t sd[BLD_EPT];
   bool bad = false;
 #pragma unroll
-  for (int q = 0; q < EPT; q++) {
+  for (int q = 0; q < BLD_EPT; q++) {
     const uint32_t e = tid + q * NEMO_BLOCK;
     const uint32_t x = e < E ? es[e] : 0u, y = e < E ? ed[e] : 0u;
     bad |= e < E && (x >= V || y >= V);
@@ -94,19 +106,19 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
     s_bad = 0;
     s_created = 0;
     s_tail = 0;
+    c.redo[g] = 0;
   }
   __syncthreads();
-  {
-    constexpr int VPT = BLD_V / NEMO_BLOCK;
-    bool r[VPT];
+  for (uint32_t base = 0; base < V; base += 8 * NEMO_BLOCK) {
+    bool r[8];
 #pragma unroll
-    for (int q = 0; q < VPT; q++) {
-      const uint32_t v = tid + q * NEMO_BLOCK;
+    for (int q = 0; q < 8; q++) {
+      const uint32_t v = base + tid + q * NEMO_BLOCK;
       r[q] = v < V && is_rule(word[v]);
     }
 #pragma unroll
-    for (int q = 0; q < VPT; q++) {
-      const uint32_t v = tid + q * NEMO_BLOCK;
+    for (int q = 0; q < 8; q++) {
+      const uint32_t v = base + tid + q * NEMO_BLOCK;
       const uint64_t m = __ballot(r[q]);
       if ((lane_id() & 31) == 0 && v < V) {
         const uint32_t bits = (uint32_t)(m >> (lane_id() & 32));
@@ -125,75 +137,77 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
   for (int dir = 0; dir < 2; dir++) {  // 0: reverse rows (parents), 1: forward rows (children)
     const int ks = dir ? 16 : 0, vs = dir ? 0 : 16;  // key / value shifts in sd
     uint32_t *optr = dir ? c.fp + n0 + g : c.rp + n0 + g, *ocol = dir ? c.fc + e0 : c.rc + e0;
-    for (uint32_t v = tid; v <= V; v += NEMO_BLOCK) L.ptr[v] = 0;
+    for (uint32_t w = tid; w < (V + 2) / 2; w += NEMO_BLOCK) ptr32[w] = 0;
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < EPT; q++)
-      if (tid + q * NEMO_BLOCK < E) atomicAdd(&L.ptr[(sd[q] >> ks) & 0xFFFFu], 1u);
+    for (int q = 0; q < BLD_EPT; q++)
+      if (tid + q * NEMO_BLOCK < E) {
+        const uint32_t k = (sd[q] >> ks) & 0xFFFFu;
+        atomicAdd(&ptr32[k >> 1], 1u << (16 * (k & 1)));
+      }
     __syncthreads();
-    if (dir == 0)
-      for (uint32_t w = tid; 2 * w < V; w += NEMO_BLOCK)
-        L.cnt[w] = L.ptr[2 * w] | (2 * w + 1 < V ? L.ptr[2 * w + 1] << 16 : 0u);
-    block_scan_inplace(L.ptr, V + 1, s_lds);
-    for (uint32_t v = tid; v <= V; v += NEMO_BLOCK) optr[v] = L.ptr[v];
+    if (dir == 0) {  // in-degrees; a graph beyond the u8 counters goes to the global tier
+      bool heavy = false;
+      for (uint32_t w = tid; 4 * w < V; w += NEMO_BLOCK) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t v = 4 * w + b, d = v < V ? ptr[v] : 0u;
+          heavy |= d > 255u;
+          x |= (d & 0xFFu) << (8 * b);
+        }
+        cnt32[w] = x;
+      }
+      if (heavy) s_bad = 1;
+      __syncthreads();
+      if (s_bad) {
+        if (tid == 0) c.redo[g] = 1;
+        return;
+      }
+    }
+    block_scan_inplace(ptr, V + 1, s_lds);
+    for (uint32_t v = tid; v <= V; v += NEMO_BLOCK) optr[v] = ptr[v];
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < EPT; q++)
-      if (tid + q * NEMO_BLOCK < E)
-        L.col[atomicAdd(&L.ptr[(sd[q] >> ks) & 0xFFFFu], 1u)] = (uint16_t)((sd[q] >> vs) & 0xFFFFu);
+    for (int q = 0; q < BLD_EPT; q++)
+      if (tid + q * NEMO_BLOCK < E) {
+        const uint32_t k = (sd[q] >> ks) & 0xFFFFu, sh = 16 * (k & 1);
+        col[(atomicAdd(&ptr32[k >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)((sd[q] >> vs) & 0xFFFFu);
+      }
     __syncthreads();
     for (uint32_t v = tid; v < V; v += NEMO_BLOCK) {
-      const uint32_t a = v ? L.ptr[v - 1] : 0u, b = L.ptr[v];
+      const uint32_t a = v ? ptr[v - 1] : 0u, b = ptr[v];
       for (uint32_t i = a + 1; i < b; i++) {
-        const uint16_t x = L.col[i];
+        const uint16_t x = col[i];
         uint32_t j = i;
-        while (j > a && L.col[j - 1] > x) {
-          L.col[j] = L.col[j - 1];
+        while (j > a && col[j - 1] > x) {
+          col[j] = col[j - 1];
           j--;
         }
-        L.col[j] = x;
+        col[j] = x;
       }
       if (dir == 0) {  // relationships created (pre-post-prov.go:150-210): distinct, goal<->rule
         const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
         for (uint32_t i = a; i < b; i++) {
-          const uint32_t t = L.col[i];
+          const uint32_t t = col[i];
           const bool rt = (s_rule[t >> 5] >> (t & 31)) & 1u;
-          if (!(i > a && L.col[i - 1] == t) && rv != rt) created++;
+          if (!(i > a && col[i - 1] == t) && rv != rt) created++;
         }
       }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < E; j += NEMO_BLOCK) ocol[j] = L.col[j];
+    for (uint32_t j = tid; j < E; j += NEMO_BLOCK) ocol[j] = col[j];
     __syncthreads();
     STAMP(12 + dir);
   }
   atomicAdd(&s_created, created);
-  // Kahn levels over the forward rows still in LDS.  Row ends are repacked to
-  // u16 (ends <= BLD_E), which frees the upper half of ptr[] for the level
-  // queue; topo[] goes to HBM once at the end.
-  uint16_t *end16 = reinterpret_cast<uint16_t *>(L.ptr);
-  uint16_t *q16 = end16 + BLD_V;
-  {
-    constexpr int VPT = BLD_V / NEMO_BLOCK;
-    uint32_t t[VPT];
-#pragma unroll
-    for (int q = 0; q < VPT; q++) {
-      const uint32_t v = tid + q * NEMO_BLOCK;
-      t[q] = v < V ? L.ptr[v] : 0u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < VPT; q++) {
-      const uint32_t v = tid + q * NEMO_BLOCK;
-      if (v < V) end16[v] = (uint16_t)t[q];
-    }
-  }
-  __syncthreads();
+  // Kahn levels over the forward rows still in LDS (ptr[v] = end of row v)
+  uint32_t *nlv = c.nlv + n0;
   for (uint32_t base = 0; base < V; base += NEMO_BLOCK) {
     const uint32_t v = base + tid;
-    const bool src = v < V && ((L.cnt[v >> 1] >> (16 * (v & 1))) & 0xFFFFu) == 0u;
+    const bool src = v < V && cnt8[v] == 0u;
     lds_append16(src, v, q16, &s_tail);
-    if (src) c.nlv[n0 + v] = 0;
+    if (src) nlv[v] = 0;
   }
   __syncthreads();
   STAMP(14);
@@ -206,19 +220,19 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
       uint32_t j = 0, je = 0;
       if (i < hi) {
         const uint32_t u = q16[i];
-        j = u ? end16[u - 1] : 0u;
-        je = end16[u];
+        j = u ? ptr[u - 1] : 0u;
+        je = ptr[u];
       }
       while (__any(j < je)) {
         bool p = false;
         uint32_t ch = 0;
         if (j < je) {
-          ch = L.col[j++];
-          const uint32_t sh = 16 * (ch & 1);
-          p = ((atomicSub(&L.cnt[ch >> 1], 1u << sh) >> sh) & 0xFFFFu) == 1u;
+          ch = col[j++];
+          const uint32_t sh = 8 * (ch & 3);
+          p = ((atomicSub(&cnt32[ch >> 2], 1u << sh) >> sh) & 0xFFu) == 1u;
         }
         lds_append16(p, ch, q16, &s_tail);
-        if (p) c.nlv[n0 + ch] = nl + 1;
+        if (p) nlv[ch] = nl + 1;
       }
     }
     __syncthreads();
@@ -252,7 +266,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
   const uint32_t g = blockIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
-  if (build_fits(c, V, E)) return;  // k_build's graph
+  if (build_fits(c, V, E) && !c.redo[g]) return;  // k_build's graph
   uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0, *rc = c.rc + e0;
   const uint32_t *es = c.esrc + e0, *ed = c.edst + e0, *word = c.word + n0;
   if (threadIdx.x == 0) {
@@ -335,7 +349,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
   if (c.err[g]) return;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0);
-  if (build_fits(c, V, (uint32_t)(c.edge_off[g + 1] - e0))) return;  // k_build's graph
+  if (build_fits(c, V, (uint32_t)(c.edge_off[g + 1] - e0)) && !c.redo[g]) return;  // k_build's graph
   const uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0;
   uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g, *cnt = c.s_a + n0 + g;
   if (threadIdx.x == 0) s_tail = 0;
@@ -384,7 +398,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
 }
 
 void launch_build(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_build, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  if (!c.bld_bytes) return;
+  hipFuncSetAttribute((const void *)k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.bld_bytes);
+  hipLaunchKernelGGL(k_build, dim3(c.G), dim3(NEMO_BLOCK), c.bld_bytes, s, c);
 }
 void launch_load(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_csr, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);

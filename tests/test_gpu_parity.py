@@ -239,3 +239,18 @@ def test_holds_before_simplify(eng, lds_max):
         assert np.array_equal(eng.flags(), orc.flags)
     finally:
         eng.set_option("graph_lds_max", -1)
+
+
+def test_build_heavy_indegree_redo(eng):
+    # a body goal shared by 300 rules: in-degree beyond k_build's u8 counters,
+    # so the graph is flagged and rebuilt by the global tier
+    goals = [{"id": "goal_hub", "label": "clock(a, b, 1, 2)", "table": "clock", "time": "1"}]
+    rules, edges = [], []
+    for i in range(300):
+        goals.append({"id": f"goal{i}", "label": f"log(a, {i}, 2)", "table": "log", "time": "2"})
+        rules.append({"id": f"rule{i}", "label": "log", "table": "log", "type": "async" if i % 3 else "next"})
+        edges += [{"from": f"goal{i}", "to": f"rule{i}"}, {"from": f"rule{i}", "to": "goal_hub"}]
+    g = {"goals": goals, "rules": rules, "edges": edges}
+    small = {"goals": goals[:3], "rules": rules[:2], "edges": edges[:4]}
+    corpus = corpus_from_graphs([(0, "success", g, small), (1, "failure", small, g)])
+    _check(eng, corpus)
