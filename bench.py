@@ -100,6 +100,7 @@ def main():
     V0 = corpus.graph_size(g0)
 
     def step():
+        # every device phase is enqueued first; host-side retrieval (which syncs) comes last
         eng.rebuild()
         eng.mark()
         eng.simplify()
@@ -107,6 +108,11 @@ def main():
         eng.protos_partial(success, d_red.data_ptr())
         if world > 1:
             dist.all_reduce(d_red)
+        eng.diffprov(failed, mode)
+        if has_run0:
+            eng.triggers()
+        eng.pull(1)
+        eng.pull(2)
         protos = eng.protos_finalize(d_red.data_ptr())
         tabs = eng.run_tables(1)
         inter = np.asarray(protos["inter"], np.int64)
@@ -115,13 +121,9 @@ def main():
         if len(fidx):
             have_i = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
             have_u = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
-        eng.diffprov(failed, mode)
         if has_run0:
-            eng.triggers()
             eng.trigger_rows()
-        eng.pull(1)
-        eng.pull(2)
-        masks = eng.diff_masks(len(failed)) if failed else None
+        masks = eng.diff_masks_view() if failed else None
         miss = eng.missing()
         flags, chain_off, chain_ht = eng.simplified_view()
         return flags, chain_off, chain_ht, masks, miss

@@ -189,6 +189,9 @@ int nemo_diffprov(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, 
 int nemo_fetch_diff_mask(nemo_ctx *ctx, uint32_t entry, uint8_t *out, uint64_t cap);
 /* D masks of every entry, entry-major (n_entries * V0 bytes).               */
 int nemo_fetch_diff_masks(nemo_ctx *ctx, uint8_t *out, uint64_t cap);
+/* Zero-copy view of every entry's D mask (n_entries x v0 bytes) in library-
+ * owned pinned memory, valid until the next nemo_diffprov.                  */
+int nemo_diff_masks_view(nemo_ctx *ctx, const uint8_t **masks, uint64_t *n_entries, uint64_t *v0);
 /* Missing rules of every entry; goals = all D-children of each rule.        */
 int nemo_fetch_missing(nemo_ctx *ctx, nemo_missing *out, uint64_t cap, uint64_t *n_out);
 

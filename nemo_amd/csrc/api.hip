@@ -85,10 +85,29 @@ struct nemo_ctx {
   uint64_t pull_hint[3] = {0, 0, 0};
   nemo::PullArgs pull_args{};
 
-  // triggers
-  bool trig_done = false;
+  // triggers: outputs sized at load from run 0's degrees (exact bounds), one
+  // launch; the row counts come back to pinned memory asynchronously
+  bool trig_done = false, trig_pending = false;
   uint32_t *d_tcounts = nullptr, *d_tpre = nullptr, *d_tpost = nullptr, *d_tasync = nullptr;
   uint32_t tcounts[3] = {0, 0, 0};
+  uint64_t tcap[3] = {0, 0, 0};
+  uint32_t *h_tcounts = nullptr;
+  hipEvent_t ev_trig = nullptr;
+
+  // pinned result hand-over, written by k_to_host (device -> pinned host)
+  uint32_t *h_red = nullptr, *h_tab = nullptr, *h_nmiss = nullptr, *h_mrows = nullptr;
+  uint8_t *h_mask = nullptr;
+  uint64_t h_red_cap = 0, h_tab_cap = 0, h_nmiss_cap = 0, h_mrows_cap = 0, h_mask_cap = 0;
+  uint32_t *h_tpre = nullptr, *h_tpost = nullptr, *h_tasync = nullptr;
+  uint64_t h_tpre_cap = 0, h_tpost_cap = 0, h_tasync_cap = 0;
+  hipEvent_t ev_protos = nullptr, ev_red = nullptr, ev_diff = nullptr, ev_misc = nullptr;
+
+  // pinned upload staging (success flags, diff sources): reused once the
+  // previous upload from the same buffer has landed (ev_up*)
+  uint8_t *h_succ = nullptr;
+  uint32_t *h_dsrc = nullptr;
+  uint64_t h_succ_cap = 0, h_dsrc_cap = 0;
+  hipEvent_t ev_up_succ = nullptr, ev_up_dsrc = nullptr;
 
   // chain gather
   uint32_t *d_chout = nullptr;
@@ -98,7 +117,7 @@ struct nemo_ctx {
   hipStream_t copy = nullptr;
   hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
   bool staged = false;
-  uint64_t staged_n = 0;
+  uint64_t staged_n = 0, staged_cap = 0, chht_hint = 0;
   uint32_t *d_chht = nullptr;
   uint64_t d_chht_cap = 0;
   uint8_t *h_flags = nullptr;
@@ -207,6 +226,11 @@ static int timed(nemo_ctx *c, const char *name, double bytes, double edges, F &&
   return NEMO_OK;
 }
 
+static int ensure_event(nemo_ctx *c, hipEvent_t *e) {
+  if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  return NEMO_OK;
+}
+
 static int run_index(nemo_ctx *c, uint32_t it, uint32_t *r) {
   auto f = c->it2run.find(it);
   if (f == c->it2run.end()) return fail(c, NEMO_ERR_NOTFOUND, "unknown run iteration %u", it);
@@ -265,11 +289,13 @@ static void release_corpus(nemo_ctx *c) {
   c->pull_slot_cap = 0;
   c->pull_which = -1;
   c->d_tcounts = c->d_tpre = c->d_tpost = c->d_tasync = nullptr;
+  c->trig_pending = false;
   c->d_chout = nullptr;
   c->d_choff = nullptr;
   c->chout_cap = 0;
   c->d_chht = nullptr;
   c->d_chht_cap = 0;
+  c->chht_hint = 0;
   c->staged = false;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
   c->mark_pending = false;
@@ -299,6 +325,17 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->h_poff) hipHostFree(c->h_poff);
   if (c->h_pcur) hipHostFree(c->h_pcur);
   if (c->ev_pull) hipEventDestroy(c->ev_pull);
+  if (c->ev_trig) hipEventDestroy(c->ev_trig);
+  if (c->ev_up_succ) hipEventDestroy(c->ev_up_succ);
+  if (c->ev_up_dsrc) hipEventDestroy(c->ev_up_dsrc);
+  if (c->h_succ) hipHostFree(c->h_succ);
+  for (void *h : {(void *)c->h_red, (void *)c->h_tab, (void *)c->h_nmiss, (void *)c->h_mrows, (void *)c->h_mask,
+                  (void *)c->h_tpre, (void *)c->h_tpost, (void *)c->h_tasync})
+    if (h) hipHostFree(h);
+  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc})
+    if (e) hipEventDestroy(e);
+  if (c->h_dsrc) hipHostFree(c->h_dsrc);
+  if (c->h_tcounts) hipHostFree(c->h_tcounts);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -590,6 +627,24 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       HIPCHK(c, hipStreamSynchronize(s));  // host vectors go out of scope
     }
   }
+  // trigger outputs of run 0: pre rows (a, g, r) <= sum over goals of in*out
+  // degree, post rows (g, r) <= edges, async rules <= nodes (corrections.go:30-34,121-125)
+  c->tcap[0] = c->tcap[1] = c->tcap[2] = 0;
+  if (c->run0 >= 0) {
+    const uint32_t gp = 2 * c->run0, gq = gp + 1;
+    const uint64_t v0 = c->node_off[gp], nv = c->node_off[gp + 1] - v0;
+    std::vector<uint32_t> din(nv, 0), dout(nv, 0);
+    for (uint64_t e = c->edge_off[gp]; e < c->edge_off[gp + 1]; e++) {
+      if (in->edge_src[e] < nv) dout[in->edge_src[e]]++;
+      if (in->edge_dst[e] < nv) din[in->edge_dst[e]]++;
+    }
+    for (uint64_t v = 0; v < nv; v++) c->tcap[0] += (uint64_t)din[v] * dout[v];
+    c->tcap[1] = c->edge_off[gq + 1] - c->edge_off[gq];
+    c->tcap[2] = nv;
+    if ((rc = dalloc(c, &c->d_tpre, 3 * c->tcap[0] + 3))) return rc;
+    if ((rc = dalloc(c, &c->d_tpost, 2 * c->tcap[1] + 2))) return rc;
+    if ((rc = dalloc(c, &c->d_tasync, c->tcap[2] + 1))) return rc;
+  }
   if ((rc = device_load(c))) return rc;
   if ((rc = check_graph_errors(c))) return rc;
   c->loaded = true;
@@ -669,7 +724,12 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   if (!c || !d_red) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_protos_partial before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<uint8_t> succ(c->n_runs, 0);
+  if (!c->ev_up_succ) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_succ, hipEventDisableTiming));
+  else HIPCHK(c, hipEventSynchronize(c->ev_up_succ));  // the previous upload has landed
+  int rg = hgrow(c, &c->h_succ, &c->h_succ_cap, std::max<uint64_t>(c->n_runs, 1));
+  if (rg) return rg;
+  uint8_t *succ = c->h_succ;
+  memset(succ, 0, c->n_runs);
   uint32_t first = NEMO_NONE;
   for (size_t i = 0; i < n_success; i++) {
     auto f = c->it2run.find(success_iters[i]);
@@ -678,7 +738,8 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
     if (i == 0) first = f->second;
   }
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->d_is_success, succ.data(), c->n_runs, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->d_is_success, succ, c->n_runs, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipEventRecord(c->ev_up_succ, s));
   HIPCHK(c, hipMemsetAsync(d_red, 0, nemo_reduce_len(c) * 4, s));
   const double V = (double)c->V, E = (double)c->E;
   int rc = timed(c, "k_proto", 8 * E + 12 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
@@ -686,7 +747,13 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   rc = timed(c, "k_reduce", (double)c->n_runs * (c->W * 8 + 8), 0,
              [&] { nemo::launch_reduce(c->dc, c->d_is_success, c->d_owned, first, d_red, s); });
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(s));  // host vector `succ` and caller's collective
+  // per-run table bitsets -> pinned host (nemo_fetch_run_tables)
+  const uint64_t rw = (uint64_t)c->n_runs * c->W;
+  if ((rc = ensure_event(c, &c->ev_protos))) return rc;
+  if ((rc = hgrow(c, &c->h_tab, &c->h_tab_cap, 2 * rw + 1))) return rc;
+  nemo::launch_to_host(c->h_tab, c->dc.proto_bits, rw * 4, s);
+  nemo::launch_to_host(c->h_tab + rw, c->dc.graph_tables, rw * 4, s);
+  HIPCHK(c, hipEventRecord(c->ev_protos, s));
   c->protos_done = true;
   return NEMO_OK;
 }
@@ -720,12 +787,16 @@ int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved,
   if (!c || !d_red) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   const uint32_t T = c->T;
-  std::vector<uint32_t> red(2 * (size_t)T + 4);
-  HIPCHK(c, hipMemcpyAsync(red.data(), d_red, red.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if ((rc = ensure_event(c, &c->ev_red))) return rc;
+  if ((rc = hgrow(c, &c->h_red, &c->h_red_cap, 2 * (uint64_t)T + 4))) return rc;
+  nemo::launch_to_host(c->h_red, d_red, (2 * (uint64_t)T + 4) * 4, c->stream);
+  HIPCHK(c, hipEventRecord(c->ev_red, c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_red));
+  const uint32_t *red = c->h_red;
   if (pre_holds) *pre_holds = red[2 * T + 2];
   if (n_runs_total) *n_runs_total = red[2 * T + 3];
-  return nemo_reduce_interpret(red.data(), T, c->table_post, achieved, inter, n_inter, uni, n_union);
+  return nemo_reduce_interpret(red, T, c->table_post, achieved, inter, n_inter, uni, n_union);
 }
 
 int nemo_prototypes(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *achieved,
@@ -744,9 +815,8 @@ int nemo_fetch_run_tables(nemo_ctx *c, int which, uint32_t *out, uint64_t cap) {
   const uint64_t n = (uint64_t)c->n_runs * c->W;
   if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)n);
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(out, which == 0 ? c->dc.proto_bits : c->dc.graph_tables, n * 4, hipMemcpyDeviceToHost,
-                           c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_protos));
+  memcpy(out, c->h_tab + (which == 0 ? 0 : n), n * 4);
   return NEMO_OK;
 }
 
@@ -782,7 +852,10 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   HIPCHK(c, hipSetDevice(c->device));
   c->n_entries = 0;
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
-  std::vector<uint32_t> src(n_failed);
+  if (!c->ev_up_dsrc) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_dsrc, hipEventDisableTiming));
+  else HIPCHK(c, hipEventSynchronize(c->ev_up_dsrc));  // the previous upload has landed
+  if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, n_failed)) return rg;
+  uint32_t *src = c->h_dsrc;
   for (size_t e = 0; e < n_failed; e++) {
     uint32_t r;
     const uint32_t it = mode == NEMO_DIFF_PER_RUN ? failed_iters[e] : failed_iters[0];
@@ -809,7 +882,8 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   }
   if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->d_dsrc, src.data(), n_failed * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->d_dsrc, src, n_failed * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
   HIPCHK(c, hipMemsetAsync(c->d_nmiss, 0, 4, s));
   nemo::DiffArgs a;
   a.g0 = g0;
@@ -826,7 +900,13 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   rc = timed(c, "k_diff", bytes, (double)n_failed * 4 * E0,
              [&] { nemo::launch_diff(c->dc, a, (uint32_t)n_failed, s); });
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(s));  // `src` host vector
+  // D masks and the missing-event count -> pinned host
+  if ((rc = ensure_event(c, &c->ev_diff))) return rc;
+  if ((rc = hgrow(c, &c->h_mask, &c->h_mask_cap, n_failed * V0))) return rc;
+  if ((rc = hgrow(c, &c->h_nmiss, &c->h_nmiss_cap, (uint64_t)1))) return rc;
+  nemo::launch_to_host(c->h_mask, c->d_dmask, n_failed * V0, s);
+  nemo::launch_to_host(c->h_nmiss, c->d_nmiss, 4, s);
+  HIPCHK(c, hipEventRecord(c->ev_diff, s));
   c->n_entries = (uint32_t)n_failed;
   return NEMO_OK;
 }
@@ -838,8 +918,8 @@ int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap
   const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
   if (cap < V0) return fail(c, NEMO_ERR_INVALID, "capacity too small");
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(out, c->d_dmask + (size_t)entry * V0, V0, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_diff));
+  memcpy(out, c->h_mask + (size_t)entry * V0, V0);
   return NEMO_OK;
 }
 
@@ -850,8 +930,21 @@ int nemo_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap) {
   const uint64_t n = (uint64_t)c->n_entries * (c->node_off[g0 + 1] - c->node_off[g0]);
   if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(out, c->d_dmask, n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_diff));
+  memcpy(out, c->h_mask, n);
+  return NEMO_OK;
+}
+
+int nemo_diff_masks_view(nemo_ctx *c, const uint8_t **masks, uint64_t *n_entries, uint64_t *v0) {
+  if (!c || !masks) return NEMO_ERR_INVALID;
+  *masks = nullptr;
+  if (n_entries) *n_entries = c->n_entries;
+  const uint32_t g0 = c->run0 >= 0 ? 2 * c->run0 + 1 : 0;
+  if (v0) *v0 = c->run0 >= 0 ? c->node_off[g0 + 1] - c->node_off[g0] : 0;
+  if (!c->n_entries) return NEMO_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventSynchronize(c->ev_diff));
+  *masks = c->h_mask;
   return NEMO_OK;
 }
 
@@ -860,16 +953,20 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
   HIPCHK(c, hipSetDevice(c->device));
   uint32_t n = 0;
   if (c->n_entries) {
-    HIPCHK(c, hipMemcpyAsync(&n, c->d_nmiss, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev_diff));
+    n = *c->h_nmiss;
   }
   if (n_out) *n_out = n;
   if (!out) return NEMO_OK;
   if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  std::vector<uint32_t> rows(2 * (size_t)n);
+  int rc;
+  if ((rc = ensure_event(c, &c->ev_misc))) return rc;
+  if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * (uint64_t)n + 2))) return rc;
+  const uint32_t *rows = c->h_mrows;
   if (n) {
-    HIPCHK(c, hipMemcpyAsync(rows.data(), c->d_miss, rows.size() * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    nemo::launch_to_host(c->h_mrows, c->d_miss, 8ull * n, c->stream);
+    HIPCHK(c, hipEventRecord(c->ev_misc, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev_misc));
   }
   std::vector<std::pair<uint32_t, uint32_t>> v(n);
   for (uint32_t i = 0; i < n; i++) v[i] = {rows[2 * i], rows[2 * i + 1]};
@@ -888,58 +985,68 @@ int nemo_triggers(nemo_ctx *c) {
   HIPCHK(c, hipSetDevice(c->device));
   c->tcounts[0] = c->tcounts[1] = c->tcounts[2] = 0;
   c->trig_done = true;
+  c->trig_pending = false;
   if (c->run0 < 0) return NEMO_OK;
   int rc;
   if (!c->d_tcounts && (rc = dalloc(c, &c->d_tcounts, 3))) return rc;
+  if (!c->h_tcounts) HIPCHK(c, hipHostMalloc((void **)&c->h_tcounts, 16));
+  if (!c->ev_trig) HIPCHK(c, hipEventCreateWithFlags(&c->ev_trig, hipEventDisableTiming));
   nemo::TrigArgs a{};
   a.g_pre = 2 * c->run0;
   a.g_post = 2 * c->run0 + 1;
   a.counts = c->d_tcounts;
-  hipStream_t s = c->stream;
-  HIPCHK(c, hipMemsetAsync(c->d_tcounts, 0, 12, s));
-  rc = timed(c, "k_triggers", 0, 0, [&] { nemo::launch_triggers(c->dc, a, 0, s); });
-  if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->tcounts, c->d_tcounts, 12, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  dfree(c, c->d_tpre);
-  dfree(c, c->d_tpost);
-  dfree(c, c->d_tasync);
-  if ((rc = dalloc(c, &c->d_tpre, 3 * (size_t)c->tcounts[0]))) return rc;
-  if ((rc = dalloc(c, &c->d_tpost, 2 * (size_t)c->tcounts[1]))) return rc;
-  if ((rc = dalloc(c, &c->d_tasync, (size_t)c->tcounts[2]))) return rc;
   a.pre = c->d_tpre;
   a.post = c->d_tpost;
   a.async_rules = c->d_tasync;
+  hipStream_t s = c->stream;
   HIPCHK(c, hipMemsetAsync(c->d_tcounts, 0, 12, s));
   rc = timed(c, "k_triggers", 0, 0, [&] { nemo::launch_triggers(c->dc, a, 1, s); });
   if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_tpre, &c->h_tpre_cap, 3 * c->tcap[0] + 3))) return rc;
+  if ((rc = hgrow(c, &c->h_tpost, &c->h_tpost_cap, 2 * c->tcap[1] + 2))) return rc;
+  if ((rc = hgrow(c, &c->h_tasync, &c->h_tasync_cap, c->tcap[2] + 1))) return rc;
+  nemo::launch_to_host(c->h_tcounts, c->d_tcounts, 12, s);
+  nemo::launch_to_host(c->h_tpre, c->d_tpre, 12 * c->tcap[0], s);
+  nemo::launch_to_host(c->h_tpost, c->d_tpost, 8 * c->tcap[1], s);
+  nemo::launch_to_host(c->h_tasync, c->d_tasync, 4 * c->tcap[2], s);
+  HIPCHK(c, hipEventRecord(c->ev_trig, s));
+  c->trig_pending = true;
   return NEMO_OK;
 }
 
+static int trig_sync(nemo_ctx *c) {
+  if (!c->trig_pending) return NEMO_OK;
+  HIPCHK(c, hipEventSynchronize(c->ev_trig));
+  for (int i = 0; i < 3; i++) {
+    if (c->h_tcounts[i] > c->tcap[i]) return fail(c, NEMO_ERR_LIMIT, "trigger rows exceed their bound");
+    c->tcounts[i] = c->h_tcounts[i];
+  }
+  c->trig_pending = false;
+  return NEMO_OK;
+}
 
 int nemo_fetch_triggers(nemo_ctx *c, uint32_t *pre, uint64_t pre_cap, uint64_t *n_pre, uint32_t *post,
                         uint64_t post_cap, uint64_t *n_post, uint32_t *async_rules, uint64_t async_cap,
                         uint64_t *n_async) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->trig_done) return fail(c, NEMO_ERR_STATE, "nemo_fetch_triggers before nemo_triggers");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rt = trig_sync(c)) return rt;
   if (n_pre) *n_pre = c->tcounts[0];
   if (n_post) *n_post = c->tcounts[1];
   if (n_async) *n_async = c->tcounts[2];
-  HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
   if (pre && c->tcounts[0]) {
     if (pre_cap < c->tcounts[0]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-    HIPCHK(c, hipMemcpyAsync(pre, c->d_tpre, 12 * (size_t)c->tcounts[0], hipMemcpyDeviceToHost, s));
+    memcpy(pre, c->h_tpre, 12 * (size_t)c->tcounts[0]);
   }
   if (post && c->tcounts[1]) {
     if (post_cap < c->tcounts[1]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-    HIPCHK(c, hipMemcpyAsync(post, c->d_tpost, 8 * (size_t)c->tcounts[1], hipMemcpyDeviceToHost, s));
+    memcpy(post, c->h_tpost, 8 * (size_t)c->tcounts[1]);
   }
   if (async_rules && c->tcounts[2]) {
     if (async_cap < c->tcounts[2]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-    HIPCHK(c, hipMemcpyAsync(async_rules, c->d_tasync, 4 * (size_t)c->tcounts[2], hipMemcpyDeviceToHost, s));
+    memcpy(async_rules, c->h_tasync, 4 * (size_t)c->tcounts[2]);
   }
-  HIPCHK(c, hipStreamSynchronize(s));
   if (pre) sort_rows<3>(pre, c->tcounts[0]);
   if (post) sort_rows<2>(post, c->tcounts[1]);
   if (async_rules) std::sort(async_rules, async_rules + c->tcounts[2]);
@@ -989,6 +1096,34 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
   return NEMO_OK;
 }
 
+// Enqueue the chain pairs at a capacity of `cap` pairs and the two bulk copies
+// (node flags, pairs) on the copy stream.
+static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
+  int rc;
+  hipStream_t s = c->stream;
+  if (2 * cap > c->d_chht_cap) {
+    HIPCHK(c, hipStreamSynchronize(s));
+    dfree(c, c->d_chht);
+    c->d_chht = nullptr;
+    c->d_chht_cap = 0;
+    if ((rc = dalloc(c, &c->d_chht, 2 * cap + 2))) return rc;
+    c->d_chht_cap = 2 * cap + 2;
+  }
+  rc = timed(c, "k_chain_pairs", 8.0 * (double)cap + 8.0 * c->G, 0,
+             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, s); });
+  if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, c->V))) return rc;
+  if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, 2 * cap + 2))) return rc;
+  nemo::launch_to_host(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, s);
+  HIPCHK(c, hipEventRecord(c->ev_ready, s));
+  HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_ready, 0));
+  if (c->V) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->dc.flags, c->V, hipMemcpyDeviceToHost, c->copy));
+  if (cap) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, 2 * cap * 4, hipMemcpyDeviceToHost, c->copy));
+  HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
+  c->staged_cap = cap;
+  return NEMO_OK;
+}
+
 int nemo_stage_simplified(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_stage_simplified before nemo_simplify");
@@ -1003,31 +1138,21 @@ int nemo_stage_simplified(nemo_ctx *c) {
   if (c->staged) HIPCHK(c, hipEventSynchronize(c->ev_copied));  // host buffers are reused
   c->staged = false;
   if (!c->d_choff && (rc = dalloc(c, &c->d_choff, (size_t)c->G + 1))) return rc;
+  if ((rc = hgrow(c, &c->h_choff, &c->h_choff_cap, (uint64_t)c->G + 1))) return rc;
   rc = timed(c, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
   if (rc) return rc;
-  if ((rc = hgrow(c, &c->h_choff, &c->h_choff_cap, (uint64_t)c->G + 1))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  const uint64_t n = c->h_choff[c->G];
-  if (2 * n > c->d_chht_cap) {
-    dfree(c, c->d_chht);
-    c->d_chht = nullptr;
-    c->d_chht_cap = 0;
-    if ((rc = dalloc(c, &c->d_chht, 2 * n + 2 * (n >> 3)))) return rc;
-    c->d_chht_cap = 2 * n + 2 * (n >> 3);
+  // the pair count is only known on the device: stage at the last count seen
+  // (no host round trip); nemo_simplified_view re-stages if it was too small
+  uint64_t cap = c->chht_hint;
+  if (!cap) {
+    if ((rc = ensure_event(c, &c->ev_misc))) return rc;
+    nemo::launch_to_host(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, s);
+    HIPCHK(c, hipEventRecord(c->ev_misc, s));
+    HIPCHK(c, hipEventSynchronize(c->ev_misc));
+    cap = c->h_choff[c->G];
   }
-  rc = timed(c, "k_chain_pairs", 8.0 * (double)n + 8.0 * c->G, 0,
-             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, s); });
-  if (rc) return rc;
-  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, c->V))) return rc;
-  if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, 2 * n))) return rc;
-  HIPCHK(c, hipEventRecord(c->ev_ready, s));
-  HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_ready, 0));
-  if (c->V) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->dc.flags, c->V, hipMemcpyDeviceToHost, c->copy));
-  if (n) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, 2 * n * 4, hipMemcpyDeviceToHost, c->copy));
-  HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
+  if ((rc = stage_enqueue(c, cap))) return rc;
   c->staged = true;
-  c->staged_n = n;
   return NEMO_OK;
 }
 
@@ -1037,6 +1162,14 @@ int nemo_simplified_view(nemo_ctx *c, const uint8_t **flags, const uint64_t **ch
   if (!c->staged) return fail(c, NEMO_ERR_STATE, "nothing staged: call nemo_stage_simplified");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipEventSynchronize(c->ev_copied));
+  const uint64_t n = c->h_choff[c->G];
+  if (n > c->staged_cap) {  // the hint was short: stage again at the real count
+    int rc = stage_enqueue(c, n);
+    if (rc) return rc;
+    HIPCHK(c, hipEventSynchronize(c->ev_copied));
+  }
+  c->chht_hint = n;
+  c->staged_n = n;
   if (flags) *flags = c->h_flags;
   if (chain_off) *chain_off = c->h_choff;
   if (chain_ht) *chain_ht = c->h_chht;
@@ -1060,9 +1193,9 @@ static int pull_launch(nemo_ctx *c) {
   // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
   int rc = timed(c, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
   if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_poff, c->d_poff, slots * 8ull, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipMemcpyAsync(c->h_pcnt, c->d_pcnt, slots * 4ull, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipMemcpyAsync(c->h_pcur, c->d_pcur, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  nemo::launch_to_host(c->h_poff, c->d_poff, slots * 8ull, s);
+  nemo::launch_to_host(c->h_pcnt, c->d_pcnt, slots * 4ull, s);
+  nemo::launch_to_host(c->h_pcur, c->d_pcur, sizeof(unsigned long long), s);
   HIPCHK(c, hipEventRecord(c->ev_pull, s));
   c->pull_synced = false;
   return NEMO_OK;

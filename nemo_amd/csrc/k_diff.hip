@@ -337,6 +337,31 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
 #undef ALIVE
 }
 
+// ---- small-result hand-over -------------------------------------------------------
+// Copies device results straight into pinned host memory with a kernel: the
+// stores cross PCIe from the CUs, so these small copies never queue behind
+// the bulk staging transfers.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_to_host(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                         uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * NEMO_BLOCK;
+  const uint64_t t = (uint64_t)blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
+    const uint64_t n16 = n >> 4;
+    for (uint64_t i = t; i < n16; i += stride) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+    for (uint64_t i = (n16 << 4) + t; i < n; i += stride) dst[i] = src[i];
+  } else {
+    for (uint64_t i = t; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  uint64_t blocks = (bytes + 16ull * NEMO_BLOCK - 1) / (16ull * NEMO_BLOCK);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_to_host, dim3((uint32_t)blocks), dim3(NEMO_BLOCK), 0, s, (uint8_t *)dst, (const uint8_t *)src,
+                     bytes);
+}
+
 // ---- run-0 trigger patterns ------------------------------------------------------
 // phase 0 counts, phase 1 writes (capacities sized from the counts).
 __global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a, int phase) {
@@ -422,16 +447,18 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chain_gather(DevCorpus c, const 
 // Dense (head, tail) pairs of every graph's accepted chains, graph g's chain k
 // at off[g] + k: with the node flags this is the whole simplified graph
 // (preprocessing.go:249-340 materialises exactly head.preds -> c -> tail.succs).
-__global__ __launch_bounds__(NEMO_BLOCK) void k_chain_pairs(DevCorpus c, const uint64_t *off, uint32_t *out) {
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chain_pairs(DevCorpus c, const uint64_t *off, uint32_t *out,
+                                                             uint64_t cap) {
   const uint32_t g = blockIdx.x;
   const uint32_t n = c.nch[g];
+  if (off[g] + n > cap) return;  // the host re-stages with the capacity off[G] asks for
   const uint32_t *ch = c.chain + 5 * c.node_off[g];
   uint2 *o = reinterpret_cast<uint2 *>(out) + off[g];
   for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) o[k] = make_uint2(ch[5 * k], ch[5 * k + 1]);
 }
 
-void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_chain_pairs, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);
+void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_pairs, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out, cap);
 }
 
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s) {

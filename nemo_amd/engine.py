@@ -73,6 +73,7 @@ def lib():
             "nemo_fetch_diff_mask": ([vp, u32, vp, u64], i32),
             "nemo_fetch_missing": ([vp, vp, u64, P(u64)], i32),
             "nemo_fetch_diff_masks": ([vp, vp, u64], i32),
+            "nemo_diff_masks_view": ([vp, vp, vp, vp], i32),
             "nemo_triggers": ([vp], i32),
             "nemo_fetch_triggers": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
             "nemo_fetch_node_flags": ([vp, u32, u32, vp, u64], i32),
@@ -263,6 +264,17 @@ class Engine:
         out = np.zeros(max(n_entries * V0, 1), np.uint8)
         self._chk(self.L.nemo_fetch_diff_masks(self.h, _p(out), n_entries * V0))
         return out[:n_entries * V0].reshape(n_entries, V0)
+
+    def diff_masks_view(self) -> np.ndarray:
+        """Zero-copy (n_entries, V0) view of the D masks in library-owned pinned memory
+        (valid until the next diffprov)."""
+        p, ne, v0 = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self.L.nemo_diff_masks_view(self.h, ctypes.byref(p), ctypes.byref(ne), ctypes.byref(v0)))
+        n = ne.value * v0.value
+        if n == 0 or not p.value:
+            return np.zeros((ne.value, v0.value), np.uint8)
+        buf = (ctypes.c_uint8 * n).from_address(p.value)
+        return np.frombuffer(buf, np.uint8).reshape(ne.value, v0.value)
 
     def missing(self) -> np.ndarray:
         n = ctypes.c_uint64()

@@ -161,6 +161,8 @@ def test_staged_simplified_views(eng):
         eng.diffprov(f, DIFF_PER_RUN)
         flags, off, ht = eng.simplified_view()
         assert np.array_equal(flags, orc.flags)
+        if f:
+            assert np.array_equal(eng.diff_masks_view(), eng.diff_masks(len(f)))
         G = corpus.n_graphs
         assert len(off) == G + 1 and int(off[-1]) == len(ht) == len(orc.chains)
         g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
