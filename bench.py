@@ -17,9 +17,9 @@ One step = the whole hot path over the rank's corpus, inputs resident in HBM:
   CreateNaiveDiffProv for every failed run (per-run label sets)  nemo_diffprov
   GenerateCorrections/Extensions trigger patterns (rank owning run 0)
   PullPrePostProv + Q24 edge pulls (device compaction of simplified + diff graphs)
-  D2H of every host-facing result: node flags + chain (head, tail) pairs (pinned,
-    async on a copy stream from right after SimplifyProv), D masks, missing events,
-    table sets, trigger rows
+  D2H of every host-facing result: 2-bit node state (alive, holds) + chain (head,
+    tail) pairs (pinned, async on a copy stream from right after SimplifyProv), D
+    masks, missing events, table sets, trigger rows
 
 Launched as `python bench.py` (N=1) or under torch.distributed.run for N>1
 (RANK/LOCAL_RANK/WORLD_SIZE from the env, backend nccl = RCCL).
@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--stage-blocks", type=int, default=0, help="bulk D2H staging by a k_to_host grid of this size (0: runtime copies)")
     return ap.parse_args()
 
 
@@ -90,6 +91,7 @@ def main():
     mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
 
     eng = Engine(local)
+    eng.set_option("stage_blocks", args.stage_blocks)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
     eng.load(corpus)
@@ -98,6 +100,8 @@ def main():
     W = (T + 31) // 32
     g0 = 2 * corpus.run_index(0) + 1
     V0 = corpus.graph_size(g0)
+
+    fidx = np.array([corpus.run_index(f) for f in failed], np.int64)  # failed runs' rows of the table sets
 
     def step():
         # every device phase is enqueued first; host-side retrieval (which syncs) comes last
@@ -117,7 +121,6 @@ def main():
         tabs = eng.run_tables(1)
         inter = np.asarray(protos["inter"], np.int64)
         uni = np.asarray(protos["union"], np.int64)
-        fidx = np.array([corpus.run_index(f) for f in failed], np.int64)
         if len(fidx):
             have_i = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
             have_u = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
@@ -125,8 +128,8 @@ def main():
             eng.trigger_rows()
         masks = eng.diff_masks_view() if failed else None
         miss = eng.missing()
-        flags, chain_off, chain_ht = eng.simplified_view()
-        return flags, chain_off, chain_ht, masks, miss
+        state, chain_off, chain_ht = eng.simplified_view()
+        return state, chain_off, chain_ht, masks, miss
 
     for _ in range(args.warmup):
         step()

@@ -209,18 +209,25 @@ int nemo_fetch_node_flags(nemo_ctx *ctx, uint32_t g_lo, uint32_t g_hi, uint8_t *
 /* Accepted @next chains of every graph, ordered by (graph, k).              */
 int nemo_fetch_chains(nemo_ctx *ctx, nemo_chain *out, uint64_t cap, uint64_t *n_out);
 /* Asynchronous hand-over of the simplification (SimplifyProv,
- * preprocessing.go:351-387) to the host: gathers every graph's accepted chains
- * as dense (head, tail) pairs (graph-local node indices; graph g's chain k at
- * chain_off[g] + k) and copies them with all node flags into library-owned
- * pinned memory on a second stream, overlapping whatever the caller launches
- * next.  Flags + pairs determine the simplified graphs exactly (collapsed rule
- * k of graph g: preds(head) -> V_g + k -> succs(tail)).                      */
+ * preprocessing.go:351-387) to the host, in the compact form a caller needs to
+ * rebuild every simplified graph: 2 bits per node (NEMO_STATE_*; node v of the
+ * corpus at byte v/4, bits 2*(v%4)) and every graph's accepted chains as dense
+ * (head, tail) pairs (graph-local node indices; graph g's chain k at
+ * chain_off[g] + k), copied into library-owned pinned memory on a second
+ * stream, overlapping whatever the caller launches next.  State + pairs
+ * determine the simplified graphs exactly (collapsed rule k of graph g:
+ * preds(head) -> V_g + k -> succs(tail)); full flags stay available through
+ * nemo_fetch_node_flags.                                                    */
+#define NEMO_STATE_ALIVE 0x1u /* node is in the simplified graph (kept, not deleted) */
+#define NEMO_STATE_HOLDS 0x2u /* condition_holds                                     */
 int nemo_stage_simplified(nemo_ctx *ctx);
-/* Waits for the staged copies and returns views into the pinned buffers
- * (flags[V], chain_off[G+1], chain_ht[2*n]); valid until the next
- * nemo_stage_simplified or nemo_ctx_destroy.  Any out-pointer may be NULL.   */
-int nemo_simplified_view(nemo_ctx *ctx, const uint8_t **flags, const uint64_t **chain_off,
-                         const uint32_t **chain_ht, uint64_t *n_chains);
+/* Waits for the staged copies and returns views into the pinned buffers:
+ * state[ceil(V/4)], chain_off[G+1] and the pairs, chain_ht[n] as u32
+ * head | tail << 16 when every graph has < 65536 nodes (*wide_pairs = 0),
+ * else chain_ht[2n] as (head, tail) u32 (*wide_pairs = 1).  Valid until the
+ * next nemo_stage_simplified or nemo_ctx_destroy.  Out-pointers may be NULL. */
+int nemo_simplified_view(nemo_ctx *ctx, const uint8_t **state, const uint64_t **chain_off,
+                         const uint32_t **chain_ht, uint64_t *n_chains, int *wide_pairs);
 /* Per-run table bitsets, words = ceil(n_tables/32) u32 per run:
  *   which = 0: proto list of the run (extractProtos, prototype.go:11-24)
  *   which = 1: all rule tables of the simplified post graph (missingFrom)   */

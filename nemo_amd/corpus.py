@@ -116,10 +116,16 @@ class Corpus:
         return int(self.node_off[g + 1] - self.node_off[g])
 
     def run_index(self, iteration: int) -> int:
-        hits = np.nonzero(self.iteration == iteration)[0]
-        if len(hits) == 0:
-            raise KeyError(f"unknown run iteration {iteration}")
-        return int(hits[0])
+        idx = getattr(self, "_run_index", None)
+        if idx is None or len(idx) != len(self.iteration):
+            idx = {}
+            for i, it in enumerate(self.iteration.tolist()):
+                idx.setdefault(int(it), i)
+            self._run_index = idx
+        try:
+            return idx[int(iteration)]
+        except KeyError:
+            raise KeyError(f"unknown run iteration {iteration}") from None
 
     def success_iters(self) -> List[int]:
         return [int(self.iteration[r]) for r in range(self.n_runs) if self.status[r] == "success"]

@@ -118,6 +118,9 @@ struct nemo_ctx {
   hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
   bool staged = false;
   uint64_t staged_n = 0, staged_cap = 0, chht_hint = 0;
+  bool pairs_wide = false;    // some graph has >= 65536 nodes: u32 pairs
+  uint32_t stage_blocks = 0;  // bulk staging: 0 = runtime copies, else k_to_host on this many blocks
+  uint32_t *d_state = nullptr;  // 2-bit node state (k_pack_state)
   uint32_t *d_chht = nullptr;
   uint64_t d_chht_cap = 0;
   uint8_t *h_flags = nullptr;
@@ -296,6 +299,7 @@ static void release_corpus(nemo_ctx *c) {
   c->d_chht = nullptr;
   c->d_chht_cap = 0;
   c->chht_hint = 0;
+  c->d_state = nullptr;
   c->staged = false;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
   c->mark_pending = false;
@@ -367,6 +371,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     }
     c->lds_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     if (c->loaded) set_lds_tier(c);
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "stage_blocks")) {
+    c->stage_blocks = value < 0 ? 0u : (uint32_t)value;
     return NEMO_OK;
   }
   if (!strcmp(name, "chains_comp_max")) {
@@ -522,6 +530,8 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   }
   if (c->node_off[0] != 0 || c->edge_off[0] != 0) return fail(c, NEMO_ERR_INVALID, "offsets must start at 0");
   c->has_rank = in->id_rank != nullptr;
+  c->pairs_wide = false;
+  for (uint32_t g = 0; g < c->G; g++) c->pairs_wide |= c->node_off[g + 1] - c->node_off[g] >= 65536;
   const size_t V = c->V, E = c->E, G = c->G, R = c->n_runs;
   DevCorpus &d = c->dc;
   int rc = 0;
@@ -1101,24 +1111,35 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
 static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
   int rc;
   hipStream_t s = c->stream;
-  if (2 * cap > c->d_chht_cap) {
+  const uint64_t pw = c->pairs_wide ? 2 : 1;  // u32 words per pair
+  if (pw * cap > c->d_chht_cap) {
     HIPCHK(c, hipStreamSynchronize(s));
     dfree(c, c->d_chht);
     c->d_chht = nullptr;
     c->d_chht_cap = 0;
-    if ((rc = dalloc(c, &c->d_chht, 2 * cap + 2))) return rc;
-    c->d_chht_cap = 2 * cap + 2;
+    if ((rc = dalloc(c, &c->d_chht, pw * cap + 2))) return rc;
+    c->d_chht_cap = pw * cap + 2;
   }
-  rc = timed(c, "k_chain_pairs", 8.0 * (double)cap + 8.0 * c->G, 0,
-             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, s); });
+  const uint64_t sbytes = 4 * ((c->V + 15) / 16);  // 2-bit node state
+  if (!c->d_state && (rc = dalloc(c, &c->d_state, sbytes / 4 + 1))) return rc;
+  rc = timed(c, "k_chain_pairs", 4.0 * pw * (double)cap + 20.0 * c->G, 0,
+             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, c->pairs_wide ? 1 : 0, s); });
   if (rc) return rc;
-  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, c->V))) return rc;
-  if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, 2 * cap + 2))) return rc;
+  rc = timed(c, "k_pack_state", (double)c->V + (double)sbytes, 0,
+             [&] { nemo::launch_pack_state(c->dc.flags, c->d_state, c->V, s); });
+  if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, sbytes + 16))) return rc;
+  if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, pw * cap + 2))) return rc;
   nemo::launch_to_host(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, s);
   HIPCHK(c, hipEventRecord(c->ev_ready, s));
   HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_ready, 0));
-  if (c->V) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->dc.flags, c->V, hipMemcpyDeviceToHost, c->copy));
-  if (cap) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, 2 * cap * 4, hipMemcpyDeviceToHost, c->copy));
+  if (c->stage_blocks) {  // CU stores into pinned memory from a small grid beside the analysis
+    nemo::launch_to_host(c->h_flags, c->d_state, sbytes, c->copy, c->stage_blocks);
+    nemo::launch_to_host(c->h_chht, c->d_chht, pw * cap * 4, c->copy, c->stage_blocks);
+  } else {  // runtime copies
+    if (sbytes) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->d_state, sbytes, hipMemcpyDeviceToHost, c->copy));
+    if (cap) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, pw * cap * 4, hipMemcpyDeviceToHost, c->copy));
+  }
   HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
   c->staged_cap = cap;
   return NEMO_OK;
@@ -1156,8 +1177,8 @@ int nemo_stage_simplified(nemo_ctx *c) {
   return NEMO_OK;
 }
 
-int nemo_simplified_view(nemo_ctx *c, const uint8_t **flags, const uint64_t **chain_off, const uint32_t **chain_ht,
-                         uint64_t *n_chains) {
+int nemo_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **chain_off, const uint32_t **chain_ht,
+                         uint64_t *n_chains, int *wide_pairs) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->staged) return fail(c, NEMO_ERR_STATE, "nothing staged: call nemo_stage_simplified");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1170,7 +1191,8 @@ int nemo_simplified_view(nemo_ctx *c, const uint8_t **flags, const uint64_t **ch
   }
   c->chht_hint = n;
   c->staged_n = n;
-  if (flags) *flags = c->h_flags;
+  if (state) *state = c->h_flags;
+  if (wide_pairs) *wide_pairs = c->pairs_wide ? 1 : 0;
   if (chain_off) *chain_off = c->h_choff;
   if (chain_ht) *chain_ht = c->h_chht;
   if (n_chains) *n_chains = c->staged_n;

@@ -52,9 +52,11 @@ void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t 
                    uint32_t *red, hipStream_t s);
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s);
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
-void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, hipStream_t s);
+void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
+                        hipStream_t s);
+void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStream_t s);
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
-void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s);
+void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 1024);
 
 }  // namespace nemo

@@ -354,10 +354,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_to_host(uint8_t *__restrict__ ds
   }
 }
 
-void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
+void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks) {
   if (!bytes) return;
   uint64_t blocks = (bytes + 16ull * NEMO_BLOCK - 1) / (16ull * NEMO_BLOCK);
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > max_blocks) blocks = max_blocks;
   hipLaunchKernelGGL(k_to_host, dim3((uint32_t)blocks), dim3(NEMO_BLOCK), 0, s, (uint8_t *)dst, (const uint8_t *)src,
                      bytes);
 }
@@ -447,18 +447,56 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chain_gather(DevCorpus c, const 
 // Dense (head, tail) pairs of every graph's accepted chains, graph g's chain k
 // at off[g] + k: with the node flags this is the whole simplified graph
 // (preprocessing.go:249-340 materialises exactly head.preds -> c -> tail.succs).
+// Pairs are (head, tail) u32 when `wide`, else packed head | tail << 16 (every
+// graph under 65536 nodes), halving the hand-over.
 __global__ __launch_bounds__(NEMO_BLOCK) void k_chain_pairs(DevCorpus c, const uint64_t *off, uint32_t *out,
-                                                             uint64_t cap) {
+                                                             uint64_t cap, int wide) {
   const uint32_t g = blockIdx.x;
   const uint32_t n = c.nch[g];
   if (off[g] + n > cap) return;  // the host re-stages with the capacity off[G] asks for
   const uint32_t *ch = c.chain + 5 * c.node_off[g];
-  uint2 *o = reinterpret_cast<uint2 *>(out) + off[g];
-  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) o[k] = make_uint2(ch[5 * k], ch[5 * k + 1]);
+  if (wide) {
+    uint2 *o = reinterpret_cast<uint2 *>(out) + off[g];
+    for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) o[k] = make_uint2(ch[5 * k], ch[5 * k + 1]);
+  } else {
+    uint32_t *o = out + off[g];
+    for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) o[k] = ch[5 * k] | (ch[5 * k + 1] << 16);
+  }
 }
 
-void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_chain_pairs, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out, cap);
+void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_pairs, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out, cap, wide);
+}
+
+// Node state for the host, 2 bits per node (4 per byte, node v at byte v/4):
+// bit 0 = the node survives into the simplified graph (KEPT, not DELETED),
+// bit 1 = condition_holds.  One thread packs 16 nodes into a u32.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pack_state(const uint8_t *__restrict__ flags, uint32_t *out,
+                                                            uint64_t V) {
+  const uint64_t w = (uint64_t)blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (16 * w >= V) return;
+  uint8_t f[16];
+  if (16 * w + 16 <= V) {
+    *reinterpret_cast<uint4 *>(f) = reinterpret_cast<const uint4 *>(flags)[w];
+  } else {
+    for (int b = 0; b < 16; b++) f[b] = 16 * w + b < V ? flags[16 * w + b] : (uint8_t)0;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const uint32_t alive = (f[b] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT;
+    const uint32_t holds = (f[b] & NEMO_F_HOLDS) != 0;
+    x |= (alive | (holds << 1)) << (2 * b);
+  }
+  out[w] = x;
+}
+
+void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStream_t s) {
+  const uint64_t words = (V + 15) / 16;
+  if (!words) return;
+  hipLaunchKernelGGL(k_pack_state, dim3((uint32_t)((words + NEMO_BLOCK - 1) / NEMO_BLOCK)), dim3(NEMO_BLOCK), 0, s,
+                     flags, out, V);
 }
 
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s) {

@@ -216,12 +216,14 @@ class Engine:
         self._chk(self.L.nemo_stage_simplified(self.h))
 
     def simplified_view(self):
-        """Zero-copy views of the staged results: (flags[V] u8, chain_off[G+1] u64,
-        chain_ht[n, 2] u32), valid until the next stage_simplified()."""
+        """Zero-copy views of the staged results: (state[ceil(V/4)] u8 with 2 bits
+        per node (NEMO_STATE_ALIVE | NEMO_STATE_HOLDS << 1), chain_off[G+1] u64,
+        chain_ht[n, 2] u16 (or u32 when a graph has >= 65536 nodes)), valid until
+        the next stage_simplified()."""
         vp = ctypes.c_void_p
-        f, o, h, n = vp(), vp(), vp(), ctypes.c_uint64()
+        f, o, h, n, w = vp(), vp(), vp(), ctypes.c_uint64(), ctypes.c_int32()
         self._chk(self.L.nemo_simplified_view(self.h, ctypes.byref(f), ctypes.byref(o), ctypes.byref(h),
-                                              ctypes.byref(n)))
+                                              ctypes.byref(n), ctypes.byref(w)))
         c = self.corpus
         V, G = int(c.node_off[-1]), c.n_graphs
 
@@ -230,10 +232,19 @@ class Engine:
                 return np.zeros(0, dtype)
             return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctype)), shape=(count,))
 
-        flags = view(f, ctypes.c_uint8, V, np.uint8)
+        state = view(f, ctypes.c_uint8, (V + 3) // 4, np.uint8)
         off = view(o, ctypes.c_uint64, G + 1, np.uint64)
-        ht = view(h, ctypes.c_uint32, 2 * n.value, np.uint32).reshape(-1, 2)
-        return flags, off, ht
+        if w.value:
+            ht = view(h, ctypes.c_uint32, 2 * n.value, np.uint32).reshape(-1, 2)
+        else:
+            ht = view(h, ctypes.c_uint16, 2 * n.value, np.uint16).reshape(-1, 2)
+        return state, off, ht
+
+    @staticmethod
+    def unpack_state(state: np.ndarray, V: int):
+        """(alive, holds) bool arrays of length V from the 2-bit staged node state."""
+        bits = np.unpackbits(state, bitorder="little")[:2 * V].reshape(V, 2)
+        return bits[:, 0].astype(bool), bits[:, 1].astype(bool)
 
     def chains(self) -> np.ndarray:
         n = ctypes.c_uint64()

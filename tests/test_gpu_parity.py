@@ -145,8 +145,8 @@ def test_large_graphs_global_paths(eng):
 
 
 def test_staged_simplified_views(eng):
-    # nemo_stage_simplified: pinned async hand-over of flags + chain (head, tail)
-    # pairs, overlapping later kernels; restaging reuses the pinned buffers
+    # nemo_stage_simplified: pinned async hand-over of the 2-bit node state and the
+    # chain (head, tail) pairs, overlapping later kernels; restaging reuses the buffers
     from tools import synth
     corpus, _ = synth.generate(30, target_nodes=2000)
     s, f = corpus.success_iters(), corpus.failed_iters()
@@ -159,15 +159,18 @@ def test_staged_simplified_views(eng):
         eng.stage_simplified()
         eng.prototypes(s)  # launched while the copies are in flight
         eng.diffprov(f, DIFF_PER_RUN)
-        flags, off, ht = eng.simplified_view()
-        assert np.array_equal(flags, orc.flags)
+        state, off, ht = eng.simplified_view()
+        from nemo_amd.corpus import F_DELETED, F_HOLDS, F_KEPT
+        alive, holds = E.Engine.unpack_state(state, len(orc.flags))
+        assert np.array_equal(alive, (orc.flags & (F_KEPT | F_DELETED)) == F_KEPT)
+        assert np.array_equal(holds, (orc.flags & F_HOLDS) != 0)
         if f:
             assert np.array_equal(eng.diff_masks_view(), eng.diff_masks(len(f)))
         G = corpus.n_graphs
         assert len(off) == G + 1 and int(off[-1]) == len(ht) == len(orc.chains)
         g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
         k = np.arange(len(ht)) - off[g].astype(np.int64)
-        got = np.stack([g, k, ht[:, 0], ht[:, 1]], 1)
+        got = np.stack([g, k, ht[:, 0].astype(np.int64), ht[:, 1].astype(np.int64)], 1)
         assert np.array_equal(got, orc.chains[:, :4].astype(np.int64))
 
 
