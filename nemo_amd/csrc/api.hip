@@ -53,6 +53,7 @@ struct nemo_ctx {
   bool has_rank = false;
   uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu, build_limit = 0xFFFFFFFFu;
   uint32_t lds_limit = 0xFFFFFFFFu;  // test knob: largest V of the LDS graph tier (0 = off)
+  uint64_t glob_min_v = 65536;       // graphs with V >= this take k_chains_glob (set before load)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
@@ -377,6 +378,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->stage_blocks = value < 0 ? 0u : (uint32_t)value;
     return NEMO_OK;
   }
+  if (!strcmp(name, "chains_glob_min_v")) {  // takes effect at the next nemo_load_corpus
+    c->glob_min_v = value < 0 ? ~0ull : (uint64_t)value;
+    return NEMO_OK;
+  }
   if (!strcmp(name, "chains_comp_max")) {
     c->comp_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.comp_limit = c->comp_limit;
@@ -568,6 +573,24 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.prehold, G);
   A(d.holdany, G);
   A(d.redo, G);
+  {
+    // deep graphs (V >= glob_min_v): k_chains_glob's per-graph scratch regions
+    std::vector<uint64_t> off(G, ~0ull);
+    uint64_t words = 0;
+    for (uint32_t g = 0; g < G; g++) {
+      const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+      if (v >= c->glob_min_v && v > 0) {
+        off[g] = words;
+        words += (nemo::glob_words(v, e) + 63) & ~63ull;
+      }
+    }
+    uint64_t *goff;
+    A(goff, G);
+    HIPCHK(c, hipMemcpy(goff, off.data(), G * 8, hipMemcpyHostToDevice));
+    d.gs_off = goff;
+    d.gscratch = nullptr;
+    if (words) A(d.gscratch, words);
+  }
   A(d.chain, 5 * V);
   A(d.chain_tmp, 5 * V);
   A(d.nch, G);

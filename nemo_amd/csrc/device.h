@@ -172,6 +172,8 @@ struct DevCorpus {
   uint32_t *prehold;                     // [G] #holding "pre" goals (pre graphs)
   uint32_t *holdany;                     // [G] 1 iff a holding goal survives simplification
   uint8_t *redo;                         // [G] k_build left the graph to the global tier
+  uint32_t *gscratch;                    // k_chains_glob scratch (deep graphs), null if none
+  const uint64_t *gs_off;                // [G] u32 offset of the graph's region, ~0 = not deep
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
   uint32_t *chain_tmp;                   // [5*V]
   uint32_t *nch;                         // [G]

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_nch, s_maxup, s_fail;
   const uint32_t g = blockIdx.x;
-  if (c.err[g]) return;
+  if (c.err[g] || c.gs_off[g] != ~0ull) return;  // deep graphs: k_chains_glob
   const GraphView gv = c.view(g);
   const uint8_t *f = gv.flags;
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_n, s_flag, s_nch, s_ncomp, s_big;
   const uint32_t g = blockIdx.x;
-  if (c.err[g] || c.nch[g] != NEMO_NONE) return;  // handled by k_chains (LDS tier)
+  if (c.err[g] || c.nch[g] != NEMO_NONE || c.gs_off[g] != ~0ull) return;  // k_chains / k_chains_glob
   const GraphView gv = c.view(g);
   uint8_t *f = gv.flags;
   uint32_t *hs = c.s_a + gv.n0 + g;                   // H* in topological order
@@ -1127,6 +1127,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
 void launch_chains(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_chains, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
   hipLaunchKernelGGL(k_chains_big, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  launch_chains_glob(c, s);
 }
 
 }  // namespace nemo

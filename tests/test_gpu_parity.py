@@ -259,3 +259,31 @@ def test_build_heavy_indegree_redo(eng):
     small = {"goals": goals[:3], "rules": rules[:2], "edges": edges[:4]}
     corpus = corpus_from_graphs([(0, "success", g, small), (1, "failure", small, g)])
     _check(eng, corpus)
+
+
+@pytest.mark.parametrize("kind", ["random", "synthetic", "branchy"])
+def test_chains_glob_tier(kind):
+    # k_chains_glob (deep-graph tier, scratch in HBM) on every graph of small corpora
+    import random as _r
+    from tests.small import random_prov
+    e = E.Engine(0)
+    try:
+        e.set_option("chains_glob_min_v", 0)
+        if kind == "random":
+            for seed in range(12):
+                corpus, _ = random_corpus(300 + seed, max_nodes=16)
+                _check(e, corpus)
+        elif kind == "synthetic":
+            from tools import synth
+            corpus, _ = synth.generate(16, target_nodes=3000)
+            _check(e, corpus, mode=DIFF_PER_RUN, pulls=True)
+        else:
+            rng = _r.Random(5)
+            graphs = []
+            for it in range(40):
+                st = "success" if it == 0 or rng.random() < 0.8 else "failure"
+                graphs.append((it, st, random_prov(rng, "pre", 40, p_edge=0.2, p_next=0.9),
+                               random_prov(rng, "post", 40, p_edge=0.2, p_next=0.9)))
+            _check(e, corpus_from_graphs(graphs))
+    finally:
+        e.close()
