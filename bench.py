@@ -46,9 +46,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--runs-per-gpu", type=int, default=10000)
-    ap.add_argument("--nodes", type=int, default=5000, help="target nodes per provenance graph")
-    ap.add_argument("--eot", type=int, default=10)
+    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
+                    help="c3: 10k runs x ~5k-node graphs per GPU (the headline line); c5: deep provenance, "
+                         "~1M-node graphs at EOT 2000")
+    ap.add_argument("--runs-per-gpu", type=int, default=None)
+    ap.add_argument("--nodes", type=int, default=None, help="target nodes per provenance graph")
+    ap.add_argument("--eot", type=int, default=None)
     ap.add_argument("--diff-mode", choices=["per_run", "reference"], default="per_run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -57,8 +60,16 @@ def parse():
     return ap.parse_args()
 
 
+CONFIGS = {"c3": {"runs": 10000, "nodes": 5000, "eot": 10, "cpu_runs": None},
+           "c5": {"runs": 128, "nodes": 1_000_000, "eot": 2000, "cpu_runs": 8}}
+
+
 def main():
     args = parse()
+    cfg = CONFIGS[args.config]
+    args.runs_per_gpu = args.runs_per_gpu or cfg["runs"]
+    args.nodes = args.nodes or cfg["nodes"]
+    args.eot = args.eot or cfg["eot"]
     import torch
     import torch.distributed as dist
 
@@ -185,15 +196,20 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
         threads = min(16, os.cpu_count() or 1)
+        sample, s_succ, s_fail, s_runs = corpus, success, failed, owned_runs
+        if cfg["cpu_runs"]:  # deep graphs: the oracle needs seconds per graph, time a bounded sample
+            sample, _ = synth.generate(cfg["cpu_runs"], target_nodes=args.nodes, eot=args.eot, threads=threads)
+            s_succ, s_fail, s_runs = sample.success_iters(), sample.failed_iters(), sample.n_runs
         reps, t_cpu = 0, 0.0
         while t_cpu < args.cpu_seconds:
             tc = time.perf_counter()
-            O.analyze(corpus, success, failed, diff_mode=mode, threads=threads, skip_pulls=True)
+            O.analyze(sample, s_succ, s_fail, diff_mode=mode, threads=threads, skip_pulls=True)
             t_cpu += time.perf_counter() - tc
             reps += 1
-        cpu = {"value": round(owned_runs * reps / t_cpu, 2), "unit": "runs/s", "cores": threads, "kind": "port",
-               "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on the same {owned_runs}-run "
-                         f"C3 corpus, {reps} full pass(es) in {t_cpu:.1f}s; same phases except the D2H/edge-list "
+        cpu = {"value": round(s_runs * reps / t_cpu, 4), "unit": "runs/s", "cores": threads, "kind": "port",
+               "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on "
+                         f"{'the same ' + str(s_runs) + '-run ' + args.config.upper() + ' corpus' if sample is corpus else str(s_runs) + ' runs of the same shape'}"
+                         f", {reps} full pass(es) in {t_cpu:.1f}s; same phases except the D2H/edge-list "
                          f"materialisation"}
     out = {
         "metric": METRIC,
@@ -208,8 +224,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance graphs "
-                               "of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated",
+        "config": {"workload": ("C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance graphs "
+                                "of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated") if args.config == "c3" else
+                               ("C5: synthetic deep-provenance corpus, runs_per_gpu runs x (pre, post) graphs of "
+                                "~nodes_per_graph nodes at EOT eot (SURVEY.md 8d), run 0 replicated"),
                    "runs_per_gpu": R, "nodes_per_graph": args.nodes, "eot": args.eot,
                    "nodes_total_rank0": int(corpus.node_off[-1]), "edges_total_rank0": int(corpus.edge_off[-1]),
                    "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,
