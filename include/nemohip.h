@@ -155,9 +155,9 @@ int nemo_simplify(nemo_ctx *ctx);
  * Every entry is a sum, so a multi-GPU job all-reduces it with ncclSum.     */
 size_t nemo_reduce_len(const nemo_ctx *ctx);
 int nemo_protos_partial(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
-                        uint32_t *d_reduce /* device, nemo_reduce_len() u32 */);
-/* Interprets a (reduced) vector: inter/union table ids, ascending, "post"
- * excluded (prototype.go:106,120).  Returns counts through n_inter/n_union;
+                        uint32_t *d_reduce /* device, nemo_reduce_len() u32; NULL = the context's own */);
+/* Interprets a (reduced) vector (d_reduce NULL = the context's own): inter/union
+ * table ids, ascending, "post" excluded (prototype.go:106,120).  Returns counts through n_inter/n_union;
  * `inter`/`uni` may be NULL to query sizes (capacity n_tables is enough).   */
 int nemo_protos_finalize(nemo_ctx *ctx, const uint32_t *d_reduce, uint32_t *achieved,
                          uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union,

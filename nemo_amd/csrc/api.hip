@@ -754,8 +754,9 @@ int nemo_simplify(nemo_ctx *c) {
 size_t nemo_reduce_len(const nemo_ctx *c) { return c ? 2 * (size_t)c->T + 4 : 0; }
 
 int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *d_red) {
-  if (!c || !d_red) return NEMO_ERR_INVALID;
+  if (!c || (!success_iters && n_success)) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_protos_partial before nemo_simplify");
+  if (!d_red) d_red = c->d_red;  // single-process callers use the context's own vector
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->ev_up_succ) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_succ, hipEventDisableTiming));
   else HIPCHK(c, hipEventSynchronize(c->ev_up_succ));  // the previous upload has landed
@@ -817,7 +818,9 @@ int nemo_reduce_interpret(const uint32_t *red, uint32_t T, uint32_t table_post, 
 int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
                          uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
                          uint32_t *n_runs_total) {
-  if (!c || !d_red) return NEMO_ERR_INVALID;
+  if (!c) return NEMO_ERR_INVALID;
+  if (!d_red) d_red = c->d_red;
+  if (!d_red) return fail(c, NEMO_ERR_STATE, "nemo_protos_finalize before nemo_load_corpus");
   HIPCHK(c, hipSetDevice(c->device));
   const uint32_t T = c->T;
   int rc;

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from nemo_amd.corpus import _molly_prefix  # noqa: E402
 from oracle import cypher_literal as CL  # noqa: E402
+from tests.golden_view import host_expected  # noqa: E402
 
 
 def G(i, table, label=None, time="1"):
@@ -142,6 +143,28 @@ def fixtures():
                  (1, "success", prov([G(0, "x")], [], []), prov(*cond_pattern("post")))],
         "check": lambda x: x["all_pre"] is True,
     }
+    # Q-TRIM-CUTSET (A.8): the receiver is strings.TrimLeft(label, table) — a cutset
+    # trim — then Trim "()" and the first ", " field.  "abba(x, 1)" with table "ab"
+    # gives "x" (a prefix trim would give "ba(x"); "ab((y), 2)" gives "y)".
+    pre = prov([G(0, "pre", time="3"), G(2, "log", "log(srv, 2)", "2"), G(4, "ab", "abba(x, 1)"),
+                G(6, "ab", "ab((y), 2)"), G(8, "leaf"), G(10, "leaf", "leaf(z, 0)")],
+               [R(1, "pre"), R(3, "log"), R(5, "tick", "next"), R(7, "snd")],
+               [E("goal0", "rule1"), E("rule1", "goal2"), E("goal2", "rule3"), E("rule3", "goal4"),
+                E("rule3", "goal6"), E("goal4", "rule5"), E("rule5", "goal8"), E("goal6", "rule7"),
+                E("rule7", "goal10")])
+    pg, pr, pe = cond_pattern("post")
+    pg[1] = G(2, "log", "log(srv, 2)", "2")
+    pg += [G(6, "ack", "ack(n, 0)", "0")]
+    pr += [R(5, "ack")]
+    pe += [E("goal4", "rule5"), E("rule5", "goal6")]
+    fx["q_trim_cutset"] = {
+        "runs": [(0, "success", pre, prov(pg, pr, pe))],
+        "check": lambda x: x["pre_rows"] and x["post_rows"] and all(
+            any("<code>x</code> needs to know that <code>srv</code>" in s for s in out)
+            and any("<code>y)</code> needs to know that <code>srv</code>" in s for s in out)
+            and any("buffer_snd(y), ...)" in s for s in out) and not any("buffer_tick" in s for s in out)
+            for out in x["corrections"]),
+    }
     return fx
 
 
@@ -186,6 +209,7 @@ def expected(runs):
         out["post_rows"] = sorted([invq[g], invq[r]] for g, r in lit["post_trig"])
         out["async"] = sorted(invp[r] for r in lit["async_rules"])
     out["all_pre"] = lit["all_pre"]
+    out.update(host_expected(lit, runs))
     return out
 
 

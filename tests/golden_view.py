@@ -1,6 +1,8 @@
 """Express oracle / engine results in the ID-keyed layout of tests/golden/*/expected.json."""
 import numpy as np
 
+from oracle import host_literal as HL
+
 from nemo_amd.corpus import F_DELETED, F_HOLDS, F_KEPT
 
 
@@ -38,3 +40,26 @@ def view(corpus, res, failed):
 
 def tables(corpus, bits):
     return sorted(corpus.tables[t] for t in range(corpus.n_tables) if (int(bits[t >> 5]) >> (t & 31)) & 1)
+
+
+def _canon_json(c):
+    nodes, edges = HL.canon(c)
+    return {"nodes": nodes, "edges": [[a, b, dict(at)] for a, b, at in edges]}
+
+
+def host_expected(lit, runs):
+    """The host side (Go) outputs: DOT graphs, missing events, corrections, extensions."""
+    db = lit["db"]
+    iters = [it for it, _, _, _ in runs]
+    dots = HL.pull_pre_post(db, iters)
+    out = {"dots": [{k: _canon_json(v) for k, v in d.items()} for d in dots]}
+    out["diff_dots"], out["failed_dots"], out["missing_events"] = [], [], []
+    for f, d in zip(lit["failed"], lit["diffs"]):
+        dd, fd = HL.create_diff_dot(db, d, f, dots[0]["post"])
+        out["diff_dots"].append(_canon_json(dd))
+        out["failed_dots"].append(_canon_json(fd))
+        out["missing_events"].append(HL.missing_records(db, d))
+    adm = HL.corrections_admissible(db, lit["pre_trig"], lit["post_trig"])
+    out["corrections"] = sorted(list(x) for x in adm) if adm is not None else None
+    out["extensions"] = HL.extensions(db, lit["async_rules"]) if not lit["all_pre"] else []
+    return out
