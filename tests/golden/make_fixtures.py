@@ -168,7 +168,7 @@ def fixtures():
     return fx
 
 
-def expected(runs):
+def expected(runs, digests=False):
     pruns = [(it, st, _molly_prefix(pre, it, "pre"), _molly_prefix(post, it, "post")) for it, st, pre, post in runs]
     lit = CL.run_reference_pipeline(pruns)
     db = lit["db"]
@@ -209,7 +209,7 @@ def expected(runs):
         out["post_rows"] = sorted([invq[g], invq[r]] for g, r in lit["post_trig"])
         out["async"] = sorted(invp[r] for r in lit["async_rules"])
     out["all_pre"] = lit["all_pre"]
-    out.update(host_expected(lit, runs))
+    out.update(host_expected(lit, runs, digests))
     return out
 
 

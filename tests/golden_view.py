@@ -1,4 +1,7 @@
 """Express oracle / engine results in the ID-keyed layout of tests/golden/*/expected.json."""
+import hashlib
+import json
+
 import numpy as np
 
 from oracle import host_literal as HL
@@ -47,8 +50,15 @@ def _canon_json(c):
     return {"nodes": nodes, "edges": [[a, b, dict(at)] for a, b, at in edges]}
 
 
-def host_expected(lit, runs):
-    """The host side (Go) outputs: DOT graphs, missing events, corrections, extensions."""
+def digest(obj) -> str:
+    """sha256 of the canonical JSON of `obj` (large DOT views are pinned by digest)."""
+    txt = json.dumps(json.loads(json.dumps(obj)), sort_keys=True, separators=(",", ":"))
+    return hashlib.sha256(txt.encode()).hexdigest()
+
+
+def host_expected(lit, runs, digests: bool = False):
+    """The host side (Go) outputs: DOT graphs, missing events, corrections, extensions.
+    With `digests`, the DOT views are stored as `<key>_sha256` digests."""
     db = lit["db"]
     iters = [it for it, _, _, _ in runs]
     dots = HL.pull_pre_post(db, iters)
@@ -62,4 +72,7 @@ def host_expected(lit, runs):
     adm = HL.corrections_admissible(db, lit["pre_trig"], lit["post_trig"])
     out["corrections"] = sorted(list(x) for x in adm) if adm is not None else None
     out["extensions"] = HL.extensions(db, lit["async_rules"]) if not lit["all_pre"] else []
+    if digests:
+        for k in ("dots", "diff_dots", "failed_dots"):
+            out[k + "_sha256"] = digest(out.pop(k))
     return out

@@ -17,7 +17,7 @@ from nemo_amd import graphing as GR
 from nemo_amd.dot import DotGraph, ProvNode, create_dot, read_dot
 from oracle import cypher_literal as CL
 from oracle import host_literal as HL
-from tests.golden_view import host_expected
+from tests.golden_view import digest, host_expected
 from tests.small import prefixed_runs, random_corpus
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -200,7 +200,7 @@ def canon_json(c):
     return {"nodes": c[0], "edges": [[a, b, dict(at)] for a, b, at in c[1]]}
 
 
-def run_mirror(corpus):
+def run_mirror(corpus, fi_dir=None):
     """main.go:106-177's graphing calls, in order."""
     db = GR.Neo4J()
     db.InitGraphDB("bolt://127.0.0.1:7687", corpus)
@@ -209,6 +209,9 @@ def run_mirror(corpus):
         s, f = corpus.success_iters(), corpus.failed_iters()
         db.LoadRawProvenance()
         db.SimplifyProv(iters)
+        hazard = None
+        if fi_dir and os.path.exists(os.path.join(fi_dir, "run_0_spacetime.dot")):
+            hazard = db.CreateHazardAnalysis(fi_dir)
         protos = db.CreatePrototypes(s, f) if s else None
         pre, post, pre_c, post_c = db.PullPrePostProv()
         diffs, faileds, missing = db.CreateNaiveDiffProv(False, f, post[0])
@@ -223,7 +226,7 @@ def run_mirror(corpus):
             "missing_events": [sorted(({"rule": m.Rule.to_json(),
                                         "goals": sorted((g.to_json() for g in m.Goals), key=lambda g: g["id"])}
                                        for m in ms), key=lambda m: m["rule"]["id"]) for ms in missing],
-            "corrections": corrections, "all_pre": all_pre, "extensions": sorted(extensions),
+            "corrections": corrections, "all_pre": all_pre, "extensions": sorted(extensions), "hazard": hazard,
             "strings": [x.string() for x in pre + post + pre_c + post_c + diffs + faileds]}
 
 
@@ -236,9 +239,11 @@ def _norm_missing(ms):
 
 
 def assert_host_equal(got, exp, success):
-    assert json.loads(json.dumps(got["dots"])) == exp["dots"]
-    assert json.loads(json.dumps(got["diff_dots"])) == exp["diff_dots"]
-    assert json.loads(json.dumps(got["failed_dots"])) == exp["failed_dots"]
+    for k in ("dots", "diff_dots", "failed_dots"):
+        if k in exp:
+            assert json.loads(json.dumps(got[k])) == exp[k], k
+        else:
+            assert digest(got[k]) == exp[k + "_sha256"], k
     assert [_norm_missing(m) for m in got["missing_events"]] == [_norm_missing(m) for m in exp["missing_events"]]
     if exp["corrections"] is not None:
         assert got["corrections"] in exp["corrections"]
@@ -265,8 +270,18 @@ def test_mirror_fixture_gpu(name):
     d = os.path.join(HERE, name)
     exp = json.load(open(os.path.join(d, "expected.json")))
     corpus = load_molly(d)
-    got = run_mirror(corpus)
+    got = run_mirror(corpus, d)
     assert_host_equal(got, exp, bool(corpus.success_iters()))
+    if got["hazard"] is not None:  # hazard-analysis.go:39-80 on the producer's space-time diagrams
+        assert len(got["hazard"]) == corpus.n_runs
+        for r, g in enumerate(got["hazard"]):
+            pre, post = GR.time_holds(corpus.runs[r], "pre"), GR.time_holds(corpus.runs[r], "post")
+            for name, attrs in g.nodes.items():
+                t = name.split("_")[-1]
+                assert attrs["style"] == '"solid, filled"'
+                assert attrs["color"] == ('"firebrick"' if t in pre else '"lightgrey"')
+                assert attrs["fillcolor"] == ('"deepskyblue"' if t in post else
+                                              '"firebrick"' if t in pre else '"lightgrey"')
 
 
 @pytest.mark.gpu
