@@ -5,7 +5,10 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -Wno-unused-value
 BUILD := build
 SRCS := $(wildcard nemo_amd/csrc/*.hip)
-OBJS := $(patsubst nemo_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS))
+HOST_SRCS := $(wildcard nemo_amd/csrc/*.cpp)
+OBJS := $(patsubst nemo_amd/csrc/%.hip,$(BUILD)/%.o,$(SRCS)) $(patsubst nemo_amd/csrc/%.cpp,$(BUILD)/%.host.o,$(HOST_SRCS))
+CXX_HOST ?= g++
+HOSTFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall
 HDRS := $(wildcard nemo_amd/csrc/*.h) include/nemohip.h
 LIB := nemo_amd/libnemohip.so
 
@@ -15,8 +18,13 @@ $(BUILD)/%.o: nemo_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+# host-only parts of the library (native Molly ingest)
+$(BUILD)/%.host.o: nemo_amd/csrc/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(CXX_HOST) $(HOSTFLAGS) -c -o $@ $<
+
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -pthread
 
 # diagnostic build with in-kernel phase stamps (never shipped as libnemohip.so)
 stamps: $(SRCS) $(HDRS)

@@ -244,6 +244,31 @@ uint64_t nemo_pulled_count(nemo_ctx *ctx, uint32_t slot);
 int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap,
                       uint64_t *n_out);
 
+/* ---- native ingest of a Molly output directory (host only) ------------------
+ * Replaces Molly.LoadOutput's per-run JSON decoding (faultinjectors/molly.go:
+ * 15-163) and the per-element interning of loadProv (pre-post-prov.go:25-213)
+ * for callers that want the corpus arrays without a Go/Python decoding pass:
+ * run_<i>_{pre,post}_provenance.json of runs i = 0..n_runs-1 are parsed on
+ * `threads` threads (<= 0: up to 16) and interned in the order the sequential
+ * loader would intern them.  `iterations[i]` is runs.json's Run.Iteration of
+ * run i (the caller parses runs.json).  Validation failures return
+ * NEMO_ERR_LOAD with the reference's message in `err`.  Node IDs are returned
+ * without the run_<iteration>_<cond>_ prefix molly.go adds (it is common to a
+ * graph, so id_rank is unaffected).                                          */
+typedef struct nemo_ingest nemo_ingest;
+#define NEMO_STR_TABLE     0  /* interned table names  (index < n_tables)      */
+#define NEMO_STR_LABEL     1  /* interned labels                               */
+#define NEMO_STR_NODE_ID   2  /* per node: Molly ID (unprefixed)               */
+#define NEMO_STR_NODE_TYPE 3  /* per node: rule type ("" for goals)            */
+#define NEMO_STR_NODE_TIME 4  /* per node: goal time after the clock rewrite   */
+int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
+                      nemo_ingest **out, char *err, size_t err_cap);
+/* Pointers into the ingest's arrays (valid until nemo_ingest_free); ready for nemo_load_corpus. */
+int nemo_ingest_corpus(const nemo_ingest *h, nemo_corpus *corpus);
+uint64_t nemo_ingest_count(const nemo_ingest *h, int kind);
+int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index, const char **s, size_t *len);
+void nemo_ingest_free(nemo_ingest *h);
+
 /* ---- instrumentation ------------------------------------------------------ */
 typedef struct nemo_timing {
   char name[32];      /* kernel name                                        */

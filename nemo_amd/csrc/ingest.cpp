@@ -1,0 +1,646 @@
+// Multi-threaded native ingest of a Molly output directory:
+// faultinjectors/molly.go:15-163 (LoadOutput: per-run provenance files, clock
+// times from labels, run_<iteration>_<cond>_ ID prefixes) fused with the
+// interning that replaces loadProv's per-element CREATE/MERGE round trips
+// (graphing/pre-post-prov.go:25-213), producing the nemo_corpus arrays.
+//
+// Graphs are parsed in parallel (one file per task); strings are interned per
+// graph in first-appearance order and merged into the global table/label ids
+// in graph order, so the result is identical to the sequential interning of
+// nemo_amd/corpus.py (tests/test_ingest.py checks it array for array).
+// Host code only; no device work.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/nemohip.h"
+
+namespace {
+
+struct Str {
+  uint32_t off, len;
+};
+
+struct Graph {
+  std::vector<char> arena;   // decoded strings of this graph
+  std::vector<Str> id, label, table, type, time;
+  uint32_t n_goals = 0;
+  std::vector<uint32_t> src, dst, rank, ltab, llab;
+  std::vector<uint8_t> tclass;
+  std::vector<Str> tabs, labs;  // local first-appearance order
+  std::string err;
+  std::string_view sv(Str s) const { return std::string_view(arena.data() + s.off, s.len); }
+};
+
+// ---- open-addressing tables (the per-graph maps are hot: one lookup per node and edge) ----
+inline uint64_t hash_sv(std::string_view s) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ s.size();
+  size_t i = 0;
+  for (; i + 8 <= s.size(); i += 8) {
+    uint64_t w;
+    memcpy(&w, s.data() + i, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  uint64_t w = 0;
+  memcpy(&w, s.data() + i, s.size() - i);
+  h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 29);
+}
+
+struct FlatMap {  // string_view -> u32, keys live in the graph's arena
+  std::vector<std::string_view> key;
+  std::vector<uint32_t> val;
+  size_t mask = 0;
+  void init(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    key.assign(cap, std::string_view());
+    val.assign(cap, ~0u);
+    mask = cap - 1;
+  }
+  // value of k, inserting v if absent; second = inserted
+  std::pair<uint32_t, bool> emplace(std::string_view k, uint32_t v) {
+    for (size_t h = hash_sv(k) & mask;; h = (h + 1) & mask) {
+      if (val[h] == ~0u) {
+        key[h] = k, val[h] = v;
+        return {v, true};
+      }
+      if (key[h] == k) return {val[h], false};
+    }
+  }
+  uint32_t find(std::string_view k) const {
+    for (size_t h = hash_sv(k) & mask;; h = (h + 1) & mask) {
+      if (val[h] == ~0u) return ~0u;
+      if (key[h] == k) return val[h];
+    }
+  }
+};
+
+struct FlatSet64 {
+  std::vector<uint64_t> slot;  // key + 1, 0 = empty
+  size_t mask = 0;
+  void init(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    slot.assign(cap, 0);
+    mask = cap - 1;
+  }
+  bool insert(uint64_t k) {
+    k += 1;
+    for (size_t h = ((k * 0x9E3779B97F4A7C15ull) >> 20) & mask;; h = (h + 1) & mask) {
+      if (!slot[h]) return slot[h] = k, true;
+      if (slot[h] == k) return false;
+    }
+  }
+};
+
+// ---- a schema-directed JSON reader (encoding/json semantics for the fields used) ----
+struct Json {
+  const char *p, *e;
+  bool ok = true;
+  std::vector<char> key;  // scratch for object keys (capacity reused)
+
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) p++;
+  }
+  bool lit(const char *s) {
+    size_t n = strlen(s);
+    if ((size_t)(e - p) >= n && !memcmp(p, s, n)) {
+      p += n;
+      return true;
+    }
+    return false;
+  }
+  static int hex(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  static void utf8(std::vector<char> &o, uint32_t cp) {
+    if (cp < 0x80) {
+      o.push_back((char)cp);
+    } else if (cp < 0x800) {
+      o.push_back((char)(0xC0 | (cp >> 6)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      o.push_back((char)(0xE0 | (cp >> 12)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      o.push_back((char)(0xF0 | (cp >> 18)));
+      o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  uint32_t u4() {
+    if (e - p < 4) return ok = false, 0;
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) {
+      int h = hex(p[i]);
+      if (h < 0) return ok = false, 0;
+      v = v * 16 + h;
+    }
+    p += 4;
+    return v;
+  }
+  // string into `o` (appended); returns false on error
+  bool str(std::vector<char> &o) {
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    p++;
+    while (p < e) {
+      const char *q = p;
+      while (q < e && *q != '"' && *q != '\\') q++;
+      o.insert(o.end(), p, q);
+      p = q;
+      if (p >= e) break;
+      if (*p == '"') {
+        p++;
+        return true;
+      }
+      p++;  // backslash
+      if (p >= e) break;
+      char c = *p++;
+      switch (c) {
+        case '"': o.push_back('"'); break;
+        case '\\': o.push_back('\\'); break;
+        case '/': o.push_back('/'); break;
+        case 'b': o.push_back('\b'); break;
+        case 'f': o.push_back('\f'); break;
+        case 'n': o.push_back('\n'); break;
+        case 'r': o.push_back('\r'); break;
+        case 't': o.push_back('\t'); break;
+        case 'u': {
+          uint32_t cp = u4();
+          if (cp >= 0xD800 && cp < 0xDC00 && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char *save = p;
+            p += 2;
+            uint32_t lo = u4();
+            if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            else p = save, cp = 0xFFFD;
+          } else if (cp >= 0xD800 && cp < 0xE000) {
+            cp = 0xFFFD;  // lone surrogate: encoding/json substitutes U+FFFD
+          }
+          utf8(o, cp);
+          break;
+        }
+        default: return ok = false;
+      }
+    }
+    return ok = false;
+  }
+  void skip() {
+    ws();
+    if (p >= e) {
+      ok = false;
+      return;
+    }
+    char c = *p;
+    if (c == '"') {
+      std::vector<char> tmp;
+      str(tmp);
+    } else if (c == '{' || c == '[') {
+      char close = c == '{' ? '}' : ']';
+      p++;
+      ws();
+      if (p < e && *p == close) {
+        p++;
+        return;
+      }
+      while (ok) {
+        if (c == '{') {
+          std::vector<char> k;
+          if (!str(k)) return;
+          ws();
+          if (p >= e || *p != ':') {
+            ok = false;
+            return;
+          }
+          p++;
+        }
+        skip();
+        ws();
+        if (p < e && *p == ',') {
+          p++;
+          continue;
+        }
+        if (p < e && *p == close) {
+          p++;
+          return;
+        }
+        ok = false;
+      }
+    } else if (lit("true") || lit("false") || lit("null")) {
+    } else {
+      const char *q = p;
+      while (p < e && (strchr("+-0123456789.eE", *p) != nullptr)) p++;
+      if (p == q) ok = false;
+    }
+  }
+};
+
+bool ieq(const std::vector<char> &k, const char *s) {
+  size_t n = strlen(s);
+  if (k.size() != n) return false;
+  for (size_t i = 0; i < n; i++)
+    if (tolower((unsigned char)k[i]) != s[i]) return false;  // encoding/json matches keys case-insensitively
+  return true;
+}
+
+// ", <digits>, __WILDCARD__)" and ", <digits>, <digits>)" (molly.go:74-89): leftmost match, group 1
+bool clock_time(std::string_view s, bool wild, std::string &out) {
+  for (size_t i = 0; i + 2 <= s.size(); i++) {
+    if (s[i] != ',' || s[i + 1] != ' ') continue;
+    size_t j = i + 2, d0 = j;
+    while (j < s.size() && isdigit((unsigned char)s[j])) j++;
+    if (j == d0 || j + 2 > s.size() || s[j] != ',' || s[j + 1] != ' ') continue;
+    size_t k = j + 2;
+    if (wild) {
+      if (s.substr(k, 13) != "__WILDCARD__)") continue;
+    } else {
+      size_t k0 = k;
+      while (k < s.size() && isdigit((unsigned char)s[k])) k++;
+      if (k == k0 || k >= s.size() || s[k] != ')') continue;
+    }
+    out.assign(s.data() + d0, j - d0);
+    return true;
+  }
+  return false;
+}
+
+bool read_file(const std::string &path, std::vector<char> &buf) {
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  buf.resize(n > 0 ? (size_t)n : 0);
+  size_t got = n > 0 ? fread(buf.data(), 1, (size_t)n, f) : 0;
+  fclose(f);
+  return got == buf.size();
+}
+
+uint8_t type_class(std::string_view t) {
+  return t == "next" ? NEMO_TYPE_NEXT : t == "async" ? NEMO_TYPE_ASYNC : NEMO_TYPE_OTHER;
+}
+
+void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g) {
+  std::vector<char> buf;
+  if (!read_file(path, buf)) {
+    g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
+            " provenance of file '" + path + "'";
+    return;
+  }
+  g.arena.reserve(2 * buf.size() + 64);  // decoded strings <= file; clock times <= their labels: no reallocation
+  Json j{buf.data(), buf.data() + buf.size()};
+  struct Rec {
+    Str f[4];
+  };
+  std::vector<Rec> goals, rules;
+  std::vector<std::pair<Str, Str>> edges;
+  j.ws();
+  if (j.lit("null")) {
+  } else if (j.p < j.e && *j.p == '{') {
+    j.p++;
+    j.ws();
+    if (j.p < j.e && *j.p == '}') j.p++;
+    else
+      while (j.ok) {
+        std::vector<char> &key = j.key;
+        key.clear();
+        if (!j.str(key)) break;
+        j.ws();
+        if (j.p >= j.e || *j.p != ':') {
+          j.ok = false;
+          break;
+        }
+        j.p++;
+        int which = ieq(key, "goals") ? 0 : ieq(key, "rules") ? 1 : ieq(key, "edges") ? 2 : -1;
+        j.ws();
+        if (which < 0 || j.lit("null")) {
+          if (which < 0) j.skip();
+        } else if (j.p < j.e && *j.p == '[') {
+          j.p++;
+          j.ws();
+          if (j.p < j.e && *j.p == ']') j.p++;
+          else
+            while (j.ok) {
+              j.ws();
+              if (j.p >= j.e || *j.p != '{') {
+                j.ok = false;
+                break;
+              }
+              j.p++;
+              Rec r{};
+              std::pair<Str, Str> ed{};
+              j.ws();
+              if (j.p < j.e && *j.p == '}') j.p++;
+              else
+                while (j.ok) {
+                  std::vector<char> &k = j.key;
+                  k.clear();
+                  if (!j.str(k)) break;
+                  j.ws();
+                  if (j.p >= j.e || *j.p != ':') {
+                    j.ok = false;
+                    break;
+                  }
+                  j.p++;
+                  static const char *gk[4] = {"id", "label", "table", "time"};
+                  static const char *rk[4] = {"id", "label", "table", "type"};
+                  int f = -1;
+                  if (which == 2) f = ieq(k, "from") ? 0 : ieq(k, "to") ? 1 : -1;
+                  else
+                    for (int q = 0; q < 4; q++)
+                      if (ieq(k, which == 0 ? gk[q] : rk[q])) f = q;
+                  j.ws();
+                  if (f < 0) {
+                    j.skip();
+                  } else if (j.lit("null")) {
+                  } else {
+                    Str s{(uint32_t)g.arena.size(), 0};
+                    if (!j.str(g.arena)) break;  // decoded straight into the arena (reserved: no reallocation)
+                    s.len = (uint32_t)(g.arena.size() - s.off);
+                    if (which == 2) (f == 0 ? ed.first : ed.second) = s;
+                    else r.f[f] = s;
+                  }
+                  j.ws();
+                  if (j.p < j.e && *j.p == ',') {
+                    j.p++;
+                    continue;
+                  }
+                  if (j.p < j.e && *j.p == '}') {
+                    j.p++;
+                    break;
+                  }
+                  j.ok = false;
+                }
+              if (which == 0) goals.push_back(r);
+              else if (which == 1) rules.push_back(r);
+              else edges.push_back(ed);
+              j.ws();
+              if (j.p < j.e && *j.p == ',') {
+                j.p++;
+                continue;
+              }
+              if (j.p < j.e && *j.p == ']') {
+                j.p++;
+                break;
+              }
+              j.ok = false;
+            }
+        } else {
+          j.ok = false;
+        }
+        j.ws();
+        if (j.p < j.e && *j.p == ',') {
+          j.p++;
+          continue;
+        }
+        if (j.p < j.e && *j.p == '}') {
+          j.p++;
+          break;
+        }
+        j.ok = false;
+      }
+  } else {
+    j.ok = false;
+  }
+  j.ws();
+  if (!j.ok || j.p != j.e) {
+    g.err = std::string("Failed to unmarshal JSON ") + (cond == std::string("pre") ? "antecedent" : "consequent") +
+            " provenance data: " + path;
+    return;
+  }
+  const size_t V = goals.size() + rules.size();
+  g.n_goals = (uint32_t)goals.size();
+  g.id.reserve(V), g.label.reserve(V), g.table.reserve(V), g.type.reserve(V), g.time.reserve(V);
+  FlatMap gidx, ridx, tabs, labs;
+  gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
+  auto intern = [&](FlatMap &m, std::vector<Str> &order, Str s) {
+    if (order.size() * 2 + 16 > m.mask) {  // grow: rehash the distinct keys seen so far
+      m.init(order.size() * 2 + 16);
+      for (uint32_t i = 0; i < order.size(); i++) m.emplace(g.sv(order[i]), i);
+    }
+    auto it = m.emplace(g.sv(s), (uint32_t)order.size());
+    if (it.second) order.push_back(s);
+    return it.first;
+  };
+  for (auto &r : goals) {
+    if (!gidx.emplace(g.sv(r.f[0]), (uint32_t)g.id.size()).second) {
+      g.err = "Run " + std::to_string(iteration) + ": duplicate goal id run_" + std::to_string(iteration) + "_" +
+              cond + "_" + std::string(g.sv(r.f[0])) + " (Goal.id IS UNIQUE, pre-post-prov.go:68)";
+      return;
+    }
+    Str t = r.f[3];
+    if (g.sv(r.f[2]) == "clock") {  // molly.go:74-89
+      std::string tm;
+      std::string_view lab = g.sv(r.f[1]);
+      bool hit = clock_time(lab, true, tm);
+      std::string tm2;
+      if (clock_time(lab, false, tm2)) tm = tm2, hit = true;
+      if (hit) {
+        t = Str{(uint32_t)g.arena.size(), (uint32_t)tm.size()};
+        g.arena.insert(g.arena.end(), tm.begin(), tm.end());
+      }
+    }
+    g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(Str{0, 0});
+    g.time.push_back(t);
+    g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
+    g.llab.push_back(intern(labs, g.labs, r.f[1]));
+    g.tclass.push_back(0);
+  }
+  for (auto &r : rules) {
+    if (!ridx.emplace(g.sv(r.f[0]), (uint32_t)g.id.size()).second) {
+      g.err = "Run " + std::to_string(iteration) + ": duplicate rule id run_" + std::to_string(iteration) + "_" +
+              cond + "_" + std::string(g.sv(r.f[0])) + " (Rule.id IS UNIQUE, pre-post-prov.go:129)";
+      return;
+    }
+    g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(r.f[3]);
+    g.time.push_back(Str{0, 0});
+    g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
+    g.llab.push_back(intern(labs, g.labs, r.f[1]));
+    g.tclass.push_back(type_class(g.sv(r.f[3])));
+  }
+  // rank of each node's ID inside the graph (the prefix is common, so unprefixed order == prefixed order)
+  std::vector<uint32_t> order(V);
+  for (uint32_t i = 0; i < V; i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return g.sv(g.id[a]) < g.sv(g.id[b]); });
+  g.rank.assign(V, 0);
+  for (uint32_t pos = 0; pos < V; pos++) g.rank[order[pos]] = pos;
+  FlatSet64 seen;
+  seen.init(edges.size());
+  size_t created = 0;
+  g.src.reserve(edges.size()), g.dst.reserve(edges.size());
+  for (auto &ed : edges) {
+    std::string_view f = g.sv(ed.first), t = g.sv(ed.second);
+    uint32_t u, v;
+    if (f.find("goal") != std::string_view::npos) {  // strings.Contains(From, "goal") (pre-post-prov.go:173)
+      u = gidx.find(f), v = ridx.find(t);
+    } else {
+      u = ridx.find(f), v = gidx.find(t);
+    }
+    if (u == ~0u || v == ~0u || !seen.insert(((uint64_t)u << 32) | v)) continue;
+    g.src.push_back(u), g.dst.push_back(v);
+    created++;
+  }
+  if (created != edges.size())
+    g.err = "Run " + std::to_string(iteration) + ": inserted number of edges (" + std::to_string(created) +
+            ") does not equal number of antecedent provenance edges (" + std::to_string(edges.size()) + ")";
+}
+
+}  // namespace
+
+struct nemo_ingest {
+  std::vector<Graph> graphs;  // 2r = pre, 2r+1 = post
+  std::vector<uint32_t> iteration;
+  std::vector<uint64_t> node_off, edge_off;
+  std::vector<uint32_t> word, label, rank, src, dst;
+  std::vector<std::string> tables, labels;
+  uint32_t table_pre = 0, table_post = 0;
+};
+
+extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
+                                 nemo_ingest **out, char *err, size_t err_cap) {
+  auto fail = [&](const std::string &m) {
+    if (err && err_cap) snprintf(err, err_cap, "%s", m.c_str());
+    return NEMO_ERR_LOAD;
+  };
+  if (!out_dir || !out || (n_runs && !iterations)) return NEMO_ERR_INVALID;
+  auto *h = new nemo_ingest();
+  h->iteration.assign(iterations, iterations + n_runs);
+  const uint32_t G = 2 * n_runs;
+  h->graphs.resize(G);
+  int nt = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  nt = std::max(1, std::min<int>(nt, (int)std::max<uint32_t>(G, 1)));
+  std::atomic<uint32_t> next{0};
+  auto work = [&] {
+    for (uint32_t g; (g = next.fetch_add(1)) < G;) {
+      const uint32_t r = g / 2;
+      const char *cond = g % 2 ? "post" : "pre";
+      // file name by index, ID prefix by iteration (molly.go:59-60 vs :92)
+      std::string path = std::string(out_dir) + "/run_" + std::to_string(r) + "_" + cond + "_provenance.json";
+      parse_graph(path, h->iteration[r], cond, h->graphs[g]);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; i++) pool.emplace_back(work);
+  work();
+  for (auto &t : pool) t.join();
+  for (uint32_t g = 0; g < G; g++)
+    if (!h->graphs[g].err.empty()) {
+      std::string m = h->graphs[g].err;
+      delete h;
+      return fail(m);
+    }
+  // global interning in graph order (== the sequential first-appearance order)
+  std::unordered_map<std::string, uint32_t> tmap, lmap;
+  std::vector<std::vector<uint32_t>> tre(G), lre(G);
+  h->node_off.assign(G + 1, 0);
+  h->edge_off.assign(G + 1, 0);
+  for (uint32_t g = 0; g < G; g++) {
+    Graph &gr = h->graphs[g];
+    for (Str s : gr.tabs) {
+      auto it = tmap.emplace(std::string(gr.sv(s)), (uint32_t)h->tables.size());
+      if (it.second) h->tables.emplace_back(gr.sv(s));
+      tre[g].push_back(it.first->second);
+    }
+    for (Str s : gr.labs) {
+      auto it = lmap.emplace(std::string(gr.sv(s)), (uint32_t)h->labels.size());
+      if (it.second) h->labels.emplace_back(gr.sv(s));
+      lre[g].push_back(it.first->second);
+    }
+    h->node_off[g + 1] = h->node_off[g] + gr.id.size();
+    h->edge_off[g + 1] = h->edge_off[g] + gr.src.size();
+  }
+  for (const char *c : {"pre", "post"}) {
+    auto it = tmap.emplace(c, (uint32_t)h->tables.size());
+    if (it.second) h->tables.emplace_back(c);
+    (c[1] == 'r' ? h->table_pre : h->table_post) = it.first->second;
+  }
+  if (h->tables.size() > NEMO_MAX_TABLES) {
+    delete h;
+    return fail("more than NEMO_MAX_TABLES distinct tables");
+  }
+  const uint64_t V = h->node_off[G], E = h->edge_off[G];
+  h->word.resize(V), h->label.resize(V), h->rank.resize(V), h->src.resize(E), h->dst.resize(E);
+  next = 0;
+  auto fill = [&] {
+    for (uint32_t g; (g = next.fetch_add(1)) < G;) {
+      const Graph &gr = h->graphs[g];
+      const uint64_t n0 = h->node_off[g], e0 = h->edge_off[g];
+      for (size_t i = 0; i < gr.id.size(); i++) {
+        h->word[n0 + i] = NEMO_WORD(i >= gr.n_goals, gr.tclass[i], tre[g][gr.ltab[i]]);
+        h->label[n0 + i] = lre[g][gr.llab[i]];
+        h->rank[n0 + i] = gr.rank[i];
+      }
+      std::copy(gr.src.begin(), gr.src.end(), h->src.begin() + e0);
+      std::copy(gr.dst.begin(), gr.dst.end(), h->dst.begin() + e0);
+    }
+  };
+  pool.clear();
+  for (int i = 1; i < nt; i++) pool.emplace_back(fill);
+  fill();
+  for (auto &t : pool) t.join();
+  *out = h;
+  return NEMO_OK;
+}
+
+extern "C" int nemo_ingest_corpus(const nemo_ingest *h, nemo_corpus *c) {
+  if (!h || !c) return NEMO_ERR_INVALID;
+  memset(c, 0, sizeof(*c));
+  c->n_runs = (uint32_t)h->iteration.size();
+  c->n_tables = (uint32_t)h->tables.size();
+  c->table_pre = h->table_pre;
+  c->table_post = h->table_post;
+  c->iteration = h->iteration.data();
+  c->owned = nullptr;
+  c->node_off = h->node_off.data();
+  c->edge_off = h->edge_off.data();
+  c->node_word = h->word.data();
+  c->label = h->label.data();
+  c->id_rank = h->rank.data();
+  c->edge_src = h->src.data();
+  c->edge_dst = h->dst.data();
+  return NEMO_OK;
+}
+
+extern "C" uint64_t nemo_ingest_count(const nemo_ingest *h, int kind) {
+  if (!h) return 0;
+  if (kind == NEMO_STR_TABLE) return h->tables.size();
+  if (kind == NEMO_STR_LABEL) return h->labels.size();
+  return h->node_off.empty() ? 0 : h->node_off.back();
+}
+
+extern "C" int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index, const char **s, size_t *len) {
+  if (!h || !s || !len) return NEMO_ERR_INVALID;
+  if (kind == NEMO_STR_TABLE || kind == NEMO_STR_LABEL) {
+    const auto &v = kind == NEMO_STR_TABLE ? h->tables : h->labels;
+    if (index >= v.size()) return NEMO_ERR_INVALID;
+    *s = v[index].data();
+    *len = v[index].size();
+    return NEMO_OK;
+  }
+  if (h->node_off.empty() || index >= h->node_off.back()) return NEMO_ERR_INVALID;
+  const uint32_t g = (uint32_t)(std::upper_bound(h->node_off.begin(), h->node_off.end(), index) - h->node_off.begin() - 1);
+  const Graph &gr = h->graphs[g];
+  const size_t i = index - h->node_off[g];
+  Str st = kind == NEMO_STR_NODE_ID ? gr.id[i] : kind == NEMO_STR_NODE_TYPE ? gr.type[i] : kind == NEMO_STR_NODE_TIME ? gr.time[i] : Str{0, 0};
+  if (kind < NEMO_STR_NODE_ID || kind > NEMO_STR_NODE_TIME) return NEMO_ERR_INVALID;
+  *s = gr.arena.data() + st.off;
+  *len = st.len;
+  return NEMO_OK;
+}
+
+extern "C" void nemo_ingest_free(nemo_ingest *h) { delete h; }

@@ -1,0 +1,96 @@
+"""Native Molly ingest (nemo_ingest_molly) against the Python
+loader (nemo_amd/corpus.load_molly): identical arrays, strings and errors.
+Host only: runs without a GPU."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from nemo_amd.corpus import LoadError, load_molly
+from nemo_amd.ingest import load_molly_native
+from tests.small import random_prov
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(d for d in os.listdir(HERE) if os.path.isfile(os.path.join(HERE, d, "runs.json")))
+
+
+def assert_same(a, b):
+    for k in ("iteration", "node_off", "edge_off", "node_word", "label", "edge_src", "edge_dst", "id_rank"):
+        assert np.array_equal(np.asarray(getattr(a, k)), np.asarray(getattr(b, k))), k
+    assert (a.n_tables, a.table_pre, a.table_post) == (b.n_tables, b.table_pre, b.table_post)
+    assert a.tables == b.tables and a.labels == b.labels and a.status == b.status
+    V = int(a.node_off[-1])
+    assert list(a.node_ids[:V]) == list(b.node_ids[:V])
+    assert list(a.node_types[:V]) == list(b.node_types[:V])
+    assert list(a.node_times[:V]) == list(b.node_times[:V])
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture_ingest_matches_python(name):
+    d = os.path.join(HERE, name)
+    assert_same(load_molly_native(d, threads=4), load_molly(d))
+
+
+def write_dir(d, runs):
+    os.makedirs(d, exist_ok=True)
+    meta = []
+    for i, (it, st, pre, post) in enumerate(runs):
+        meta.append({"iteration": it, "status": st})
+        json.dump(pre, open(os.path.join(d, f"run_{i}_pre_provenance.json"), "w"))
+        json.dump(post, open(os.path.join(d, f"run_{i}_post_provenance.json"), "w"))
+    json.dump(meta, open(os.path.join(d, "runs.json"), "w"))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_ingest_matches_python(tmp_path, seed):
+    rng = random.Random(seed)
+    runs = []
+    for it in range(rng.randint(1, 6)):
+        runs.append((it, "success" if it == 0 or rng.random() < 0.6 else "fail",
+                     random_prov(rng, "pre", 30), random_prov(rng, "post", 30)))
+    # clock goals, escapes and non-ASCII labels
+    runs[0][2]["goals"].append({"id": "goalc", "label": "clock(a, b, 3, 4)", "table": "clock", "time": "9"})
+    runs[0][2]["goals"].append({"id": "goalw", "label": "clock(a, a, 2, __WILDCARD__)", "table": "clock"})
+    runs[0][3]["goals"].append({"id": "goalu", "label": "café(\"q\", \\, \U0001F600)", "table": "té"})
+    write_dir(str(tmp_path), runs)
+    n1 = load_molly_native(str(tmp_path), threads=1)
+    n4 = load_molly_native(str(tmp_path), threads=4)
+    py = load_molly(str(tmp_path))
+    assert_same(n1, py)
+    assert_same(n4, py)
+    r0 = n1.graph_nodes(0)
+    times = {n1.node_ids[i]: n1.node_times[i] for i in r0}
+    assert times["run_0_pre_goalc"] == "3" and times["run_0_pre_goalw"] == "2"
+
+
+@pytest.mark.parametrize("case", ["dangling", "dup_goal", "dup_edge", "bad_json", "missing"])
+def test_ingest_errors_match_python(tmp_path, case):
+    pre = {"goals": [{"id": "goal0", "label": "pre(a)", "table": "pre", "time": "1"}],
+           "rules": [{"id": "rule1", "label": "pre", "table": "pre", "type": "single"}],
+           "edges": [{"from": "goal0", "to": "rule1"}]}
+    post = json.loads(json.dumps(pre))
+    if case == "dangling":
+        post["edges"].append({"from": "rule1", "to": "goal9"})
+    elif case == "dup_goal":
+        post["goals"].append(dict(post["goals"][0]))
+    elif case == "dup_edge":
+        post["edges"].append({"from": "goal0", "to": "rule1"})
+    write_dir(str(tmp_path), [(0, "success", pre, post)])
+    if case == "bad_json":
+        open(os.path.join(str(tmp_path), "run_0_post_provenance.json"), "w").write('{"goals": [')
+    if case == "missing":
+        os.remove(os.path.join(str(tmp_path), "run_0_post_provenance.json"))
+    with pytest.raises(LoadError) as native:
+        load_molly_native(str(tmp_path))
+    if case in ("dangling", "dup_goal", "dup_edge"):
+        with pytest.raises(LoadError) as py:
+            load_molly(str(tmp_path))
+        assert str(native.value) == str(py.value)
+
+
+def test_null_and_empty_sections(tmp_path):
+    write_dir(str(tmp_path), [(0, "success", {"goals": None, "rules": [], "edges": None}, {})])
+    c = load_molly_native(str(tmp_path))
+    assert int(c.node_off[-1]) == 0 and c.tables == ["pre", "post"]
