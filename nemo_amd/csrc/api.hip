@@ -743,8 +743,9 @@ int nemo_simplify(nemo_ctx *c) {
     rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, false, c->stream); });
     if (rc) return rc;
   }
-  const double V = (double)c->V;
-  rc = timed(c, "k_chains", 9 * V, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
+  const double V = (double)c->V, E = (double)c->E;
+  // reads: flags 1 + Kahn level 4 + node word 4 (+ ID rank 4) per node, the edge list 8 per edge
+  rc = timed(c, "k_chains", (c->has_rank ? 13 : 9) * V + 8 * E, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
   if (rc) return rc;
   c->simplified = true;
   c->protos_done = false;

@@ -351,19 +351,31 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
     }
     __syncthreads();
     const uint32_t *es = c.esrc + gv.e0, *ed = c.edst + gv.e0;
+    // one round (E <= CF_EPT x block, the common case): the H*-mapped edges of
+    // pass 0 stay in registers for pass 1, so the edge list is read once
+    const bool one_e = gv.E <= CF_EPT * NEMO_BLOCK;
+    uint32_t ab[CF_EPT];
     for (int pass = 0; pass < 2; pass++) {
       for (uint32_t ebase = 0; ebase < gv.E; ebase += CF_EPT * NEMO_BLOCK) {
-        uint32_t sd[CF_EPT];
+        if (!(one_e && pass == 1)) {
+          uint32_t sd[CF_EPT];
 #pragma unroll
-        for (int q = 0; q < CF_EPT; q++) {
-          const uint32_t e = ebase + q * NEMO_BLOCK + tid;
-          sd[q] = e < gv.E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
+          for (int q = 0; q < CF_EPT; q++) {
+            const uint32_t e = ebase + q * NEMO_BLOCK + tid;
+            sd[q] = e < gv.E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
+          }
+#pragma unroll
+          for (int q = 0; q < CF_EPT; q++) {
+            ab[q] = 0xFFFFFFFFu;
+            if (sd[q] == 0xFFFFFFFFu) continue;
+            const uint32_t a = hmap[sd[q] >> 16], b = hmap[sd[q] & 0xFFFFu];
+            if (a != 0xFFFFu && b != 0xFFFFu) ab[q] = (a << 16) | b;
+          }
         }
 #pragma unroll
         for (int q = 0; q < CF_EPT; q++) {
-          if (sd[q] == 0xFFFFFFFFu) continue;
-          const uint32_t a = hmap[sd[q] >> 16], b = hmap[sd[q] & 0xFFFFu];
-          if (a == 0xFFFFu || b == 0xFFFFu) continue;
+          if (ab[q] == 0xFFFFFFFFu) continue;
+          const uint32_t a = ab[q] >> 16, b = ab[q] & 0xFFFFu;
           const uint32_t sa = 16u * (a & 1u), sb = 16u * (b & 1u);
           if (pass == 0) {
             atomicAdd(&cc32[a >> 1], 1u << sa);
