@@ -202,14 +202,19 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 
 
 // ---- first tier: first(v) over an LDS-resident chain subgraph ------------------
-#define HCAP 2048  // H* nodes staged in LDS
-#define ECAP 2048  // H* edges staged in LDS (each direction)
+// Two instantiations (launch_chains): <1664, 120> keeps the LDS image at
+// 40 KB, so four workgroups share a CU, and takes the graphs it can; the
+// <2048, 512> tier then runs only the graphs the first one handed back.
+//   HCAP: H* nodes (and H* edges per direction) staged in LDS
+//   UCAP: Kahn levels of the graph / distinct prefix lengths (longest chain path + 2)
 #define NIL16 0xFFFFu
-#define UCAP 512   // distinct prefix lengths (longest chain path + 2)
 #define CF_ROWS 20  // topo positions per thread per compaction round (fast front)
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
 
+template <int HCAP, int UCAP>
 struct ChainsLDS {
+  static constexpr int ECAP = HCAP;
+  static_assert(HCAP % 32 == 0 && HCAP <= 2048 && UCAP >= HCAP / 32 + 64, "isrule words; rank bitmap + 64 prefix words in cur[]");
   uint16_t crank[HCAP];  // rank of the node's ID among H* nodes
   int16_t up[HCAP], down[HCAP];
   uint16_t nxt[HCAP], bp[HCAP], po[HCAP];
@@ -231,12 +236,15 @@ struct ChainsLDS {
   } u;
 };
 
-__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
-  __shared__ ChainsLDS L;
+template <int HCAP, int UCAP>
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t second) {
+  constexpr uint32_t ECAP = HCAP;
+  __shared__ ChainsLDS<HCAP, UCAP> L;
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_nch, s_maxup, s_fail;
   const uint32_t g = blockIdx.x;
   if (c.err[g] || c.gs_off[g] != ~0ull) return;  // deep graphs: k_chains_glob
+  if (second && c.nch[g] != NEMO_NONE) return;   // done by the first tier
   const GraphView gv = c.view(g);
   const uint8_t *f = gv.flags;
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
@@ -509,6 +517,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   } else {
     uint32_t N2 = 1;
     while (N2 < n) N2 <<= 1;
+    if (N2 > HCAP) {  // the network needs a power of two: the next tier
+      if (tid == 0) c.nch[g] = NEMO_NONE;
+      return;
+    }
     for (uint32_t i = tid; i < N2; i += NEMO_BLOCK)
       L.u.kk[i] = i < n ? (((unsigned long long)gv.rank_of(hs[i]) << 16) | i) : ~0ull;
     __syncthreads();
@@ -1137,7 +1149,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
 }
 
 void launch_chains(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_chains, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  hipLaunchKernelGGL((k_chains<1664, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, 0u);
+  hipLaunchKernelGGL((k_chains<2048, 512>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, 1u);
   hipLaunchKernelGGL(k_chains_big, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
   launch_chains_glob(c, s);
 }

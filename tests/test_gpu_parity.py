@@ -287,3 +287,27 @@ def test_chains_glob_tier(kind):
             _check(e, corpus_from_graphs(graphs))
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("shape", ["wide_hstar", "many_levels", "long_chains"])
+def test_chains_lds_tiers(eng, shape):
+    # k_chains<1664, 120> (4 workgroups/CU) hands graphs whose chain subgraph,
+    # level count or longest prefix exceed it to k_chains<2048, 512>; both
+    # against the oracle on graphs that land in each tier
+    from nemo_amd.corpus import corpus_from_graphs
+    from tools import synth
+    if shape == "wide_hstar":  # H* of ~1.7-2k nodes: past the first tier's 1664
+        corpus, _ = synth.generate(8, target_nodes=5600, eot=10)
+    elif shape == "many_levels":  # > 120 Kahn levels: the first tier's old front
+        corpus, _ = synth.generate(8, target_nodes=3000, eot=60)
+    else:  # one @next chain of 80 rules (prefix length 159 > 118): the second tier
+        def chain(cond, n):
+            goals = [{"id": f"goal{i}", "label": f"log(a, {i})", "table": cond if i == 0 else "log", "time": "1"}
+                     for i in range(n + 1)]
+            rules = [{"id": f"rule{i}", "label": "log", "table": "log", "type": "next"} for i in range(n)]
+            edges = [e for i in range(n) for e in ({"from": f"goal{i}", "to": f"rule{i}"},
+                                                   {"from": f"rule{i}", "to": f"goal{i + 1}"})]
+            return {"goals": goals, "rules": rules, "edges": edges}
+        corpus = corpus_from_graphs([(0, "success", chain("pre", 80), chain("post", 80)),
+                                     (1, "failure", chain("pre", 40), chain("post", 70))])
+    _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
