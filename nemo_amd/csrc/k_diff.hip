@@ -239,10 +239,31 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
 }
 
 
-// k_pull over the LDS graph tier (raw / simplified graphs): the graph's rows
-// and flags staged in LDS, per-node output offsets from one block scan, the
-// same order as k_pull.
-#define PULL_BLOCK 512
+// k_pull over the LDS graph tier (raw / simplified graphs): the forward rows
+// and the flags staged in LDS (the reverse rows are read from HBM for the
+// chain heads only), per-node output offsets from one block scan, the same
+// order as k_pull.  The image is ~5V + 2E bytes, so four workgroups share a CU.
+#define PULL_BLOCK 256
+struct PullLds {
+  uint16_t *fp, *fc, *cnt;
+  uint8_t *fl;
+};
+__host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t e) {
+  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(2u * v) + lds_align(v);
+}
+__device__ __forceinline__ PullLds pull_carve(void *base, uint32_t V, uint32_t E) {
+  uint8_t *p = (uint8_t *)base;
+  PullLds L;
+  L.fp = (uint16_t *)p;
+  p += lds_align(2u * (V + 1u));
+  L.fc = (uint16_t *)p;
+  p += lds_align(2u * E);
+  L.cnt = (uint16_t *)p;
+  p += lds_align(2u * V);
+  L.fl = p;
+  return L;
+}
+
 __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lds[PULL_BLOCK / 64];
@@ -253,18 +274,17 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   const GraphView gv = c.view(g);
   if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V;
-  LdsGraph L = lds_carve(dyn, V, gv.E, gv.nlev, c.words);
+  PullLds L = pull_carve(dyn, V, gv.E);
   {
-    const StageDesc d[5] = {{gv.rp, L.rp, V + 1, ST_U16}, {gv.fp, L.fp, V + 1, ST_U16}, {gv.rc, L.rc, gv.E, ST_U16},
-                            {gv.fc, L.fc, gv.E, ST_U16},  {gv.flags, L.a, V, ST_U8}};
-    stage_lds<5, PULL_BLOCK>(d);
+    const StageDesc d[3] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}, {gv.flags, L.fl, V, ST_U8}};
+    stage_lds<3, PULL_BLOCK>(d);
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
   const uint32_t which = a.which;
-  const uint8_t *fl = L.a;
+  const uint8_t *fl = L.fl;
 #define ALIVE(v) (which == 0 || (fl[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
-  uint16_t *cnt = L.topo;  // per-node edge counts -> output offsets
+  uint16_t *cnt = L.cnt;  // per-node edge counts -> output offsets
   for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
     uint32_t n = 0;
     if (ALIVE(u))
@@ -276,7 +296,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   uint32_t nc = 0;
   for (uint32_t k = tid; k < nch; k += PULL_BLOCK) {
     const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
-    for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) nc += ALIVE(L.rc[j]);
+    for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) nc += ALIVE(gv.rc[j]);
     for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) nc += ALIVE(L.fc[j]);
   }
   for (int d = 32; d >= 1; d >>= 1) nc += __shfl_xor(nc, d);
@@ -311,14 +331,14 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
     if (k < nch) {
       h = ch[5 * k];
       t = ch[5 * k + 1];
-      for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) n += ALIVE(L.rc[j]);
+      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += ALIVE(gv.rc[j]);
       for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) n += ALIVE(L.fc[j]);
     }
     uint32_t tot;
     uint64_t o = pos + block_exscan<PULL_BLOCK>(n, &tot, s_lds);
     if (k < nch) {
-      for (uint32_t j = L.rp[h]; j < L.rp[h + 1]; j++) {
-        const uint32_t p = L.rc[j];
+      for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) {
+        const uint32_t p = gv.rc[j];
         if (!ALIVE(p)) continue;
         a.src[o] = p;
         a.dst[o] = V + k;
@@ -509,8 +529,9 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipS
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
   if (a.which != 2 && c.lds_bytes) {
-    hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
-    hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), c.lds_bytes, s, c, a);
+    const uint32_t bytes = pull_lds_bytes(c.lds_v, c.lds_e);
+    hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
   }
   hipLaunchKernelGGL(k_pull, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
 }
