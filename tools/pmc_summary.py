@@ -62,6 +62,7 @@ def main():
              "WAIT_ANY % | WAIT_INST % | ACTIVE % | LDS insts | VALU insts |",
              "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     kern = bj.get("kernels", {})
+    base_hbm = defaultdict(lambda: [0.0, 0.0, 0.0, 0])  # template tiers (k_chains<H, U>) add up per base kernel
     for k in sorted(fetch, key=lambda k: -sum(fetch[k]["FETCH_SIZE"])):
         f = fetch[k]["FETCH_SIZE"]
         w = write.get(k, {}).get("WRITE_SIZE", [0.0])
@@ -79,9 +80,15 @@ def main():
         lines.append(f"| {k} | {n} | {fk:.0f} | {wk:.0f} | {hbm / 1e6:.1f} | {alg / 1e6 if alg else float('nan'):.1f} | "
                      f"{m('SQ_WAVES'):.0f} | {100 * m('SQ_WAIT_ANY') / cyc:.1f} | {100 * m('SQ_WAIT_INST_ANY') / cyc:.1f} | "
                      f"{100 * m('SQ_ACTIVE_INST_ANY') / cyc:.1f} | {m('SQ_INSTS_LDS'):.0f} | {m('SQ_INSTS_VALU'):.0f} |")
+        b = base_hbm[k.split("<")[0]]
+        b[0] += hbm
+        b[1] += fk
+        b[2] += wk
+        b[3] = max(b[3], n)
+    for k, (hbm, fk, wk, n) in base_hbm.items():
         json.dump({"kernel": k, "workload_nodes": nodes, "hbm_bytes_per_launch": round(hbm),
                    "fetch_kib": fk, "write_kib": wk, "launches": n, "round": tag,
-                   "rule": "2*FETCH_SIZE + WRITE_SIZE, KiB->bytes"},
+                   "rule": "2*FETCH_SIZE + WRITE_SIZE, KiB->bytes (summed over template tiers)"},
                   open(os.path.join(prof, f"pmc_{k}.json"), "w"), indent=1)
     open(os.path.join(prof, f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
