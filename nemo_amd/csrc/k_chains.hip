@@ -796,12 +796,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t sec
     while (L.up[h] > 0) h = L.bp[h];
     while (L.nxt[t] != NIL16) t = L.nxt[t];
     const uint32_t k = atomicAdd(&s_nch, 1u);
-    uint32_t *r = tmp + 5 * k;
-    r[0] = h;
-    r[1] = t;
-    r[2] = (uint32_t)(L.up[i] + L.down[i]);
-    r[3] = L.crank[h];
-    r[4] = i;
+    // packed record: compact head | tail << 16, length | representative << 16
+    tmp[2 * k] = h | (t << 16);
+    tmp[2 * k + 1] = (uint32_t)(L.up[i] + L.down[i]) | (i << 16);
   }
   __threadfence_block();
   __syncthreads();
@@ -870,7 +867,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t sec
     for (uint32_t q = tid; q < ((nch + 3) & ~3u); q += NEMO_BLOCK) {
       uint32_t k = 0xFFFFFFFFu;
       if (q < nch) {
-        const uint32_t len = tmp[5 * q + 2], rep = tmp[5 * q + 4];
+        const uint32_t len = tmp[2 * q + 1] & 0xFFFFu, rep = tmp[2 * q + 1] >> 16;
         k = ((0xFFFFu - len) << 16) | pre[rep];
       }
       key[q] = k;
@@ -893,9 +890,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t sec
   for (uint32_t pos = tid; pos < nch; pos += NEMO_BLOCK) {
     const uint32_t q = ord[pos];
     uint32_t *w = out + 5 * pos;
-    w[0] = hs[tmp[5 * q]];
-    w[1] = hs[tmp[5 * q + 1]];
-    w[2] = tmp[5 * q + 2];
+    w[0] = hs[tmp[2 * q] & 0xFFFFu];
+    w[1] = hs[tmp[2 * q] >> 16];
+    w[2] = tmp[2 * q + 1] & 0xFFFFu;
     w[3] = gv.rank_of(w[0]);
     w[4] = 0;
   }
@@ -903,7 +900,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t sec
   __syncthreads();
 #endif
   STAMP(8);
-  for (uint32_t i = tid; i < n; i += NEMO_BLOCK) c.tail_first[gv.n0 + hs[i]] = NEMO_NONE;
+  // tail lists: only F_TAIL nodes (= the tails of accepted chains) are ever read
+  __threadfence_block();
+  __syncthreads();  // out[] rows of other threads
+  for (uint32_t k = tid; k < nch; k += NEMO_BLOCK) c.tail_first[gv.n0 + out[5 * k + 1]] = NEMO_NONE;
   __threadfence_block();
   __syncthreads();
   for (uint32_t k = tid; k < nch; k += NEMO_BLOCK) {

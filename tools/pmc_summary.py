@@ -31,13 +31,13 @@ def rows(pattern):
 
 
 def short(name):
-    return name.split("(")[0].replace("nemo::", "")
+    return name.split("(")[0].replace("void ", "", 1).replace("nemo::", "")
 
 
 def per_kernel(pattern, counter=None):
     acc = defaultdict(lambda: defaultdict(list))
     for r in rows(pattern):
-        if not r["Kernel_Name"].startswith("nemo::"):
+        if not r["Kernel_Name"].replace("void ", "", 1).startswith("nemo::"):
             continue
         acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
