@@ -65,6 +65,7 @@ struct nemo_ctx {
   // diff
   uint32_t n_entries = 0, diff_cap = 0;
   uint32_t *d_r0lab = nullptr, *d_r0idx = nullptr, n_r0lab = 0;
+  uint32_t *d_r0hkey = nullptr, *d_r0hval = nullptr, r0hmask = 0;
   uint32_t *d_dsrc = nullptr, *d_miss = nullptr, *d_nmiss = nullptr;
   uint8_t *d_dbits = nullptr, *d_dmask = nullptr;
   int32_t *d_ddepth = nullptr;
@@ -280,6 +281,8 @@ static void release_corpus(nemo_ctx *c) {
   c->d_owned = c->d_is_success = nullptr;
   c->d_red = nullptr;
   c->d_r0lab = c->d_r0idx = c->d_dsrc = c->d_miss = c->d_nmiss = nullptr;
+  c->d_r0hkey = c->d_r0hval = nullptr;
+  c->r0hmask = 0;
   c->d_dbits = c->d_dmask = nullptr;
   c->d_ddepth = nullptr;
   c->n_entries = c->diff_cap = 0;
@@ -652,13 +655,30 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       ix[i] = lab[i].second;
     }
     c->n_r0lab = (uint32_t)lab.size();
+    // label -> first sorted entry, open-addressed at load factor <= 1/2, so a
+    // lookup is one or two independent probes instead of a binary search
+    uint32_t hcap = 16;
+    while (hcap < 2 * lab.size()) hcap <<= 1;
+    std::vector<uint32_t> hkey(hcap, 0u), hval(hcap, 0u);
+    for (size_t i = 0; i < l.size(); i++) {
+      if (i && l[i] == l[i - 1]) continue;
+      uint32_t h = hash_label(l[i]) & (hcap - 1);
+      while (hkey[h]) h = (h + 1) & (hcap - 1);
+      hkey[h] = l[i] + 1u;
+      hval[h] = (uint32_t)i;
+    }
+    c->r0hmask = hcap - 1;
     if ((rc = dalloc(c, &c->d_r0lab, l.size()))) return rc;
     if ((rc = dalloc(c, &c->d_r0idx, l.size()))) return rc;
+    if ((rc = dalloc(c, &c->d_r0hkey, hcap))) return rc;
+    if ((rc = dalloc(c, &c->d_r0hval, hcap))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_r0hkey, hkey.data(), hcap * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_r0hval, hval.data(), hcap * 4, hipMemcpyHostToDevice, s));
     if (!l.empty()) {
       HIPCHK(c, hipMemcpyAsync(c->d_r0lab, l.data(), l.size() * 4, hipMemcpyHostToDevice, s));
       HIPCHK(c, hipMemcpyAsync(c->d_r0idx, ix.data(), ix.size() * 4, hipMemcpyHostToDevice, s));
-      HIPCHK(c, hipStreamSynchronize(s));  // host vectors go out of scope
     }
+    HIPCHK(c, hipStreamSynchronize(s));  // host vectors go out of scope
   }
   // trigger outputs of run 0: pre rows (a, g, r) <= sum over goals of in*out
   // degree, post rows (g, r) <= edges, async rules <= nodes (corrections.go:30-34,121-125)
@@ -928,6 +948,9 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   a.r0lab = c->d_r0lab;
   a.r0idx = c->d_r0idx;
   a.n_r0lab = c->n_r0lab;
+  a.r0hkey = c->d_r0hkey;
+  a.r0hval = c->d_r0hval;
+  a.r0hmask = c->r0hmask;
   a.bits = c->d_dbits;
   a.depth = c->d_ddepth;
   a.mask = c->d_dmask;

@@ -216,6 +216,11 @@ struct DevCorpus {
 #define NW_NEXT 0x4000u
 #define NW_TABLE 0x3FFFu
 __host__ __device__ __forceinline__ uint32_t lds_align(uint32_t b) { return (b + 15u) & ~15u; }
+// slot hash of an interned label (the diff's failGoals table, api.hip / k_diff.hip)
+__host__ __device__ __forceinline__ uint32_t hash_label(uint32_t x) {
+  x *= 0x9E3779B1u;
+  return x ^ (x >> 15);
+}
 // accepted @next chains of a tier graph held in LDS (head + per-tail list link)
 __host__ __device__ __forceinline__ uint32_t lds_chain_cap(uint32_t v) { return v / 4u < 32766u ? v / 4u : 32766u; }
 __host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t e, uint32_t l, uint32_t words) {

@@ -14,6 +14,9 @@ struct DiffArgs {
   const uint32_t *r0lab;    // sorted goal labels of g0
   const uint32_t *r0idx;    // local node of each sorted label
   uint32_t n_r0lab;
+  const uint32_t *r0hkey;   // open-addressed label -> first sorted entry: key = label + 1 (0 empty)
+  const uint32_t *r0hval;
+  uint32_t r0hmask;         // table size - 1 (power of two)
   uint8_t *bits;            // [entries * V0] scratch
   int32_t *depth;           // [entries * V0] scratch
   uint8_t *mask;            // [entries * V0] D mask (output)

@@ -13,6 +13,82 @@ namespace nemo {
 #define DB_D 0x10u
 #define DB_LP 0x20u
 
+// LDS image of run 0's post graph for k_diff_lds: u16 rows both ways, a rule
+// bitmap and the entry's node bits (~5V + 4E bytes, three workgroups per CU
+// at the tier caps, so a few hundred diff entries run in one round); the Kahn
+// order (coalesced, one load per level) and the depths stay in HBM.
+struct DiffLds {
+  uint16_t *rp, *fp, *rc, *fc;
+  uint32_t *rule;
+  uint8_t *bits;
+};
+__host__ __device__ __forceinline__ uint32_t diff_lds_bytes(uint32_t v, uint32_t e, uint32_t l) {
+  return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + lds_align(4u * ((v + 31u) / 32u)) + lds_align(v);
+}
+__device__ __forceinline__ DiffLds diff_carve(void *base, uint32_t V, uint32_t E, uint32_t L) {
+  uint8_t *p = (uint8_t *)base;
+  DiffLds d;
+  d.rp = (uint16_t *)p;
+  p += lds_align(2u * (V + 1u));
+  d.fp = (uint16_t *)p;
+  p += lds_align(2u * (V + 1u));
+  d.rc = (uint16_t *)p;
+  p += lds_align(2u * E);
+  d.fc = (uint16_t *)p;
+  p += lds_align(2u * E);
+  d.rule = (uint32_t *)p;
+  p += lds_align(4u * ((V + 31u) / 32u));
+  d.bits = p;
+  return d;
+}
+__device__ __forceinline__ bool diff_lds_fits(const DevCorpus &c, const GraphView &gv) {
+  return lds_fits(c, gv.V, gv.E, gv.nlev);
+}
+
+// failGoals = collect(failed.label) (:23-24): every run-0 post goal whose label
+// is a post-goal label of the source graph gets DB_PRESENT.  Each thread takes
+// DL_BATCH source nodes and walks their hash probes together, so a pass costs
+// a few rounds of independent loads rather than a binary search per node.
+#define DL_BATCH 8
+__device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphView &src, uint8_t *bits) {
+  for (uint32_t base = 0; base < src.V; base += DL_BATCH * NEMO_BLOCK) {
+    uint32_t lab[DL_BATCH], h[DL_BATCH], pos[DL_BATCH], live = 0;
+#pragma unroll
+    for (int q = 0; q < DL_BATCH; q++) {
+      const uint32_t x = base + q * NEMO_BLOCK + threadIdx.x;
+      const bool in = x < src.V && !is_rule(src.word[x]);
+      lab[q] = in ? src.label[x] : 0u;
+      h[q] = hash_label(lab[q]) & a.r0hmask;
+      pos[q] = NEMO_NONE;
+      live |= (in ? 1u : 0u) << q;
+    }
+    while (live) {
+      uint32_t k[DL_BATCH];
+#pragma unroll
+      for (int q = 0; q < DL_BATCH; q++) k[q] = ((live >> q) & 1u) ? a.r0hkey[h[q]] : 0u;
+#pragma unroll
+      for (int q = 0; q < DL_BATCH; q++) {
+        if (!((live >> q) & 1u)) continue;
+        if (k[q] == lab[q] + 1u) {
+          pos[q] = h[q];
+          live &= ~(1u << q);
+        } else if (k[q] == 0u) {
+          live &= ~(1u << q);
+        } else {
+          h[q] = (h[q] + 1u) & a.r0hmask;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < DL_BATCH; q++)
+      if (pos[q] != NEMO_NONE) pos[q] = a.r0hval[pos[q]];
+#pragma unroll
+    for (int q = 0; q < DL_BATCH; q++)
+      if (pos[q] != NEMO_NONE)
+        for (uint32_t i = pos[q]; i < a.n_r0lab && a.r0lab[i] == lab[q]; i++) bits[a.r0idx[i]] = DB_PRESENT;
+  }
+}
+
 // One workgroup per diff entry, all over run 0's post graph g0:
 //   Good = goals of g0 whose label is absent from the source run's post goals
 //   D    = Fwd*(Good) ∩ Bwd*(Good)                       (:22-32, APOC export)
@@ -21,6 +97,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
   __shared__ int32_t s_max;
   const uint32_t e = blockIdx.x;
   const GraphView gv = c.view(a.g0);
+  if (diff_lds_fits(c, gv)) return;  // k_diff_lds's graph
   const GraphView src = c.view(a.src[e]);
   const uint32_t V = gv.V;
   uint8_t *bits = a.bits + (size_t)e * V;
@@ -29,18 +106,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
   if (threadIdx.x == 0) s_max = -1;
   for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) bits[v] = 0;
   __syncthreads();
-  // failGoals = collect(failed.label) (:23-24), looked up in run 0's sorted goal labels
-  for (uint32_t x = threadIdx.x; x < src.V; x += NEMO_BLOCK) {
-    if (is_rule(src.word[x])) continue;
-    const uint32_t lab = src.label[x];
-    uint32_t lo = 0, hi = a.n_r0lab;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.r0lab[mid] < lab) lo = mid + 1;
-      else hi = mid;
-    }
-    for (uint32_t i = lo; i < a.n_r0lab && a.r0lab[i] == lab; i++) bits[a.r0idx[i]] = DB_PRESENT;
-  }
+  diff_fail_goals(a, src, bits);
   __syncthreads();
 #define GOOD(v) (!is_rule(gv.word[v]) && !(bits[v] & DB_PRESENT))
   for (uint32_t l = 0; l < gv.nlev; l++) {
@@ -108,6 +174,110 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
       a.missing[2 * k + 1] = r;
     }
   }
+}
+
+// k_diff over the LDS graph tier: the same three level sweeps (Fwd*, Bwd*,
+// depth) with run 0's post graph rows and the entry's node bits in LDS, so
+// the dependent parent/child probes of a level are LDS round trips.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_diff_lds(DevCorpus c, DiffArgs a) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  __shared__ int32_t s_max;
+  const uint32_t e = blockIdx.x, tid = threadIdx.x;
+  const GraphView gv = c.view(a.g0);
+  if (!diff_lds_fits(c, gv)) return;  // k_diff's graph
+  const GraphView src = c.view(a.src[e]);
+  const uint32_t V = gv.V, nl = gv.nlev;
+  DiffLds L = diff_carve(dyn, V, gv.E, nl);
+  uint8_t *mask = a.mask + (size_t)e * V;
+  int32_t *depth = a.depth + (size_t)e * V;  // HBM: only D nodes touch it
+  {
+    const StageDesc d[4] = {{gv.rp, L.rp, V + 1, ST_U16}, {gv.fp, L.fp, V + 1, ST_U16},
+                            {gv.rc, L.rc, gv.E, ST_U16},  {gv.fc, L.fc, gv.E, ST_U16}};
+    stage_lds<4, NEMO_BLOCK>(d);
+  }
+  for (uint32_t w = tid; w < (V + 31) / 32; w += NEMO_BLOCK) L.rule[w] = 0;
+  for (uint32_t v = tid; v < V; v += NEMO_BLOCK) L.bits[v] = 0;
+  if (tid == 0) s_max = -1;
+  __syncthreads();
+  for (uint32_t base = 0; base < V; base += NEMO_BLOCK) {
+    const uint32_t v = base + tid;
+    const uint64_t m = __ballot(v < V && is_rule(gv.word[v]));
+    if ((lane_id() & 31) == 0 && v < V) {
+      const uint32_t b = (uint32_t)(m >> (lane_id() & 32));
+      if (b) atomicOr(&L.rule[v >> 5], b);
+    }
+  }
+  uint8_t *bits = L.bits;
+  diff_fail_goals(a, src, bits);
+  __syncthreads();
+#define LRULE(v) ((L.rule[(v) >> 5] >> ((v) & 31)) & 1u)
+#define GOOD(v) (!LRULE(v) && !(bits[v] & DB_PRESENT))
+  for (uint32_t l = 0; l < nl; l++) {
+    for (uint32_t i = gv.lvl[l] + tid; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      bool fw = GOOD(v);
+      for (uint32_t j = L.rp[v]; j < L.rp[v + 1] && !fw; j++) fw = (bits[L.rc[j]] & DB_F) != 0;
+      if (fw) bits[v] |= DB_F;
+    }
+    __syncthreads();
+  }
+  for (uint32_t l = nl; l-- > 0;) {
+    for (uint32_t i = gv.lvl[l] + tid; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      bool bw = GOOD(v);
+      for (uint32_t j = L.fp[v]; j < L.fp[v + 1] && !bw; j++) bw = (bits[L.fc[j]] & DB_B) != 0;
+      uint8_t b = bits[v];
+      if (bw) b |= DB_B;
+      if ((b & DB_F) && bw) b |= DB_D;
+      bits[v] = b;
+    }
+    __syncthreads();
+  }
+#undef GOOD
+  // longest path from a D root (Kahn-level DP restricted to D)
+  for (uint32_t l = 0; l < nl; l++) {
+    for (uint32_t i = gv.lvl[l] + tid; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+      const uint32_t v = gv.topo[i];
+      const uint8_t b = bits[v];
+      if (!(b & DB_D)) continue;
+      uint32_t d = 0;
+      for (uint32_t j = L.rp[v]; j < L.rp[v + 1]; j++) {
+        const uint32_t p = L.rc[j];
+        if (bits[p] & DB_D) d = max(d, (uint32_t)depth[p] + 1u);
+      }
+      depth[v] = (int32_t)d;
+      if (!LRULE(v)) {
+        bool leaf = true;
+        for (uint32_t j = L.fp[v]; j < L.fp[v + 1]; j++)
+          if (bits[L.fc[j]] & DB_D) leaf = false;
+        if (leaf) bits[v] = b | DB_LEAF;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t v = tid; v < V; v += NEMO_BLOCK) mask[v] = (bits[v] & DB_D) ? 1 : 0;
+  for (uint32_t r = tid; r < V; r += NEMO_BLOCK) {
+    if (!(bits[r] & DB_D) || !LRULE(r)) continue;
+    bool lp = false;
+    for (uint32_t j = L.fp[r]; j < L.fp[r + 1]; j++) {
+      const uint32_t x = L.fc[j];
+      if ((bits[x] & (DB_D | DB_LEAF)) == (DB_D | DB_LEAF)) lp = true;
+    }
+    if (lp) {
+      bits[r] |= DB_LP;
+      atomicMax(&s_max, depth[r] + 1);
+    }
+  }
+  __syncthreads();
+  const int32_t mx = s_max;
+  for (uint32_t r = tid; r < V; r += NEMO_BLOCK) {
+    if ((bits[r] & DB_LP) && depth[r] + 1 == mx) {
+      const uint32_t k = atomicAdd(a.n_missing, 1u);
+      a.missing[2 * k] = e;
+      a.missing[2 * k + 1] = r;
+    }
+  }
+#undef LRULE
 }
 
 // ---- edge pulls: which 0 = raw, 1 = simplified (graph'), 2 = diff entry ---------
@@ -525,6 +695,11 @@ void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipSt
 }
 
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s) {
+  if (c.lds_bytes) {
+    const uint32_t bytes = diff_lds_bytes(c.lds_v, c.lds_e, c.lds_l);
+    hipFuncSetAttribute((const void *)k_diff_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    hipLaunchKernelGGL(k_diff_lds, dim3(n_entries), dim3(NEMO_BLOCK), bytes, s, c, a);
+  }
   hipLaunchKernelGGL(k_diff, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
