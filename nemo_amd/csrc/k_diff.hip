@@ -287,27 +287,39 @@ __device__ __forceinline__ bool pull_alive(uint32_t which, const uint8_t *f, con
   return m[v] != 0;
 }
 
-// exclusive scan of cnt[0..n) into off[0..n], one workgroup
-__global__ __launch_bounds__(NEMO_BLOCK) void k_scan64(const uint32_t *cnt, uint64_t *off, uint32_t n) {
-  __shared__ unsigned long long s_part[NEMO_BLOCK];
-  unsigned long long carry = 0;
-  for (uint32_t base = 0; base < n; base += NEMO_BLOCK) {
-    const uint32_t i = base + threadIdx.x;
-    const unsigned long long x = i < n ? cnt[i] : 0ull;
-    s_part[threadIdx.x] = x;
-    __syncthreads();
-    for (uint32_t d = 1; d < NEMO_BLOCK; d <<= 1) {
-      unsigned long long y = threadIdx.x >= d ? s_part[threadIdx.x - d] : 0ull;
-      __syncthreads();
-      s_part[threadIdx.x] += y;
-      __syncthreads();
-    }
-    if (i < n) off[i] = carry + s_part[threadIdx.x] - x;
-    const unsigned long long tot = s_part[NEMO_BLOCK - 1];
-    __syncthreads();
-    carry += tot;
+// exclusive scan of cnt[0..n) into off[0..n], one workgroup: every thread
+// sums a contiguous slice (independent loads), one block scan of the slice
+// sums, then each slice is written from its base
+#define SCAN_BLOCK 1024
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan64(const uint32_t *cnt, uint64_t *off, uint32_t n) {
+  __shared__ unsigned long long s_w[SCAN_BLOCK / 64];
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const uint32_t per = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
+  unsigned long long sum = 0;
+  for (uint32_t i = lo; i < hi; i++) sum += cnt[i];
+  unsigned long long inc = sum;  // inclusive scan inside the wave
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(inc, d);
+    if (lane >= d) inc += y;
   }
-  if (threadIdx.x == 0) off[n] = carry;
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (uint32_t w = 0; w < SCAN_BLOCK / 64; w++) {
+      const unsigned long long x = s_w[w];
+      s_w[w] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  unsigned long long o = s_w[wv] + inc - sum;
+  for (uint32_t i = lo; i < hi; i++) {
+    off[i] = o;
+    o += cnt[i];
+  }
+  if (t == SCAN_BLOCK - 1) off[n] = s_w[wv] + inc;
 }
 
 // One pass per slot (graph, or diff entry over run 0's post graph): count the
@@ -690,7 +702,7 @@ void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStrea
 }
 
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan64, dim3(1), dim3(NEMO_BLOCK), 0, s, c.nch, off, c.G);
+  hipLaunchKernelGGL(k_scan64, dim3(1), dim3(SCAN_BLOCK), 0, s, c.nch, off, c.G);
   if (out) hipLaunchKernelGGL(k_chain_gather, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);
 }
 
