@@ -566,12 +566,16 @@ void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, u
 
 // ---- run-0 trigger patterns ------------------------------------------------------
 // phase 0 counts, phase 1 writes (capacities sized from the counts).
+#define TRIG_SPLIT 16
 __global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a, int phase) {
   const GraphView gp = c.view(a.g_pre), gq = c.view(a.g_post);
+  // TRIG_SPLIT workgroups per pattern, nodes strided over them (row order is free)
+  const uint32_t pat = blockIdx.x % 3, x0 = (blockIdx.x / 3) * NEMO_BLOCK + threadIdx.x;
+  const uint32_t step = (gridDim.x / 3) * NEMO_BLOCK;
 #define HOLDS(gg, v) (((gg).flags[v] & NEMO_F_HOLDS) != 0)
-  if (blockIdx.x == 0) {
+  if (pat == 0) {
     // findPreTriggers (corrections.go:30-34): (a:Rule)->(g:Goal{holds:false})->(r:Rule), (h{holds})->(a)
-    for (uint32_t x = threadIdx.x; x < gp.V; x += NEMO_BLOCK) {
+    for (uint32_t x = x0; x < gp.V; x += step) {
       if (is_rule(gp.word[x]) || HOLDS(gp, x)) continue;
       for (uint32_t j = gp.rp[x]; j < gp.rp[x + 1]; j++) {
         const uint32_t ar = gp.rc[j];
@@ -589,9 +593,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a
           }
       }
     }
-  } else if (blockIdx.x == 1) {
+  } else if (pat == 1) {
     // findPostTriggers (corrections.go:121-125)
-    for (uint32_t x = threadIdx.x; x < gq.V; x += NEMO_BLOCK) {
+    for (uint32_t x = x0; x < gq.V; x += step) {
       if (is_rule(gq.word[x]) || !HOLDS(gq, x) || gq.indeg(x) == 0) continue;
       for (uint32_t j = gq.fp[x]; j < gq.fp[x + 1]; j++) {
         const uint32_t r = gq.fc[j];
@@ -610,7 +614,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_triggers(DevCorpus c, TrigArgs a
     }
   } else {
     // GenerateExtensions' async rules (extensions.go:63-67)
-    for (uint32_t r = threadIdx.x; r < gp.V; r += NEMO_BLOCK) {
+    for (uint32_t r = x0; r < gp.V; r += step) {
       const uint32_t w = gp.word[r];
       if (!is_rule(w) || type_of(w) != NEMO_TYPE_ASYNC) continue;
       bool hp = false, np = false, down = false;
@@ -723,7 +727,7 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
   hipLaunchKernelGGL(k_pull, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
-  hipLaunchKernelGGL(k_triggers, dim3(3), dim3(NEMO_BLOCK), 0, s, c, a, phase);
+  hipLaunchKernelGGL(k_triggers, dim3(3 * TRIG_SPLIT), dim3(NEMO_BLOCK), 0, s, c, a, phase);
 }
 
 }  // namespace nemo
