@@ -46,9 +46,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
-                    help="c3: 10k runs x ~5k-node graphs per GPU (the headline line); c5: deep provenance, "
-                         "~1M-node graphs at EOT 2000")
+    ap.add_argument("--config", choices=["c3", "c4", "c5"], default="c3",
+                    help="c3: 10k runs x ~5k-node graphs per GPU (the headline line, weak scaling); c4: 100k runs "
+                         "in total sharded over the ranks (strong scaling); c5: deep provenance, ~1M-node graphs "
+                         "at EOT 2000")
     ap.add_argument("--runs-per-gpu", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None, help="target nodes per provenance graph")
     ap.add_argument("--eot", type=int, default=None)
@@ -63,13 +64,14 @@ def parse():
 
 
 CONFIGS = {"c3": {"runs": 10000, "nodes": 5000, "eot": 10, "cpu_runs": None},
+           "c4": {"runs_total": 100000, "nodes": 5000, "eot": 10, "cpu_runs": 5000},
            "c5": {"runs": 128, "nodes": 1_000_000, "eot": 2000, "cpu_runs": 8}}
 
 
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
-    args.runs_per_gpu = args.runs_per_gpu or cfg["runs"]
+    strong = "runs_total" in cfg
     args.nodes = args.nodes or cfg["nodes"]
     args.eot = args.eot or cfg["eot"]
     import torch
@@ -81,6 +83,10 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n_gpus = world
+    if strong:  # C4: a fixed corpus split over the ranks
+        args.runs_per_gpu = args.runs_per_gpu or (cfg["runs_total"] + world - 1) // world
+    else:
+        args.runs_per_gpu = args.runs_per_gpu or cfg["runs"]
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -90,6 +96,8 @@ def main():
     from tools import synth
 
     R = args.runs_per_gpu
+    if strong:
+        R = max(0, min(R, cfg["runs_total"] - rank * R))
     t0 = time.time()
     corpus, info = synth.generate(R, target_nodes=args.nodes, eot=args.eot, run_base=rank * R,
                                   prepend_run0=True, threads=min(16, os.cpu_count() or 1))
@@ -227,14 +235,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": ("C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance graphs "
-                                "of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated") if args.config == "c3" else
-                               ("C5: synthetic deep-provenance corpus, runs_per_gpu runs x (pre, post) graphs of "
-                                "~nodes_per_graph nodes at EOT eot (SURVEY.md 8d), run 0 replicated"),
+        "config": {"workload": {"c3": "C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance "
+                                      "graphs of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated",
+                                "c4": "C4: synthetic Molly-shaped corpus of 100k runs in total, run-sharded over the "
+                                      "ranks (runs_per_gpu each), ~nodes_per_graph-node graphs, run 0 replicated",
+                                "c5": "C5: synthetic deep-provenance corpus, runs_per_gpu runs x (pre, post) graphs of "
+                                      "~nodes_per_graph nodes at EOT eot (SURVEY.md 8d), run 0 replicated"}[args.config],
                    "runs_per_gpu": R, "nodes_per_graph": args.nodes, "eot": args.eot,
                    "nodes_total_rank0": int(corpus.node_off[-1]), "edges_total_rank0": int(corpus.edge_off[-1]),
                    "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,
