@@ -54,6 +54,7 @@ struct nemo_ctx {
   uint32_t hcap_limit = 0xFFFFFFFFu, comp_limit = 0xFFFFFFFFu, build_limit = 0xFFFFFFFFu;
   uint32_t lds_limit = 0xFFFFFFFFu;  // test knob: largest V of the LDS graph tier (0 = off)
   uint64_t glob_min_v = 65536;       // graphs with V >= this take k_chains_glob (set before load)
+  uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
@@ -132,6 +133,7 @@ struct nemo_ctx {
 };
 
 static void set_lds_tier(nemo_ctx *c);
+static void set_global_block(nemo_ctx *c);
 static void set_build_tier(nemo_ctx *c);
 static int ensure_marked(nemo_ctx *c);
 
@@ -385,6 +387,12 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->glob_min_v = value < 0 ? ~0ull : (uint64_t)value;
     return NEMO_OK;
   }
+  if (!strcmp(name, "global_block")) {  // 256, 1024, or -1 = by corpus shape (set_global_block)
+    if (value != 256 && value != 1024 && value != -1) return fail(c, NEMO_ERR_INVALID, "global_block must be 256, 1024 or -1");
+    c->gblock_force = value < 0 ? 0u : (uint32_t)value;
+    if (c->loaded) set_global_block(c);
+    return NEMO_OK;
+  }
   if (!strcmp(name, "chains_comp_max")) {
     c->comp_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.comp_limit = c->comp_limit;
@@ -401,6 +409,17 @@ int nemo_set_timing(nemo_ctx *c, int enable) {
 
 uint64_t nemo_num_nodes(const nemo_ctx *c) { return c ? c->V : 0; }
 uint64_t nemo_num_edges(const nemo_ctx *c) { return c ? c->E : 0; }
+
+// Workgroup size of the global-tier kernels: deep corpora (at least one graph
+// in eight over 64k nodes) have few graphs per CU and long per-node passes,
+// so they get 1024 threads (16 waves of memory-level parallelism per graph);
+// corpora of small graphs keep 256 so the early-exit workgroups of the LDS
+// tier's graphs stay cheap.
+static void set_global_block(nemo_ctx *c) {
+  uint32_t deep = 0;
+  for (uint32_t g = 0; g < c->G; g++) deep += (c->node_off[g + 1] - c->node_off[g]) >= 65536u;
+  c->dc.gblock = c->gblock_force ? c->gblock_force : ((uint64_t)deep * 8u >= c->G && deep ? 1024u : NEMO_BLOCK);
+}
 
 // LDS graph tier caps (device.h): the largest graphs, smallest first, whose
 // staged form fits LDS_TIER_BUDGET, i.e. two workgroups per CU.
@@ -630,6 +649,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   set_build_tier(c);
   d.comp_limit = c->comp_limit;
   set_lds_tier(c);
+  set_global_block(c);
   d.n_runs = c->n_runs;
   d.n_tables = c->T;
   d.words = c->W;

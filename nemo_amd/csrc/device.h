@@ -156,6 +156,7 @@ struct DevCorpus {
   uint32_t bld_v, bld_e, bld_bytes;      // k_build's LDS caps and image size (0 = tier off)
   uint32_t lds_v, lds_e, lds_l;          // LDS graph tier caps (V, E, Kahn levels); 0 = tier off
   uint32_t lds_bytes;                    // dynamic LDS of the tier's kernels
+  uint32_t gblock;                       // workgroup size of the global-tier kernels (256, or 1024 for deep corpora)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
   const uint32_t *esrc, *edst;

@@ -11,7 +11,8 @@ namespace nemo {
 // goals (LDS bitset); if Tq is non-empty every goal whose table is C or in Tq
 // holds.  Also counts holding "pre" goals for GenerateExtensions
 // (extensions.go:25-49).  Resets every other flag bit of the graph.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c, int skip_tier) {
+template <int B>
+__global__ __launch_bounds__(B) void k_mark(DevCorpus c, int skip_tier) {
   __shared__ uint32_t s_tq[NEMO_MAX_TABLES / 32];
   __shared__ uint32_t s_any, s_pre;
   const uint32_t g = blockIdx.x;
@@ -19,13 +20,13 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c, int skip_tier)
   const GraphView gv = c.view(g);
   if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
-  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) s_tq[i] = 0;
+  for (uint32_t i = threadIdx.x; i < c.words; i += B) s_tq[i] = 0;
   if (threadIdx.x == 0) {
     s_any = 0;
     s_pre = 0;
   }
   __syncthreads();
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     const uint32_t w = gv.word[x];
     if (is_rule(w) || gv.outdeg(x) == 0) continue;
     bool pos = false, neg = false;
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c, int skip_tier)
   __syncthreads();
   const bool any = s_any != 0;
   uint32_t pre = 0;
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     const uint32_t w = gv.word[x];
     const uint32_t t = table_of(w);
     const bool h = any && !is_rule(w) && (t == C || ((s_tq[t >> 5] >> (t & 31)) & 1u));
@@ -64,21 +65,22 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_mark(DevCorpus c, int skip_tier)
 // on the clean graph a goal with a next-rule parent and a next-rule child, or
 // a next rule with a next-rule grandparent or grandchild, lies on an @next
 // chain and is DETACH DELETEd; heads/tails are the chain ends.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c, int skip_tier) {
+template <int B>
+__global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier) {
   __shared__ uint32_t s_hold;
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
   if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   uint8_t *f = gv.flags;
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     uint8_t fl = f[x] & NEMO_F_HOLDS;
     if (!is_rule(gv.word[x]) || (gv.indeg(x) > 0 && gv.outdeg(x) > 0)) fl |= NEMO_F_KEPT;
     f[x] = fl;
   }
   __syncthreads();
 #define ISNEXT(v) (is_rule(gv.word[v]) && type_of(gv.word[v]) == NEMO_TYPE_NEXT && (f[v] & NEMO_F_KEPT))
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     if (is_rule(gv.word[x])) continue;
     uint8_t b = 0;
     for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++)
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c, int 
     f[x] |= b;
   }
   __syncthreads();
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     if (!ISNEXT(x)) continue;
     bool gp = false, gc = false;
     for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) gp |= (f[gv.rc[j]] & FT_NP) != 0;
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_simplify_flags(DevCorpus c, int 
 #undef ISNEXT
   __syncthreads();
   bool hold = false;
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     if (is_rule(gv.word[x])) continue;
     uint8_t fl = f[x];
     if ((fl & FT_NP) && (fl & FT_NC)) fl |= NEMO_F_DELETED;
@@ -127,7 +129,8 @@ __device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphVi
 // set (:143-147) on the simplified post graph, without materialising it:
 // collapsed rule k is reached through its head (preds(r1) = goal parents of
 // the head) and leads to the goal children of its tail.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
+template <int B>
+__global__ __launch_bounds__(B) void k_proto(DevCorpus c) {
   __shared__ uint32_t s_s[NEMO_MAX_TABLES / 32];
   __shared__ uint32_t s_t[NEMO_MAX_TABLES / 32];
   __shared__ uint32_t s_gate;
@@ -142,21 +145,21 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t *tf = c.tail_first + gv.n0, *nt = c.chain_nt + gv.n0;
   const uint32_t nch = c.nch[g];
-  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) {
+  for (uint32_t i = threadIdx.x; i < c.words; i += B) {
     s_s[i] = 0;
     s_t[i] = 0;
   }
   if (threadIdx.x == 0) s_gate = 0;
   __syncthreads();
   // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
-  for (uint32_t x = threadIdx.x; x < pre.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < pre.V; x += B) {
     const uint8_t fl = pre.flags[x];
     if (!is_rule(pre.word[x]) && (fl & NEMO_F_HOLDS) && !(fl & NEMO_F_DELETED)) s_gate = 1;
   }
 #define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
 #define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
 #define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     const uint32_t w = gv.word[x];
     uint8_t b = 0;
     if (is_rule(w)) {
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   }
   __syncthreads();
   // R1: rule children of roots (regular rules, and collapsed rules via their head)
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     const uint32_t w = gv.word[x];
     if (!is_rule(w) || !(REG(x) || (f[x] & NEMO_F_HEAD))) continue;
     bool r1 = false;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   }
   __syncthreads();
   // G2: goal children of R1 rules; collapsed R1 rules that have a goal child with a rule child
-  for (uint32_t x = threadIdx.x; x < gv.V; x += NEMO_BLOCK) {
+  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     if (is_rule(gv.word[x]) || DEL(x)) continue;
     bool g2 = false;
     for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1] && !g2; j++) {
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
     }
     if (g2) sb[x] |= SB_G2;
   }
-  for (uint32_t k = threadIdx.x; k < nch; k += NEMO_BLOCK) {
+  for (uint32_t k = threadIdx.x; k < nch; k += B) {
     const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
     if (!(sb[h] & SB_R1)) continue;
     for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) {
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
   __syncthreads();
   // rules reachable from G2 (forward level sweep over graph')
   for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
       const uint32_t x = gv.topo[i];
       const uint32_t w = gv.word[x];
       bool rch = false;
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_proto(DevCorpus c) {
 #undef REG
 #undef ADD
   const bool gate = s_gate != 0;
-  for (uint32_t i = threadIdx.x; i < c.words; i += NEMO_BLOCK) {
+  for (uint32_t i = threadIdx.x; i < c.words; i += B) {
     c.proto_bits[(size_t)r * c.words + i] = gate ? s_s[i] : 0u;
     c.graph_tables[(size_t)r * c.words + i] = s_t[i];
   }
@@ -595,10 +598,16 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_
 }
 
 void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s) {
-  hipLaunchKernelGGL(k_mark, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_mark<1024>, dim3(c.G), dim3(1024), 0, s, c, skip_tier ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_mark<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
 }
 void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s) {
-  hipLaunchKernelGGL(k_simplify_flags, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_simplify_flags<1024>, dim3(c.G), dim3(1024), 0, s, c, skip_tier ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_simplify_flags<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
 }
 void launch_marksimp(const DevCorpus &c, hipStream_t s) {
   if (!c.lds_bytes) return;
@@ -610,7 +619,10 @@ void launch_proto(const DevCorpus &c, hipStream_t s) {
     hipFuncSetAttribute((const void *)k_proto_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
     hipLaunchKernelGGL(k_proto_lds, dim3(c.n_runs), dim3(PROTO_BLOCK), c.lds_bytes, s, c);
   }
-  hipLaunchKernelGGL(k_proto, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_proto<1024>, dim3(c.n_runs), dim3(1024), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_proto<NEMO_BLOCK>, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s) {

@@ -50,12 +50,13 @@ __device__ __forceinline__ bool diff_lds_fits(const DevCorpus &c, const GraphVie
 // DL_BATCH source nodes and walks their hash probes together, so a pass costs
 // a few rounds of independent loads rather than a binary search per node.
 #define DL_BATCH 8
+template <int B = NEMO_BLOCK>
 __device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphView &src, uint8_t *bits) {
-  for (uint32_t base = 0; base < src.V; base += DL_BATCH * NEMO_BLOCK) {
+  for (uint32_t base = 0; base < src.V; base += DL_BATCH * B) {
     uint32_t lab[DL_BATCH], h[DL_BATCH], pos[DL_BATCH], live = 0;
 #pragma unroll
     for (int q = 0; q < DL_BATCH; q++) {
-      const uint32_t x = base + q * NEMO_BLOCK + threadIdx.x;
+      const uint32_t x = base + q * B + threadIdx.x;
       const bool in = x < src.V && !is_rule(src.word[x]);
       lab[q] = in ? src.label[x] : 0u;
       h[q] = hash_label(lab[q]) & a.r0hmask;
@@ -93,7 +94,8 @@ __device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphVi
 //   Good = goals of g0 whose label is absent from the source run's post goals
 //   D    = Fwd*(Good) ∩ Bwd*(Good)                       (:22-32, APOC export)
 //   missing = D rules with a D-leaf child at maximal depth (:82-98)
-__global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
+template <int B>
+__global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   __shared__ int32_t s_max;
   const uint32_t e = blockIdx.x;
   const GraphView gv = c.view(a.g0);
@@ -104,13 +106,13 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
   int32_t *depth = a.depth + (size_t)e * V;
   uint8_t *mask = a.mask + (size_t)e * V;
   if (threadIdx.x == 0) s_max = -1;
-  for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) bits[v] = 0;
+  for (uint32_t v = threadIdx.x; v < V; v += B) bits[v] = 0;
   __syncthreads();
-  diff_fail_goals(a, src, bits);
+  diff_fail_goals<B>(a, src, bits);
   __syncthreads();
 #define GOOD(v) (!is_rule(gv.word[v]) && !(bits[v] & DB_PRESENT))
   for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
       const uint32_t v = gv.topo[i];
       bool fw = GOOD(v);
       for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1] && !fw; j++) fw = (bits[gv.rc[j]] & DB_F) != 0;
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
     __syncthreads();
   }
   for (uint32_t l = gv.nlev; l-- > 0;) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
       const uint32_t v = gv.topo[i];
       bool bw = GOOD(v);
       for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1] && !bw; j++) bw = (bits[gv.fc[j]] & DB_B) != 0;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
 #undef GOOD
   // longest path from a D root (Kahn-level DP restricted to D)
   for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += NEMO_BLOCK) {
+    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
       const uint32_t v = gv.topo[i];
       const uint8_t b = bits[v];
       mask[v] = (b & DB_D) ? 1 : 0;
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
     }
     __syncthreads();
   }
-  for (uint32_t r = threadIdx.x; r < V; r += NEMO_BLOCK) {
+  for (uint32_t r = threadIdx.x; r < V; r += B) {
     if (!(bits[r] & DB_D) || !is_rule(gv.word[r])) continue;
     bool lp = false;
     for (uint32_t j = gv.fp[r]; j < gv.fp[r + 1]; j++) {
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff(DevCorpus c, DiffArgs a) {
   }
   __syncthreads();
   const int32_t mx = s_max;
-  for (uint32_t r = threadIdx.x; r < V; r += NEMO_BLOCK) {
+  for (uint32_t r = threadIdx.x; r < V; r += B) {
     if ((bits[r] & DB_LP) && depth[r] + 1 == mx) {
       const uint32_t k = atomicAdd(a.n_missing, 1u);
       a.missing[2 * k] = e;
@@ -329,8 +331,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan64(const uint32_t *cnt, uint
 // (pred->V+k for the head's goal parents, V+k->succ for the tail's goal
 // children).  A region past a.cap is not written: the host re-runs the pull
 // with the capacity the cursor reports.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
-  __shared__ uint32_t s_lds[NEMO_WAVES];
+template <int B>
+__global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_lds[(B / 64)];
   __shared__ uint32_t s_cnt;
   __shared__ unsigned long long s_base;
   const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
@@ -350,11 +353,11 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   uint32_t n = 0;
-  for (uint32_t u = threadIdx.x; u < gv.V; u += NEMO_BLOCK) {
+  for (uint32_t u = threadIdx.x; u < gv.V; u += B) {
     if (!pull_alive(a.which, gv.flags, m, u)) continue;
     for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
   }
-  for (uint32_t k = threadIdx.x; k < nch; k += NEMO_BLOCK) {
+  for (uint32_t k = threadIdx.x; k < nch; k += B) {
     const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
     for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
     for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
@@ -371,14 +374,14 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
   __syncthreads();
   uint64_t pos = s_base;
   if (pos + s_cnt > a.cap) return;
-  for (uint32_t base = 0; base < gv.V; base += NEMO_BLOCK) {
+  for (uint32_t base = 0; base < gv.V; base += B) {
     const uint32_t u = base + threadIdx.x;
     uint32_t n = 0;
     const bool au = u < gv.V && pull_alive(a.which, gv.flags, m, u);
     if (au)
       for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
     uint32_t tot;
-    uint64_t o = pos + block_exscan(n, &tot, s_lds);
+    uint64_t o = pos + block_exscan<B>(n, &tot, s_lds);
     if (au)
       for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) {
         const uint32_t v = gv.fc[j];
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
       }
     pos += tot;
   }
-  for (uint32_t base = 0; base < nch; base += NEMO_BLOCK) {
+  for (uint32_t base = 0; base < nch; base += B) {
     const uint32_t k = base + threadIdx.x;
     uint32_t n = 0, h = 0, t = 0;
     if (k < nch) {
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull(DevCorpus c, PullArgs a) {
       for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
     }
     uint32_t tot;
-    uint64_t o = pos + block_exscan(n, &tot, s_lds);
+    uint64_t o = pos + block_exscan<B>(n, &tot, s_lds);
     if (k < nch) {
       for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) {
         const uint32_t p = gv.rc[j];
@@ -716,7 +719,10 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipS
     hipFuncSetAttribute((const void *)k_diff_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_diff_lds, dim3(n_entries), dim3(NEMO_BLOCK), bytes, s, c, a);
   }
-  hipLaunchKernelGGL(k_diff, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_diff<1024>, dim3(n_entries), dim3(1024), 0, s, c, a);
+  else
+    hipLaunchKernelGGL(k_diff<NEMO_BLOCK>, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
   if (a.which != 2 && c.lds_bytes) {
@@ -724,7 +730,10 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
   }
-  hipLaunchKernelGGL(k_pull, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_pull<1024>, dim3(slots), dim3(1024), 0, s, c, a);
+  else
+    hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
   hipLaunchKernelGGL(k_triggers, dim3(3 * TRIG_SPLIT), dim3(NEMO_BLOCK), 0, s, c, a, phase);

@@ -259,9 +259,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
 // Graphs with V < CSR_LDS count degrees, scan and hand out cursors in LDS;
 // larger ones do the same with global atomics.
 #define CSR_LDS 8192
-__global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
+template <int B>
+__global__ __launch_bounds__(B) void k_csr(DevCorpus c) {
   __shared__ uint32_t s_cnt[CSR_LDS];
-  __shared__ uint32_t s_lds[NEMO_WAVES];
+  __shared__ uint32_t s_lds[(B / 64)];
   __shared__ uint32_t s_bad, s_created;
   const uint32_t g = blockIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
     s_bad = 0;
     s_created = 0;
   }
-  for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK)
+  for (uint32_t e = threadIdx.x; e < E; e += B)
     if (es[e] >= V || ed[e] >= V) s_bad = 1;
   __syncthreads();
   if (s_bad) {
@@ -284,36 +285,36 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
     for (int dir = 0; dir < 2; dir++) {
       const uint32_t *key = dir ? ed : es, *val = dir ? es : ed;
       uint32_t *ptr = dir ? rp : fp, *col = dir ? rc : fc;
-      for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) s_cnt[v] = 0;
+      for (uint32_t v = threadIdx.x; v <= V; v += B) s_cnt[v] = 0;
       __syncthreads();
-      for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) atomicAdd(&s_cnt[key[e]], 1u);
+      for (uint32_t e = threadIdx.x; e < E; e += B) atomicAdd(&s_cnt[key[e]], 1u);
       __syncthreads();
-      block_scan_inplace(s_cnt, V + 1, s_lds);
-      for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) ptr[v] = s_cnt[v];
+      block_scan_inplace<B>(s_cnt, V + 1, s_lds);
+      for (uint32_t v = threadIdx.x; v <= V; v += B) ptr[v] = s_cnt[v];
       __syncthreads();
-      for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) col[atomicAdd(&s_cnt[key[e]], 1u)] = val[e];
+      for (uint32_t e = threadIdx.x; e < E; e += B) col[atomicAdd(&s_cnt[key[e]], 1u)] = val[e];
       __syncthreads();
     }
   } else {
     uint32_t *cf = c.s_a + n0 + g, *cr = c.s_b + n0 + g;
-    for (uint32_t v = threadIdx.x; v <= V; v += NEMO_BLOCK) {
+    for (uint32_t v = threadIdx.x; v <= V; v += B) {
       fp[v] = 0;
       rp[v] = 0;
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
+    for (uint32_t e = threadIdx.x; e < E; e += B) {
       atomicAdd(&fp[es[e]], 1u);
       atomicAdd(&rp[ed[e]], 1u);
     }
     __syncthreads();
-    block_scan_inplace(fp, V + 1, s_lds);
-    block_scan_inplace(rp, V + 1, s_lds);
-    for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) {
+    block_scan_inplace<B>(fp, V + 1, s_lds);
+    block_scan_inplace<B>(rp, V + 1, s_lds);
+    for (uint32_t v = threadIdx.x; v < V; v += B) {
       cf[v] = fp[v];
       cr[v] = rp[v];
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < E; e += NEMO_BLOCK) {
+    for (uint32_t e = threadIdx.x; e < E; e += B) {
       const uint32_t s = es[e], d = ed[e];
       fc[atomicAdd(&cf[s], 1u)] = d;
       rc[atomicAdd(&cr[d], 1u)] = s;
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
   }
   __threadfence_block();
   uint32_t created = 0;
-  for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) {
+  for (uint32_t v = threadIdx.x; v < V; v += B) {
     const uint32_t a = fp[v], b = fp[v + 1];
     sort_row(fc + a, b - a);
     sort_row(rc + rp[v], rp[v + 1] - rp[v]);
@@ -343,7 +344,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_csr(DevCorpus c) {
 
 // Kahn levels: topo[] lists the graph's nodes level by level, lvl[l]..lvl[l+1]
 // is level l (longest path from a source).  A graph with a cycle is refused.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
+template <int B>
+__global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
   __shared__ uint32_t s_tail;
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
@@ -353,9 +355,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
   const uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0;
   uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g, *cnt = c.s_a + n0 + g;
   if (threadIdx.x == 0) s_tail = 0;
-  for (uint32_t v = threadIdx.x; v < V; v += NEMO_BLOCK) cnt[v] = rp[v + 1] - rp[v];
+  for (uint32_t v = threadIdx.x; v < V; v += B) cnt[v] = rp[v + 1] - rp[v];
   __syncthreads();
-  for (uint32_t base = 0; base < V; base += NEMO_BLOCK) {
+  for (uint32_t base = 0; base < V; base += B) {
     const uint32_t v = base + threadIdx.x;
     wave_append(v < V && cnt[v] == 0u, v, topo, &s_tail);
     if (v < V && cnt[v] == 0u) c.nlv[n0 + v] = 0;
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_topo(DevCorpus c) {
   if (threadIdx.x == 0) lvl[0] = 0;
   __syncthreads();
   while (lo < hi) {
-    for (uint32_t base = lo; base < hi; base += NEMO_BLOCK) {
+    for (uint32_t base = lo; base < hi; base += B) {
       const uint32_t i = base + threadIdx.x;
       uint32_t j = 0, je = 0;
       if (i < hi) {
@@ -403,10 +405,16 @@ void launch_build(const DevCorpus &c, hipStream_t s) {
   hipLaunchKernelGGL(k_build, dim3(c.G), dim3(NEMO_BLOCK), c.bld_bytes, s, c);
 }
 void launch_load(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_csr, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_csr<1024>, dim3(c.G), dim3(1024), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_csr<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_topo(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL(k_topo, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  if (c.gblock == 1024)
+    hipLaunchKernelGGL(k_topo<1024>, dim3(c.G), dim3(1024), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
 }
 
 }  // namespace nemo

@@ -311,3 +311,23 @@ def test_chains_lds_tiers(eng, shape):
         corpus = corpus_from_graphs([(0, "success", chain("pre", 80), chain("post", 80)),
                                      (1, "failure", chain("pre", 40), chain("post", 70))])
     _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+
+
+@pytest.mark.parametrize("block", [256, 1024])
+def test_global_tier_block(eng, block):
+    # every graph on the global-memory kernels (k_csr, k_topo, k_mark,
+    # k_simplify_flags, k_proto, k_diff, k_pull) at both workgroup sizes; deep
+    # corpora select 1024 threads by shape
+    from tools import synth
+    corpus, _ = synth.generate(24, target_nodes=2500)
+    for k, v in (("graph_lds_max", 0), ("build_lds_max", 0), ("global_block", block)):
+        eng.set_option(k, v)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+        _check(eng, corpus, mode=DIFF_REFERENCE)
+        for seed in range(4):
+            c2, _ = random_corpus(900 + seed, max_nodes=24)
+            _check(eng, c2)
+    finally:
+        for k in ("graph_lds_max", "build_lds_max", "global_block"):
+            eng.set_option(k, -1)
