@@ -75,21 +75,24 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
 }
 
 // In-place exclusive scan of a[0..n) by one workgroup of B threads; returns the total.
-template <int B = NEMO_BLOCK, typename T>
+// Each round takes PER consecutive elements per thread: 4 for LDS arrays (few
+// bank conflicts), 16 for HBM arrays (16 independent loads in flight per
+// thread, so a long scan costs few latency-bound rounds).
+template <int B = NEMO_BLOCK, int PER = 4, typename T>
 __device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_t *lds) {
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < n; base += B * 4) {
-    const uint32_t i0 = base + threadIdx.x * 4;
-    uint32_t x[4], s = 0;
+  for (uint32_t base = 0; base < n; base += B * PER) {
+    const uint32_t i0 = base + threadIdx.x * PER;
+    uint32_t x[PER], s = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < PER; k++) {
       x[k] = (i0 + k < n) ? a[i0 + k] : 0u;
       s += x[k];
     }
     uint32_t tot;
     uint32_t ex = block_exscan<B>(s, &tot, lds) + carry;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < PER; k++) {
       if (i0 + k < n) a[i0 + k] = (T)ex;
       ex += x[k];
     }

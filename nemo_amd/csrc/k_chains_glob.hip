@@ -4,7 +4,7 @@
 // desc then the preorder of the representatives in the best-prefix forest)
 // with every per-node array in a global scratch region, so it scales to
 // chain subgraphs of hundreds of thousands of nodes and thousands of levels
-// (1M-node graphs, EOT ~ 2000).  One 512-thread workgroup per
+// (1M-node graphs, EOT ~ 2000).  One 1024-thread workgroup per
 // graph; long walks (chain heads and tails, ancestor sums) use pointer
 // jumping, the final order a bitonic sort of 64-bit keys.  The graphs are the
 // ones the host gave a scratch region (DevCorpus::gs_off, V >= glob_min_v);
@@ -14,7 +14,7 @@
 
 namespace nemo {
 
-#define GB 512  // threads per workgroup
+#define GB 1024  // threads per workgroup
 #define GNIL 0xFFFFFFFFu
 
 // Scratch layout (u32 units) for a graph of V nodes and E edges.
@@ -107,6 +107,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     s_nch = 0;
     s_fail = 0;
   }
+  STAMP(0);
   // ---- H* in level order, compact ID ranks ------------------------------------
   for (uint32_t l = tid; l <= ns; l += GB) S.seg[l] = 0;
   for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   for (uint32_t x = tid; x < V; x += GB)
     if (f[x] & NEMO_F_DELETED) atomicAdd(&S.seg[nlv[x]], 1u);
   __syncthreads();
-  const uint32_t n = block_scan_inplace<GB>(S.seg, ns + 1, s_lds);
+  const uint32_t n = block_scan_inplace<GB, 16>(S.seg, ns + 1, s_lds);
   if (n == 0) {
     if (tid == 0) c.nch[g] = 0;
     return;
@@ -134,11 +135,12 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   for (uint32_t w = tid; w < nw; w += GB) S.bmpre[w] = __popc(S.bm[w]);
   __syncthreads();
-  block_scan_inplace<GB>(S.bmpre, nw, s_lds);
+  block_scan_inplace<GB, 16>(S.bmpre, nw, s_lds);
   for (uint32_t i = tid; i < n; i += GB) {
     const uint32_t r = S.crank[i];
     S.crank[i] = S.bmpre[r >> 5] + __popc(S.bm[r >> 5] & ((1u << (r & 31)) - 1u));
   }
+  STAMP(1);
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
   for (uint32_t i = tid; i <= n; i += GB) {
     S.ccoff[i] = 0;
@@ -154,8 +156,8 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     atomicAdd(&S.pcoff[hidx[b]], 1u);
   }
   __syncthreads();
-  block_scan_inplace<GB>(S.ccoff, n + 1, s_lds);
-  block_scan_inplace<GB>(S.pcoff, n + 1, s_lds);
+  block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
+  block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
   for (uint32_t i = tid; i < n; i += GB) {
     S.ccur[i] = S.ccoff[i];
     S.pcur[i] = S.pcoff[i];
@@ -170,6 +172,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   }
 #undef INH
   __syncthreads();
+  STAMP(2);
   // ---- up (forward) and down/nxt (backward), half the workgroup each -------------
   {
     constexpr uint32_t HALF = GB / 2;
@@ -208,6 +211,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       __syncthreads();
     }
   }
+  STAMP(3);
   uint32_t mu = 0, ml = 0;
   for (uint32_t i = tid; i < n; i += GB) {
     mu = max(mu, (uint32_t)max(S.up[i], 0));
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   for (uint32_t i = tid; i < n; i += GB) atomicAdd(&S.uoff[S.up[i]], 1u);
   __syncthreads();
-  block_scan_inplace<GB>(S.uoff, maxup + 2, s_lds);
+  block_scan_inplace<GB, 16>(S.uoff, maxup + 2, s_lds);
   for (uint32_t k = tid; k <= maxup + 1; k += GB) S.cnt[k] = S.uoff[k];
   __syncthreads();
   for (uint32_t i = tid; i < n; i += GB) S.ub[atomicAdd(&S.cnt[S.up[i]], 1u)] = i;
@@ -238,6 +242,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     S.bp[i] = cn > 1 ? MULTI : cand;
   }
   __syncthreads();
+  STAMP(4);
   // ---- prefix ranks per up-level: roots by ID rank, then groups by po(bp) -----------
   for (uint32_t k = 0; k <= maxup; k++) {
     const uint32_t a = S.uoff[k], b = S.uoff[k + 1];
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       __syncthreads();
       for (uint32_t w = tid; w < rw; w += GB) S.bmpre[w] = __popc(S.bm[w]);
       __syncthreads();
-      block_scan_inplace<GB>(S.bmpre, rw, s_lds);
+      block_scan_inplace<GB, 16>(S.bmpre, rw, s_lds);
       for (uint32_t j = a + tid; j < b; j += GB) {
         const uint32_t i = S.ub[j], cr = S.crank[i];
         S.po[i] = S.bmpre[cr >> 5] + __popc(S.bm[cr >> 5] & ((1u << (cr & 31)) - 1u));
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       atomicAdd(&S.cnt[S.po[bpi]], 1u);
     }
     __syncthreads();
-    block_scan_inplace<GB>(S.cnt, mp + 1, s_lds);  // group bases
+    block_scan_inplace<GB, 16>(S.cnt, mp + 1, s_lds);  // group bases
     for (uint32_t j = a + tid; j < b; j += GB) {
       const uint32_t i = S.ub[j];
       S.grp[atomicAdd(&S.cnt[S.po[S.bp[i]]], 1u)] = i;
@@ -297,6 +302,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     }
     __syncthreads();
   }
+  STAMP(5);
   // ---- heads (roots of the bp forest) and tails (ends of nxt) by pointer jumping -----
   uint32_t *h0 = S.ha, *h1 = S.hb, *t0 = S.ta, *t1 = S.tb;
   for (uint32_t i = tid; i < n; i += GB) {
@@ -332,6 +338,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __threadfence_block();
   __syncthreads();
   const uint32_t nch = s_nch;
+  STAMP(6);
   // ---- preorder of the representatives: pre(v) = up(v) + sum of off over v and its bp
   // ancestors, off = sizes of the earlier siblings (sizes laid out in (level, po) order)
   for (uint32_t i = tid; i < n; i += GB) S.S[i] = 1;
@@ -345,7 +352,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   }
   for (uint32_t i = tid; i < n; i += GB) S.A[S.uoff[S.up[i]] + S.po[i]] = S.S[i];
   __syncthreads();
-  block_scan_inplace<GB>(S.A, n, s_lds);
+  block_scan_inplace<GB, 16>(S.A, n, s_lds);
   uint32_t *va = S.va, *vb = S.vb, *pa = S.pa, *pb = S.pb;
   for (uint32_t i = tid; i < n; i += GB) {
     const uint32_t k = S.up[i], base = S.uoff[k];
@@ -372,6 +379,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     pa = pb;
     pb = x;
   }
+  STAMP(7);
   // ---- acceptance order: keys (len desc, preorder asc) are unique; bitonic sort -------
   uint32_t N2 = 1;
   while (N2 < nch) N2 <<= 1;
@@ -404,6 +412,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       __syncthreads();
     }
   }
+  STAMP(8);
   uint32_t *out = c.chain + 5 * gv.n0;
   for (uint32_t pos = tid; pos < nch; pos += GB) {
     const uint32_t q = S.grp[(uint32_t)(S.key[pos] & 0xFFFFFFFFu)];
@@ -421,6 +430,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     const uint32_t t = out[5 * k + 1];
     c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
   }
+  STAMP(9);
   if (tid == 0) {
     c.nch[g] = nch;
     if (s_fail) c.err[g] = NEMO_ERR_INVALID;

@@ -307,8 +307,8 @@ __global__ __launch_bounds__(B) void k_csr(DevCorpus c) {
       atomicAdd(&rp[ed[e]], 1u);
     }
     __syncthreads();
-    block_scan_inplace<B>(fp, V + 1, s_lds);
-    block_scan_inplace<B>(rp, V + 1, s_lds);
+    block_scan_inplace<B, 16>(fp, V + 1, s_lds);
+    block_scan_inplace<B, 16>(rp, V + 1, s_lds);
     for (uint32_t v = threadIdx.x; v < V; v += B) {
       cf[v] = fp[v];
       cr[v] = rp[v];

@@ -1,0 +1,28 @@
+"""Diagnostic: per-phase cycle shares of k_chains_glob (deep graphs) from the stamps build.
+
+usage: python tools/stamps_glob.py [RUNS] [NODES] [EOT]
+"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import nemo_amd.engine as E
+E.LIB_PATH = os.path.join(os.path.dirname(E.LIB_PATH), "libnemohip_stamps.so")
+from tools import synth
+runs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+eot = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
+corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16)
+eng = E.Engine(0)
+eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
+G = corpus.n_graphs
+st = eng.debug_copy("stamps", 0, 16 * 8 * G).view(np.uint64).reshape(G, 16).astype(np.int64)
+names = ["H* compact + ranks", "adjacency", "up/down", "bucket + bp", "prefix ranks", "heads/tails + reps",
+         "preorder", "bitonic sort", "output + tail lists"]
+ok = st[:, 9] > 0
+d = np.diff(st[ok][:, :10], axis=1)
+print("graphs", int(ok.sum()), "total ticks per graph: median", np.median(d.sum(1)))
+for i, nm in enumerate(names):
+    print(f"{nm:22s} median {np.median(d[:, i]):12.0f}  share {d[:, i].sum() / d.sum():.3f}")
+ch = eng.chains()
+print("chains per graph", len(ch) / G, "max chain length", int(np.max(ch[:, 4])) if len(ch) else 0)
+eng.close()
