@@ -953,7 +953,7 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
     if ((rc = dalloc(c, &c->d_dsrc, n_failed))) return rc;
     if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_ddepth, (n_failed + 1) * V0))) return rc;  // + g0's inverse Kahn order
     if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
     c->diff_cap = (uint32_t)n_failed;
   }
@@ -973,6 +973,7 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   a.r0hmask = c->r0hmask;
   a.bits = c->d_dbits;
   a.depth = c->d_ddepth;
+  a.tpos = (uint32_t *)(c->d_ddepth + (size_t)c->diff_cap * V0);
   a.mask = c->d_dmask;
   a.missing = c->d_miss;
   a.n_missing = c->d_nmiss;
@@ -1413,6 +1414,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   if (n == "topo") base = c->dc.topo;
   else if (n == "lvl") base = c->dc.lvl;
   else if (n == "nlv") base = c->dc.nlv;
+  else if (n == "diff_tpos") base = c->d_ddepth ? c->d_ddepth + (size_t)c->diff_cap * (c->node_off[2 * c->run0 + 2] - c->node_off[2 * c->run0 + 1]) : nullptr;
   else if (n == "nlev") base = c->dc.nlev;
   else if (n == "fp") base = c->dc.fp;
   else if (n == "fc") base = c->dc.fc;

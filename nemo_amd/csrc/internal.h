@@ -19,6 +19,7 @@ struct DiffArgs {
   uint32_t r0hmask;         // table size - 1 (power of two)
   uint8_t *bits;            // [entries * V0] scratch
   int32_t *depth;           // [entries * V0] scratch
+  uint32_t *tpos;           // [V0] inverse Kahn order of g0 (global tier)
   uint8_t *mask;            // [entries * V0] D mask (output)
   uint32_t *missing;        // [2 * cap] (entry, rule)
   uint32_t *n_missing;      // counter

@@ -90,12 +90,291 @@ __device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphVi
   }
 }
 
+// ---- windowed level sweeps (global tier: run 0's post graph outside LDS) ------
+// A level-synchronous sweep over a deep graph (C5: ~4900 Kahn levels of ~200
+// nodes) is bound by dependent HBM round trips per level (topo -> row ->
+// neighbour -> neighbour's bit).  Here the Kahn order is cut into windows of
+// DW_N consecutive positions.  One staging pass per window issues all of
+// those loads at once: neighbours outside the window are final and fold
+// into an accumulator, neighbours inside it become LDS links (topo position
+// - window start, via the inverse order tpos).  The window's levels are then
+// swept in LDS with one barrier each, so a window of ~20 levels costs about
+// one round of HBM latency instead of ~20 rounds of four.
+#define DW_N 4096u    // Kahn positions per window
+#define DW_E 8192u    // in-window links past each node's first two, staged in LDS
+#define DW_SPILL 0xFFFFu
+#ifndef DW_NREG
+#define DW_NREG 2u    // links per node held in registers
+#endif
+struct DiffWin {
+  uint32_t off[DW_N];     // first extra link of node k
+  int32_t dep[DW_N];      // depth (mode 2)
+  uint16_t ln[DW_N];      // extra link count, DW_SPILL = re-read the row from HBM
+  uint16_t adj[DW_E];     // window-local index of each extra in-window link
+  uint16_t u0[DW_N], u1[DW_N];  // first two in-window links (DW_SPILL = none)
+  uint8_t val[DW_N];      // F / B bit (modes 0, 1), D bit (mode 2)
+  uint32_t l0, l1;        // first and last Kahn level in the window
+};
+
+// mode 0: F = Good | any F parent        (Fwd*(Good), forward over parents)
+// mode 1: B = Good | any B child; D = F&B (Bwd*(Good), backward over children)
+// mode 2: depth = max(0, depth(p) + 1 over D parents p), D nodes only
+// Thread t owns window positions t, t + B, ...: the node, its level, its
+// accumulator and its first two in-window links stay in registers, so a
+// level of the sweep is one LDS probe per link and one barrier.
+template <int B, int MODE>
+__device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32_t *nlv, const uint32_t *tpos, uint8_t *bits,
+                                  int32_t *depth, DiffWin &W, uint32_t *s_red, unsigned long long *st) {
+#ifdef NEMO_STAMPS
+  unsigned long long acc_s = 0, acc_l = 0, acc_w = 0, t_a, t_b;
+#define DW_T(t) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory")
+#else
+#define DW_T(t) \
+  do {          \
+  } while (0)
+#endif
+  constexpr int PT = (int)(DW_N / B);
+  constexpr bool FWD = MODE != 1;
+  constexpr uint32_t NIL = 0xFFFFFFFFu;
+  const uint32_t V = gv.V, tid = threadIdx.x;
+  const uint32_t *ptr = FWD ? gv.rp : gv.fp, *col = FWD ? gv.rc : gv.fc;
+  const uint32_t nwin = (V + DW_N - 1) / DW_N;
+  for (uint32_t wi = 0; wi < nwin; wi++) {
+    // forward: windows in Kahn order; backward: from the end
+    const uint32_t a = FWD ? wi * DW_N : (V > (wi + 1) * DW_N ? V - (wi + 1) * DW_N : 0u);
+    const uint32_t b = FWD ? min(V, a + DW_N) : V - wi * DW_N;
+    const uint32_t n = b - a;
+#ifdef NEMO_STAMPS
+    DW_T(t_a);
+#endif
+    uint32_t vv[PT], r0[PT], r1[PT], lev[PT], p0[PT], p1[PT], u0[PT], u1[PT], cx[PT];
+    int32_t x[PT];
+    uint8_t ob[PT];
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * B;
+      vv[q] = k < n ? gv.topo[a + k] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * B;
+      const bool in = k < n;
+      const uint32_t v = vv[q];
+      r0[q] = in ? ptr[v] : 0u;
+      r1[q] = in ? ptr[v + 1] : 0u;
+      lev[q] = in ? nlv[v] : NIL;
+      ob[q] = in ? bits[v] : 0u;
+      const bool good = in && !is_rule(gv.word[v]) && !(ob[q] & DB_PRESENT);
+      x[q] = MODE == 2 ? 0 : (good ? 1 : 0);
+      if (MODE == 2 && !(ob[q] & DB_D)) r1[q] = r0[q];  // only D nodes get a depth
+      if (MODE != 2 && good) r1[q] = r0[q];             // Good: set regardless of neighbours
+      if (in && k == 0) W.l0 = lev[q];
+      if (in && k == n - 1) W.l1 = lev[q];
+    }
+    // first two neighbours of every node in one batch of loads
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      p0[q] = (DW_NREG >= 1 && r1[q] > r0[q]) ? col[r0[q]] : NIL;
+      p1[q] = (DW_NREG >= 2 && r1[q] > r0[q] + 1) ? col[r0[q] + 1] : NIL;
+    }
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      uint32_t t0 = 0, t1 = 0;
+      uint8_t b0 = 0, b1 = 0;
+      int32_t d0 = 0, d1 = 0;
+      if (p0[q] != NIL) {
+        t0 = tpos[p0[q]];
+        b0 = bits[p0[q]];
+        if (MODE == 2) d0 = depth[p0[q]];
+      }
+      if (p1[q] != NIL) {
+        t1 = tpos[p1[q]];
+        b1 = bits[p1[q]];
+        if (MODE == 2) d1 = depth[p1[q]];
+      }
+      u0[q] = u1[q] = NIL;
+      if (p0[q] != NIL) {
+        const bool inw = FWD ? t0 >= a : t0 < b;
+        if (MODE == 2) {
+          if (b0 & DB_D) {
+            if (inw) u0[q] = t0 - a;
+            else x[q] = max(x[q], d0 + 1);
+          }
+        } else if (inw) {
+          u0[q] = t0 - a;
+        } else if (b0 & (MODE == 0 ? DB_F : DB_B)) {
+          x[q] = 1;
+        }
+      }
+      if (p1[q] != NIL) {
+        const bool inw = FWD ? t1 >= a : t1 < b;
+        if (MODE == 2) {
+          if (b1 & DB_D) {
+            if (inw) u1[q] = t1 - a;
+            else x[q] = max(x[q], d1 + 1);
+          }
+        } else if (inw) {
+          u1[q] = t1 - a;
+        } else if (b1 & (MODE == 0 ? DB_F : DB_B)) {
+          x[q] = 1;
+        }
+      }
+    }
+    // the rest of long rows (rare): out-of-window links fold, in-window ones are counted
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      cx[q] = 0;
+      for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
+        const uint32_t p = col[j], tp = tpos[p];
+        const bool inw = FWD ? tp >= a : tp < b;
+        if (MODE == 2) {
+          if (!(bits[p] & DB_D)) continue;
+          if (inw) cx[q]++;
+          else x[q] = max(x[q], depth[p] + 1);
+        } else if (inw) {
+          cx[q]++;
+        } else if (bits[p] & (MODE == 0 ? DB_F : DB_B)) {
+          x[q] = 1;
+        }
+      }
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PT; q++) sum += cx[q];
+    uint32_t tot;
+    uint32_t base = block_exscan<B>(sum, &tot, s_red);
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * B;
+      if (k >= n) continue;
+      if (MODE == 2) {
+        W.dep[k] = x[q];
+        W.val[k] = (ob[q] & DB_D) ? 1 : 0;
+      } else {
+        W.val[k] = (uint8_t)x[q];
+      }
+      W.u0[k] = u0[q] == NIL ? (uint16_t)DW_SPILL : (uint16_t)u0[q];
+      W.u1[k] = u1[q] == NIL ? (uint16_t)DW_SPILL : (uint16_t)u1[q];
+      if (!cx[q]) continue;
+      const bool spill = base + cx[q] > DW_E;
+      W.off[k] = base;
+      W.ln[k] = spill ? (uint16_t)DW_SPILL : (uint16_t)cx[q];
+      if (!spill) {
+        uint32_t o = base;
+        for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
+          const uint32_t p = col[j], tp = tpos[p];
+          const bool inw = FWD ? tp >= a : tp < b;
+          if (inw && (MODE != 2 || (bits[p] & DB_D))) W.adj[o++] = (uint16_t)(tp - a);
+        }
+      }
+      base += cx[q];
+    }
+    __syncthreads();
+#ifdef NEMO_STAMPS
+    DW_T(t_b);
+    acc_s += t_b - t_a;
+    t_a = t_b;
+#endif
+    const uint32_t l0 = W.l0, nl = W.l1 - l0 + 1u;
+    for (uint32_t i = 0; i < nl; i++) {
+      const uint32_t li = l0 + (FWD ? i : nl - 1 - i);
+#pragma unroll
+      for (int q = 0; q < PT; q++) {
+        if (lev[q] != li) continue;
+        const uint32_t k = tid + q * B;
+        if (MODE != 2) {
+          if (x[q]) continue;
+          const uint32_t w0 = W.u0[k], w1 = W.u1[k];
+          // plain ORs, no short-circuit: the ROCm 7.2 compiler mis-evaluated
+          // `(w0 && val[w0]) || (w1 && val[w1])` in the 1024-thread instance
+          uint32_t hv = 0;
+          if (w0 != DW_SPILL) hv |= W.val[w0];
+          if (w1 != DW_SPILL) hv |= W.val[w1];
+          bool hit = hv != 0;
+          if (!hit && cx[q]) {
+            if (W.ln[k] != DW_SPILL) {
+              const uint32_t o = W.off[k], m = W.ln[k];
+              for (uint32_t t = 0; t < m; t++) hv |= W.val[W.adj[o + t]];
+              hit = hv != 0;
+            } else {
+              for (uint32_t j = r0[q] + DW_NREG; j < r1[q] && !hit; j++) {
+                const uint32_t tp = tpos[col[j]];
+                if (FWD ? tp >= a : tp < b) hit = W.val[tp - a] != 0;
+              }
+            }
+          }
+          if (hit) {
+            x[q] = 1;
+            W.val[k] = 1;
+          }
+        } else {
+          if (!(ob[q] & DB_D)) continue;
+          int32_t d = x[q];
+          const uint32_t w0 = W.u0[k], w1 = W.u1[k];
+          if (w0 != DW_SPILL) d = max(d, W.dep[w0] + 1);
+          if (w1 != DW_SPILL) d = max(d, W.dep[w1] + 1);
+          if (cx[q]) {
+            if (W.ln[k] != DW_SPILL) {
+              const uint32_t o = W.off[k], m = W.ln[k];
+              for (uint32_t t = 0; t < m; t++) d = max(d, W.dep[W.adj[o + t]] + 1);
+            } else {
+              for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
+                const uint32_t p = col[j], tp = tpos[p];
+                if (tp >= a && (bits[p] & DB_D)) d = max(d, W.dep[tp - a] + 1);
+              }
+            }
+          }
+          x[q] = d;
+          W.dep[k] = d;
+        }
+      }
+      __syncthreads();
+    }
+#ifdef NEMO_STAMPS
+    DW_T(t_b);
+    acc_l += t_b - t_a;
+    t_a = t_b;
+#endif
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * B;
+      if (k >= n) continue;
+      if (MODE == 0) {
+        if (x[q]) bits[vv[q]] = ob[q] | DB_F;
+      } else if (MODE == 1) {
+        if (x[q]) bits[vv[q]] = ob[q] | DB_B | ((ob[q] & DB_F) ? DB_D : 0u);
+      } else if (ob[q] & DB_D) {
+        depth[vv[q]] = x[q];
+      }
+    }
+    // the window's HBM writes must be performed before the next window (or
+    // sweep) stages: a workgroup barrier alone does not wait for them
+    __threadfence();
+    __syncthreads();
+#ifdef NEMO_STAMPS
+    DW_T(t_b);
+    acc_w += t_b - t_a;
+#endif
+  }
+#ifdef NEMO_STAMPS
+  if (tid == 0 && st) {
+    st[3 * MODE] = acc_s;
+    st[3 * MODE + 1] = acc_l;
+    st[3 * MODE + 2] = acc_w;
+  }
+#endif
+#undef DW_T
+}
+
 // One workgroup per diff entry, all over run 0's post graph g0:
 //   Good = goals of g0 whose label is absent from the source run's post goals
 //   D    = Fwd*(Good) ∩ Bwd*(Good)                       (:22-32, APOC export)
 //   missing = D rules with a D-leaf child at maximal depth (:82-98)
+// Fwd*, Bwd* and the depths are windowed level sweeps (diff_window_sweep).
 template <int B>
 __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
+  __shared__ DiffWin W;
+  __shared__ uint32_t s_red[B / 64];
   __shared__ int32_t s_max;
   const uint32_t e = blockIdx.x;
   const GraphView gv = c.view(a.g0);
@@ -105,56 +384,37 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   uint8_t *bits = a.bits + (size_t)e * V;
   int32_t *depth = a.depth + (size_t)e * V;
   uint8_t *mask = a.mask + (size_t)e * V;
+  const uint32_t *nlv = c.nlv + gv.n0;
   if (threadIdx.x == 0) s_max = -1;
-  for (uint32_t v = threadIdx.x; v < V; v += B) bits[v] = 0;
+  // inverse Kahn order of g0 (every entry writes the same values)
+  for (uint32_t i = threadIdx.x; i < V; i += B) {
+    a.tpos[gv.topo[i]] = i;
+    bits[i] = 0;
+  }
+  __threadfence();
   __syncthreads();
   diff_fail_goals<B>(a, src, bits);
+  __threadfence();
   __syncthreads();
-#define GOOD(v) (!is_rule(gv.word[v]) && !(bits[v] & DB_PRESENT))
-  for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
-      const uint32_t v = gv.topo[i];
-      bool fw = GOOD(v);
-      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1] && !fw; j++) fw = (bits[gv.rc[j]] & DB_F) != 0;
-      if (fw) bits[v] |= DB_F;
-    }
-    __syncthreads();
+#ifdef NEMO_STAMPS
+  unsigned long long *st = c.stamps ? c.stamps + 16 * (size_t)e : nullptr;
+#else
+  unsigned long long *st = nullptr;
+#endif
+  diff_window_sweep<B, 0>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
+  diff_window_sweep<B, 1>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
+  diff_window_sweep<B, 2>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
+  // D mask; goal leaves of D (no D child)
+  for (uint32_t v = threadIdx.x; v < V; v += B) {
+    const uint8_t b = bits[v];
+    mask[v] = (b & DB_D) ? 1 : 0;
+    if (!(b & DB_D) || is_rule(gv.word[v])) continue;
+    bool leaf = true;
+    for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++)
+      if (bits[gv.fc[j]] & DB_D) leaf = false;
+    if (leaf) bits[v] = b | DB_LEAF;
   }
-  for (uint32_t l = gv.nlev; l-- > 0;) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
-      const uint32_t v = gv.topo[i];
-      bool bw = GOOD(v);
-      for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1] && !bw; j++) bw = (bits[gv.fc[j]] & DB_B) != 0;
-      uint8_t b = bits[v];
-      if (bw) b |= DB_B;
-      if ((b & DB_F) && bw) b |= DB_D;
-      bits[v] = b;
-    }
-    __syncthreads();
-  }
-#undef GOOD
-  // longest path from a D root (Kahn-level DP restricted to D)
-  for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
-      const uint32_t v = gv.topo[i];
-      const uint8_t b = bits[v];
-      mask[v] = (b & DB_D) ? 1 : 0;
-      if (!(b & DB_D)) continue;
-      int32_t d = 0;
-      for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) {
-        const uint32_t p = gv.rc[j];
-        if (bits[p] & DB_D) d = max(d, depth[p] + 1);
-      }
-      depth[v] = d;
-      if (!is_rule(gv.word[v])) {
-        bool leaf = true;
-        for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++)
-          if (bits[gv.fc[j]] & DB_D) leaf = false;
-        if (leaf) bits[v] = b | DB_LEAF;
-      }
-    }
-    __syncthreads();
-  }
+  __syncthreads();
   for (uint32_t r = threadIdx.x; r < V; r += B) {
     if (!(bits[r] & DB_D) || !is_rule(gv.word[r])) continue;
     bool lp = false;
