@@ -70,6 +70,7 @@ struct nemo_ctx {
   uint32_t *d_dsrc = nullptr, *d_miss = nullptr, *d_nmiss = nullptr;
   uint8_t *d_dbits = nullptr, *d_dmask = nullptr;
   int32_t *d_ddepth = nullptr;
+  uint32_t *d_dtopo = nullptr;       // g0 in Kahn order (DiffArgs::tpos ...)
   uint64_t miss_cap = 0;
 
   // pulls: per-slot (offset, count) and the region cursor come back to pinned
@@ -287,6 +288,7 @@ static void release_corpus(nemo_ctx *c) {
   c->r0hmask = 0;
   c->d_dbits = c->d_dmask = nullptr;
   c->d_ddepth = nullptr;
+  c->d_dtopo = nullptr;
   c->n_entries = c->diff_cap = 0;
   c->miss_cap = 0;
   c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
@@ -953,7 +955,9 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
     if ((rc = dalloc(c, &c->d_dsrc, n_failed))) return rc;
     if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_ddepth, (n_failed + 1) * V0))) return rc;  // + g0's inverse Kahn order
+    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
+    dfree(c, c->d_dtopo);
+    if ((rc = dalloc(c, &c->d_dtopo, 4 * V0 + 2 * E0 + 2 + c->n_r0lab))) return rc;
     if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
     c->diff_cap = (uint32_t)n_failed;
   }
@@ -973,13 +977,23 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   a.r0hmask = c->r0hmask;
   a.bits = c->d_dbits;
   a.depth = c->d_ddepth;
-  a.tpos = (uint32_t *)(c->d_ddepth + (size_t)c->diff_cap * V0);
+  a.tpos = c->d_dtopo;
+  a.tinfo = a.tpos + V0;
+  a.trp = a.tinfo + V0;
+  a.tfp = a.trp + V0 + 1;
+  a.trc = a.tfp + V0 + 1;
+  a.tfc = a.trc + E0;
+  a.r0pos = a.tfc + E0;
   a.mask = c->d_dmask;
   a.missing = c->d_miss;
   a.n_missing = c->d_nmiss;
   double bytes = (double)n_failed * (3.0 * (4 * E0 + 9 * V0) + 6 * V0);
   rc = timed(c, "k_diff", bytes, (double)n_failed * 4 * E0,
-             [&] { nemo::launch_diff(c->dc, a, (uint32_t)n_failed, s); });
+             [&] {
+               // the Kahn-order relayout only when g0 may fall outside the LDS tier
+               const bool lds = c->dc.lds_bytes && V0 <= c->dc.lds_v && E0 <= c->dc.lds_e && V0 <= c->dc.lds_l;
+               nemo::launch_diff(c->dc, a, (uint32_t)n_failed, lds ? 0u : (uint32_t)V0, s);
+             });
   if (rc) return rc;
   // D masks and the missing-event count -> pinned host
   if ((rc = ensure_event(c, &c->ev_diff))) return rc;
@@ -1414,7 +1428,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   if (n == "topo") base = c->dc.topo;
   else if (n == "lvl") base = c->dc.lvl;
   else if (n == "nlv") base = c->dc.nlv;
-  else if (n == "diff_tpos") base = c->d_ddepth ? c->d_ddepth + (size_t)c->diff_cap * (c->node_off[2 * c->run0 + 2] - c->node_off[2 * c->run0 + 1]) : nullptr;
+  else if (n == "diff_tpos") base = c->d_dtopo;
   else if (n == "nlev") base = c->dc.nlev;
   else if (n == "fp") base = c->dc.fp;
   else if (n == "fc") base = c->dc.fc;

@@ -19,7 +19,9 @@ struct DiffArgs {
   uint32_t r0hmask;         // table size - 1 (power of two)
   uint8_t *bits;            // [entries * V0] scratch
   int32_t *depth;           // [entries * V0] scratch
-  uint32_t *tpos;           // [V0] inverse Kahn order of g0 (global tier)
+  // g0 in Kahn order for the global tier (k_dprep_*): node -> position,
+  // parent / child rows as positions, level << 1 | rule, label nodes as positions
+  uint32_t *tpos, *trp, *tfp, *trc, *tfc, *tinfo, *r0pos;
   uint8_t *mask;            // [entries * V0] D mask (output)
   uint32_t *missing;        // [2 * cap] (entry, rule)
   uint32_t *n_missing;      // counter
@@ -56,7 +58,7 @@ uint64_t glob_words(uint64_t V, uint64_t E);  // k_chains_glob scratch of one gr
 void launch_proto(const DevCorpus &c, hipStream_t s);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s);
-void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s);
+void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint32_t V0, hipStream_t s);
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
 void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
                         hipStream_t s);

@@ -51,7 +51,8 @@ __device__ __forceinline__ bool diff_lds_fits(const DevCorpus &c, const GraphVie
 // a few rounds of independent loads rather than a binary search per node.
 #define DL_BATCH 8
 template <int B = NEMO_BLOCK>
-__device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphView &src, uint8_t *bits) {
+__device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphView &src, uint8_t *bits,
+                                                const uint32_t *idx) {
   for (uint32_t base = 0; base < src.V; base += DL_BATCH * B) {
     uint32_t lab[DL_BATCH], h[DL_BATCH], pos[DL_BATCH], live = 0;
 #pragma unroll
@@ -86,26 +87,25 @@ __device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphVi
 #pragma unroll
     for (int q = 0; q < DL_BATCH; q++)
       if (pos[q] != NEMO_NONE)
-        for (uint32_t i = pos[q]; i < a.n_r0lab && a.r0lab[i] == lab[q]; i++) bits[a.r0idx[i]] = DB_PRESENT;
+        for (uint32_t i = pos[q]; i < a.n_r0lab && a.r0lab[i] == lab[q]; i++) bits[idx[i]] = DB_PRESENT;
   }
 }
 
-// ---- windowed level sweeps (global tier: run 0's post graph outside LDS) ------
+// ---- global tier: run 0's post graph relaid in Kahn order, windowed sweeps ----
 // A level-synchronous sweep over a deep graph (C5: ~4900 Kahn levels of ~200
-// nodes) is bound by dependent HBM round trips per level (topo -> row ->
-// neighbour -> neighbour's bit).  Here the Kahn order is cut into windows of
-// DW_N consecutive positions.  One staging pass per window issues all of
-// those loads at once: neighbours outside the window are final and fold
-// into an accumulator, neighbours inside it become LDS links (topo position
-// - window start, via the inverse order tpos).  The window's levels are then
-// swept in LDS with one barrier each, so a window of ~20 levels costs about
-// one round of HBM latency instead of ~20 rounds of four.
+// nodes) done node by node costs several dependent gathers per level, and a
+// diff entry is one workgroup, so those gathers all queue on one CU.  All
+// entries share g0, so g0 is first relaid once per diffprov call by
+// whole-GPU kernels (k_dprep_*): nodes in Kahn order, rows of parents and
+// children as Kahn positions, the level and rule bit packed per position.
+// Every entry then works in Kahn-position space: its bits and depths are
+// contiguous, a window of DW_N consecutive positions (~20 levels) is staged
+// with coalesced loads (links inside the window become LDS links, links
+// before/after it read final values), and the window's levels are swept in
+// LDS with one barrier each.
 #define DW_N 4096u    // Kahn positions per window
 #define DW_E 8192u    // in-window links past each node's first two, staged in LDS
 #define DW_SPILL 0xFFFFu
-#ifndef DW_NREG
-#define DW_NREG 2u    // links per node held in registers
-#endif
 struct DiffWin {
   uint32_t off[DW_N];     // first extra link of node k
   int32_t dep[DW_N];      // depth (mode 2)
@@ -116,117 +116,132 @@ struct DiffWin {
   uint32_t l0, l1;        // first and last Kahn level in the window
 };
 
+// g0 in Kahn order, pass 1 (one thread per position): inverse order, row
+// lengths, level << 1 | rule
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dprep_a(DevCorpus c, DiffArgs a) {
+  const GraphView gv = c.view(a.g0);
+  if (diff_lds_fits(c, gv)) return;
+  const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i == 0) {
+    a.trp[gv.V] = 0;
+    a.tfp[gv.V] = 0;
+  }
+  if (i >= gv.V) return;
+  const uint32_t v = gv.topo[i];
+  a.tpos[v] = i;
+  a.trp[i] = gv.rp[v + 1] - gv.rp[v];
+  a.tfp[i] = gv.fp[v + 1] - gv.fp[v];
+  a.tinfo[i] = (c.nlv[gv.n0 + v] << 1) | (is_rule(gv.word[v]) ? 1u : 0u);
+}
+// pass 2 (one workgroup): row starts
+__global__ __launch_bounds__(1024) void k_dprep_scan(DevCorpus c, DiffArgs a) {
+  __shared__ uint32_t s_red[16];
+  const GraphView gv = c.view(a.g0);
+  if (diff_lds_fits(c, gv)) return;
+  block_scan_inplace<1024, 16>(a.trp, gv.V + 1, s_red);
+  block_scan_inplace<1024, 16>(a.tfp, gv.V + 1, s_red);
+}
+// pass 3 (one thread per position): rows as Kahn positions; label nodes as positions
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dprep_b(DevCorpus c, DiffArgs a) {
+  const GraphView gv = c.view(a.g0);
+  if (diff_lds_fits(c, gv)) return;
+  const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i < a.n_r0lab) a.r0pos[i] = a.tpos[a.r0idx[i]];
+  if (i >= gv.V) return;
+  const uint32_t v = gv.topo[i];
+  uint32_t o = a.trp[i];
+  for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) a.trc[o++] = a.tpos[gv.rc[j]];
+  o = a.tfp[i];
+  for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) a.tfc[o++] = a.tpos[gv.fc[j]];
+}
+
 // mode 0: F = Good | any F parent        (Fwd*(Good), forward over parents)
 // mode 1: B = Good | any B child; D = F&B (Bwd*(Good), backward over children)
 // mode 2: depth = max(0, depth(p) + 1 over D parents p), D nodes only
-// Thread t owns window positions t, t + B, ...: the node, its level, its
-// accumulator and its first two in-window links stay in registers, so a
-// level of the sweep is one LDS probe per link and one barrier.
+// bits/depth are indexed by Kahn position.  Thread t owns window positions
+// t, t + B, ...: its nodes' level and accumulator stay in registers.
 template <int B, int MODE>
-__device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32_t *nlv, const uint32_t *tpos, uint8_t *bits,
-                                  int32_t *depth, DiffWin &W, uint32_t *s_red, unsigned long long *st) {
+__device__ __noinline__ void diff_window_sweep(uint32_t V, const DiffArgs &a, uint8_t *bits, int32_t *depth,
+                                               DiffWin &W, uint32_t *s_red, unsigned long long *st) {
 #ifdef NEMO_STAMPS
   unsigned long long acc_s = 0, acc_l = 0, acc_w = 0, t_a, t_b;
 #define DW_T(t) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory")
-#else
-#define DW_T(t) \
-  do {          \
-  } while (0)
 #endif
   constexpr int PT = (int)(DW_N / B);
   constexpr bool FWD = MODE != 1;
   constexpr uint32_t NIL = 0xFFFFFFFFu;
-  const uint32_t V = gv.V, tid = threadIdx.x;
-  const uint32_t *ptr = FWD ? gv.rp : gv.fp, *col = FWD ? gv.rc : gv.fc;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t *ptr = FWD ? a.trp : a.tfp, *col = FWD ? a.trc : a.tfc;
   const uint32_t nwin = (V + DW_N - 1) / DW_N;
   for (uint32_t wi = 0; wi < nwin; wi++) {
     // forward: windows in Kahn order; backward: from the end
-    const uint32_t a = FWD ? wi * DW_N : (V > (wi + 1) * DW_N ? V - (wi + 1) * DW_N : 0u);
-    const uint32_t b = FWD ? min(V, a + DW_N) : V - wi * DW_N;
-    const uint32_t n = b - a;
+    const uint32_t w0 = FWD ? wi * DW_N : (V > (wi + 1) * DW_N ? V - (wi + 1) * DW_N : 0u);
+    const uint32_t w1 = FWD ? min(V, w0 + DW_N) : V - wi * DW_N;
+    const uint32_t n = w1 - w0;
 #ifdef NEMO_STAMPS
     DW_T(t_a);
 #endif
-    uint32_t vv[PT], r0[PT], r1[PT], lev[PT], p0[PT], p1[PT], u0[PT], u1[PT], cx[PT];
+    uint32_t r0[PT], r1[PT], lev[PT], p0[PT], p1[PT], cx[PT];
     int32_t x[PT];
     uint8_t ob[PT];
 #pragma unroll
     for (int q = 0; q < PT; q++) {
-      const uint32_t k = tid + q * B;
-      vv[q] = k < n ? gv.topo[a + k] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < PT; q++) {
-      const uint32_t k = tid + q * B;
+      const uint32_t k = tid + q * B, i = w0 + k;
       const bool in = k < n;
-      const uint32_t v = vv[q];
-      r0[q] = in ? ptr[v] : 0u;
-      r1[q] = in ? ptr[v + 1] : 0u;
-      lev[q] = in ? nlv[v] : NIL;
-      ob[q] = in ? bits[v] : 0u;
-      const bool good = in && !is_rule(gv.word[v]) && !(ob[q] & DB_PRESENT);
+      const uint32_t info = in ? a.tinfo[i] : 0u;
+      r0[q] = in ? ptr[i] : 0u;
+      r1[q] = in ? ptr[i + 1] : 0u;
+      lev[q] = in ? info >> 1 : NIL;
+      ob[q] = in ? bits[i] : 0u;
+      const bool good = in && !(info & 1u) && !(ob[q] & DB_PRESENT);
       x[q] = MODE == 2 ? 0 : (good ? 1 : 0);
       if (MODE == 2 && !(ob[q] & DB_D)) r1[q] = r0[q];  // only D nodes get a depth
       if (MODE != 2 && good) r1[q] = r0[q];             // Good: set regardless of neighbours
       if (in && k == 0) W.l0 = lev[q];
       if (in && k == n - 1) W.l1 = lev[q];
     }
-    // first two neighbours of every node in one batch of loads
 #pragma unroll
     for (int q = 0; q < PT; q++) {
-      p0[q] = (DW_NREG >= 1 && r1[q] > r0[q]) ? col[r0[q]] : NIL;
-      p1[q] = (DW_NREG >= 2 && r1[q] > r0[q] + 1) ? col[r0[q] + 1] : NIL;
+      p0[q] = r1[q] > r0[q] ? col[r0[q]] : NIL;
+      p1[q] = r1[q] > r0[q] + 1 ? col[r0[q] + 1] : NIL;
     }
+    // links leaving the window read final values; links inside it go to LDS
 #pragma unroll
     for (int q = 0; q < PT; q++) {
-      uint32_t t0 = 0, t1 = 0;
-      uint8_t b0 = 0, b1 = 0;
-      int32_t d0 = 0, d1 = 0;
-      if (p0[q] != NIL) {
-        t0 = tpos[p0[q]];
-        b0 = bits[p0[q]];
-        if (MODE == 2) d0 = depth[p0[q]];
-      }
-      if (p1[q] != NIL) {
-        t1 = tpos[p1[q]];
-        b1 = bits[p1[q]];
-        if (MODE == 2) d1 = depth[p1[q]];
-      }
-      u0[q] = u1[q] = NIL;
-      if (p0[q] != NIL) {
-        const bool inw = FWD ? t0 >= a : t0 < b;
+      uint32_t u0 = NIL, u1 = NIL;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t p = h ? p1[q] : p0[q];
+        if (p == NIL) continue;
+        const bool inw = FWD ? p >= w0 : p < w1;
+        uint32_t u = NIL;
         if (MODE == 2) {
-          if (b0 & DB_D) {
-            if (inw) u0[q] = t0 - a;
-            else x[q] = max(x[q], d0 + 1);
+          const uint8_t bp = bits[p];
+          if (bp & DB_D) {
+            if (inw) u = p - w0;
+            else x[q] = max(x[q], depth[p] + 1);
           }
         } else if (inw) {
-          u0[q] = t0 - a;
-        } else if (b0 & (MODE == 0 ? DB_F : DB_B)) {
+          u = p - w0;
+        } else if (bits[p] & (MODE == 0 ? DB_F : DB_B)) {
           x[q] = 1;
         }
+        if (h) u1 = u;
+        else u0 = u;
       }
-      if (p1[q] != NIL) {
-        const bool inw = FWD ? t1 >= a : t1 < b;
-        if (MODE == 2) {
-          if (b1 & DB_D) {
-            if (inw) u1[q] = t1 - a;
-            else x[q] = max(x[q], d1 + 1);
-          }
-        } else if (inw) {
-          u1[q] = t1 - a;
-        } else if (b1 & (MODE == 0 ? DB_F : DB_B)) {
-          x[q] = 1;
-        }
+      const uint32_t k = tid + q * B;
+      if (k < n) {
+        W.u0[k] = u0 == NIL ? (uint16_t)DW_SPILL : (uint16_t)u0;
+        W.u1[k] = u1 == NIL ? (uint16_t)DW_SPILL : (uint16_t)u1;
       }
     }
-    // the rest of long rows (rare): out-of-window links fold, in-window ones are counted
+    // the rest of long rows (rare)
 #pragma unroll
     for (int q = 0; q < PT; q++) {
       cx[q] = 0;
-      for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
-        const uint32_t p = col[j], tp = tpos[p];
-        const bool inw = FWD ? tp >= a : tp < b;
+      for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
+        const uint32_t p = col[j];
+        const bool inw = FWD ? p >= w0 : p < w1;
         if (MODE == 2) {
           if (!(bits[p] & DB_D)) continue;
           if (inw) cx[q]++;
@@ -253,18 +268,16 @@ __device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32
       } else {
         W.val[k] = (uint8_t)x[q];
       }
-      W.u0[k] = u0[q] == NIL ? (uint16_t)DW_SPILL : (uint16_t)u0[q];
-      W.u1[k] = u1[q] == NIL ? (uint16_t)DW_SPILL : (uint16_t)u1[q];
       if (!cx[q]) continue;
       const bool spill = base + cx[q] > DW_E;
       W.off[k] = base;
       W.ln[k] = spill ? (uint16_t)DW_SPILL : (uint16_t)cx[q];
       if (!spill) {
         uint32_t o = base;
-        for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
-          const uint32_t p = col[j], tp = tpos[p];
-          const bool inw = FWD ? tp >= a : tp < b;
-          if (inw && (MODE != 2 || (bits[p] & DB_D))) W.adj[o++] = (uint16_t)(tp - a);
+        for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
+          const uint32_t p = col[j];
+          const bool inw = FWD ? p >= w0 : p < w1;
+          if (inw && (MODE != 2 || (bits[p] & DB_D))) W.adj[o++] = (uint16_t)(p - w0);
         }
       }
       base += cx[q];
@@ -282,45 +295,42 @@ __device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32
       for (int q = 0; q < PT; q++) {
         if (lev[q] != li) continue;
         const uint32_t k = tid + q * B;
+        const uint32_t v0 = W.u0[k], v1 = W.u1[k];
         if (MODE != 2) {
           if (x[q]) continue;
-          const uint32_t w0 = W.u0[k], w1 = W.u1[k];
           // plain ORs, no short-circuit: the ROCm 7.2 compiler mis-evaluated
-          // `(w0 && val[w0]) || (w1 && val[w1])` in the 1024-thread instance
+          // `(u0 && val[u0]) || (u1 && val[u1])` in the 1024-thread instance
           uint32_t hv = 0;
-          if (w0 != DW_SPILL) hv |= W.val[w0];
-          if (w1 != DW_SPILL) hv |= W.val[w1];
-          bool hit = hv != 0;
-          if (!hit && cx[q]) {
+          if (v0 != DW_SPILL) hv |= W.val[v0];
+          if (v1 != DW_SPILL) hv |= W.val[v1];
+          if (!hv && cx[q]) {
             if (W.ln[k] != DW_SPILL) {
               const uint32_t o = W.off[k], m = W.ln[k];
               for (uint32_t t = 0; t < m; t++) hv |= W.val[W.adj[o + t]];
-              hit = hv != 0;
             } else {
-              for (uint32_t j = r0[q] + DW_NREG; j < r1[q] && !hit; j++) {
-                const uint32_t tp = tpos[col[j]];
-                if (FWD ? tp >= a : tp < b) hit = W.val[tp - a] != 0;
+              for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
+                const uint32_t p = col[j];
+                if (FWD ? p >= w0 : p < w1) hv |= W.val[p - w0];
               }
             }
           }
-          if (hit) {
+          if (hv) {
             x[q] = 1;
             W.val[k] = 1;
           }
         } else {
           if (!(ob[q] & DB_D)) continue;
           int32_t d = x[q];
-          const uint32_t w0 = W.u0[k], w1 = W.u1[k];
-          if (w0 != DW_SPILL) d = max(d, W.dep[w0] + 1);
-          if (w1 != DW_SPILL) d = max(d, W.dep[w1] + 1);
+          if (v0 != DW_SPILL) d = max(d, W.dep[v0] + 1);
+          if (v1 != DW_SPILL) d = max(d, W.dep[v1] + 1);
           if (cx[q]) {
             if (W.ln[k] != DW_SPILL) {
               const uint32_t o = W.off[k], m = W.ln[k];
               for (uint32_t t = 0; t < m; t++) d = max(d, W.dep[W.adj[o + t]] + 1);
             } else {
-              for (uint32_t j = r0[q] + DW_NREG; j < r1[q]; j++) {
-                const uint32_t p = col[j], tp = tpos[p];
-                if (tp >= a && (bits[p] & DB_D)) d = max(d, W.dep[tp - a] + 1);
+              for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
+                const uint32_t p = col[j];
+                if (p >= w0 && (bits[p] & DB_D)) d = max(d, W.dep[p - w0] + 1);
               }
             }
           }
@@ -337,14 +347,14 @@ __device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32
 #endif
 #pragma unroll
     for (int q = 0; q < PT; q++) {
-      const uint32_t k = tid + q * B;
+      const uint32_t k = tid + q * B, i = w0 + k;
       if (k >= n) continue;
       if (MODE == 0) {
-        if (x[q]) bits[vv[q]] = ob[q] | DB_F;
+        if (x[q]) bits[i] = ob[q] | DB_F;
       } else if (MODE == 1) {
-        if (x[q]) bits[vv[q]] = ob[q] | DB_B | ((ob[q] & DB_F) ? DB_D : 0u);
+        if (x[q]) bits[i] = ob[q] | DB_B | ((ob[q] & DB_F) ? DB_D : 0u);
       } else if (ob[q] & DB_D) {
-        depth[vv[q]] = x[q];
+        depth[i] = x[q];
       }
     }
     // the window's HBM writes must be performed before the next window (or
@@ -362,15 +372,14 @@ __device__ __noinline__ void diff_window_sweep(const GraphView &gv, const uint32
     st[3 * MODE + 1] = acc_l;
     st[3 * MODE + 2] = acc_w;
   }
-#endif
 #undef DW_T
+#endif
 }
 
-// One workgroup per diff entry, all over run 0's post graph g0:
+// One workgroup per diff entry, all over run 0's post graph g0 (in Kahn order):
 //   Good = goals of g0 whose label is absent from the source run's post goals
 //   D    = Fwd*(Good) ∩ Bwd*(Good)                       (:22-32, APOC export)
 //   missing = D rules with a D-leaf child at maximal depth (:82-98)
-// Fwd*, Bwd* and the depths are windowed level sweeps (diff_window_sweep).
 template <int B>
 __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   __shared__ DiffWin W;
@@ -381,19 +390,14 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   if (diff_lds_fits(c, gv)) return;  // k_diff_lds's graph
   const GraphView src = c.view(a.src[e]);
   const uint32_t V = gv.V;
-  uint8_t *bits = a.bits + (size_t)e * V;
-  int32_t *depth = a.depth + (size_t)e * V;
-  uint8_t *mask = a.mask + (size_t)e * V;
-  const uint32_t *nlv = c.nlv + gv.n0;
+  uint8_t *bits = a.bits + (size_t)e * V;     // by Kahn position
+  int32_t *depth = a.depth + (size_t)e * V;   // by Kahn position
+  uint8_t *mask = a.mask + (size_t)e * V;     // by node
   if (threadIdx.x == 0) s_max = -1;
-  // inverse Kahn order of g0 (every entry writes the same values)
-  for (uint32_t i = threadIdx.x; i < V; i += B) {
-    a.tpos[gv.topo[i]] = i;
-    bits[i] = 0;
-  }
+  for (uint32_t i = threadIdx.x; i < V; i += B) bits[i] = 0;
   __threadfence();
   __syncthreads();
-  diff_fail_goals<B>(a, src, bits);
+  diff_fail_goals<B>(a, src, bits, a.r0pos);
   __threadfence();
   __syncthreads();
 #ifdef NEMO_STAMPS
@@ -401,39 +405,39 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
 #else
   unsigned long long *st = nullptr;
 #endif
-  diff_window_sweep<B, 0>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
-  diff_window_sweep<B, 1>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
-  diff_window_sweep<B, 2>(gv, nlv, a.tpos, bits, depth, W, s_red, st);
-  // D mask; goal leaves of D (no D child)
-  for (uint32_t v = threadIdx.x; v < V; v += B) {
-    const uint8_t b = bits[v];
-    mask[v] = (b & DB_D) ? 1 : 0;
-    if (!(b & DB_D) || is_rule(gv.word[v])) continue;
+  diff_window_sweep<B, 0>(V, a, bits, depth, W, s_red, st);
+  diff_window_sweep<B, 1>(V, a, bits, depth, W, s_red, st);
+  diff_window_sweep<B, 2>(V, a, bits, depth, W, s_red, st);
+  // D mask (by node); goal leaves of D (no D child)
+  for (uint32_t i = threadIdx.x; i < V; i += B) {
+    const uint8_t b = bits[i];
+    mask[gv.topo[i]] = (b & DB_D) ? 1 : 0;
+    if (!(b & DB_D) || (a.tinfo[i] & 1u)) continue;
     bool leaf = true;
-    for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++)
-      if (bits[gv.fc[j]] & DB_D) leaf = false;
-    if (leaf) bits[v] = b | DB_LEAF;
+    for (uint32_t j = a.tfp[i]; j < a.tfp[i + 1]; j++)
+      if (bits[a.tfc[j]] & DB_D) leaf = false;
+    if (leaf) bits[i] = b | DB_LEAF;
   }
+  __threadfence();
   __syncthreads();
-  for (uint32_t r = threadIdx.x; r < V; r += B) {
-    if (!(bits[r] & DB_D) || !is_rule(gv.word[r])) continue;
+  for (uint32_t i = threadIdx.x; i < V; i += B) {
+    if (!(bits[i] & DB_D) || !(a.tinfo[i] & 1u)) continue;
     bool lp = false;
-    for (uint32_t j = gv.fp[r]; j < gv.fp[r + 1]; j++) {
-      const uint32_t x = gv.fc[j];
-      if ((bits[x] & (DB_D | DB_LEAF)) == (DB_D | DB_LEAF)) lp = true;
-    }
+    for (uint32_t j = a.tfp[i]; j < a.tfp[i + 1]; j++)
+      if ((bits[a.tfc[j]] & (DB_D | DB_LEAF)) == (DB_D | DB_LEAF)) lp = true;
     if (lp) {
-      bits[r] |= DB_LP;
-      atomicMax(&s_max, depth[r] + 1);
+      bits[i] |= DB_LP;
+      atomicMax(&s_max, depth[i] + 1);
     }
   }
+  __threadfence();
   __syncthreads();
   const int32_t mx = s_max;
-  for (uint32_t r = threadIdx.x; r < V; r += B) {
-    if ((bits[r] & DB_LP) && depth[r] + 1 == mx) {
+  for (uint32_t i = threadIdx.x; i < V; i += B) {
+    if ((bits[i] & DB_LP) && depth[i] + 1 == mx) {
       const uint32_t k = atomicAdd(a.n_missing, 1u);
       a.missing[2 * k] = e;
-      a.missing[2 * k + 1] = r;
+      a.missing[2 * k + 1] = gv.topo[i];
     }
   }
 }
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff_lds(DevCorpus c, DiffArgs a
     }
   }
   uint8_t *bits = L.bits;
-  diff_fail_goals(a, src, bits);
+  diff_fail_goals(a, src, bits, a.r0idx);
   __syncthreads();
 #define LRULE(v) ((L.rule[(v) >> 5] >> ((v) & 31)) & 1u)
 #define GOOD(v) (!LRULE(v) && !(bits[v] & DB_PRESENT))
@@ -973,7 +977,13 @@ void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipSt
   if (out) hipLaunchKernelGGL(k_chain_gather, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, off, out);
 }
 
-void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, hipStream_t s) {
+void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint32_t V0, hipStream_t s) {
+  if (V0) {  // g0 in Kahn order for the global tier (each kernel returns at once for an LDS-tier g0)
+    const uint32_t nb = (std::max(V0, a.n_r0lab) + NEMO_BLOCK - 1) / NEMO_BLOCK;
+    hipLaunchKernelGGL(k_dprep_a, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, a);
+    hipLaunchKernelGGL(k_dprep_scan, dim3(1), dim3(1024), 0, s, c, a);
+    hipLaunchKernelGGL(k_dprep_b, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, a);
+  }
   if (c.lds_bytes) {
     const uint32_t bytes = diff_lds_bytes(c.lds_v, c.lds_e, c.lds_l);
     hipFuncSetAttribute((const void *)k_diff_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
