@@ -775,7 +775,7 @@ int nemo_simplify(nemo_ctx *c) {
   if (rc) return rc;
   if (c->mark_pending) {
     const double V = c->tierV, E = c->tierE, Vg = (double)c->V - V, Eg = (double)c->E - E;
-    rc = timed(c, "k_marksimp", 8 * E + 13 * V, 4 * E, [&] { nemo::launch_marksimp(c->dc, c->stream); });
+    rc = timed(c, "k_marksimp", 8 * E + 5 * V, 5 * E, [&] { nemo::launch_marksimp(c->dc, c->stream); });
     if (rc) return rc;
     rc = timed(c, "k_simplify", 8 * Eg + 14 * Vg, 2 * Eg, [&] { nemo::launch_simplify(c->dc, true, c->stream); });
     if (rc) return rc;

@@ -71,7 +71,7 @@ __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint3
 __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lds[NEMO_WAVES];
-  __shared__ uint32_t s_bad, s_created, s_tail;
+  __shared__ uint32_t s_bad, s_created, s_tail, s_cnt[3];
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
@@ -106,6 +106,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
     s_bad = 0;
     s_created = 0;
     s_tail = 0;
+    s_cnt[0] = 0;
     c.redo[g] = 0;
   }
   __syncthreads();
@@ -212,9 +213,14 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
   __syncthreads();
   STAMP(14);
   uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g;
+  // one barrier per level: level k appends behind the frontier through its
+  // own counter s_cnt[k % 3]; the counter of level k + 1 is cleared during
+  // level k (its last readers passed the barrier of level k - 1)
   uint32_t lo = 0, hi = s_tail, nl = 0;
   if (tid == 0) lvl[0] = 0;
   while (lo < hi) {
+    uint32_t *cur = &s_cnt[nl % 3];
+    if (tid == 0) s_cnt[(nl + 1) % 3] = 0;
     for (uint32_t base = lo; base < hi; base += NEMO_BLOCK) {
       const uint32_t i = base + tid;
       uint32_t j = 0, je = 0;
@@ -231,16 +237,15 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
           const uint32_t sh = 8 * (ch & 3);
           p = ((atomicSub(&cnt32[ch >> 2], 1u << sh) >> sh) & 0xFFu) == 1u;
         }
-        lds_append16(p, ch, q16, &s_tail);
+        lds_append16(p, ch, q16 + hi, cur);
         if (p) nlv[ch] = nl + 1;
       }
     }
     __syncthreads();
     nl++;
     lo = hi;
-    hi = s_tail;
+    hi += *(volatile uint32_t *)cur;
     if (tid == 0) lvl[nl] = lo;
-    __syncthreads();
   }
   for (uint32_t i = tid; i < hi; i += NEMO_BLOCK) topo[i] = q16[i];
   STAMP(15);

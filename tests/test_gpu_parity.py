@@ -331,3 +331,39 @@ def test_global_tier_block(eng, block):
     finally:
         for k in ("graph_lds_max", "build_lds_max", "global_block"):
             eng.set_option(k, -1)
+
+
+@pytest.mark.parametrize("lds_max", [-1, 0])
+def test_dense_graph_edge_reload(eng, lds_max):
+    # a dense LDS-tier graph (2000 nodes, > 8192 edges): k_marksimp re-reads
+    # its edge list from HBM per pass instead of holding it in registers
+    import random
+    rng = random.Random(11)
+    tabs = ["pre", "post", "log", "ack", "node", "clock"]
+
+    def dense(cond):
+        goals, rules, edges = [], [], []
+        for t in range(10):
+            for i in range(100):
+                tb = rng.choice(tabs)
+                goals.append({"id": f"goal{t}_{i}", "label": f"{tb}(a, {i}, {t})", "table": tb, "time": str(t)})
+                rt = cond if rng.random() < 0.3 else rng.choice(tabs)
+                rules.append({"id": f"r{t}_{i}", "label": rt, "table": rt,
+                              "type": "next" if rng.random() < 0.5 else rng.choice(["async", "single"])})
+        for t in range(10):
+            for i in range(100):
+                for j in rng.sample(range(100), 5):
+                    edges.append({"from": f"goal{t}_{i}", "to": f"r{t}_{j}"})
+                if t < 9:
+                    for j in rng.sample(range(100), 4):
+                        edges.append({"from": f"r{t}_{i}", "to": f"goal{t + 1}_{j}"})
+        return {"goals": goals, "rules": rules, "edges": edges}
+
+    graphs = [(0, "success", dense("pre"), dense("post")), (1, "failure", dense("pre"), dense("post"))]
+    corpus = corpus_from_graphs(graphs)
+    assert max(corpus.edge_off[g + 1] - corpus.edge_off[g] for g in range(corpus.n_graphs)) > 8192
+    eng.set_option("graph_lds_max", lds_max)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+    finally:
+        eng.set_option("graph_lds_max", -1)
