@@ -56,6 +56,7 @@ struct nemo_ctx {
   uint64_t glob_min_v = 65536;       // graphs with V >= this take k_chains_glob (set before load)
   uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
+  double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
   DevCorpus dc{};
@@ -500,7 +501,7 @@ static int check_graph_errors(nemo_ctx *c) {
 
 static int device_load(nemo_ctx *c) {
   int rc;
-  HIPCHK(c, hipMemsetAsync(c->dc.err, 0, c->G * sizeof(uint32_t), c->stream));
+  nemo::launch_zero(c->dc.err, c->G * sizeof(uint32_t), c->stream);
   // graphs within k_build's LDS caps vs the global tier
   double Vb = 0, Eb = 0;
   for (uint32_t g = 0; g < c->G && c->dc.bld_bytes; g++) {
@@ -543,6 +544,11 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   c->edge_off.assign(in->edge_off, in->edge_off + c->G + 1);
   c->V = c->node_off[c->G];
   c->E = c->edge_off[c->G];
+  c->postV = c->postE = 0;
+  for (uint32_t g = 1; g < c->G; g += 2) {
+    c->postV += (double)(c->node_off[g + 1] - c->node_off[g]);
+    c->postE += (double)(c->edge_off[g + 1] - c->edge_off[g]);
+  }
   c->it2run.clear();
   c->run0 = -1;
   for (uint32_t r = 0; r < c->n_runs; r++) {
@@ -815,12 +821,16 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
     if (i == 0) first = f->second;
   }
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->d_is_success, succ, c->n_runs, hipMemcpyHostToDevice, s));
-  HIPCHK(c, hipEventRecord(c->ev_up_succ, s));
-  HIPCHK(c, hipMemsetAsync(d_red, 0, nemo_reduce_len(c) * 4, s));
-  const double V = (double)c->V, E = (double)c->E;
-  int rc = timed(c, "k_proto", 8 * E + 12 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
+  // k_proto first: it is what the analysis stream has ready when a bulk
+  // staging copy starts beside it (a kernel queued behind the copy's start
+  // waits for the copy's blit to drain); the reduction's inputs follow it
+  // post graphs only: both CSR directions 8(V+1) + 8E, Kahn order + level offsets 4V, node word 4V, flags 1V
+  const double V = c->postV, E = c->postE;
+  int rc = timed(c, "k_proto", 8 * E + 17 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
   if (rc) return rc;
+  nemo::launch_to_host(c->d_is_success, succ, c->n_runs, s);  // pinned -> device by a copy kernel (no blit queue)
+  HIPCHK(c, hipEventRecord(c->ev_up_succ, s));
+  nemo::launch_zero(d_red, nemo_reduce_len(c) * 4, s);
   rc = timed(c, "k_reduce", (double)c->n_runs * (c->W * 8 + 8), 0,
              [&] { nemo::launch_reduce(c->dc, c->d_is_success, c->d_owned, first, d_red, s); });
   if (rc) return rc;
@@ -963,9 +973,9 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   }
   if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->d_dsrc, src, n_failed * 4, hipMemcpyHostToDevice, s));
+  nemo::launch_to_host(c->d_dsrc, src, n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
-  HIPCHK(c, hipMemsetAsync(c->d_nmiss, 0, 4, s));
+  nemo::launch_zero(c->d_nmiss, 4, s);
   nemo::DiffArgs a;
   a.g0 = g0;
   a.src = c->d_dsrc;
@@ -1094,7 +1104,7 @@ int nemo_triggers(nemo_ctx *c) {
   a.post = c->d_tpost;
   a.async_rules = c->d_tasync;
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemsetAsync(c->d_tcounts, 0, 12, s));
+  nemo::launch_zero(c->d_tcounts, 12, s);
   rc = timed(c, "k_triggers", 0, 0, [&] { nemo::launch_triggers(c->dc, a, 1, s); });
   if (rc) return rc;
   if ((rc = hgrow(c, &c->h_tpre, &c->h_tpre_cap, 3 * c->tcap[0] + 3))) return rc;
@@ -1296,7 +1306,7 @@ static int pull_launch(nemo_ctx *c) {
     V = (double)slots * (double)a.mask_stride;
     E = (double)slots * (double)(c->edge_off[a.g0 + 1] - c->edge_off[a.g0]);
   }
-  HIPCHK(c, hipMemsetAsync(c->d_pcur, 0, sizeof(unsigned long long), s));
+  nemo::launch_zero(c->d_pcur, sizeof(unsigned long long), s);
   // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
   int rc = timed(c, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
   if (rc) return rc;

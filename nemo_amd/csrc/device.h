@@ -45,7 +45,7 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t *q
   const int leader = __ffsll((long long)m) - 1;
   uint32_t base = 0;
   if ((int)lane_id() == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
-  base = __shfl(base, leader);
+  base = __builtin_amdgcn_readlane(base, leader);  // leader is wave-uniform: no LDS round trip
   if (pred) q[base + mbcnt(m)] = val;
 }
 

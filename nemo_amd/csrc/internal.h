@@ -66,5 +66,6 @@ void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStrea
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
 void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 1024);
+void launch_zero(void *dst, uint64_t bytes, hipStream_t s);
 
 }  // namespace nemo

@@ -831,6 +831,22 @@ void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, u
                      bytes);
 }
 
+// Device memset as a kernel: rocclr's fill blits queue behind a bulk copy
+// blit running on the copy stream, so the per-step clears on the analysis
+// stream are plain vector stores instead.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_zero(uint32_t *__restrict__ dst, uint64_t words) {
+  const uint64_t stride = (uint64_t)gridDim.x * NEMO_BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * NEMO_BLOCK + threadIdx.x; i < words; i += stride) dst[i] = 0u;
+}
+
+void launch_zero(void *dst, uint64_t bytes, hipStream_t s) {
+  const uint64_t words = bytes / 4;  // callers clear whole u32 / u64 arrays
+  if (!words) return;
+  uint64_t blocks = (words + NEMO_BLOCK - 1) / NEMO_BLOCK;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_zero, dim3((uint32_t)blocks), dim3(NEMO_BLOCK), 0, s, (uint32_t *)dst, words);
+}
+
 // ---- run-0 trigger patterns ------------------------------------------------------
 // phase 0 counts, phase 1 writes (capacities sized from the counts).
 #define TRIG_SPLIT 16
