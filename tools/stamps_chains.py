@@ -18,6 +18,9 @@ d = d[ok]
 print("graphs", ok.sum(), "total cycles per graph: median", np.median(d.sum(1)), "p90", np.percentile(d.sum(1), 90))
 for i, nm in enumerate(names):
     print(f"{nm:14s} median {np.median(d[:, i]):10.0f}  mean {d[:, i].mean():10.0f}  share {d[:, i].sum() / d.sum():.3f}")
+sub = st[ok]
+for a, b, nm in [(0, 10, "  zero maps"), (10, 11, "  loads+hist"), (11, 1, "  scan+scatter")]:
+    print(f"{nm:14s} median {np.median(sub[:, b] - sub[:, a]):10.0f}")
 nch = []
 ch = eng.chains()
 import collections
