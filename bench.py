@@ -65,7 +65,12 @@ def parse():
 
 CONFIGS = {"c3": {"runs": 10000, "nodes": 5000, "eot": 10, "cpu_runs": None},
            "c4": {"runs_total": 100000, "nodes": 5000, "eot": 10, "cpu_runs": 5000},
-           "c5": {"runs": 128, "nodes": 1_000_000, "eot": 2000, "cpu_runs": 8}}
+           # C5 "1M-node / 4M-edge graphs": rule bodies of 1-3 atoms plus 0..12 extra ones over a key space
+           # small enough to share body goals (~0.95M nodes, ~4.0M edges per graph at EOT 2000)
+           # the CPU oracle is superlinear in graph size on this shape (>15 min per 1M-node run), so its
+           # bounded sample is 4 runs of the same shape at 50k-node graphs (EOT 100, same density)
+           "c5": {"runs": 128, "nodes": 1_000_000, "eot": 2000, "cpu_runs": 4,
+                  "gen": {"body_extra": 6, "nval": 3, "nloc": 4}, "cpu_sample": {"nodes": 50_000, "eot": 100}}}
 
 
 def main():
@@ -99,8 +104,9 @@ def main():
     if strong:
         R = max(0, min(R, cfg["runs_total"] - rank * R))
     t0 = time.time()
+    gen = cfg.get("gen", {})
     corpus, info = synth.generate(R, target_nodes=args.nodes, eot=args.eot, run_base=rank * R,
-                                  prepend_run0=True, threads=min(16, os.cpu_count() or 1))
+                                  prepend_run0=True, threads=min(16, os.cpu_count() or 1), **gen)
     gen_s = time.time() - t0
     owned = corpus.owned if corpus.owned is not None else np.ones(corpus.n_runs, np.uint8)
     status_ok = np.array([s == "success" for s in corpus.status])
@@ -213,7 +219,8 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         sample, s_succ, s_fail, s_runs = corpus, success, failed, owned_runs
         if cfg["cpu_runs"]:  # deep graphs: the oracle needs seconds per graph, time a bounded sample
-            sample, _ = synth.generate(cfg["cpu_runs"], target_nodes=args.nodes, eot=args.eot, threads=threads)
+            cs = cfg.get("cpu_sample", {"nodes": args.nodes, "eot": args.eot})
+            sample, _ = synth.generate(cfg["cpu_runs"], target_nodes=cs["nodes"], eot=cs["eot"], threads=threads, **gen)
             s_succ, s_fail, s_runs = sample.success_iters(), sample.failed_iters(), sample.n_runs
         reps, t_cpu = 0, 0.0
         while t_cpu < args.cpu_seconds:
@@ -224,6 +231,7 @@ def main():
         cpu = {"value": round(s_runs * reps / t_cpu, 4), "unit": "runs/s", "cores": threads, "kind": "port",
                "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on "
                          f"{'the same ' + str(s_runs) + '-run ' + args.config.upper() + ' corpus' if sample is corpus else str(s_runs) + ' runs of the same shape'}"
+                         f"{' at ' + str(cfg['cpu_sample']['nodes']) + '-node graphs (EOT ' + str(cfg['cpu_sample']['eot']) + ')' if 'cpu_sample' in cfg else ''}"
                          f", {reps} full pass(es) in {t_cpu:.1f}s; same phases except the D2H/edge-list "
                          f"materialisation"}
     out = {
@@ -244,7 +252,8 @@ def main():
                                 "c4": "C4: synthetic Molly-shaped corpus of 100k runs in total, run-sharded over the "
                                       "ranks (runs_per_gpu each), ~nodes_per_graph-node graphs, run 0 replicated",
                                 "c5": "C5: synthetic deep-provenance corpus, runs_per_gpu runs x (pre, post) graphs of "
-                                      "~nodes_per_graph nodes at EOT eot (SURVEY.md 8d), run 0 replicated"}[args.config],
+                                      "~nodes_per_graph nodes / ~4 edges per node at EOT eot (SURVEY.md 8d), run 0 "
+                                      "replicated"}[args.config],
                    "runs_per_gpu": R, "nodes_per_graph": args.nodes, "eot": args.eot,
                    "nodes_total_rank0": int(corpus.node_off[-1]), "edges_total_rank0": int(corpus.edge_off[-1]),
                    "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,

@@ -367,3 +367,22 @@ def test_dense_graph_edge_reload(eng, lds_max):
         _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
     finally:
         eng.set_option("graph_lds_max", -1)
+
+
+@pytest.mark.parametrize("tiers", ["default", "deep"])
+def test_dense_c5_shape(eng, tiers):
+    # bench.py's C5 generator settings (~4 edges per node, body goals shared
+    # across rules) at 15k-node graphs; "deep" forces every kernel onto the
+    # tiers the 1M-node C5 graphs take (global CSR/Kahn, k_chains_glob, 1024 threads)
+    from tools import synth
+    corpus, _ = synth.generate(16, target_nodes=20000, eot=20, body_extra=6, nval=3, nloc=4)
+    assert corpus.edge_off[-1] > 3.5 * corpus.node_off[-1] and corpus.failed_iters()
+    knobs = (("graph_lds_max", 0), ("build_lds_max", 0), ("chains_glob_min_v", 0), ("global_block", 1024))
+    if tiers == "deep":
+        for k, v in knobs:
+            eng.set_option(k, v)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+    finally:
+        for k, _ in knobs:
+            eng.set_option(k, 65536 if k == "chains_glob_min_v" else -1)  # the library's defaults

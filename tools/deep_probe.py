@@ -1,6 +1,7 @@
 """Deep-graph probe (SURVEY §8d C5 shape: ~1M-node graphs, EOT 2000) on one GPU.
 
-usage: python tools/deep_probe.py RUNS [NODES] [EOT] [--check]
+usage: python tools/deep_probe.py RUNS [NODES] [EOT] [--check] [--dense]
+--dense: bench.py's C5 generator settings (~4 edges per node).
 Prints per-kernel HIP-event times of one analysis pass; --check compares every
 device result with the CPU oracle (slow: the oracle needs seconds per graph).
 """
@@ -17,8 +18,9 @@ runs = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 nodes = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else 1_000_000
 eot = int(sys.argv[3]) if len(sys.argv) > 3 and not sys.argv[3].startswith("-") else 2000
 check = "--check" in sys.argv
+gen = dict(body_extra=6, nval=3, nloc=4) if "--dense" in sys.argv else {}
 t = time.time()
-corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16)
+corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16, **gen)
 print(f"generated {runs} runs, {int(corpus.node_off[-1])} nodes, {int(corpus.edge_off[-1])} edges "
       f"in {time.time() - t:.1f}s", flush=True)
 s, f = corpus.success_iters(), corpus.failed_iters()
@@ -50,8 +52,17 @@ for rep in range(2):
 if check:
     from oracle import oracle as O
     from tests.compare import assert_same
+    import threading
     t = time.time()
-    orc = O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN, threads=16)
+    box = {}
+    th = threading.Thread(target=lambda: box.setdefault("orc", O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN,
+                                                                          threads=16)))
+    th.start()
+    while th.is_alive():  # heartbeat: the oracle needs minutes on dense 1M-node graphs
+        th.join(30)
+        if th.is_alive():
+            print(f"  oracle running {time.time() - t:.0f}s", flush=True)
+    orc = box["orc"]
     print(f"oracle {time.time() - t:.1f}s", flush=True)
     res = E.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN, engine=eng, pulls=True)
     assert_same(corpus, res, orc, len(f))

@@ -40,6 +40,7 @@ typedef struct synth_params {
   uint32_t max_drops;    /* async rule instances dropped in a faulty run (1..max) */
   int prepend_run0;      /* shard mode: add run 0 (not owned) when run_base > 0 */
   int threads;
+  uint32_t body_extra;   /* extra body atoms per rule, uniform on 0..2*body_extra (0: Molly-like 1-3 atoms) */
 } synth_params;
 
 typedef struct synth_out {
@@ -209,6 +210,7 @@ static void gen_base(base_t *b, const synth_params *p, uint32_t C, uint64_t seed
       add_edge(b, x, r);
       double ub = urand(&s);
       uint32_t nb = ub < 0.45 ? 1 : (ub < 0.85 ? 2 : 3);
+      if (p->body_extra) nb += urange(&s, 2 * p->body_extra + 1);  /* denser corpora (C5's 4 edges per node) */
       for (uint32_t k = 0; k < nb; k++) {
         uint32_t bt, bl, bv, tt;
         if (type == NEMO_TYPE_NEXT) {

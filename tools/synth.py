@@ -28,7 +28,7 @@ class CParams(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("n_runs", ctypes.c_uint32), ("run_base", ctypes.c_uint32),
                 ("eot", ctypes.c_uint32), ("nloc", ctypes.c_uint32), ("nval", ctypes.c_uint32),
                 ("target_nodes", ctypes.c_uint32), ("p_fault", ctypes.c_double), ("max_drops", ctypes.c_uint32),
-                ("prepend_run0", ctypes.c_int), ("threads", ctypes.c_int)]
+                ("prepend_run0", ctypes.c_int), ("threads", ctypes.c_int), ("body_extra", ctypes.c_uint32)]
 
 
 class COut(ctypes.Structure):
@@ -74,14 +74,14 @@ class SynthInfo:
 
 def generate(n_runs: int, target_nodes: int = 5000, eot: int = 10, nloc: int = 5, nval: int = 8,
              p_fault: float = 0.15, max_drops: int = 2, seed: int = SEED, run_base: int = 0,
-             prepend_run0: bool = False, threads: Optional[int] = None):
+             prepend_run0: bool = False, threads: Optional[int] = None, body_extra: int = 0):
     """Returns (Corpus, SynthInfo).  Runs are iterations run_base .. run_base+n_runs-1
     (plus a replicated, not-owned run 0 first when prepend_run0 and run_base > 0)."""
     L = lib()
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
     p = CParams(seed, n_runs, run_base, eot, nloc, nval, target_nodes, p_fault, max_drops, int(prepend_run0),
-                threads)
+                threads, body_extra)
     o = COut()
     rc = L.synth_generate(ctypes.byref(p), ctypes.byref(o))
     if rc != 0:
