@@ -27,6 +27,8 @@
 // path holding an unseen node"), one wave per component in LDS, or a
 // workgroup-wide sweep over global memory for the largest components.  Both
 // tiers produce the same acceptance index k = rank of (len desc, lex asc).
+#include <algorithm>
+
 #include "device.h"
 #include "internal.h"
 
@@ -237,14 +239,12 @@ struct ChainsLDS {
 };
 
 template <int HCAP, int UCAP>
-__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c, uint32_t second) {
+__device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g) {
   constexpr uint32_t ECAP = HCAP;
   __shared__ ChainsLDS<HCAP, UCAP> L;
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_nch, s_maxup, s_fail;
-  const uint32_t g = blockIdx.x;
   if (c.err[g] || c.gs_off[g] != ~0ull) return;  // deep graphs: k_chains_glob
-  if (second && c.nch[g] != NEMO_NONE) return;   // done by the first tier
   const GraphView gv = c.view(g);
   const uint8_t *f = gv.flags;
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
@@ -1148,9 +1148,40 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
   if (threadIdx.x == 0) c.nch[g] = n;
 }
 
+// The second tier lists the graphs the first handed back (k_chains_sel) and
+// runs a small grid over that list: one early-exit workgroup per graph of the
+// 52.5 KB tier cost ~29 us per step at C3, where the list is empty.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains_sel(DevCorpus c) {
+  const uint32_t g = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  const bool need = g < c.G && !c.err[g] && c.gs_off[g] == ~0ull && c.nch[g] == NEMO_NONE;
+  uint32_t *sel = c.sel + c.G + 1;
+  wave_append(need, g, sel + 1, sel);
+}
+
+template <int HCAP, int UCAP>
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
+  chains_graph<HCAP, UCAP>(c, blockIdx.x);
+}
+
+// The list gets a kernel of its own, so the first tier's stays at 119 VGPRs
+// (four waves per SIMD); this one is held to three, as its LDS allows.
+template <int HCAP, int UCAP>
+__global__ __launch_bounds__(NEMO_BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void k_chains_list(DevCorpus c) {
+  const uint32_t *sel = c.sel + c.G + 1;
+  const uint32_t n = sel[0];
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    chains_graph<HCAP, UCAP>(c, sel[1 + k]);
+    __syncthreads();  // the LDS image of this graph is done before the next one
+  }
+}
+
+#define CHAINS_GRID 1024u
 void launch_chains(const DevCorpus &c, hipStream_t s) {
-  hipLaunchKernelGGL((k_chains<1664, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, 0u);
-  hipLaunchKernelGGL((k_chains<2048, 512>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, 1u);
+  if (!c.G) return;
+  hipLaunchKernelGGL((k_chains<1664, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  launch_zero(c.sel + c.G + 1, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_chains_sel, dim3((c.G + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
+  hipLaunchKernelGGL((k_chains_list<2048, 512>), dim3(std::min(c.G, CHAINS_GRID)), dim3(NEMO_BLOCK), 0, s, c);
   hipLaunchKernelGGL(k_chains_big, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
   launch_chains_glob(c, s);
 }

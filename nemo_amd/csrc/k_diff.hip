@@ -596,12 +596,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan64(const uint32_t *cnt, uint
 // children).  A region past a.cap is not written: the host re-runs the pull
 // with the capacity the cursor reports.
 template <int B>
-__global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
+__device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, const uint32_t slot) {
   __shared__ uint32_t s_lds[(B / 64)];
   __shared__ uint32_t s_cnt;
   __shared__ unsigned long long s_base;
-  const uint32_t g = a.which == 2 ? a.g0 : blockIdx.x;
-  const uint32_t slot = blockIdx.x;
+  const uint32_t g = a.which == 2 ? a.g0 : slot;
   if (c.err[g]) {
     if (threadIdx.x == 0) {
       a.cnt[slot] = 0;
@@ -684,6 +683,35 @@ __global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
       }
     }
     pos += tot;
+  }
+}
+
+// Raw / simplified pulls: the graphs k_pull_lds leaves (errors, past the LDS
+// caps) are listed first, so k_pull runs a small grid over that list instead
+// of one mostly-empty workgroup per graph (~20k early exits cost ~38 us at C3).
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pull_sel(DevCorpus c, uint32_t slots) {
+  const uint32_t g = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  bool need = false;
+  if (g < slots) {
+    if (c.err[g]) {
+      need = true;
+    } else {
+      const GraphView gv = c.view(g);
+      need = !lds_fits(c, gv.V, gv.E, gv.nlev);
+    }
+  }
+  wave_append(need, g, c.sel + 1, c.sel);
+}
+
+#define PULL_GRID 2048u
+template <int B>
+__global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
+  // diff pulls: one workgroup per entry (gridDim.x == slots)
+  const bool list = a.which != 2;
+  const uint32_t n = list ? c.sel[0] : gridDim.x;
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    pull_slot<B>(c, a, list ? c.sel[1 + k] : k);
+    __syncthreads();  // LDS of this graph is done before the next one starts
   }
 }
 
@@ -1016,10 +1044,17 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
   }
+  uint32_t grid = slots;
+  if (a.which != 2) {
+    if (!slots) return;
+    launch_zero(c.sel, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_pull_sel, dim3((slots + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c, slots);
+    grid = std::min(slots, PULL_GRID);
+  }
   if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_pull<1024>, dim3(slots), dim3(1024), 0, s, c, a);
+    hipLaunchKernelGGL(k_pull<1024>, dim3(grid), dim3(1024), 0, s, c, a);
   else
-    hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(slots), dim3(NEMO_BLOCK), 0, s, c, a);
+    hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
   hipLaunchKernelGGL(k_triggers, dim3(3 * TRIG_SPLIT), dim3(NEMO_BLOCK), 0, s, c, a, phase);
