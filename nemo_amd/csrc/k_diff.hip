@@ -609,7 +609,7 @@ __device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, c
     return;
   }
   const GraphView gv = c.view(g);
-  if (a.which != 2 && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph
+  if (lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph or diff entry
   const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
@@ -716,7 +716,8 @@ __global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
 }
 
 
-// k_pull over the LDS graph tier (raw / simplified graphs): the forward rows
+// k_pull over the LDS graph tier (raw / simplified graphs, and the diff
+// entries over run 0's graph, D mask in place of the flags): the forward rows
 // and the flags staged in LDS (the reverse rows are read from HBM for the
 // chain heads only), per-node output offsets from one block scan, the same
 // order as k_pull.  The image is ~5V + 2E bytes, so four workgroups share a CU.
@@ -746,21 +747,24 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   __shared__ uint32_t s_lds[PULL_BLOCK / 64];
   __shared__ uint32_t s_cnt;
   __shared__ unsigned long long s_base;
-  const uint32_t g = blockIdx.x, tid = threadIdx.x;
+  const uint32_t which = a.which, slot = blockIdx.x, tid = threadIdx.x;
+  const uint32_t g = which == 2 ? a.g0 : slot;
   if (c.err[g]) return;  // k_pull writes the empty slot
   const GraphView gv = c.view(g);
   if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V;
   PullLds L = pull_carve(dyn, V, gv.E);
   {
-    const StageDesc d[3] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}, {gv.flags, L.fl, V, ST_U8}};
+    // diff pulls stage the entry's D mask where the others stage the flags
+    const uint8_t *fsrc = which == 2 ? a.mask + (size_t)slot * a.mask_stride : gv.flags;
+    const StageDesc d[3] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}, {fsrc, L.fl, V, ST_U8}};
     stage_lds<3, PULL_BLOCK>(d);
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  const uint32_t which = a.which;
   const uint8_t *fl = L.fl;
-#define ALIVE(v) (which == 0 || (fl[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+#define ALIVE(v) \
+  (which == 0 || (which == 1 ? (fl[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT : fl[v] != 0))
   uint16_t *cnt = L.cnt;  // per-node edge counts -> output offsets
   for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
     uint32_t n = 0;
@@ -784,8 +788,8 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
     const uint32_t tot = nn + s_cnt;
     const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)tot);
     s_base = base;
-    a.off[g] = base;
-    a.cnt[g] = tot;
+    a.off[slot] = base;
+    a.cnt[slot] = tot;
   }
   __syncthreads();
   const uint64_t base = s_base;
@@ -1039,7 +1043,7 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint
     hipLaunchKernelGGL(k_diff<NEMO_BLOCK>, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
-  if (a.which != 2 && c.lds_bytes) {
+  if (c.lds_bytes && slots) {
     const uint32_t bytes = pull_lds_bytes(c.lds_v, c.lds_e);
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
