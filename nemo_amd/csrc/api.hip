@@ -624,7 +624,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.chain, 5 * V);
   A(d.chain_tmp, 5 * V);
   A(d.nch, G);
-  A(d.sel, 2 * ((size_t)G + 1));
+  A(d.sel, 3 * ((size_t)G + 1));
   A(d.tail_first, V);
   A(d.chain_nt, V);
   A(d.proto_bits, R * c->W);

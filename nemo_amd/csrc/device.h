@@ -181,7 +181,7 @@ struct DevCorpus {
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
   uint32_t *chain_tmp;                   // [5*V]
   uint32_t *nch;                         // [G]
-  uint32_t *sel;                         // [2 (G + 1)] fallback-tier worklists (count first): k_pull's, then k_chains'
+  uint32_t *sel;                         // [3 (G + 1)] fallback-tier worklists (count first): k_pull's, k_chains', k_csr/k_topo's
   uint32_t *tail_first;                  // [V] head of per-tail chain list
   uint32_t *chain_nt;                    // [V] next chain with the same tail
   uint32_t *proto_bits, *graph_tables;   // [n_runs*words]

@@ -1,5 +1,7 @@
 // k_load.hip — device side of loadProv (graphing/pre-post-prov.go:25-213):
 // per-graph CSR build with the reference's edge validations, and Kahn levels.
+#include <algorithm>
+
 #include "device.h"
 #include "internal.h"
 
@@ -265,11 +267,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
 // larger ones do the same with global atomics.
 #define CSR_LDS 8192
 template <int B>
-__global__ __launch_bounds__(B) void k_csr(DevCorpus c) {
+__device__ __forceinline__ void csr_graph(const DevCorpus c, const uint32_t g) {
   __shared__ uint32_t s_cnt[CSR_LDS];
   __shared__ uint32_t s_lds[(B / 64)];
   __shared__ uint32_t s_bad, s_created;
-  const uint32_t g = blockIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   if (build_fits(c, V, E) && !c.redo[g]) return;  // k_build's graph
@@ -350,9 +351,8 @@ __global__ __launch_bounds__(B) void k_csr(DevCorpus c) {
 // Kahn levels: topo[] lists the graph's nodes level by level, lvl[l]..lvl[l+1]
 // is level l (longest path from a source).  A graph with a cycle is refused.
 template <int B>
-__global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
+__device__ __forceinline__ void topo_graph(const DevCorpus c, const uint32_t g) {
   __shared__ uint32_t s_tail;
-  const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0);
@@ -404,22 +404,62 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
   }
 }
 
+// The global-tier rebuild runs over a list of the graphs k_build did not take
+// (past its LDS caps, or handed back): one early-exit workgroup per graph cost
+// ~30 us per step at C3, where the list is empty.  k_csr and k_topo share it.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_load_sel(DevCorpus c) {
+  const uint32_t g = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  bool need = false;
+  if (g < c.G) {
+    const uint32_t V = (uint32_t)(c.node_off[g + 1] - c.node_off[g]);
+    const uint32_t E = (uint32_t)(c.edge_off[g + 1] - c.edge_off[g]);
+    need = !build_fits(c, V, E) || c.redo[g];
+  }
+  uint32_t *sel = c.sel + 2 * ((size_t)c.G + 1);
+  wave_append(need, g, sel + 1, sel);
+}
+template <int B>
+__global__ __launch_bounds__(B) void k_csr(DevCorpus c) {
+  const uint32_t *sel = c.sel + 2 * ((size_t)c.G + 1);
+  const uint32_t n = sel[0];
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    csr_graph<B>(c, sel[1 + k]);
+    __syncthreads();  // LDS of this graph is done before the next one starts
+  }
+}
+template <int B>
+__global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
+  const uint32_t *sel = c.sel + 2 * ((size_t)c.G + 1);
+  const uint32_t n = sel[0];
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    topo_graph<B>(c, sel[1 + k]);
+    __syncthreads();
+  }
+}
+#define LOAD_GRID 2048u
+
 void launch_build(const DevCorpus &c, hipStream_t s) {
   if (!c.bld_bytes) return;
   hipFuncSetAttribute((const void *)k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.bld_bytes);
   hipLaunchKernelGGL(k_build, dim3(c.G), dim3(NEMO_BLOCK), c.bld_bytes, s, c);
 }
 void launch_load(const DevCorpus &c, hipStream_t s) {
+  if (!c.G) return;
+  launch_zero(c.sel + 2 * ((size_t)c.G + 1), sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_load_sel, dim3((c.G + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
+  const uint32_t grid = std::min(c.G, LOAD_GRID);
   if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_csr<1024>, dim3(c.G), dim3(1024), 0, s, c);
+    hipLaunchKernelGGL(k_csr<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
-    hipLaunchKernelGGL(k_csr<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(k_csr<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);
 }
-void launch_topo(const DevCorpus &c, hipStream_t s) {
+void launch_topo(const DevCorpus &c, hipStream_t s) {  // after launch_load: its list
+  if (!c.G) return;
+  const uint32_t grid = std::min(c.G, LOAD_GRID);
   if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_topo<1024>, dim3(c.G), dim3(1024), 0, s, c);
+    hipLaunchKernelGGL(k_topo<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
-    hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);
 }
 
 }  // namespace nemo
