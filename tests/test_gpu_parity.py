@@ -386,3 +386,38 @@ def test_dense_c5_shape(eng, tiers):
     finally:
         for k, _ in knobs:
             eng.set_option(k, 65536 if k == "chains_glob_min_v" else -1)  # the library's defaults
+
+
+def _next_chain(cond, n):
+    goals = [{"id": f"goal{i}", "label": f"log(a, {i})", "table": cond if i == 0 else "log", "time": "1"}
+             for i in range(n + 1)]
+    rules = [{"id": f"rule{i}", "label": "log", "table": "log", "type": "next"} for i in range(n)]
+    edges = [e for i in range(n) for e in ({"from": f"goal{i}", "to": f"rule{i}"},
+                                           {"from": f"rule{i}", "to": f"goal{i + 1}"})]
+    return {"goals": goals, "rules": rules, "edges": edges}
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+def test_fallback_worklists_stride(eng, fallback):
+    # The fallback tiers run over worklists with a capped grid (k_chains_list:
+    # 1024 workgroups, k_csr/k_topo/k_pull: 2048), so a workgroup takes several
+    # listed graphs in turn.  1400 runs, two thirds of them 70-rule @next chains
+    # (141 Kahn levels: the first k_chains tier hands them to k_chains_list),
+    # the rest 10-rule chains (kept by the first tier): ~1870 listed graphs.
+    # With the graph and build LDS tiers off, all 2800 graphs go through the
+    # k_csr/k_topo and k_pull lists.
+    graphs = []
+    for r in range(1400):
+        n = 10 if r % 3 == 0 else 70
+        st = "failure" if r % 7 == 3 else "success"
+        graphs.append((r, st, _next_chain("pre", n), _next_chain("post", n - (r % 5))))
+    corpus = corpus_from_graphs(graphs)
+    keys = ("graph_lds_max", "build_lds_max")
+    if fallback:
+        for k in keys:
+            eng.set_option(k, 0)
+    try:
+        _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+    finally:
+        for k in keys:
+            eng.set_option(k, -1)
