@@ -14,7 +14,7 @@ One step = the whole hot path over the rank's corpus, inputs resident in HBM:
   SimplifyProv: cleanCopyProv + collapseNextChains           nemo_simplify
   CreatePrototypes: extractProtos partial -> RCCL all-reduce (N>1) -> finalize,
                     missingFrom for every failed run (table sets D2H)
-  CreateNaiveDiffProv for every failed run (per-run label sets)  nemo_diffprov
+  CreateNaiveDiffProv for every failed run (reference label set)  nemo_diffprov(_labels)
   GenerateCorrections/Extensions trigger patterns (rank owning run 0)
   PullPrePostProv + Q24 edge pulls (device compaction of simplified + diff graphs)
   D2H of every host-facing result: 2-bit node state (alive, holds) + chain (head,
@@ -46,16 +46,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=["c3", "c4", "c5"], default="c3",
-                    help="c3: 10k runs x ~5k-node graphs per GPU (the headline line, weak scaling); c4: 100k runs "
-                         "in total sharded over the ranks (strong scaling); c5: deep provenance, ~1M-node graphs "
-                         "at EOT 2000")
+    ap.add_argument("--config", choices=["c3", "c3_molly", "c4", "c5"], default="c3",
+                    help="c3: 10k runs x ~5k-node graphs (E ~ 1.5 V) per GPU, the headline line (weak scaling); "
+                         "c3_molly: the same at Molly's own 1-3-atom bodies (E ~ 1.18 V); c4: 100k runs in total, "
+                         "LPT-sharded over the ranks (strong scaling); c5: deep provenance, ~1M-node graphs at EOT 2000")
     ap.add_argument("--runs-per-gpu", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None, help="target nodes per provenance graph")
     ap.add_argument("--eot", type=int, default=None)
-    ap.add_argument("--diff-mode", choices=["per_run", "reference"], default="per_run")
+    ap.add_argument("--diff-mode", choices=["per_run", "reference"], default="reference",
+                    help="reference: differential-provenance.go:22-43's failedRuns[0] label set for every entry "
+                         "(broadcast from its owner rank when N>1); per_run: each failed run's own labels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU time budget of each baseline leg")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                     help="off: the timed steps run without per-launch HIP events (two extra steps collect them)")
@@ -63,50 +65,76 @@ def parse():
     return ap.parse_args()
 
 
-CONFIGS = {"c3": {"runs": 10000, "nodes": 5000, "eot": 10, "cpu_runs": None},
-           "c4": {"runs_total": 100000, "nodes": 5000, "eot": 10, "cpu_runs": 5000},
-           # C5 "1M-node / 4M-edge graphs": rule bodies of 1-3 atoms plus 0..12 extra ones over a key space
-           # small enough to share body goals (~0.95M nodes, ~4.0M edges per graph at EOT 2000)
-           # the CPU oracle is superlinear in graph size on this shape (>15 min per 1M-node run), so its
+# workload per config (generator settings: tools/synth.py CONFIGS); cpu_runs: the bounded sample the CPU
+# baseline times when a whole pass would take minutes
+CONFIGS = {"c3": {"runs": 10000, "gen": "c3", "cpu_runs": None},
+           "c3_molly": {"runs": 10000, "gen": "c3_molly", "cpu_runs": None},
+           "c4": {"runs_total": 100000, "gen": "c3", "cpu_runs": 5000},
+           # the CPU oracle is superlinear in graph size on C5's shape (>15 min per 1M-node run), so its
            # bounded sample is 4 runs of the same shape at 50k-node graphs (EOT 100, same density)
-           "c5": {"runs": 128, "nodes": 1_000_000, "eot": 2000, "cpu_runs": 4,
-                  "gen": {"body_extra": 6, "nval": 3, "nloc": 4}, "cpu_sample": {"nodes": 50_000, "eot": 100}}}
+           "c5": {"runs": 128, "gen": "c5", "cpu_runs": 4, "cpu_sample": {"target_nodes": 50_000, "eot": 100}}}
+
+
+def cpu_info():
+    """Host CPU facts for cpu_baseline: nproc, the cores this process may use, the model string."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(usable, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else usable
+    return {"nproc": os.cpu_count(), "usable_cores": usable, "threads": threads, "model": model}
 
 
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
     strong = "runs_total" in cfg
-    args.nodes = args.nodes or cfg["nodes"]
-    args.eot = args.eot or cfg["eot"]
     import torch
     import torch.distributed as dist
 
+    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE
+    from nemo_amd.engine import Engine
+    from tools import synth
+
+    gen = dict(synth.CONFIGS[cfg["gen"]])
+    if args.nodes:
+        gen["target_nodes"] = args.nodes
+    if args.eot:
+        gen["eot"] = args.eot
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n_gpus = world
-    if strong:  # C4: a fixed corpus split over the ranks
-        args.runs_per_gpu = args.runs_per_gpu or (cfg["runs_total"] + world - 1) // world
-    else:
-        args.runs_per_gpu = args.runs_per_gpu or cfg["runs"]
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE
-    from nemo_amd.engine import Engine
-    from tools import synth
-
-    R = args.runs_per_gpu
-    if strong:
-        R = max(0, min(R, cfg["runs_total"] - rank * R))
+    threads = min(16, cpu_info()["threads"])
     t0 = time.time()
-    gen = cfg.get("gen", {})
-    corpus, info = synth.generate(R, target_nodes=args.nodes, eot=args.eot, run_base=rank * R,
-                                  prepend_run0=True, threads=min(16, os.cpu_count() or 1), **gen)
+    if strong:  # C4: one fixed corpus, LPT-sharded by Σ(V+E) (nemo_partition_runs), run 0 replicated
+        R_total = args.runs_per_gpu * world if args.runs_per_gpu else cfg["runs_total"]
+        full, _ = synth.generate(R_total, threads=threads, **gen)
+        if world > 1:
+            from nemo_amd.shard import shard_layout
+            runs, own = shard_layout(full, rank, world)
+            corpus = full.subset(runs, own)
+        else:
+            corpus = full
+        del full
+    else:  # weak scaling: every rank its own block of runs (iterations rank*R ..), run 0 replicated
+        R = args.runs_per_gpu or cfg["runs"]
+        corpus, _ = synth.generate(R, run_base=rank * R, prepend_run0=True, threads=threads, **gen)
     gen_s = time.time() - t0
     owned = corpus.owned if corpus.owned is not None else np.ones(corpus.n_runs, np.uint8)
     status_ok = np.array([s == "success" for s in corpus.status])
@@ -123,10 +151,21 @@ def main():
     eng.set_stream(stream.cuda_stream)
     eng.load(corpus)
     d_red = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda")
-    T = corpus.n_tables
-    W = (T + 31) // 32
-    g0 = 2 * corpus.run_index(0) + 1
-    V0 = corpus.graph_size(g0)
+    V0 = corpus.graph_size(2 * corpus.run_index(0) + 1)
+
+    # sharded reference mode: failedRuns[0] = the lowest failed iteration of the whole job; its owner
+    # extracts the post-goal label set on the device and RCCL broadcasts it (differential-provenance.go:22-43)
+    label_bcast = world > 1 and mode == DIFF_REFERENCE
+    if label_bcast:
+        t = torch.tensor([min(failed) if failed else 2 ** 62, int(np.diff(corpus.node_off.astype(np.int64)).max()) + 1],
+                         dtype=torch.int64, device="cuda")
+        dist.all_reduce(t[0:1], op=dist.ReduceOp.MIN)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.MAX)
+        f0, lab_cap = int(t[0].item()), int(t[1].item())
+        o = torch.tensor([rank if f0 in set(failed) else world], dtype=torch.int64, device="cuda")
+        dist.all_reduce(o, op=dist.ReduceOp.MIN)
+        lab_owner = int(o.item())
+        d_lab = torch.zeros(lab_cap, dtype=torch.int32, device="cuda")
 
     fidx = np.array([corpus.run_index(f) for f in failed], np.int64)  # failed runs' rows of the table sets
 
@@ -139,7 +178,13 @@ def main():
         eng.protos_partial(success, d_red.data_ptr())
         if world > 1:
             dist.all_reduce(d_red)
-        eng.diffprov(failed, mode)
+        if label_bcast:
+            if rank == lab_owner:
+                eng.goal_labels(f0, 1, d_lab.data_ptr(), lab_cap)
+            dist.broadcast(d_lab, lab_owner)
+            eng.diffprov_labels(failed, d_lab.data_ptr(), lab_cap)
+        else:
+            eng.diffprov(failed, mode)
         if has_run0:
             eng.triggers()
         eng.pull(1)
@@ -148,9 +193,9 @@ def main():
         tabs = eng.run_tables(1)
         inter = np.asarray(protos["inter"], np.int64)
         uni = np.asarray(protos["union"], np.int64)
-        if len(fidx):
-            have_i = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
-            have_u = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
+        if len(fidx):  # missingFrom (prototype.go:141-206) for every failed run
+            _ = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
+            _ = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
         if has_run0:
             eng.trigger_rows()
         masks = eng.diff_masks_view() if failed else None
@@ -185,18 +230,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     owned_runs = int(owned.sum())
-    total_runs = owned_runs * world if world > 1 else owned_runs
+    total_runs = owned_runs
     if world > 1:
         t = torch.tensor([owned_runs], dtype=torch.int64, device="cuda")
         dist.all_reduce(t)
         total_runs = int(t.item())
     runs_per_s = total_runs * args.steps / elapsed
-    kern_ms = sum(v["ms"] for v in tim.values())
     edges = sum(v["edges"] for v in tim.values())
     if world > 1:
-        t = torch.tensor([edges, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([edges], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
-        edges, kern_ms_sum = float(t[0].item()), float(t[1].item())
+        edges = float(t.item())
     # edges/s: edges examined by all traversal kernels of all ranks over the wall time
     edges_per_s = edges / elapsed
     dom = max(tim.items(), key=lambda kv: kv[1]["ms"])
@@ -205,35 +249,19 @@ def main():
     avg_ms = d["ms"] / d["launches"]
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{dname}.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc):
         try:
-            pj = json.load(open(pmc))
+            pj = json.load(open(pmc)).get(dname, {})
             if pj.get("workload_nodes") == int(corpus.node_off[-1]):
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import oracle as O
-        threads = min(16, os.cpu_count() or 1)
-        sample, s_succ, s_fail, s_runs = corpus, success, failed, owned_runs
-        if cfg["cpu_runs"]:  # deep graphs: the oracle needs seconds per graph, time a bounded sample
-            cs = cfg.get("cpu_sample", {"nodes": args.nodes, "eot": args.eot})
-            sample, _ = synth.generate(cfg["cpu_runs"], target_nodes=cs["nodes"], eot=cs["eot"], threads=threads, **gen)
-            s_succ, s_fail, s_runs = sample.success_iters(), sample.failed_iters(), sample.n_runs
-        reps, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds:
-            tc = time.perf_counter()
-            O.analyze(sample, s_succ, s_fail, diff_mode=mode, threads=threads, skip_pulls=True)
-            t_cpu += time.perf_counter() - tc
-            reps += 1
-        cpu = {"value": round(s_runs * reps / t_cpu, 4), "unit": "runs/s", "cores": threads, "kind": "port",
-               "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on "
-                         f"{'the same ' + str(s_runs) + '-run ' + args.config.upper() + ' corpus' if sample is corpus else str(s_runs) + ' runs of the same shape'}"
-                         f"{' at ' + str(cfg['cpu_sample']['nodes']) + '-node graphs (EOT ' + str(cfg['cpu_sample']['eot']) + ')' if 'cpu_sample' in cfg else ''}"
-                         f", {reps} full pass(es) in {t_cpu:.1f}s; same phases except the D2H/edge-list "
-                         f"materialisation"}
+        cpu = cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode)
+    E = int(corpus.edge_off[-1])
+    Vn = int(corpus.node_off[-1])
     out = {
         "metric": METRIC,
         "value": round(runs_per_s, 2),
@@ -248,26 +276,31 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {"workload": {"c3": "C3: synthetic Molly-shaped corpus, runs_per_gpu runs x (pre, post) provenance "
-                                      "graphs of ~nodes_per_graph nodes (SURVEY.md 8d), run 0 replicated",
-                                "c4": "C4: synthetic Molly-shaped corpus of 100k runs in total, run-sharded over the "
-                                      "ranks (runs_per_gpu each), ~nodes_per_graph-node graphs, run 0 replicated",
+                                      "graphs of ~nodes_per_graph nodes, E ~ 1.5 V (SURVEY.md 8d), run 0 replicated",
+                                "c3_molly": "C3 at Molly's own rule-body sizes (1-3 atoms, E ~ 1.18 V)",
+                                "c4": "C4: synthetic Molly-shaped corpus of 100k runs in total, LPT-sharded over the "
+                                      "ranks by nodes+edges, ~nodes_per_graph-node graphs, run 0 replicated",
                                 "c5": "C5: synthetic deep-provenance corpus, runs_per_gpu runs x (pre, post) graphs of "
                                       "~nodes_per_graph nodes / ~4 edges per node at EOT eot (SURVEY.md 8d), run 0 "
                                       "replicated"}[args.config],
-                   "runs_per_gpu": R, "nodes_per_graph": args.nodes, "eot": args.eot,
-                   "nodes_total_rank0": int(corpus.node_off[-1]), "edges_total_rank0": int(corpus.edge_off[-1]),
+                   "runs_per_gpu": int(corpus.n_runs), "nodes_per_graph": gen["target_nodes"], "eot": gen["eot"],
+                   "nodes_total_rank0": Vn, "edges_total_rank0": E, "edges_per_node": round(E / max(Vn, 1), 3),
                    "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,
-                   "parallelism": f"run-sharded x{n_gpus}, RCCL all-reduce of the prototype vector"},
+                   "parallelism": f"run-sharded x{n_gpus}, RCCL all-reduce of the prototype vector"
+                                  + (" + broadcast of failedRuns[0]'s label set" if label_bcast else "")},
         "edges_traversed_per_s": round(edges_per_s, 1),
         "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(avg_ms, 4)},
+                     "bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(avg_ms, 4),
+                     "bytes_formula": "DESIGN.md section 3 (HBM lower bound per launch)"},
         "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
                         "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
                     for k, v in sorted(tim.items(), key=lambda kv: -kv[1]["ms"])},
         "gen_seconds_rank0": round(gen_s, 2),
     }
+    if "k_diff" in tim:  # all entries of a diffprov call run concurrently: the launch time is each entry's latency
+        out["k_diff_entry_latency_ms"] = round(tim["k_diff"]["ms"] / tim["k_diff"]["launches"], 4)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -278,6 +311,48 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):
+    """oracle/nemo_oracle.c timed on the host (rank 0, N=1): OpenMP over graphs on every usable core
+    (capped by OMP_NUM_THREADS) and on one core, each leg for about --cpu-seconds of a bounded sample."""
+    from oracle import oracle as O
+    from tools import synth
+    info = cpu_info()
+    threads = info["threads"]
+    sample, s_succ, s_fail, s_runs = corpus, success, failed, owned_runs
+    desc = f"the same {s_runs}-run {args.config.upper()} corpus"
+    if cfg["cpu_runs"]:  # deep graphs / huge corpora: a bounded sample of the same shape
+        g = dict(gen)
+        g.update(cfg.get("cpu_sample", {}))
+        sample, _ = synth.generate(cfg["cpu_runs"], threads=min(16, threads), **g)
+        s_succ, s_fail, s_runs = sample.success_iters(), sample.failed_iters(), sample.n_runs
+        desc = f"{s_runs} runs of the same shape" + (f" at {g['target_nodes']}-node graphs (EOT {g['eot']})"
+                                                    if "cpu_sample" in cfg else "")
+
+    def leg(n_threads, smp, su, fa, runs):
+        reps, t = 0, 0.0
+        while t < args.cpu_seconds or reps == 0:
+            tc = time.perf_counter()
+            O.analyze(smp, su, fa, diff_mode=mode, threads=n_threads, skip_pulls=False)
+            t += time.perf_counter() - tc
+            reps += 1
+        return runs * reps / t, reps, t
+
+    v_all, reps, t_all = leg(threads, sample, s_succ, s_fail, s_runs)
+    # one core: the first 500 runs (run 0 included) of the sample
+    n1 = min(sample.n_runs, 500)
+    one = sample.subset(np.arange(n1)) if n1 < sample.n_runs else sample
+    own1 = one.owned if one.owned is not None else np.ones(one.n_runs, np.uint8)
+    su1 = [x for x in s_succ if x in set(one.iteration.tolist())]
+    fa1 = [x for x in s_fail if x in set(one.iteration.tolist())]
+    v_one, reps1, t_one = leg(1, one, su1, fa1, int(own1.sum()))
+    return {"value": round(v_all, 4), "unit": "runs/s", "cores": threads, "kind": "port",
+            "value_1core": round(v_one, 4), "nproc": info["nproc"], "usable_cores": info["usable_cores"],
+            "cpu_model": info["model"],
+            "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on {desc}, {reps} full pass(es) "
+                      f"in {t_all:.1f}s, the same phases incl. the edge-list materialisation; 1-core leg: the "
+                      f"first {n1} runs of it, {reps1} pass(es) in {t_one:.1f}s"}
 
 
 if __name__ == "__main__":

@@ -104,6 +104,14 @@ typedef struct nemo_missing {
   uint32_t rule;   /* local index of the rule in run 0's post graph               */
 } nemo_missing;
 
+/* ---- run sharding --------------------------------------------
+ * part_of_run[r] in [0, n_parts) for every run of the corpus: longest-first
+ * (LPT) by the run's nodes + edges (pre + post graphs), each run to the least
+ * loaded part, ties by index.  Host only; the node context (below) and the
+ * one-process-per-GPU path use the same assignment.  The good run 0 is
+ * replicated on every part by the caller (owned there by its own part only). */
+int nemo_partition_runs(const nemo_corpus *corpus, uint32_t n_parts, uint32_t *part_of_run);
+
 /* ---- context --------------------------------------------------------------
  * Replaces InitGraphDB / CloseDB (graphing/helpers.go:17-55, 58-86): no docker,
  * no 10 s sleep, no Bolt; binds one HIP device.                             */
@@ -114,13 +122,24 @@ const char *nemo_last_error(const nemo_ctx *ctx);
 int nemo_abi_version(void);
 /* Launch every kernel on `stream` (a hipStream_t, NULL = the context's own). */
 int nemo_set_stream(nemo_ctx *ctx, void *stream);
-/* Tuning / test knobs (-1 = default): "chains_lds_max" = largest chain
- * subgraph (nodes) the first @next-chain tier stages in LDS; larger graphs go
- * to the component tier, where "chains_comp_max" = largest component run in
- * LDS by one wave (larger ones take the workgroup-wide global-memory path);
- * "build_lds_max" = largest graph (nodes) whose CSR + Kahn levels are built
- * in LDS by k_build (also capped at 6144 nodes / 8192 edges); applies from the
- * next nemo_load_corpus / nemo_rebuild.                                      */
+/* Tuning / test knobs (value -1 restores the default).  None changes a result;
+ * each selects which kernel tier runs, so the parity tests force every tier.
+ *   "chains_lds_max"    largest chain subgraph H* (nodes) the @next-chain LDS
+ *                       tiers take; larger graphs go to the component tier
+ *   "chains_comp_max"   largest component the component tier runs in LDS on one
+ *                       wave (larger ones take its workgroup-wide global path)
+ *   "chains_glob_min_v" graphs with at least this many nodes take the deep
+ *                       k_chains_glob tier (default 65536; next nemo_load_corpus)
+ *   "build_lds_max"     largest graph (nodes) whose CSR + Kahn levels k_build
+ *                       builds in LDS (also capped at 16384 nodes / 8192 edges
+ *                       and by the corpus-sized LDS budget); from the next
+ *                       nemo_load_corpus / nemo_rebuild
+ *   "graph_lds_max"     largest graph (nodes) of the LDS graph tier of k_marksimp,
+ *                       k_proto_lds, k_diff_lds and k_pull_lds (0 = off)
+ *   "global_block"      workgroup size of the global-memory tiers: 256 or 1024
+ *                       (default: 1024 when >= 1/8 of the graphs have >= 64k nodes)
+ *   "stage_blocks"      nemo_stage_simplified's bulk copies: 0 = runtime copies
+ *                       (default), else a copy kernel on this many workgroups   */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);
@@ -185,6 +204,16 @@ int nemo_missing_from(nemo_ctx *ctx, uint32_t failed_iter, const uint32_t *proto
 #define NEMO_DIFF_REFERENCE 0
 #define NEMO_DIFF_PER_RUN   1
 int nemo_diffprov(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, int mode);
+/* The run-sharded form of the reference mode (differential-provenance.go:22-43:
+ * every entry uses failedRuns[0]'s labels, but that run lives on one shard).
+ * nemo_goal_labels writes the goal labels of run `iteration`'s pre (cond 0) or
+ * post (cond 1) graph into device memory as [n, label...] (cap >= the graph's
+ * nodes + 1), enqueued on the context's stream without a host round trip; the
+ * owner's buffer is then broadcast (RCCL) and every shard runs
+ * nemo_diffprov_labels with it: failGoals = that set for every entry. */
+int nemo_goal_labels(nemo_ctx *ctx, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap);
+int nemo_diffprov_labels(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, const uint32_t *d_labels,
+                         uint64_t labels_cap);
 /* D node mask over run 0's post graph for entry e (1 byte per node).        */
 int nemo_fetch_diff_mask(nemo_ctx *ctx, uint32_t entry, uint8_t *out, uint64_t cap);
 /* D masks of every entry, entry-major (n_entries * V0 bytes).               */
@@ -243,6 +272,13 @@ int nemo_pull_edges(nemo_ctx *ctx, int which);
 uint64_t nemo_pulled_count(nemo_ctx *ctx, uint32_t slot);
 int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap,
                       uint64_t *n_out);
+/* Every slot at once (one call where the Go side would make one per graph):
+ * off[slot] / cnt[slot] (pulled-slot count entries each) locate slot s's edges
+ * in src/dst, whose used extent is *n_used (regions are claimed in device
+ * order, so they are disjoint but not sorted by slot).  src/dst may be NULL
+ * to query *n_used; then cap >= *n_used.                                   */
+int nemo_fetch_pulled_all(nemo_ctx *ctx, uint64_t *off, uint32_t *cnt, uint32_t *src, uint32_t *dst, uint64_t cap,
+                          uint64_t *n_used);
 
 /* ---- native ingest of a Molly output directory (host only) ------------------
  * Replaces Molly.LoadOutput's per-run JSON decoding (faultinjectors/molly.go:

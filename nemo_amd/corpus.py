@@ -133,6 +133,31 @@ class Corpus:
     def failed_iters(self) -> List[int]:
         return [int(self.iteration[r]) for r in range(self.n_runs) if self.status[r] != "success"]
 
+    def subset(self, runs: Sequence[int], owned: Optional[Sequence[int]] = None) -> "Corpus":
+        """The corpus of runs `runs` (run indices, in that order) with their two graphs each;
+        `owned` marks which of them count in cross-run reductions (None: all).  Numeric
+        arrays only: the host string tables stay with the parent corpus."""
+        runs = np.asarray(runs, np.int64)
+        gs = np.stack([2 * runs, 2 * runs + 1], 1).reshape(-1)
+        n0, n1 = self.node_off[gs].astype(np.int64), self.node_off[gs + 1].astype(np.int64)
+        e0, e1 = self.edge_off[gs].astype(np.int64), self.edge_off[gs + 1].astype(np.int64)
+        nv, ne = n1 - n0, e1 - e0
+        node_off = np.concatenate([[0], np.cumsum(nv)]).astype(np.uint64)
+        edge_off = np.concatenate([[0], np.cumsum(ne)]).astype(np.uint64)
+        vi = np.repeat(n0 - node_off[:-1].astype(np.int64), nv) + np.arange(int(node_off[-1]), dtype=np.int64)
+        ei = np.repeat(e0 - edge_off[:-1].astype(np.int64), ne) + np.arange(int(edge_off[-1]), dtype=np.int64)
+        own = None
+        if owned is not None:
+            own = np.ascontiguousarray(owned, dtype=np.uint8)
+            if own.all():
+                own = None
+        return Corpus(iteration=np.ascontiguousarray(self.iteration[runs]), node_off=node_off, edge_off=edge_off,
+                      node_word=self.node_word[vi], label=self.label[vi], edge_src=self.edge_src[ei],
+                      edge_dst=self.edge_dst[ei], n_tables=self.n_tables, table_pre=self.table_pre,
+                      table_post=self.table_post, id_rank=None if self.id_rank is None else self.id_rank[vi],
+                      owned=own, status=None if self.status is None else [self.status[int(r)] for r in runs],
+                      tables=self.tables)
+
     def c_struct(self) -> CCorpus:
         arrs = [self.iteration, self.node_off, self.edge_off, self.node_word, self.label, self.edge_src,
                 self.edge_dst, self.id_rank, self.owned]

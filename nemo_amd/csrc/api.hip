@@ -159,9 +159,12 @@ template <class T>
 static int dalloc(nemo_ctx *c, T **p, size_t n) {
   void *q = nullptr;
   if (n == 0) n = 1;
-  hipError_t e = hipMalloc(&q, n * sizeof(T));
+  // whole 16-byte chunks: stage_lds (device.h) loads aligned 16-B chunks, so
+  // the chunk holding a buffer's last byte must lie inside the allocation
+  const size_t bytes = (n * sizeof(T) + 15) & ~(size_t)15;
+  hipError_t e = hipMalloc(&q, bytes);
   if (e != hipSuccess)
-    return fail(c, NEMO_ERR_HIP, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+    return fail(c, NEMO_ERR_HIP, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
   c->allocs.push_back(q);
   *p = (T *)q;
   return NEMO_OK;
@@ -260,6 +263,33 @@ static void sort_rows(uint32_t *rows, uint64_t n) {
 extern "C" {
 
 int nemo_abi_version(void) { return NEMOHIP_ABI_VERSION; }
+
+// Run sharding: longest-processing-time-first over the runs'
+// node + edge counts (both graphs), ties by run index; each run goes to the
+// least-loaded part so far (ties by part index).  Deterministic, so every
+// rank of a torchrun job and the in-library node context agree.
+int nemo_partition_runs(const nemo_corpus *in, uint32_t n_parts, uint32_t *part_of_run) {
+  if (!in || !part_of_run || n_parts == 0 || (in->n_runs && (!in->node_off || !in->edge_off))) return NEMO_ERR_INVALID;
+  const uint32_t R = in->n_runs;
+  std::vector<std::pair<uint64_t, uint32_t>> w(R);
+  for (uint32_t r = 0; r < R; r++)
+    w[r] = {in->node_off[2 * r + 2] - in->node_off[2 * r] + in->edge_off[2 * r + 2] - in->edge_off[2 * r], r};
+  std::sort(w.begin(), w.end(), [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  });
+  using Load = std::pair<uint64_t, uint32_t>;  // (load, part): min-heap
+  std::vector<Load> heap(n_parts);
+  for (uint32_t p = 0; p < n_parts; p++) heap[p] = {0, p};
+  auto cmp = [](const Load &a, const Load &b) { return a > b; };
+  std::make_heap(heap.begin(), heap.end(), cmp);
+  for (auto &x : w) {
+    std::pop_heap(heap.begin(), heap.end(), cmp);
+    part_of_run[x.second] = heap.back().second;
+    heap.back().first += x.first;
+    std::push_heap(heap.begin(), heap.end(), cmp);
+  }
+  return NEMO_OK;
+}
 
 int nemo_ctx_create(int device, nemo_ctx **out) {
   if (!out) return NEMO_ERR_INVALID;
@@ -512,8 +542,10 @@ static int device_load(nemo_ctx *c) {
     }
   }
   const double V = (double)c->V - Vb, E = (double)c->E - Eb;
-  // k_build: read edges twice + words; write both CSRs, topo, levels
-  if ((rc = timed(c, "k_build", 20 * Eb + 32 * Vb, 2 * Eb, [&] { nemo::launch_build(c->dc, c->stream); })))
+  // k_build, HBM lower bound: read the edge list (8E) and node words (4V);
+  // write both column arrays (8E), both row-pointer arrays (8V), the Kahn
+  // order (4V) and per-node level (4V); the level offsets are per level
+  if ((rc = timed(c, "k_build", 16 * Eb + 20 * Vb, 2 * Eb, [&] { nemo::launch_build(c->dc, c->stream); })))
     return rc;
   if ((rc = timed(c, "k_csr", 16 * E + 12 * V, E, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
@@ -935,8 +967,13 @@ int nemo_missing_from(nemo_ctx *c, uint32_t failed_iter, const uint32_t *proto, 
   return NEMO_OK;
 }
 
-int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode) {
+// d_labels != NULL: label mode, every entry's failGoals is the device label
+// set [n, label...] (n <= labels_cap), e.g. broadcast from the shard that owns
+// failedRuns[0]; mode is then ignored.
+static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode,
+                         const uint32_t *d_labels, uint64_t labels_cap) {
   if (!c || (!failed_iters && n_failed)) return NEMO_ERR_INVALID;
+  if (mode != NEMO_DIFF_REFERENCE && mode != NEMO_DIFF_PER_RUN) return fail(c, NEMO_ERR_INVALID, "unknown diff mode %d", mode);
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_diffprov before nemo_mark_holds");
   if (int rm = ensure_marked(c)) return rm;
   HIPCHK(c, hipSetDevice(c->device));
@@ -946,13 +983,16 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   else HIPCHK(c, hipEventSynchronize(c->ev_up_dsrc));  // the previous upload has landed
   if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, n_failed)) return rg;
   uint32_t *src = c->h_dsrc;
+  double src_bytes = 0;  // the label sources' HBM reads (word + label per node, or the label set)
   for (size_t e = 0; e < n_failed; e++) {
     uint32_t r;
-    const uint32_t it = mode == NEMO_DIFF_PER_RUN ? failed_iters[e] : failed_iters[0];
-    int rc = run_index(c, it, &r);
+    const uint32_t it = mode == NEMO_DIFF_PER_RUN && !d_labels ? failed_iters[e] : failed_iters[0];
+    int rc = run_index(c, d_labels ? failed_iters[e] : it, &r);
     if (rc) return rc;
     src[e] = 2 * r + 1;
+    src_bytes += d_labels ? 0.0 : 8.0 * (double)(c->node_off[2 * r + 2] - c->node_off[2 * r + 1]);
   }
+  if (d_labels) src_bytes = 4.0 * (double)labels_cap;  // read once, then L2-resident for every entry
   const uint32_t g0 = 2 * c->run0 + 1;
   const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
   const uint64_t E0 = c->edge_off[g0 + 1] - c->edge_off[g0];
@@ -980,6 +1020,7 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   nemo::DiffArgs a;
   a.g0 = g0;
   a.src = c->d_dsrc;
+  a.ref_labels = d_labels;
   a.r0lab = c->d_r0lab;
   a.r0idx = c->d_r0idx;
   a.n_r0lab = c->n_r0lab;
@@ -998,8 +1039,12 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   a.mask = c->d_dmask;
   a.missing = c->d_miss;
   a.n_missing = c->d_nmiss;
-  double bytes = (double)n_failed * (3.0 * (4 * E0 + 9 * V0) + 6 * V0);
-  rc = timed(c, "k_diff", bytes, (double)n_failed * 4 * E0,
+  // HBM lower bound: run 0's post graph once (rows both ways, node word, Kahn
+  // order: 8E0 + 16V0 -- every entry re-reads it from L2), each entry's label
+  // source and its D mask (V0); the three reachability sweeps per entry are
+  // counted as traversed edges, not as HBM bytes
+  const double bytes = 8.0 * E0 + 16.0 * V0 + src_bytes + (double)n_failed * V0;
+  rc = timed(c, "k_diff", bytes, (double)n_failed * 3 * E0,
              [&] {
                // the Kahn-order relayout only when g0 may fall outside the LDS tier
                const bool lds = c->dc.lds_bytes && V0 <= c->dc.lds_v && E0 <= c->dc.lds_e && V0 <= c->dc.lds_l;
@@ -1015,6 +1060,30 @@ int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, in
   HIPCHK(c, hipEventRecord(c->ev_diff, s));
   c->n_entries = (uint32_t)n_failed;
   return NEMO_OK;
+}
+
+int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode) {
+  return diffprov_impl(c, failed_iters, n_failed, mode, nullptr, 0);
+}
+
+int nemo_diffprov_labels(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, const uint32_t *d_labels,
+                         uint64_t labels_cap) {
+  if (!d_labels) return c ? fail(c, NEMO_ERR_INVALID, "no label set") : NEMO_ERR_INVALID;
+  return diffprov_impl(c, failed_iters, n_failed, NEMO_DIFF_REFERENCE, d_labels, labels_cap);
+}
+
+int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap) {
+  if (!c || !d_out || (cond != 0 && cond != 1)) return NEMO_ERR_INVALID;
+  if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
+  uint32_t r;
+  int rc = run_index(c, iteration, &r);
+  if (rc) return rc;
+  const uint32_t g = 2 * r + (uint32_t)cond;
+  const uint64_t V = c->node_off[g + 1] - c->node_off[g];
+  if (cap < V + 1) return fail(c, NEMO_ERR_INVALID, "label capacity %llu < %llu", (unsigned long long)cap,
+                               (unsigned long long)(V + 1));
+  HIPCHK(c, hipSetDevice(c->device));
+  return timed(c, "k_goal_labels", 8.0 * (double)V, 0, [&] { nemo::launch_goal_labels(c->dc, g, d_out, c->stream); });
 }
 
 int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap) {
@@ -1431,6 +1500,27 @@ int nemo_fetch_pulled(nemo_ctx *c, uint32_t slot, uint32_t *src, uint32_t *dst, 
   return NEMO_OK;
 }
 
+int nemo_fetch_pulled_all(nemo_ctx *c, uint64_t *off, uint32_t *cnt, uint32_t *src, uint32_t *dst, uint64_t cap,
+                          uint64_t *n_used) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = pull_sync(c);
+  if (rc) return rc;
+  const uint64_t used = c->pull_slots ? *c->h_pcur : 0;
+  if (n_used) *n_used = used;
+  if (off && c->pull_slots) memcpy(off, c->h_poff, c->pull_slots * 8ull);
+  if (cnt && c->pull_slots) memcpy(cnt, c->h_pcnt, c->pull_slots * 4ull);
+  if (!src && !dst) return NEMO_OK;
+  if (cap < used) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  if (used) {
+    if (src) HIPCHK(c, hipMemcpyAsync(src, c->d_psrc, used * 4, hipMemcpyDeviceToHost, c->stream));
+    if (dst) HIPCHK(c, hipMemcpyAsync(dst, c->d_pdst, used * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return NEMO_OK;
+}
+
 // Debug/inspection: copy `bytes` bytes at byte `offset` of an internal device array.
 int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, uint64_t bytes) {
   if (!c || !name || !out) return NEMO_ERR_INVALID;
@@ -1451,6 +1541,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "r0lab") base = c->d_r0lab;
   else if (n == "r0idx") base = c->d_r0idx;
   else if (n == "stamps") base = c->dc.stamps;
+  else if (n == "sel") base = c->dc.sel;  // worklists: [3][G+1] u32, count first (pulls, chains, load)
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));

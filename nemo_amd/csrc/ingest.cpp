@@ -107,6 +107,8 @@ struct FlatSet64 {
 struct Json {
   const char *p, *e;
   bool ok = true;
+  int depth = 0;  // nesting of skip(): untrusted input cannot grow the ingest thread's stack unboundedly
+  static constexpr int kMaxDepth = 512;
   std::vector<char> key;  // scratch for object keys (capacity reused)
 
   void ws() {
@@ -211,6 +213,15 @@ struct Json {
       std::vector<char> tmp;
       str(tmp);
     } else if (c == '{' || c == '[') {
+      if (depth >= kMaxDepth) {
+        ok = false;
+        return;
+      }
+      struct Nest {
+        int &d;
+        explicit Nest(int &x) : d(x) { d++; }
+        ~Nest() { d--; }
+      } nest(depth);
       char close = c == '{' ? '}' : ']';
       p++;
       ws();
@@ -244,7 +255,8 @@ struct Json {
     } else if (lit("true") || lit("false") || lit("null")) {
     } else {
       const char *q = p;
-      while (p < e && (strchr("+-0123456789.eE", *p) != nullptr)) p++;
+      auto numch = [](char x) { return (x >= '0' && x <= '9') || x == '+' || x == '-' || x == '.' || x == 'e' || x == 'E'; };
+      while (p < e && numch(*p)) p++;
       if (p == q) ok = false;
     }
   }

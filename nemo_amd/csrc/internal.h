@@ -11,6 +11,7 @@ namespace nemo {
 struct DiffArgs {
   uint32_t g0;              // run 0's post graph
   const uint32_t *src;      // [entries] label-source graph per entry
+  const uint32_t *ref_labels;  // label mode: [n, label...] used by every entry (NULL: src)
   const uint32_t *r0lab;    // sorted goal labels of g0
   const uint32_t *r0idx;    // local node of each sorted label
   uint32_t n_r0lab;
@@ -65,6 +66,7 @@ void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, 
 void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStream_t s);
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
+void launch_goal_labels(const DevCorpus &c, uint32_t g, uint32_t *out, hipStream_t s);
 void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 1024);
 void launch_zero(void *dst, uint64_t bytes, hipStream_t s);
 

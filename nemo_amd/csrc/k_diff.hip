@@ -49,16 +49,28 @@ __device__ __forceinline__ bool diff_lds_fits(const DevCorpus &c, const GraphVie
 // is a post-goal label of the source graph gets DB_PRESENT.  Each thread takes
 // DL_BATCH source nodes and walks their hash probes together, so a pass costs
 // a few rounds of independent loads rather than a binary search per node.
+// The label source is the post graph of the entry's source run, or (label
+// mode) a label set handed over in device memory as [n, label...]: the set of
+// failedRuns[0]'s post-goal labels broadcast from the shard that owns it.
 #define DL_BATCH 8
+struct LabelSrc {
+  const uint32_t *label, *word;  // word == nullptr: every entry is a goal label
+  uint32_t n;
+};
+__device__ __forceinline__ LabelSrc diff_label_src(const DevCorpus &c, const DiffArgs &a, uint32_t e) {
+  if (a.ref_labels) return {a.ref_labels + 1, nullptr, a.ref_labels[0]};
+  const GraphView s = c.view(a.src[e]);
+  return {s.label, s.word, s.V};
+}
 template <int B = NEMO_BLOCK>
-__device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const GraphView &src, uint8_t *bits,
+__device__ __forceinline__ void diff_fail_goals(const DiffArgs &a, const LabelSrc &src, uint8_t *bits,
                                                 const uint32_t *idx) {
-  for (uint32_t base = 0; base < src.V; base += DL_BATCH * B) {
+  for (uint32_t base = 0; base < src.n; base += DL_BATCH * B) {
     uint32_t lab[DL_BATCH], h[DL_BATCH], pos[DL_BATCH], live = 0;
 #pragma unroll
     for (int q = 0; q < DL_BATCH; q++) {
       const uint32_t x = base + q * B + threadIdx.x;
-      const bool in = x < src.V && !is_rule(src.word[x]);
+      const bool in = x < src.n && (!src.word || !is_rule(src.word[x]));
       lab[q] = in ? src.label[x] : 0u;
       h[q] = hash_label(lab[q]) & a.r0hmask;
       pos[q] = NEMO_NONE;
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   const uint32_t e = blockIdx.x;
   const GraphView gv = c.view(a.g0);
   if (diff_lds_fits(c, gv)) return;  // k_diff_lds's graph
-  const GraphView src = c.view(a.src[e]);
+  const LabelSrc src = diff_label_src(c, a, e);
   const uint32_t V = gv.V;
   uint8_t *bits = a.bits + (size_t)e * V;     // by Kahn position
   int32_t *depth = a.depth + (size_t)e * V;   // by Kahn position
@@ -451,7 +463,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_diff_lds(DevCorpus c, DiffArgs a
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   const GraphView gv = c.view(a.g0);
   if (!diff_lds_fits(c, gv)) return;  // k_diff's graph
-  const GraphView src = c.view(a.src[e]);
+  const LabelSrc src = diff_label_src(c, a, e);
   const uint32_t V = gv.V, nl = gv.nlev;
   DiffLds L = diff_carve(dyn, V, gv.E, nl);
   uint8_t *mask = a.mask + (size_t)e * V;
@@ -1060,6 +1072,23 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
   else
     hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c, a);
 }
+// failGoals' label set of one graph (differential-provenance.go:23-24) into
+// device memory as [n, label...]: the hand-over a sharded reference-mode
+// diff broadcasts from the shard owning failedRuns[0].  Order is irrelevant
+// (the set only gates run 0's goals), duplicates are harmless.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_goal_labels(DevCorpus c, uint32_t g, uint32_t *out) {
+  const GraphView gv = c.view(g);
+  for (uint32_t base = blockIdx.x * NEMO_BLOCK; base < gv.V; base += gridDim.x * NEMO_BLOCK) {
+    const uint32_t v = base + threadIdx.x;
+    const bool goal = v < gv.V && !is_rule(gv.word[v]);
+    wave_append(goal, goal ? gv.label[v] : 0u, out + 1, out);
+  }
+}
+void launch_goal_labels(const DevCorpus &c, uint32_t g, uint32_t *out, hipStream_t s) {
+  launch_zero(out, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_goal_labels, dim3(256), dim3(NEMO_BLOCK), 0, s, c, g, out);
+}
+
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s) {
   hipLaunchKernelGGL(k_triggers, dim3(3 * TRIG_SPLIT), dim3(NEMO_BLOCK), 0, s, c, a, phase);
 }

@@ -270,20 +270,16 @@ template <int B>
 __device__ __forceinline__ void csr_graph(const DevCorpus c, const uint32_t g) {
   __shared__ uint32_t s_cnt[CSR_LDS];
   __shared__ uint32_t s_lds[(B / 64)];
-  __shared__ uint32_t s_bad, s_created;
+  __shared__ uint32_t s_created;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   if (build_fits(c, V, E) && !c.redo[g]) return;  // k_build's graph
   uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0, *rc = c.rc + e0;
   const uint32_t *es = c.esrc + e0, *ed = c.edst + e0, *word = c.word + n0;
-  if (threadIdx.x == 0) {
-    s_bad = 0;
-    s_created = 0;
-  }
-  for (uint32_t e = threadIdx.x; e < E; e += B)
-    if (es[e] >= V || ed[e] >= V) s_bad = 1;
-  __syncthreads();
-  if (s_bad) {
+  if (threadIdx.x == 0) s_created = 0;  // first read after the barrier below
+  bool bad = false;
+  for (uint32_t e = threadIdx.x; e < E; e += B) bad |= es[e] >= V || ed[e] >= V;
+  if (__syncthreads_or(bad)) {  // block-wide OR: no shared flag to reset racily
     if (threadIdx.x == 0) c.err[g] = NEMO_ERR_INVALID;
     return;
   }

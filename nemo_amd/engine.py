@@ -52,6 +52,7 @@ def lib():
         P = ctypes.POINTER
         sig = {
             "nemo_abi_version": ([], i32),
+            "nemo_partition_runs": ([vp, u32, vp], i32),
             "nemo_ctx_create": ([i32, P(vp)], i32),
             "nemo_ctx_destroy": ([vp], None),
             "nemo_last_error": ([vp], ctypes.c_char_p),
@@ -70,6 +71,8 @@ def lib():
             "nemo_prototypes": ([vp, vp, sz, P(u32), vp, P(u32), vp, P(u32)], i32),
             "nemo_missing_from": ([vp, u32, vp, u32, vp, P(u32)], i32),
             "nemo_diffprov": ([vp, vp, sz, i32], i32),
+            "nemo_diffprov_labels": ([vp, vp, sz, vp, u64], i32),
+            "nemo_goal_labels": ([vp, u32, i32, vp, u64], i32),
             "nemo_fetch_diff_mask": ([vp, u32, vp, u64], i32),
             "nemo_fetch_missing": ([vp, vp, u64, P(u64)], i32),
             "nemo_fetch_diff_masks": ([vp, vp, u64], i32),
@@ -85,6 +88,7 @@ def lib():
             "nemo_reduce_interpret": ([vp, u32, u32, P(u32), vp, P(u32), vp, P(u32)], i32),
             "nemo_pulled_count": ([vp, u32], u64),
             "nemo_fetch_pulled": ([vp, u32, vp, vp, u64, P(u64)], i32),
+            "nemo_fetch_pulled_all": ([vp, vp, vp, vp, vp, u64, P(u64)], i32),
             "nemo_timings": ([vp, vp, u32, P(u32)], i32),
             "nemo_reset_timings": ([vp], i32),
             "nemo_synchronize": ([vp], i32),
@@ -192,6 +196,15 @@ class Engine:
     def diffprov(self, failed: Sequence[int], mode: int = 0) -> None:
         f = np.ascontiguousarray(failed, dtype=np.uint32)
         self._chk(self.L.nemo_diffprov(self.h, _p(f), len(f), mode))
+
+    def goal_labels(self, iteration: int, cond: int, d_out_ptr: int, cap: int) -> None:
+        """nemo_goal_labels: [n, label...] of a run's goal labels into device memory."""
+        self._chk(self.L.nemo_goal_labels(self.h, iteration, cond, ctypes.c_void_p(d_out_ptr), cap))
+
+    def diffprov_labels(self, failed: Sequence[int], d_labels_ptr: int, cap: int) -> None:
+        """nemo_diffprov_labels: reference-mode diff with a (broadcast) device label set."""
+        f = np.ascontiguousarray(failed, dtype=np.uint32)
+        self._chk(self.L.nemo_diffprov_labels(self.h, _p(f), len(f), ctypes.c_void_p(d_labels_ptr), cap))
 
     def triggers(self) -> None:
         self._chk(self.L.nemo_triggers(self.h))
@@ -313,6 +326,17 @@ class Engine:
         self._chk(self.L.nemo_fetch_pulled(self.h, slot, _p(s), _p(d), n.value, ctypes.byref(n)))
         return s[:n.value], d[:n.value]
 
+    def pulled_all(self, n_slots: int):
+        """(off[n_slots], cnt[n_slots], src, dst) of the last pull in one call (nemo_fetch_pulled_all)."""
+        off = np.zeros(max(n_slots, 1), np.uint64)
+        cnt = np.zeros(max(n_slots, 1), np.uint32)
+        n = ctypes.c_uint64()
+        self._chk(self.L.nemo_fetch_pulled_all(self.h, _p(off), _p(cnt), None, None, 0, ctypes.byref(n)))
+        src = np.zeros(max(n.value, 1), np.uint32)
+        dst = np.zeros(max(n.value, 1), np.uint32)
+        self._chk(self.L.nemo_fetch_pulled_all(self.h, None, None, _p(src), _p(dst), n.value, ctypes.byref(n)))
+        return off[:n_slots], cnt[:n_slots], src[:n.value], dst[:n.value]
+
     def debug_copy(self, name: str, offset: int, nbytes: int) -> np.ndarray:
         out = np.zeros(max(nbytes, 1), np.uint8)
         self._chk(self.L.nemo_debug_copy(self.h, name.encode(), _p(out), offset, nbytes))
@@ -375,7 +399,8 @@ def analyze(corpus: Corpus, success: Sequence[int], failed: Sequence[int], diff_
     pulled = None
     if pulls:
         eng.pull(1)
-        pulled = [eng.pulled(g) for g in range(corpus.n_graphs)]
+        off, cnt, src, dst = eng.pulled_all(corpus.n_graphs)
+        pulled = [(src[int(a):int(a) + int(n)], dst[int(a):int(a) + int(n)]) for a, n in zip(off, cnt)]
     has0 = 0 in set(int(x) for x in corpus.iteration)
     masks = np.stack([eng.diff_mask(e) for e in range(len(failed))]) if (has0 and len(failed)) else np.zeros((0, 0))
     pre, post, asy = eng.trigger_rows()

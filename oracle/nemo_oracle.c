@@ -491,14 +491,20 @@ static int cmp_u32x3(const void *a, const void *b) {
 }
 
 /* differential provenance for one entry (graphing/differential-provenance.go:22-146) */
-static void diff_entry(const graph_t *g0, const graph_t *gf, uint8_t *D, uint32_t entry, nemo_missing **miss,
-                       uint64_t *nmiss, uint64_t *capmiss) {
+/* gf == NULL: failGoals is the given label set (the sharded reference mode's
+ * broadcast of failedRuns[0]'s labels, same set by construction) */
+static void diff_entry(const graph_t *g0, const graph_t *gf, const uint32_t *set, uint32_t n_set, uint8_t *D,
+                       uint32_t entry, nemo_missing **miss, uint64_t *nmiss, uint64_t *capmiss) {
   const uint32_t V = g0->V;
   /* failGoals = collect(failed.label) over (failed:Goal{run: F, condition:'post'}) (:23-24) */
   uint32_t nl = 0;
-  uint32_t *L = malloc(((size_t)gf->V + 1) * sizeof *L);
-  for (uint32_t v = 0; v < gf->V; v++)
-    if (!IS_RULE(gf->word[v])) L[nl++] = gf->label[v];
+  uint32_t *L = malloc(((size_t)(gf ? gf->V : n_set) + 1) * sizeof *L);
+  if (gf) {
+    for (uint32_t v = 0; v < gf->V; v++)
+      if (!IS_RULE(gf->word[v])) L[nl++] = gf->label[v];
+  } else {
+    for (uint32_t i = 0; i < n_set; i++) L[nl++] = set[i];
+  }
   qsort(L, nl, sizeof *L, cmp_u32);
   uint8_t *fw = calloc(V + 1, 1), *bw = calloc(V + 1, 1);
   uint32_t *q = malloc(((size_t)V + 1) * sizeof *q);
@@ -726,13 +732,14 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
     out->diff_mask = calloc((size_t)o->n_failed * g0->V + 1, 1);
     uint64_t capm = 0;
     for (uint32_t e = 0; e < o->n_failed; e++) {
-      uint32_t src = o->diff_mode == NEMO_DIFF_PER_RUN ? o->failed_iters[e] : o->failed_iters[0];
-      int fr = find_run(c, src);
+      uint32_t src = o->diff_mode == NEMO_DIFF_PER_RUN && !o->diff_labels ? o->failed_iters[e] : o->failed_iters[0];
+      int fr = find_run(c, o->diff_labels ? o->failed_iters[e] : src);
       if (fr < 0) {
         oerr(out, NEMO_ERR_NOTFOUND, "unknown failed run %u", src);
         goto done;
       }
-      diff_entry(g0, &gs[2 * fr + 1], out->diff_mask + (size_t)e * g0->V, e, &out->missing, &out->n_missing, &capm);
+      diff_entry(g0, o->diff_labels ? NULL : &gs[2 * fr + 1], o->diff_labels, (uint32_t)o->n_diff_labels,
+                 out->diff_mask + (size_t)e * g0->V, e, &out->missing, &out->n_missing, &capm);
     }
   } else if (out->run0 >= 0) {
     out->v0 = gs[2 * out->run0 + 1].V;

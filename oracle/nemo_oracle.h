@@ -34,6 +34,9 @@ typedef struct oracle_opts {
   size_t n_failed;
   int diff_mode;                  /* NEMO_DIFF_REFERENCE / NEMO_DIFF_PER_RUN     */
   int skip_pulls;                 /* 1: do not materialise simplified edge lists */
+  const uint32_t *diff_labels;    /* non-NULL: failGoals label set of every diff entry
+                                     (sharded reference mode: failedRuns[0]'s labels) */
+  size_t n_diff_labels;
 } oracle_opts;
 
 typedef struct oracle_out {

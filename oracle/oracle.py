@@ -67,6 +67,8 @@ class COpts(ctypes.Structure):
         ("n_failed", ctypes.c_size_t),
         ("diff_mode", ctypes.c_int),
         ("skip_pulls", ctypes.c_int),
+        ("diff_labels", ctypes.c_void_p),
+        ("n_diff_labels", ctypes.c_size_t),
     ]
 
 
@@ -129,13 +131,16 @@ class OracleResult:
 
 
 def analyze(corpus: Corpus, success: Sequence[int], failed: Sequence[int], diff_mode: int = 0,
-            threads: int = 1, skip_pulls: bool = False) -> OracleResult:
+            threads: int = 1, skip_pulls: bool = False, diff_labels: Optional[Sequence[int]] = None) -> OracleResult:
+    """diff_labels: failGoals label set of every diff entry (the sharded reference mode's broadcast set)."""
     L = lib()
     cs = corpus.c_struct()
     s = np.asarray(success, dtype=np.uint32)
     f = np.asarray(failed, dtype=np.uint32)
+    dl = None if diff_labels is None else np.ascontiguousarray(diff_labels, dtype=np.uint32)
+    dbuf = None if dl is None else (dl if len(dl) else np.zeros(1, np.uint32))  # non-NULL even when empty
     o = COpts(threads, s.ctypes.data if len(s) else None, len(s), f.ctypes.data if len(f) else None, len(f),
-              diff_mode, int(skip_pulls))
+              diff_mode, int(skip_pulls), None if dbuf is None else dbuf.ctypes.data, 0 if dl is None else len(dl))
     out = COut()
     rc = L.oracle_analyze(ctypes.byref(cs), ctypes.byref(o), ctypes.byref(out))
     try:

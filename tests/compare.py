@@ -19,10 +19,23 @@ def assert_same(corpus, eng, orc, n_failed: int, check_pulls: bool = True):
         assert np.array_equal(eng.post_rows, orc.post_rows), "post trigger rows differ"
         assert np.array_equal(np.sort(eng.async_rules), np.sort(orc.async_rules)), "async rules differ"
     if check_pulls and eng.pulled is not None:
-        for g in range(corpus.n_graphs):
-            s, d = eng.pulled[g]
-            os_, od = orc.pulled(g)
-            assert sorted(zip(s.tolist(), d.tolist())) == sorted(zip(os_.tolist(), od.tolist())), f"pulled g={g}"
+        G = corpus.n_graphs
+        gi = np.repeat(np.arange(G, dtype=np.int64), [len(s) for s, _ in eng.pulled])
+        es = np.concatenate([s for s, _ in eng.pulled] + [np.zeros(0, np.uint32)])
+        ed = np.concatenate([d for _, d in eng.pulled] + [np.zeros(0, np.uint32)])
+        po = orc.pulled_off.astype(np.int64)
+        og = np.repeat(np.arange(G, dtype=np.int64), np.diff(po))
+        a, b = _edge_multiset(gi, es, ed), _edge_multiset(og, orc.pulled_src, orc.pulled_dst)
+        if not (len(a) == len(b) and np.array_equal(a, b)):
+            bad = next((g for g in range(G) if not np.array_equal(a[a[:, 0] == g], b[b[:, 0] == g])), None)
+            raise AssertionError(f"pulled edge multisets differ (gpu {len(a)} vs oracle {len(b)} edges), first graph {bad}")
+
+
+def _edge_multiset(g, s, d):
+    """(graph, src, dst) rows in a canonical order: the multiset of pulled edges, vectorised."""
+    g, s, d = (np.asarray(x, np.int64) for x in (g, s, d))
+    order = np.lexsort((d, s, g))
+    return np.stack([g[order], s[order], d[order]], 1)
 
 
 def _first_diff(name, a, b):

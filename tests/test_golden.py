@@ -75,5 +75,12 @@ def test_fixture_gpu(name):
         n0 = int(corpus.node_off[2 * r0 + 1])
         for e in range(len(f)):
             assert sorted(ids[n0 + i] for i in np.nonzero(res.diff_mask[e])[0]) == exp["diff"][e]
+        # trigger rows (corrections.go:30-34,121-125), async rules and allAchievedPre (extensions.go:25-67)
+        np0 = int(corpus.node_off[2 * r0])
+        assert sorted([ids[np0 + a], ids[np0 + g], ids[np0 + r]] for a, g, r in res.pre_rows.tolist()) == exp["pre_rows"]
+        assert sorted([ids[n0 + g], ids[n0 + r]] for g, r in res.post_rows.tolist()) == exp["post_rows"]
+        assert sorted(ids[np0 + r] for r in res.async_rules.tolist()) == exp["async"]
+        if len(s):
+            assert (not (eng.protos_finalize(0)["pre_holds"] < corpus.n_runs)) == exp["all_pre"]
     finally:
         eng.close()

@@ -418,6 +418,42 @@ def test_fallback_worklists_stride(eng, fallback):
             eng.set_option(k, 0)
     try:
         _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
+        # the lists really were longer than their grids (k += gridDim.x taken);
+        # sel = [pull list | chains list | load list], G+1 u32 each, count first
+        G = corpus.n_graphs
+        sel = eng.debug_copy("sel", 0, 4 * 3 * (G + 1)).view(np.uint32)
+        n_pull, n_chains, n_load = int(sel[0]), int(sel[G + 1]), int(sel[2 * (G + 1)])
+        assert n_chains > 1024, n_chains
+        if fallback:
+            assert n_load > 2048 and n_pull > 2048, (n_load, n_pull)
     finally:
         for k in keys:
             eng.set_option(k, -1)
+
+
+def test_diff_label_set_mode(eng):
+    # nemo_goal_labels (device label set of failedRuns[0]) -> nemo_diffprov_labels
+    # equals the reference mode's in-place substitution (differential-provenance.go:22-43)
+    import torch
+    from tools import synth
+    corpus, _ = synth.generate(30, target_nodes=2000, p_fault=0.5)
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    assert len(f) >= 2
+    orc = O.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, skip_pulls=True)
+    eng.load(corpus)
+    eng.mark()
+    eng.simplify()
+    cap = corpus.graph_size(2 * corpus.run_index(f[0]) + 1) + 1
+    d = torch.zeros(cap, dtype=torch.int32, device="cuda:0")
+    eng.goal_labels(f[0], 1, d.data_ptr(), cap)
+    eng.synchronize()
+    g = 2 * corpus.run_index(f[0]) + 1
+    n0, n1 = int(corpus.node_off[g]), int(corpus.node_off[g + 1])
+    want = corpus.label[n0:n1][(corpus.node_word[n0:n1] & 0x80000000) == 0]
+    h = d.cpu().numpy().view(np.uint32)
+    assert int(h[0]) == len(want) and sorted(h[1:1 + len(want)].tolist()) == sorted(want.tolist())
+    eng.diffprov_labels(f, d.data_ptr(), cap)
+    assert np.array_equal(eng.diff_masks(len(f)), orc.diff_mask)
+    assert np.array_equal(eng.missing(), orc.missing)
+    with pytest.raises(E.NemoError):
+        eng.goal_labels(f[0], 1, d.data_ptr(), cap - 1)  # capacity below the graph's nodes + 1

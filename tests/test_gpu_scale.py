@@ -1,0 +1,158 @@
+"""GPU parity at BASELINE.json's configuration sizes.
+
+The small cases in test_gpu_parity.py cover every tier and quirk; these run
+the bench workloads themselves (or their deep-graph shape) through the C ABI
+and compare with the CPU oracle, bit-exact:
+
+  C3  the whole 10k-run corpus bench.py times (E ~ 1.5 V), every field incl.
+      edge pulls, both diff modes
+  C5  graphs of 70k-1M nodes at the library's default thresholds: every graph
+      takes the deep tiers (k_chains_glob at V >= 65536, global CSR/Kahn, the
+      u32 wide_pairs hand-over of nemo_stage_simplified)
+  C4  the 100k-run corpus on one context: the run-sharded partial reduction
+      vectors (nemo_partition_runs' LPT shards, run 0 replicated) sum to the
+      single-context vector, and a random sample of runs (flags, chains, table
+      sets, diff masks) equals the oracle on those runs
+
+Reference semantics: preprocessing.go:13-348, prototype.go:9-206,
+differential-provenance.go:18-146 (the oracle's citations).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from nemo_amd import engine as E
+from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE, F_DELETED, F_HOLDS, F_KEPT
+from oracle import oracle as O
+from tests.compare import assert_same
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def _check_staged(eng, corpus, orc):
+    """nemo_stage_simplified / nemo_simplified_view against the oracle (2-bit state + chain pairs)."""
+    eng.stage_simplified()
+    state, off, ht = eng.simplified_view()
+    alive, holds = E.Engine.unpack_state(state, len(orc.flags))
+    assert np.array_equal(alive, (orc.flags & (F_KEPT | F_DELETED)) == F_KEPT)
+    assert np.array_equal(holds, (orc.flags & F_HOLDS) != 0)
+    G = corpus.n_graphs
+    assert len(off) == G + 1 and int(off[-1]) == len(ht) == len(orc.chains)
+    g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
+    k = np.arange(len(ht)) - off[g].astype(np.int64)
+    got = np.stack([g, k, ht[:, 0].astype(np.int64), ht[:, 1].astype(np.int64)], 1)
+    assert np.array_equal(got, orc.chains[:, :4].astype(np.int64))
+
+
+@pytest.mark.timeout(600)
+def test_c3_full_corpus(eng):
+    corpus, _ = synth.generate(10000, threads=THREADS, **synth.CONFIGS["c3"])
+    V, Ed = int(corpus.node_off[-1]), int(corpus.edge_off[-1])
+    assert V > 45_000_000 and 1.4 < Ed / V < 1.6
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    assert len(f) > 100
+    res = E.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, engine=eng, pulls=True)
+    orc = O.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, threads=THREADS)
+    assert_same(corpus, res, orc, len(f))
+    del res
+    _check_staged(eng, corpus, orc)
+    del orc
+    # the bench's per-run diff mode on the same resident corpus
+    eng.diffprov(f, DIFF_PER_RUN)
+    orc = O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN, threads=THREADS, skip_pulls=True)
+    assert np.array_equal(eng.diff_masks(len(f)), orc.diff_mask)
+    assert np.array_equal(eng.missing(), orc.missing)
+
+
+# (runs, nodes per graph, EOT, generator extras): Molly-density deep graphs and C5's ~4 edges per node
+DEEP = {
+    "molly_200k": (4, 200_000, 400, {}),
+    "dense_70k": (2, 70_000, 140, {"body_extra": 6, "nval": 3, "nloc": 4}),
+    "molly_1m": (2, 1_000_000, 2000, {}),
+}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("shape", sorted(DEEP))
+def test_c5_deep_graphs_default_tiers(eng, shape):
+    n, nodes, eot, gen = DEEP[shape]
+    corpus, _ = synth.generate(n, target_nodes=nodes, eot=eot, p_fault=1.0, threads=THREADS, **gen)
+    assert min(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 65536  # every graph on the deep tiers
+    for mode in (DIFF_REFERENCE, DIFF_PER_RUN):
+        s, f = corpus.success_iters(), corpus.failed_iters()
+        res = E.analyze(corpus, s, f, diff_mode=mode, engine=eng, pulls=mode == DIFF_REFERENCE)
+        orc = O.analyze(corpus, s, f, diff_mode=mode, threads=THREADS, skip_pulls=mode != DIFF_REFERENCE)
+        assert_same(corpus, res, orc, len(f), check_pulls=mode == DIFF_REFERENCE)
+    _check_staged(eng, corpus, orc)  # u32 (head, tail) pairs: graphs of >= 65536 nodes
+
+
+def _reduce_vector(eng, success):
+    import torch
+    d = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda:0")
+    eng.protos_partial(success, d.data_ptr())
+    eng.synchronize()
+    return d.cpu().numpy().view(np.uint32).astype(np.int64)
+
+
+@pytest.mark.timeout(900)
+def test_c4_sharded_partials_and_sample(eng):
+    from nemo_amd.shard import shard_layout
+    R, parts = 100_000, 8
+    corpus, _ = synth.generate(R, threads=THREADS, **synth.CONFIGS["c3"])
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    eng.load(corpus)
+    eng.mark()
+    eng.simplify()
+    full = _reduce_vector(eng, s)
+    T = corpus.n_tables
+    assert full[2 * T + 3] == R and full[2 * T] > 0
+    rng = np.random.default_rng(0x4E454D4F)
+    sample = np.unique(np.concatenate([[0], rng.choice(R, 48, replace=False),
+                                       rng.choice([corpus.run_index(x) for x in f], 16, replace=False)]))
+    # per-run results of the sampled runs from the full context
+    flags = {int(r): (eng.flags(2 * int(r), 2 * int(r) + 1), eng.flags(2 * int(r) + 1, 2 * int(r) + 2)) for r in sample}
+    chains = eng.chains()
+    tabs = (eng.run_tables(0)[sample], eng.run_tables(1)[sample])
+    f_sample = [int(corpus.iteration[r]) for r in sample if corpus.status[int(r)] != "success"]
+    eng.diffprov(f_sample, DIFF_PER_RUN)
+    masks = eng.diff_masks(len(f_sample))
+    # the sample against the oracle on a corpus of just those runs
+    sub = corpus.subset(sample)
+    orc = O.analyze(sub, sub.success_iters(), f_sample, diff_mode=DIFF_PER_RUN, threads=THREADS, skip_pulls=True)
+    for i, r in enumerate(sample):
+        a, b = int(sub.node_off[2 * i]), int(sub.node_off[2 * i + 1])
+        c = int(sub.node_off[2 * i + 2])
+        assert np.array_equal(flags[int(r)][0], orc.flags[a:b]), f"pre flags of run {r}"
+        assert np.array_equal(flags[int(r)][1], orc.flags[b:c]), f"post flags of run {r}"
+    gmap = {2 * int(r) + k: 2 * i + k for i, r in enumerate(sample) for k in (0, 1)}
+    mine = chains[np.isin(chains[:, 0], list(gmap))].copy()
+    mine[:, 0] = [gmap[int(g)] for g in mine[:, 0]]
+    assert np.array_equal(mine[np.lexsort((mine[:, 1], mine[:, 0]))], orc.chains)
+    assert np.array_equal(tabs[1], orc.graph_tables)
+    # proto lists depend on the run alone (prototype.go:11-24); rows of failed runs are not computed
+    ok = np.array([corpus.status[int(r)] == "success" for r in sample])
+    assert np.array_equal(tabs[0][ok], orc.proto_bits[ok])
+    assert np.array_equal(masks, orc.diff_mask)
+    # run-sharded partial vectors (bench.py / nemo_ctx_create_node layout) sum to the full one
+    total = np.zeros_like(full)
+    for rank in range(parts):
+        runs, owned = shard_layout(corpus, rank, parts)
+        shard = corpus.subset(runs, owned)
+        eng.load(shard)
+        eng.mark()
+        eng.simplify()
+        own = shard.owned if shard.owned is not None else np.ones(shard.n_runs, np.uint8)
+        succ = [0] + [int(it) for it, o, st in zip(shard.iteration, own, shard.status)
+                      if o and st == "success" and it != 0]
+        total += _reduce_vector(eng, succ)
+    assert np.array_equal(total, full)

@@ -6,7 +6,7 @@ Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python3 bench.py`
   profiles/<tag>_bench.json         the bench line of the unprofiled run
   profiles/<tag>_pmc.md             per-kernel HBM bytes + SQ counters per launch
-  profiles/pmc_<kernel>.json        per-launch HBM traffic that bench.py reports as roofline.traffic
+  profiles/pmc_summary.json         per-launch HBM traffic per kernel (bench.py's roofline.traffic)
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
 FETCH_SIZE tallies 128-B read requests at 64 B (MI355X_MICROARCH.md, HBM
 section), WRITE_SIZE is exact for wide stores.  Other widths are uncalibrated.
@@ -85,11 +85,11 @@ def main():
         b[1] += fk
         b[2] += wk
         b[3] = max(b[3], n)
-    for k, (hbm, fk, wk, n) in base_hbm.items():
-        json.dump({"kernel": k, "workload_nodes": nodes, "hbm_bytes_per_launch": round(hbm),
-                   "fetch_kib": fk, "write_kib": wk, "launches": n, "round": tag,
-                   "rule": "2*FETCH_SIZE + WRITE_SIZE, KiB->bytes (summed over template tiers)"},
-                  open(os.path.join(prof, f"pmc_{k}.json"), "w"), indent=1)
+    summary = {k: {"workload_nodes": nodes, "hbm_bytes_per_launch": round(hbm), "fetch_kib": round(fk, 1),
+                   "write_kib": round(wk, 1), "launches": n, "round": tag}
+               for k, (hbm, fk, wk, n) in sorted(base_hbm.items())}
+    summary["_rule"] = "2*FETCH_SIZE + WRITE_SIZE, KiB->bytes (summed over template tiers)"
+    json.dump(summary, open(os.path.join(prof, "pmc_summary.json"), "w"), indent=1)
     open(os.path.join(prof, f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 

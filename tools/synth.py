@@ -24,6 +24,19 @@ TABLE_NAMES = ["log", "ack", "bcast", "rbcast", "node", "member", "vote", "commi
                "missing_log", "clock", "pre", "post"]
 
 
+# Generator settings of BASELINE.json's synthetic configurations, shared by bench.py
+# and the parity tests at those sizes.
+#   c3: ~5k-node graphs, E ~ 1.5 V (Molly-like bodies of 1-3 atoms give 1.18; body_extra 4 adds 0-8
+#       shared body atoms per rule, which lands at E/V ~ 1.48), EOT 10
+#   c5: deep provenance, ~1M nodes / ~4M edges per graph at EOT 2000 (body goals shared over a small
+#       key space so that 0-12 extra atoms per rule give ~4 edges per node)
+CONFIGS = {
+    "c3": {"target_nodes": 5000, "eot": 10, "body_extra": 4},
+    "c3_molly": {"target_nodes": 5000, "eot": 10, "body_extra": 0},
+    "c5": {"target_nodes": 1_000_000, "eot": 2000, "body_extra": 6, "nval": 3, "nloc": 4},
+}
+
+
 class CParams(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("n_runs", ctypes.c_uint32), ("run_base", ctypes.c_uint32),
                 ("eot", ctypes.c_uint32), ("nloc", ctypes.c_uint32), ("nval", ctypes.c_uint32),
