@@ -454,33 +454,63 @@ static void set_global_block(nemo_ctx *c) {
   c->dc.gblock = c->gblock_force ? c->gblock_force : ((uint64_t)deep * 8u >= c->G && deep ? 1024u : NEMO_BLOCK);
 }
 
-// LDS graph tier caps (device.h): the largest graphs, smallest first, whose
-// staged form fits LDS_TIER_BUDGET, i.e. two workgroups per CU.
+// LDS tiers (device.h Tier): for each tiered kernel, the largest graphs,
+// smallest first, whose image in that kernel's LDS layout fits LDS_TIER_BUDGET,
+// i.e. two workgroups per CU.  Graphs outside a kernel's caps run its
+// global-memory variant.  `graph_lds_max` caps V of every tier (test knob).
 #define LDS_TIER_BUDGET (78u * 1024u)
-static void set_lds_tier(nemo_ctx *c) {
+#define NO_LEVEL_CAP 0xFFFFFFFFu
+typedef uint32_t (*TierBytes)(uint32_t v, uint32_t e, uint32_t l, uint32_t words);
+static Tier fit_tier(nemo_ctx *c, uint64_t vmax, uint64_t emax, uint32_t lcap, TierBytes bytes) {
   std::vector<std::pair<uint32_t, uint32_t>> ve;
   ve.reserve(c->G);
   for (uint32_t g = 0; g < c->G; g++) {
     const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
-    if (v <= std::min<uint64_t>(16384, c->lds_limit) && e <= 65535) ve.push_back({(uint32_t)v, (uint32_t)e});
+    if (v <= std::min<uint64_t>(vmax, c->lds_limit) && e <= emax) ve.push_back({(uint32_t)v, (uint32_t)e});
   }
   std::sort(ve.begin(), ve.end());
-  uint32_t cv = 0, ce = 0, emax = 0;
+  uint32_t cv = 0, ce = 0, em = 0;
   for (auto &x : ve) {
-    emax = std::max(emax, x.second);
-    const uint32_t l = std::min(x.first, 512u);
-    if (lds_tier_bytes(x.first, emax, l, c->W) > LDS_TIER_BUDGET) break;
+    em = std::max(em, x.second);
+    const uint32_t l = std::min(x.first, lcap);
+    if (bytes(x.first, em, l, c->W) > LDS_TIER_BUDGET) break;
     cv = x.first;
-    ce = emax;
+    ce = em;
   }
-  c->dc.lds_v = cv;
-  c->dc.lds_e = ce;
-  c->dc.lds_l = std::min(cv, 512u);
-  c->dc.lds_bytes = cv ? lds_tier_bytes(cv, ce, c->dc.lds_l, c->W) : 0;
-  c->tierV = c->tierE = 0;
-  for (uint32_t g = 0; g < c->G && cv; g++) {
+  Tier t{0, 0, 0, 0};
+  if (!cv) return t;
+  t.v = cv;
+  t.e = ce;
+  t.l = std::min(cv, lcap);
+  t.bytes = bytes(cv, ce, t.l, c->W);
+  return t;
+}
+
+static void set_lds_tier(nemo_ctx *c) {
+  // k_proto_lds: u16 CSR both ways, Kahn order + level offsets (<= 512 levels), node word, two node bytes, chains
+  const Tier tp = fit_tier(c, 16384, 65535, 512u, [](uint32_t v, uint32_t e, uint32_t l, uint32_t w) {
+    return lds_tier_bytes(v, e, l, w);
+  });
+  c->dc.lds_v = tp.v;
+  c->dc.lds_e = tp.e;
+  c->dc.lds_l = tp.l;
+  c->dc.lds_bytes = tp.bytes;
+  // k_marksimp: node word + two node bytes (the edge list stays in registers / HBM); (src << 16 | dst) pairs
+  c->dc.t_ms = fit_tier(c, 16384, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t, uint32_t, uint32_t w) {
+    return marksimp_bytes(v, w);
+  });
+  // k_diff_lds: u16 CSR both ways + rule bitmap + node bits (Kahn order and depths stay in HBM)
+  c->dc.t_diff = fit_tier(c, 16384, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t e, uint32_t l, uint32_t) {
+    return diff_lds_bytes(v, e, l);
+  });
+  // k_pull_lds: forward u16 CSR + per-node counts + flags
+  c->dc.t_pull = fit_tier(c, 16384, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t e, uint32_t, uint32_t) {
+    return pull_lds_bytes(v, e);
+  });
+  c->tierV = c->tierE = 0;  // k_marksimp's graphs (the deferred markConditionHolds)
+  for (uint32_t g = 0; g < c->G && c->dc.t_ms.bytes; g++) {
     const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
-    if (v <= cv && e <= ce) {
+    if (v <= c->dc.t_ms.v && e <= c->dc.t_ms.e) {
       c->tierV += (double)v;
       c->tierE += (double)e;
     }
@@ -797,7 +827,7 @@ int nemo_mark_holds(nemo_ctx *c) {
   const double V = (double)c->V - c->tierV, E = (double)c->E - c->tierE;
   int rc = guard_staged(c);
   if (rc) return rc;
-  const bool defer = c->dc.lds_bytes != 0;
+  const bool defer = c->dc.t_ms.bytes != 0;
   rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, defer, c->stream); });
   if (rc) return rc;
   c->mark_pending = defer;
@@ -1047,7 +1077,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   rc = timed(c, "k_diff", bytes, (double)n_failed * 3 * E0,
              [&] {
                // the Kahn-order relayout only when g0 may fall outside the LDS tier
-               const bool lds = c->dc.lds_bytes && V0 <= c->dc.lds_v && E0 <= c->dc.lds_e && V0 <= c->dc.lds_l;
+               const bool lds = c->dc.t_diff.bytes && V0 <= c->dc.t_diff.v && E0 <= c->dc.t_diff.e;
                nemo::launch_diff(c->dc, a, (uint32_t)n_failed, lds ? 0u : (uint32_t)V0, s);
              });
   if (rc) return rc;

@@ -151,14 +151,22 @@ struct GraphView {
   __device__ __forceinline__ uint32_t outdeg(uint32_t v) const { return fp[v + 1] - fp[v]; }
 };
 
+// One kernel's LDS graph tier: graphs with V <= v, E <= e and nlev <= l are
+// staged by that kernel's LDS variant (bytes = its dynamic LDS; 0 = tier off).
+// Each kernel's image differs, so each has its own caps (api.hip set_lds_tier).
+struct Tier {
+  uint32_t v, e, l, bytes;
+};
+
 // Device-side arrays of a loaded corpus (all graphs concatenated).
 struct DevCorpus {
   uint32_t G, n_runs, n_tables, words, table_pre, table_post;
   uint32_t hcap_limit;                   // largest chain subgraph H* k_chains stages in LDS (test knob)
   uint32_t comp_limit;                   // largest H* component k_chains_big stages in LDS (test knob)
   uint32_t bld_v, bld_e, bld_bytes;      // k_build's LDS caps and image size (0 = tier off)
-  uint32_t lds_v, lds_e, lds_l;          // LDS graph tier caps (V, E, Kahn levels); 0 = tier off
-  uint32_t lds_bytes;                    // dynamic LDS of the tier's kernels
+  uint32_t lds_v, lds_e, lds_l;          // k_proto_lds's LDS tier caps (V, E, Kahn levels); 0 = tier off
+  uint32_t lds_bytes;                    // dynamic LDS of k_proto_lds
+  Tier t_ms, t_diff, t_pull;             // the LDS tiers of k_marksimp, k_diff_lds, k_pull_lds
   uint32_t gblock;                       // workgroup size of the global-tier kernels (256, or 1024 for deep corpora)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
@@ -235,6 +243,19 @@ __host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t
 
 __device__ __forceinline__ bool lds_fits(const DevCorpus &c, uint32_t V, uint32_t E, uint32_t nlev) {
   return c.lds_bytes != 0u && V <= c.lds_v && E <= c.lds_e && nlev <= c.lds_l;
+}
+__host__ __device__ __forceinline__ bool tier_fits(const Tier &t, uint32_t V, uint32_t E, uint32_t nlev) {
+  return t.bytes != 0u && V <= t.v && E <= t.e && nlev <= t.l;
+}
+// LDS images of the other tiered kernels (k_analysis.hip / k_diff.hip carve them)
+__host__ __device__ __forceinline__ uint32_t marksimp_bytes(uint32_t v, uint32_t words) {
+  return lds_align(8u * words) + lds_align(2u * v) + 2u * lds_align(v);
+}
+__host__ __device__ __forceinline__ uint32_t diff_lds_bytes(uint32_t v, uint32_t e, uint32_t l) {
+  return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + lds_align(4u * ((v + 31u) / 32u)) + lds_align(v);
+}
+__host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t e) {
+  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(2u * v) + lds_align(v);
 }
 
 struct LdsGraph {

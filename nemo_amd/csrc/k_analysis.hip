@@ -18,7 +18,7 @@ __global__ __launch_bounds__(B) void k_mark(DevCorpus c, int skip_tier) {
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
-  if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
+  if (skip_tier && tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
   for (uint32_t i = threadIdx.x; i < c.words; i += B) s_tq[i] = 0;
   if (threadIdx.x == 0) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
-  if (skip_tier && lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
+  if (skip_tier && tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
   uint8_t *f = gv.flags;
   for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     uint8_t fl = f[x] & NEMO_F_HOLDS;
@@ -459,9 +459,6 @@ __device__ __forceinline__ void or8(uint8_t *b, uint32_t v, uint32_t bits) {
   atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (v & 3u)));
 }
 
-__host__ __device__ __forceinline__ uint32_t marksimp_bytes(uint32_t v, uint32_t words) {
-  return lds_align(8u * words) + lds_align(2u * v) + 2u * lds_align(v);
-}
 
 __global__ __launch_bounds__(MS_BLOCK) void k_marksimp(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
@@ -469,7 +466,7 @@ __global__ __launch_bounds__(MS_BLOCK) void k_marksimp(DevCorpus c) {
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
-  if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
+  if (!tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V, E = gv.E, W = c.words, tid = threadIdx.x;
   uint8_t *p = dyn;
   uint32_t *tq = (uint32_t *)p;
@@ -677,8 +674,8 @@ void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s) {
     hipLaunchKernelGGL(k_simplify_flags<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
 }
 void launch_marksimp(const DevCorpus &c, hipStream_t s) {
-  if (!c.lds_bytes) return;
-  const uint32_t b = marksimp_bytes(c.lds_v, c.words);
+  if (!c.t_ms.bytes) return;
+  const uint32_t b = c.t_ms.bytes;
   hipFuncSetAttribute((const void *)k_marksimp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
   hipLaunchKernelGGL(k_marksimp, dim3(c.G), dim3(MS_BLOCK), b, s, c);
 }

@@ -22,9 +22,6 @@ struct DiffLds {
   uint32_t *rule;
   uint8_t *bits;
 };
-__host__ __device__ __forceinline__ uint32_t diff_lds_bytes(uint32_t v, uint32_t e, uint32_t l) {
-  return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + lds_align(4u * ((v + 31u) / 32u)) + lds_align(v);
-}
 __device__ __forceinline__ DiffLds diff_carve(void *base, uint32_t V, uint32_t E, uint32_t L) {
   uint8_t *p = (uint8_t *)base;
   DiffLds d;
@@ -42,7 +39,7 @@ __device__ __forceinline__ DiffLds diff_carve(void *base, uint32_t V, uint32_t E
   return d;
 }
 __device__ __forceinline__ bool diff_lds_fits(const DevCorpus &c, const GraphView &gv) {
-  return lds_fits(c, gv.V, gv.E, gv.nlev);
+  return tier_fits(c.t_diff, gv.V, gv.E, gv.nlev);
 }
 
 // failGoals = collect(failed.label) (:23-24): every run-0 post goal whose label
@@ -621,7 +618,7 @@ __device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, c
     return;
   }
   const GraphView gv = c.view(g);
-  if (lds_fits(c, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph or diff entry
+  if (tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph or diff entry
   const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
@@ -709,7 +706,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pull_sel(DevCorpus c, uint32_t s
       need = true;
     } else {
       const GraphView gv = c.view(g);
-      need = !lds_fits(c, gv.V, gv.E, gv.nlev);
+      need = !tier_fits(c.t_pull, gv.V, gv.E, gv.nlev);
     }
   }
   wave_append(need, g, c.sel + 1, c.sel);
@@ -738,9 +735,6 @@ struct PullLds {
   uint16_t *fp, *fc, *cnt;
   uint8_t *fl;
 };
-__host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t e) {
-  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(2u * v) + lds_align(v);
-}
 __device__ __forceinline__ PullLds pull_carve(void *base, uint32_t V, uint32_t E) {
   uint8_t *p = (uint8_t *)base;
   PullLds L;
@@ -763,7 +757,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   const uint32_t g = which == 2 ? a.g0 : slot;
   if (c.err[g]) return;  // k_pull writes the empty slot
   const GraphView gv = c.view(g);
-  if (!lds_fits(c, gv.V, gv.E, gv.nlev)) return;
+  if (!tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V;
   PullLds L = pull_carve(dyn, V, gv.E);
   {
@@ -1044,8 +1038,8 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint
     hipLaunchKernelGGL(k_dprep_scan, dim3(1), dim3(1024), 0, s, c, a);
     hipLaunchKernelGGL(k_dprep_b, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, a);
   }
-  if (c.lds_bytes) {
-    const uint32_t bytes = diff_lds_bytes(c.lds_v, c.lds_e, c.lds_l);
+  if (c.t_diff.bytes) {
+    const uint32_t bytes = c.t_diff.bytes;
     hipFuncSetAttribute((const void *)k_diff_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_diff_lds, dim3(n_entries), dim3(NEMO_BLOCK), bytes, s, c, a);
   }
@@ -1055,8 +1049,8 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint
     hipLaunchKernelGGL(k_diff<NEMO_BLOCK>, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
-  if (c.lds_bytes && slots) {
-    const uint32_t bytes = pull_lds_bytes(c.lds_v, c.lds_e);
+  if (c.t_pull.bytes && slots) {
+    const uint32_t bytes = c.t_pull.bytes;
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
   }

@@ -32,6 +32,10 @@ pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
 
 
+def _say(*a):
+    print("[scale]", *a, flush=True)  # progress for long cases (run with -s)
+
+
 @pytest.fixture(scope="module")
 def eng():
     e = E.Engine(0)
@@ -61,9 +65,13 @@ def test_c3_full_corpus(eng):
     assert V > 45_000_000 and 1.4 < Ed / V < 1.6
     s, f = corpus.success_iters(), corpus.failed_iters()
     assert len(f) > 100
+    _say("c3 generated", V, Ed)
     res = E.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, engine=eng, pulls=True)
+    _say("c3 gpu done")
     orc = O.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, threads=THREADS)
+    _say("c3 oracle done")
     assert_same(corpus, res, orc, len(f))
+    _say("c3 compared")
     del res
     _check_staged(eng, corpus, orc)
     del orc
@@ -93,6 +101,7 @@ def test_c5_deep_graphs_default_tiers(eng, shape):
         res = E.analyze(corpus, s, f, diff_mode=mode, engine=eng, pulls=mode == DIFF_REFERENCE)
         orc = O.analyze(corpus, s, f, diff_mode=mode, threads=THREADS, skip_pulls=mode != DIFF_REFERENCE)
         assert_same(corpus, res, orc, len(f), check_pulls=mode == DIFF_REFERENCE)
+        _say(shape, "mode", mode, "ok")
     _check_staged(eng, corpus, orc)  # u32 (head, tail) pairs: graphs of >= 65536 nodes
 
 
@@ -110,10 +119,12 @@ def test_c4_sharded_partials_and_sample(eng):
     R, parts = 100_000, 8
     corpus, _ = synth.generate(R, threads=THREADS, **synth.CONFIGS["c3"])
     s, f = corpus.success_iters(), corpus.failed_iters()
+    _say("c4 generated", int(corpus.node_off[-1]))
     eng.load(corpus)
     eng.mark()
     eng.simplify()
     full = _reduce_vector(eng, s)
+    _say("c4 full pass")
     T = corpus.n_tables
     assert full[2 * T + 3] == R and full[2 * T] > 0
     rng = np.random.default_rng(0x4E454D4F)
@@ -129,6 +140,7 @@ def test_c4_sharded_partials_and_sample(eng):
     # the sample against the oracle on a corpus of just those runs
     sub = corpus.subset(sample)
     orc = O.analyze(sub, sub.success_iters(), f_sample, diff_mode=DIFF_PER_RUN, threads=THREADS, skip_pulls=True)
+    _say("c4 sample oracle")
     for i, r in enumerate(sample):
         a, b = int(sub.node_off[2 * i]), int(sub.node_off[2 * i + 1])
         c = int(sub.node_off[2 * i + 2])
@@ -155,4 +167,5 @@ def test_c4_sharded_partials_and_sample(eng):
         succ = [0] + [int(it) for it, o, st in zip(shard.iteration, own, shard.status)
                       if o and st == "success" and it != 0]
         total += _reduce_vector(eng, succ)
+        _say("c4 shard", rank)
     assert np.array_equal(total, full)
