@@ -24,7 +24,7 @@ $(BUILD)/%.host.o: nemo_amd/csrc/%.cpp $(HDRS)
 	$(CXX_HOST) $(HOSTFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -pthread
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -pthread -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # diagnostic build with in-kernel phase stamps (never shipped as libnemohip.so)
 stamps: $(SRCS) $(HDRS)

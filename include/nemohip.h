@@ -117,6 +117,23 @@ int nemo_partition_runs(const nemo_corpus *corpus, uint32_t n_parts, uint32_t *p
  * no 10 s sleep, no Bolt; binds one HIP device.                             */
 typedef struct nemo_ctx nemo_ctx;
 int nemo_ctx_create(int device, nemo_ctx **out);
+/* Node context (SURVEY.md §8b Threading, §8e): one process drives `ndev`
+ * devices (`devices` NULL = 0..ndev-1; ndev <= 0 = every visible device).  The
+ * corpus given to nemo_load_corpus is run-sharded over them with
+ * nemo_partition_runs (run 0 replicated), every entry point fans out over the
+ * shards' streams and returns results in the corpus' global numbering
+ * (graphs, runs, diff entries, pull slots), and the two cross-run exchanges
+ * happen inside the library: the prototype vector is all-reduced with RCCL
+ * (ncclSum over one communicator per device) and the reference diff mode's
+ * failedRuns[0] label set is broadcast (ncclBroadcast) from its owner.  Shards
+ * may share a device (a layout for testing on one GPU): they then exchange by
+ * peer copies instead of RCCL.  nemo_protos_partial/_finalize take d_reduce =
+ * NULL, nemo_set_stream / nemo_goal_labels / nemo_diffprov_labels are for
+ * single-device contexts only.  Replaces InitGraphDB's one database for the
+ * whole node (graphing/helpers.go:17-55; main.go:95 constructs one Neo4J). */
+int nemo_ctx_create_node(int ndev, const int *devices, nemo_ctx **out);
+/* Devices of a context (its shards' devices for a node context); returns the count. */
+int nemo_node_devices(const nemo_ctx *ctx, int *devices, int cap);
 void nemo_ctx_destroy(nemo_ctx *ctx);
 const char *nemo_last_error(const nemo_ctx *ctx);
 int nemo_abi_version(void);
@@ -185,6 +202,10 @@ int nemo_protos_finalize(nemo_ctx *ctx, const uint32_t *d_reduce, uint32_t *achi
  * context or device (nemo_protos_finalize = D2H + this). */
 int nemo_reduce_interpret(const uint32_t *h_reduce, uint32_t n_tables, uint32_t table_post, uint32_t *achieved,
                           uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union);
+/* The context's own (for a node context: the all-reduced) vector to host
+ * memory, nemo_reduce_len() u32: for callers that reduce across processes
+ * themselves from host memory.                                              */
+int nemo_fetch_reduce(nemo_ctx *ctx, uint32_t *out, uint64_t cap);
 /* Single-process convenience: partial + finalize with the context's own buffer. */
 int nemo_prototypes(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
                     uint32_t *achieved, uint32_t *inter, uint32_t *n_inter,

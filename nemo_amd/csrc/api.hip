@@ -16,6 +16,7 @@
 
 #include "device.h"
 #include "internal.h"
+#include "node.h"
 
 namespace {
 
@@ -33,6 +34,7 @@ struct PendingEv {
 }  // namespace
 
 struct nemo_ctx {
+  Node *node = nullptr;  // node context: every entry point dispatches to node.hip
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   std::string err;
@@ -260,6 +262,27 @@ static void sort_rows(uint32_t *rows, uint64_t n) {
     for (int k = 0; k < K; k++) rows[K * i + k] = v[i][k];
 }
 
+// ---- accessors for the node context (node.h) ----
+Node *ctx_node(const nemo_ctx *c) { return c ? c->node : nullptr; }
+nemo_ctx *ctx_new_facade(Node *n) {
+  nemo_ctx *c = new nemo_ctx();
+  c->node = n;
+  return c;
+}
+void ctx_delete_facade(nemo_ctx *c) { delete c; }
+int ctx_fail(nemo_ctx *c, int code, const char *msg) {
+  if (c) c->err = msg;
+  return code;
+}
+uint32_t *ctx_reduce_buf(nemo_ctx *c) { return c->d_red; }
+hipStream_t ctx_stream(nemo_ctx *c) { return c->stream; }
+int ctx_device(const nemo_ctx *c) { return c->device; }
+
+#define DISPATCH(call)              \
+  do {                              \
+    if (c && c->node) return call; \
+  } while (0)
+
 extern "C" {
 
 int nemo_abi_version(void) { return NEMOHIP_ABI_VERSION; }
@@ -346,6 +369,11 @@ static void release_corpus(nemo_ctx *c) {
 
 void nemo_ctx_destroy(nemo_ctx *c) {
   if (!c) return;
+  if (c->node) {
+    node_destroy(c->node);
+    ctx_delete_facade(c);
+    return;
+  }
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   if (c->copy) hipStreamSynchronize(c->copy);
@@ -386,12 +414,14 @@ void nemo_ctx_destroy(nemo_ctx *c) {
 const char *nemo_last_error(const nemo_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
 int nemo_set_stream(nemo_ctx *c, void *stream) {
+  DISPATCH(node_set_stream(c, stream));
   if (!c) return NEMO_ERR_INVALID;
   c->stream = stream ? (hipStream_t)stream : c->own;
   return NEMO_OK;
 }
 
 int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
+  DISPATCH(node_set_option(c, name, value));
   if (!c || !name) return NEMO_ERR_INVALID;
   if (!strcmp(name, "chains_lds_max")) {
     c->hcap_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
@@ -435,13 +465,14 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
 }
 
 int nemo_set_timing(nemo_ctx *c, int enable) {
+  DISPATCH(node_set_timing(c, enable));
   if (!c) return NEMO_ERR_INVALID;
   c->timing = enable != 0;
   return NEMO_OK;
 }
 
-uint64_t nemo_num_nodes(const nemo_ctx *c) { return c ? c->V : 0; }
-uint64_t nemo_num_edges(const nemo_ctx *c) { return c ? c->E : 0; }
+uint64_t nemo_num_nodes(const nemo_ctx *c) { return c ? (c->node ? node_num_nodes(c) : c->V) : 0; }
+uint64_t nemo_num_edges(const nemo_ctx *c) { return c ? (c->node ? node_num_edges(c) : c->E) : 0; }
 
 // Workgroup size of the global-tier kernels: deep corpora (at least one graph
 // in eight over 64k nodes) have few graphs per CU and long per-node passes,
@@ -583,6 +614,7 @@ static int device_load(nemo_ctx *c) {
 }
 
 int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
+  DISPATCH(node_load_corpus(c, in));
   if (!c || !in) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -796,6 +828,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
 }
 
 int nemo_rebuild(nemo_ctx *c) {
+  DISPATCH(node_rebuild(c));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   HIPCHK(c, hipSetDevice(c->device));
@@ -821,6 +854,7 @@ static int ensure_marked(nemo_ctx *c) {
 }
 
 int nemo_mark_holds(nemo_ctx *c) {
+  DISPATCH(node_mark_holds(c));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_mark_holds before nemo_load_corpus");
   HIPCHK(c, hipSetDevice(c->device));
@@ -837,6 +871,7 @@ int nemo_mark_holds(nemo_ctx *c) {
 }
 
 int nemo_simplify(nemo_ctx *c) {
+  DISPATCH(node_simplify(c));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_simplify before nemo_mark_holds");
   HIPCHK(c, hipSetDevice(c->device));
@@ -863,9 +898,10 @@ int nemo_simplify(nemo_ctx *c) {
   return NEMO_OK;
 }
 
-size_t nemo_reduce_len(const nemo_ctx *c) { return c ? 2 * (size_t)c->T + 4 : 0; }
+size_t nemo_reduce_len(const nemo_ctx *c) { return c ? (c->node ? node_reduce_len(c) : 2 * (size_t)c->T + 4) : 0; }
 
 int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *d_red) {
+  DISPATCH(node_protos_partial(c, success_iters, n_success, d_red));
   if (!c || (!success_iters && n_success)) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_protos_partial before nemo_simplify");
   if (!d_red) d_red = c->d_red;  // single-process callers use the context's own vector
@@ -934,6 +970,7 @@ int nemo_reduce_interpret(const uint32_t *red, uint32_t T, uint32_t table_post, 
 int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
                          uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
                          uint32_t *n_runs_total) {
+  DISPATCH(node_protos_finalize(c, d_red, achieved, inter, n_inter, uni, n_union, pre_holds, n_runs_total));
   if (!c) return NEMO_ERR_INVALID;
   if (!d_red) d_red = c->d_red;
   if (!d_red) return fail(c, NEMO_ERR_STATE, "nemo_protos_finalize before nemo_load_corpus");
@@ -951,17 +988,30 @@ int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved,
   return nemo_reduce_interpret(red, T, c->table_post, achieved, inter, n_inter, uni, n_union);
 }
 
+int nemo_fetch_reduce(nemo_ctx *c, uint32_t *out, uint64_t cap) {
+  DISPATCH(node_fetch_reduce(c, out, cap));
+  if (!c || !out) return NEMO_ERR_INVALID;
+  if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "nemo_fetch_reduce before nemo_protos_partial");
+  const uint64_t n = 2 * (uint64_t)c->T + 4;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)n);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_red, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return NEMO_OK;
+}
+
 int nemo_prototypes(nemo_ctx *c, const uint32_t *success_iters, size_t n_success, uint32_t *achieved,
                     uint32_t *inter, uint32_t *n_inter, uint32_t *uni, uint32_t *n_union) {
   if (!c) return NEMO_ERR_INVALID;
   if (n_success == 0)
     return fail(c, NEMO_ERR_INVALID, "no successful runs: extractProtos indexes iterProv[0] (prototype.go:80)");
-  int rc = nemo_protos_partial(c, success_iters, n_success, c->d_red);
+  int rc = nemo_protos_partial(c, success_iters, n_success, nullptr);  // the context's own vector
   if (rc) return rc;
-  return nemo_protos_finalize(c, c->d_red, achieved, inter, n_inter, uni, n_union, nullptr, nullptr);
+  return nemo_protos_finalize(c, nullptr, achieved, inter, n_inter, uni, n_union, nullptr, nullptr);
 }
 
 int nemo_fetch_run_tables(nemo_ctx *c, int which, uint32_t *out, uint64_t cap) {
+  DISPATCH(node_fetch_run_tables(c, which, out, cap));
   if (!c || !out) return NEMO_ERR_INVALID;
   if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "run tables before nemo_protos_partial");
   const uint64_t n = (uint64_t)c->n_runs * c->W;
@@ -974,6 +1024,7 @@ int nemo_fetch_run_tables(nemo_ctx *c, int which, uint32_t *out, uint64_t cap) {
 
 int nemo_missing_from(nemo_ctx *c, uint32_t failed_iter, const uint32_t *proto, uint32_t n_proto, uint32_t *out,
                       uint32_t *n_out) {
+  DISPATCH(node_missing_from(c, failed_iter, proto, n_proto, out, n_out));
   if (!c || (!proto && n_proto)) return NEMO_ERR_INVALID;
   if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "nemo_missing_from before prototypes");
   uint32_t r;
@@ -1093,16 +1144,19 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
 }
 
 int nemo_diffprov(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, int mode) {
+  DISPATCH(node_diffprov(c, failed_iters, n_failed, mode));
   return diffprov_impl(c, failed_iters, n_failed, mode, nullptr, 0);
 }
 
 int nemo_diffprov_labels(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, const uint32_t *d_labels,
                          uint64_t labels_cap) {
+  DISPATCH(node_diffprov_labels(c, failed_iters, n_failed, d_labels, labels_cap));
   if (!d_labels) return c ? fail(c, NEMO_ERR_INVALID, "no label set") : NEMO_ERR_INVALID;
   return diffprov_impl(c, failed_iters, n_failed, NEMO_DIFF_REFERENCE, d_labels, labels_cap);
 }
 
 int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap) {
+  DISPATCH(node_goal_labels(c, iteration, cond, d_out, cap));
   if (!c || !d_out || (cond != 0 && cond != 1)) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   uint32_t r;
@@ -1117,6 +1171,7 @@ int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out,
 }
 
 int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap) {
+  DISPATCH(node_fetch_diff_mask(c, entry, out, cap));
   if (!c || !out) return NEMO_ERR_INVALID;
   if (entry >= c->n_entries) return fail(c, NEMO_ERR_INVALID, "diff entry %u out of range", entry);
   const uint32_t g0 = 2 * c->run0 + 1;
@@ -1129,6 +1184,7 @@ int nemo_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap
 }
 
 int nemo_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap) {
+  DISPATCH(node_fetch_diff_masks(c, out, cap));
   if (!c || !out) return NEMO_ERR_INVALID;
   if (!c->n_entries) return NEMO_OK;
   const uint32_t g0 = 2 * c->run0 + 1;
@@ -1141,6 +1197,7 @@ int nemo_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap) {
 }
 
 int nemo_diff_masks_view(nemo_ctx *c, const uint8_t **masks, uint64_t *n_entries, uint64_t *v0) {
+  DISPATCH(node_diff_masks_view(c, masks, n_entries, v0));
   if (!c || !masks) return NEMO_ERR_INVALID;
   *masks = nullptr;
   if (n_entries) *n_entries = c->n_entries;
@@ -1154,6 +1211,7 @@ int nemo_diff_masks_view(nemo_ctx *c, const uint8_t **masks, uint64_t *n_entries
 }
 
 int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n_out) {
+  DISPATCH(node_fetch_missing(c, out, cap, n_out));
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   uint32_t n = 0;
@@ -1184,6 +1242,7 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
 }
 
 int nemo_triggers(nemo_ctx *c) {
+  DISPATCH(node_triggers(c));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_triggers before nemo_mark_holds");
   if (int rm = ensure_marked(c)) return rm;
@@ -1233,6 +1292,7 @@ static int trig_sync(nemo_ctx *c) {
 int nemo_fetch_triggers(nemo_ctx *c, uint32_t *pre, uint64_t pre_cap, uint64_t *n_pre, uint32_t *post,
                         uint64_t post_cap, uint64_t *n_post, uint32_t *async_rules, uint64_t async_cap,
                         uint64_t *n_async) {
+  DISPATCH(node_fetch_triggers(c, pre, pre_cap, n_pre, post, post_cap, n_post, async_rules, async_cap, n_async));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->trig_done) return fail(c, NEMO_ERR_STATE, "nemo_fetch_triggers before nemo_triggers");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1259,6 +1319,7 @@ int nemo_fetch_triggers(nemo_ctx *c, uint32_t *pre, uint64_t pre_cap, uint64_t *
 }
 
 int nemo_fetch_node_flags(nemo_ctx *c, uint32_t g_lo, uint32_t g_hi, uint8_t *out, uint64_t cap) {
+  DISPATCH(node_fetch_node_flags(c, g_lo, g_hi, out, cap));
   if (!c || !out || g_lo > g_hi || g_hi > c->G) return NEMO_ERR_INVALID;
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "no flags before nemo_mark_holds");
   const uint64_t a = c->node_off[g_lo], b = c->node_off[g_hi];
@@ -1273,6 +1334,7 @@ int nemo_fetch_node_flags(nemo_ctx *c, uint32_t g_lo, uint32_t g_hi, uint8_t *ou
 }
 
 int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_out) {
+  DISPATCH(node_fetch_chains(c, out, cap, n_out));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "no chains before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1341,6 +1403,7 @@ static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
 }
 
 int nemo_stage_simplified(nemo_ctx *c) {
+  DISPATCH(node_stage_simplified(c));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_stage_simplified before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1374,6 +1437,7 @@ int nemo_stage_simplified(nemo_ctx *c) {
 
 int nemo_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **chain_off, const uint32_t **chain_ht,
                          uint64_t *n_chains, int *wide_pairs) {
+  DISPATCH(node_simplified_view(c, state, chain_off, chain_ht, n_chains, wide_pairs));
   if (!c) return NEMO_ERR_INVALID;
   if (!c->staged) return fail(c, NEMO_ERR_STATE, "nothing staged: call nemo_stage_simplified");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1449,6 +1513,7 @@ static int pull_sync(nemo_ctx *c) {
 }
 
 int nemo_pull_edges(nemo_ctx *c, int which) {
+  DISPATCH(node_pull_edges(c, which));
   if (!c || which < 0 || which > 2) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
@@ -1506,12 +1571,14 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
 }
 
 uint64_t nemo_pulled_count(nemo_ctx *c, uint32_t slot) {
+  DISPATCH(node_pulled_count(c, slot));
   if (!c || c->pull_which < 0 || slot >= c->pull_slots) return 0;
   if (pull_sync(c)) return 0;
   return c->h_pcnt[slot];
 }
 
 int nemo_fetch_pulled(nemo_ctx *c, uint32_t slot, uint32_t *src, uint32_t *dst, uint64_t cap, uint64_t *n_out) {
+  DISPATCH(node_fetch_pulled(c, slot, src, dst, cap, n_out));
   if (!c) return NEMO_ERR_INVALID;
   if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
   if (slot >= c->pull_slots) return fail(c, NEMO_ERR_INVALID, "slot %u out of range", slot);
@@ -1532,6 +1599,7 @@ int nemo_fetch_pulled(nemo_ctx *c, uint32_t slot, uint32_t *src, uint32_t *dst, 
 
 int nemo_fetch_pulled_all(nemo_ctx *c, uint64_t *off, uint32_t *cnt, uint32_t *src, uint32_t *dst, uint64_t cap,
                           uint64_t *n_used) {
+  DISPATCH(node_fetch_pulled_all(c, off, cnt, src, dst, cap, n_used));
   if (!c) return NEMO_ERR_INVALID;
   if (c->pull_which < 0) return fail(c, NEMO_ERR_STATE, "nothing pulled");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1553,6 +1621,7 @@ int nemo_fetch_pulled_all(nemo_ctx *c, uint64_t *off, uint32_t *cnt, uint32_t *s
 
 // Debug/inspection: copy `bytes` bytes at byte `offset` of an internal device array.
 int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, uint64_t bytes) {
+  DISPATCH(node_debug_copy(c, name, out, offset, bytes));
   if (!c || !name || !out) return NEMO_ERR_INVALID;
   const void *base = nullptr;
   const std::string n(name);
@@ -1580,6 +1649,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
 }
 
 int nemo_synchronize(nemo_ctx *c) {
+  DISPATCH(node_synchronize(c));
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1587,6 +1657,7 @@ int nemo_synchronize(nemo_ctx *c) {
 }
 
 int nemo_timings(nemo_ctx *c, nemo_timing *out, uint32_t cap, uint32_t *n_out) {
+  DISPATCH(node_timings(c, out, cap, n_out));
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   for (auto &p : c->pending) {
@@ -1619,6 +1690,7 @@ int nemo_timings(nemo_ctx *c, nemo_timing *out, uint32_t cap, uint32_t *n_out) {
 }
 
 int nemo_reset_timings(nemo_ctx *c) {
+  DISPATCH(node_reset_timings(c));
   if (!c) return NEMO_ERR_INVALID;
   uint32_t n;
   int rc = nemo_timings(c, nullptr, 0, &n);

@@ -234,10 +234,12 @@ __host__ __device__ __forceinline__ uint32_t hash_label(uint32_t x) {
   x *= 0x9E3779B1u;
   return x ^ (x >> 15);
 }
-// accepted @next chains of a tier graph held in LDS (head + per-tail list link)
+// accepted @next chains of a tier graph held in LDS as (head, tail) u16 pairs
 __host__ __device__ __forceinline__ uint32_t lds_chain_cap(uint32_t v) { return v / 4u < 32766u ? v / 4u : 32766u; }
+// k_proto_lds's image: forward u16 CSR, Kahn order, level offsets, u16 node
+// word, flags + SB bytes, table bitsets, chain (head, tail) pairs
 __host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t e, uint32_t l, uint32_t words) {
-  return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + 2u * lds_align(2u * v) + lds_align(2u * (l + 1u)) +
+  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + 2u * lds_align(2u * v) + lds_align(2u * (l + 1u)) +
          2u * lds_align(v) + lds_align(8u * words) + 2u * lds_align(2u * lds_chain_cap(v));
 }
 
@@ -258,29 +260,26 @@ __host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t
   return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(2u * v) + lds_align(v);
 }
 
-struct LdsGraph {
-  uint16_t *rp, *rc, *fp, *fc, *topo, *lv, *nw;
-  uint16_t *chd, *cnx;  // chain head, next chain with the same tail (0x7FFF ends)
-  uint8_t *a, *b;       // two bytes of per-node state
+struct ProtoLds {
+  uint16_t *fp, *fc, *topo, *lv, *nw;
+  uint16_t *chd, *ctl;  // chain head, chain tail (bit 15: reach pushed)
+  uint8_t *a, *b;       // flags, SB_* bits
   uint32_t *words;      // 2 * c.words u32 of table bitsets
 };
 
-// Carve the tier's dynamic LDS for a graph of V nodes / E edges / L levels.
-__device__ __forceinline__ LdsGraph lds_carve(void *base, uint32_t V, uint32_t E, uint32_t L, uint32_t words) {
+// Carve k_proto_lds's dynamic LDS for a graph of V nodes / E edges / L levels.
+__device__ __forceinline__ ProtoLds proto_carve(void *base, uint32_t V, uint32_t E, uint32_t L, uint32_t words,
+                                                uint32_t chain_cap) {
   uint8_t *p = (uint8_t *)base;
-  LdsGraph g;
+  ProtoLds g;
   g.chd = (uint16_t *)p;
-  p += lds_align(2u * lds_chain_cap(V));
-  g.cnx = (uint16_t *)p;
-  p += lds_align(2u * lds_chain_cap(V));
+  p += lds_align(2u * chain_cap);
+  g.ctl = (uint16_t *)p;
+  p += lds_align(2u * chain_cap);
   g.words = (uint32_t *)p;
   p += lds_align(8u * words);
-  g.rp = (uint16_t *)p;
-  p += lds_align(2u * (V + 1u));
   g.fp = (uint16_t *)p;
   p += lds_align(2u * (V + 1u));
-  g.rc = (uint16_t *)p;
-  p += lds_align(2u * E);
   g.fc = (uint16_t *)p;
   p += lds_align(2u * E);
   g.topo = (uint16_t *)p;

@@ -119,6 +119,10 @@ __global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier
   if (threadIdx.x == 0) c.holdany[g] = s_hold;
 }
 
+__device__ __forceinline__ void or8(uint8_t *b, uint32_t v, uint32_t bits) {
+  atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (v & 3u)));
+}
+
 // k_proto_lds takes the graphs within the LDS tier (and its chain cap)
 #define LCH_END 0x7FFFu
 __device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphView &gv) {
@@ -267,11 +271,24 @@ __global__ __launch_bounds__(B) void k_proto(DevCorpus c) {
   if (threadIdx.x == 0) c.gate[r] = gate ? 1 : 0;
 }
 
-// k_proto's LDS tier: the same phases over the post graph staged in LDS
-// (device.h LdsGraph).  Node byte a = flags, byte b = SB_* bits with bit 7 =
-// rule.  Tables are added in coalesced passes over the node words, so the
-// level sweep never leaves LDS; chain lists stay in HBM (read at tails only).
+// k_proto's LDS tier, push form: every phase propagates along forward rows
+// only, so LDS holds the forward u16 CSR, Kahn order + level offsets, the u16
+// node word, the flags byte, an SB_* byte per node and the graph's chains as
+// (head, tail) u16 pairs -- no reverse CSR and no per-tail chain lists
+// (device.h proto_lds_bytes, ~11 B/node + 2 B/edge).  The same predicates as
+// k_proto's pull form:
+//   ROOT  goal, not deleted, no REG or TAIL parent        (push SB_NR from REG/TAIL rules)
+//   R1    REG/HEAD rule with a ROOT parent                  (push from ROOT goals)
+//   G2    live goal below an R1 REG rule or below the tail of a chain with an R1 head
+//   RCH   Kahn-level sweep: live G2/RCH goals reach their REG/HEAD rule children,
+//         RCH REG rules their live goal children, an RCH head its chain's tail's
+//         live goal children (chains are rescanned each level until their head is
+//         reached; the tail's children lie two levels below the head or deeper)
+// Per-node bits are ORed with LDS atomics (or8): pushes from different threads
+// meet in the same bytes.
 #define PROTO_BLOCK 512
+#define SB_NR 0x20u      // goal has a REG or TAIL parent (not a root)
+#define PCH_DONE 0x8000u // chain tail word: the head's reach was pushed
 __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
   const uint32_t r = blockIdx.x;
@@ -281,151 +298,121 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   if (!proto_lds_fits(c, gv)) return;
   const uint32_t V = gv.V, W = c.words, tid = threadIdx.x;
   STAMP(0);
-  LdsGraph L = lds_carve(dyn, V, gv.E, gv.nlev, W);
+  const uint32_t nch = c.nch[g];
+  ProtoLds L = proto_carve(dyn, V, gv.E, gv.nlev, W, lds_chain_cap(V));
   uint32_t *s_s = L.words, *s_t = L.words + W;
   const uint32_t *ch = c.chain + 5 * gv.n0;
-  const uint32_t *tf = c.tail_first + gv.n0, *nt = c.chain_nt + gv.n0;
-  const uint32_t nch = c.nch[g];
   for (uint32_t i = tid; i < 2 * W; i += PROTO_BLOCK) L.words[i] = 0;
   {
-    const StageDesc d[9] = {{gv.rp, L.rp, V + 1, ST_U16},  {gv.fp, L.fp, V + 1, ST_U16},
-                            {gv.rc, L.rc, gv.E, ST_U16},   {gv.fc, L.fc, gv.E, ST_U16},
-                            {gv.topo, L.topo, V, ST_U16},  {gv.lvl, L.lv, gv.nlev + 1, ST_U16},
-                            {gv.word, L.nw, V, ST_WORD},   {gv.flags, L.a, V, ST_U8},
-                            {nt, L.cnx, nch, ST_U16}};
-    stage_lds<9, PROTO_BLOCK>(d);
+    const StageDesc d[6] = {{gv.fp, L.fp, V + 1, ST_U16},         {gv.fc, L.fc, gv.E, ST_U16},
+                            {gv.topo, L.topo, V, ST_U16},         {gv.lvl, L.lv, gv.nlev + 1, ST_U16},
+                            {gv.word, L.nw, V, ST_WORD},          {gv.flags, L.a, V, ST_U8}};
+    stage_lds<6, PROTO_BLOCK>(d);
   }
-  __syncthreads();
-  STAMP(1);
   for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
     L.chd[k] = (uint16_t)ch[5 * k];
-    const uint32_t nx = L.cnx[k];
-    L.cnx[k] = (uint16_t)(nx < nch ? nx : LCH_END);
+    L.ctl[k] = (uint16_t)ch[5 * k + 1];
   }
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) L.b[x] = 0;
+  for (uint32_t x4 = tid; x4 < (V + 3) / 4; x4 += PROTO_BLOCK) ((uint32_t *)L.b)[x4] = 0;
   // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
   const bool gt = c.holdany[g - 1] != 0;
   __syncthreads();
-  // a tail's node word carries the first chain of its list (tails are read only through the list)
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK)
-    if (L.a[x] & NEMO_F_TAIL) {
-      const uint32_t k = tf[x];
-      L.nw[x] = (uint16_t)(NW_RULE | (k == NEMO_NONE ? LCH_END : k));
-    }
-  __syncthreads();
-  STAMP(2);
+  STAMP(1);
   const uint8_t *f = L.a;
   uint8_t *sb = L.b;
 #define LRULE(v) ((L.nw[v] & NW_RULE) != 0)
+#define LTAB(v) (L.nw[v] & NW_TABLE)
 #define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
 #define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+#define RULEISH(v) (REG(v) || (f[v] & NEMO_F_HEAD))
 #define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
-#define TAIL_ANY(p, bit, out)                                                                  \
-  for (uint32_t k_ = L.nw[p] & LCH_END, n_ = 0; k_ < nch && n_ < nch && !(out); k_ = L.cnx[k_], n_++) \
-    if (sb[L.chd[k_]] & (bit)) out = true;
+#define SET(v, bit) or8(sb, (v), (bit))
+  // missingFrom's table set; not-root marks; goals with a rule child (HASRC)
   for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    const uint32_t j0 = L.fp[x], j1 = L.fp[x + 1];
     if (LRULE(x)) {
-      if (REG(x) || (f[x] & NEMO_F_HEAD)) ADD(s_t, L.nw[x] & NW_TABLE);
+      if (RULEISH(x)) ADD(s_t, LTAB(x));
+      if (REG(x) || (f[x] & NEMO_F_TAIL))
+        for (uint32_t j = j0; j < j1; j++) SET(L.fc[j], SB_NR);
     } else if (!DEL(x)) {
-      bool root = true, hasrc = false;
-      for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) {
-        const uint32_t p = L.rc[j];
-        if (REG(p) || (f[p] & NEMO_F_TAIL)) root = false;
-      }
-      for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
-        const uint32_t q = L.fc[j];
-        if (REG(q) || (f[q] & NEMO_F_HEAD)) hasrc = true;
-      }
-      sb[x] = (root ? SB_ROOT : 0) | (hasrc ? SB_HASRC : 0);
+      bool hasrc = false;
+      for (uint32_t j = j0; j < j1 && !hasrc; j++) hasrc = RULEISH(L.fc[j]);
+      if (hasrc) SET(x, SB_HASRC);
     }
+  }
+  __syncthreads();
+  STAMP(2);
+  // R1: REG/HEAD rule children of roots
+  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
+    if (LRULE(x) || DEL(x) || (sb[x] & SB_NR)) continue;
+    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
+      if (RULEISH(L.fc[j])) SET(L.fc[j], SB_R1);
   }
   __syncthreads();
   STAMP(3);
-  // R1: rule children of roots (regular rules, and collapsed rules via their head)
+  // G2 below R1 rules (regular, and collapsed through their chain's tail), with
+  // the R1 tables whose rule has a goal child that has a rule child
   for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
-    if (!LRULE(x) || !(REG(x) || (f[x] & NEMO_F_HEAD))) continue;
-    bool r1 = false;
-    for (uint32_t j = L.rp[x]; j < L.rp[x + 1]; j++) {
-      const uint32_t p = L.rc[j];
-      if (!DEL(p) && (sb[p] & SB_ROOT)) r1 = true;
+    if (!LRULE(x) || !REG(x) || !(sb[x] & SB_R1)) continue;
+    bool add = false;
+    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
+      const uint32_t q = L.fc[j];
+      if (DEL(q)) continue;
+      SET(q, SB_G2);
+      add |= (sb[q] & SB_HASRC) != 0;
     }
-    if (!r1) continue;
-    sb[x] |= SB_R1;
-    if (REG(x)) {
-      for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
-        const uint32_t q = L.fc[j];
-        if (!DEL(q) && (sb[q] & SB_HASRC)) {
-          ADD(s_s, L.nw[x] & NW_TABLE);
-          break;
-        }
-      }
+    if (add) ADD(s_s, LTAB(x));
+  }
+  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
+    const uint32_t h = L.chd[k], t = L.ctl[k];
+    if (!(sb[h] & SB_R1)) continue;
+    bool add = false;
+    for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) {
+      const uint32_t q = L.fc[j];
+      if (DEL(q)) continue;
+      SET(q, SB_G2);
+      add |= (sb[q] & SB_HASRC) != 0;
     }
+    if (add) ADD(s_s, LTAB(h));
   }
   __syncthreads();
   STAMP(4);
-  // G2: goal children of R1 rules; collapsed R1 rules that have a goal child with a rule child
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
-    if (LRULE(x) || DEL(x)) continue;
-    bool g2 = false;
-    for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !g2; j++) {
-      const uint32_t p = L.rc[j];
-      if (REG(p)) {
-        g2 = (sb[p] & SB_R1) != 0;
-      } else if (f[p] & NEMO_F_TAIL) {
-        TAIL_ANY(p, SB_R1, g2);
-      }
-    }
-    if (g2) sb[x] |= SB_G2;
-  }
-  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-    const uint32_t h = L.chd[k];
-    if (!(sb[h] & SB_R1)) continue;
-    const uint32_t t = ch[5 * k + 1];
-    for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) {
-      const uint32_t q = L.fc[j];
-      if (!DEL(q) && (sb[q] & SB_HASRC)) {
-        ADD(s_s, L.nw[h] & NW_TABLE);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  STAMP(5);
-  // rules reachable from G2 (forward level sweep over graph'), all in LDS
+  // rules reachable from G2: one barrier per Kahn level; a node's own bits are
+  // final when its level starts (every parent lies on an earlier level)
   for (uint32_t l = 0; l < gv.nlev; l++) {
     const uint32_t e = L.lv[l + 1];
     for (uint32_t i = L.lv[l] + tid; i < e; i += PROTO_BLOCK) {
       const uint32_t x = L.topo[i];
-      bool rch = false;
+      const uint32_t bx = sb[x];
       if (!LRULE(x)) {
-        if (DEL(x)) continue;
-        for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !rch; j++) {
-          const uint32_t p = L.rc[j];
-          if (REG(p)) {
-            rch = (sb[p] & SB_RCH) != 0;
-          } else if (f[p] & NEMO_F_TAIL) {
-            TAIL_ANY(p, SB_RCH, rch);
-          }
-        }
-      } else if (REG(x) || (f[x] & NEMO_F_HEAD)) {
-        for (uint32_t j = L.rp[x]; j < L.rp[x + 1] && !rch; j++) {
-          const uint32_t p = L.rc[j];
-          if (!DEL(p) && (sb[p] & (SB_G2 | SB_RCH))) rch = true;
-        }
+        if (DEL(x) || !(bx & (SB_G2 | SB_RCH))) continue;
+        for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
+          if (RULEISH(L.fc[j])) SET(L.fc[j], SB_RCH);
+      } else if (REG(x) && (bx & SB_RCH)) {
+        for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
+          if (!DEL(L.fc[j])) SET(L.fc[j], SB_RCH);
       }
-      if (rch) sb[x] |= SB_RCH;
+    }
+    for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
+      const uint32_t t = L.ctl[k];
+      if ((t & PCH_DONE) || !(sb[L.chd[k]] & SB_RCH)) continue;
+      L.ctl[k] = (uint16_t)(t | PCH_DONE);
+      for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++)
+        if (!DEL(L.fc[j])) SET(L.fc[j], SB_RCH);
     }
     __syncthreads();
   }
   STAMP(6);
-  // tables of the reached rules
+  // tables of the reached rules (RCH is only ever set on REG / HEAD rules and live goals)
   for (uint32_t x = tid; x < V; x += PROTO_BLOCK)
-    if (LRULE(x) && !(f[x] & NEMO_F_TAIL) && (sb[x] & SB_RCH)) ADD(s_s, L.nw[x] & NW_TABLE);
-#undef TAIL_ANY
+    if (LRULE(x) && (sb[x] & SB_RCH)) ADD(s_s, LTAB(x));
 #undef LRULE
+#undef LTAB
 #undef DEL
 #undef REG
+#undef RULEISH
 #undef ADD
+#undef SET
   __syncthreads();
   for (uint32_t i = tid; i < W; i += PROTO_BLOCK) {
     c.proto_bits[(size_t)r * W + i] = gt ? s_s[i] : 0u;
@@ -455,9 +442,6 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
 #define A_GP 0x40u   // kept next rule: a parent goal has a kept next-rule parent
 #define A_GC 0x80u   // kept next rule: a child goal has a kept next-rule child
 
-__device__ __forceinline__ void or8(uint8_t *b, uint32_t v, uint32_t bits) {
-  atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (v & 3u)));
-}
 
 
 __global__ __launch_bounds__(MS_BLOCK) void k_marksimp(DevCorpus c) {

@@ -54,6 +54,8 @@ def lib():
             "nemo_abi_version": ([], i32),
             "nemo_partition_runs": ([vp, u32, vp], i32),
             "nemo_ctx_create": ([i32, P(vp)], i32),
+            "nemo_ctx_create_node": ([i32, vp, P(vp)], i32),
+            "nemo_node_devices": ([vp, vp, i32], i32),
             "nemo_ctx_destroy": ([vp], None),
             "nemo_last_error": ([vp], ctypes.c_char_p),
             "nemo_set_stream": ([vp, vp], i32),
@@ -68,6 +70,7 @@ def lib():
             "nemo_reduce_len": ([vp], sz),
             "nemo_protos_partial": ([vp, vp, sz, vp], i32),
             "nemo_protos_finalize": ([vp, vp, P(u32), vp, P(u32), vp, P(u32), P(u64), P(u32)], i32),
+            "nemo_fetch_reduce": ([vp, vp, u64], i32),
             "nemo_prototypes": ([vp, vp, sz, P(u32), vp, P(u32), vp, P(u32)], i32),
             "nemo_missing_from": ([vp, u32, vp, u32, vp, P(u32)], i32),
             "nemo_diffprov": ([vp, vp, sz, i32], i32),
@@ -109,14 +112,24 @@ def _p(a: Optional[np.ndarray]):
 class Engine:
     """One libnemohip context bound to one HIP device."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
+        """devices: a node context over these devices (nemo_ctx_create_node; repeats allowed)."""
         self.L = lib()
         h = ctypes.c_void_p()
-        rc = self.L.nemo_ctx_create(device, ctypes.byref(h))
+        if devices is None:
+            rc = self.L.nemo_ctx_create(device, ctypes.byref(h))
+        else:
+            d = np.ascontiguousarray(devices, dtype=np.int32)
+            rc = self.L.nemo_ctx_create_node(len(d), d.ctypes.data, ctypes.byref(h))
         if rc != 0:
-            raise NemoError(rc, "nemo_ctx_create failed (no HIP device?)")
+            raise NemoError(rc, "context creation failed (no HIP device?)")
         self.h = h
         self.corpus: Optional[Corpus] = None
+
+    def devices(self) -> List[int]:
+        out = np.zeros(64, np.int32)
+        n = self.L.nemo_node_devices(self.h, out.ctypes.data, 64)
+        return out[:n].tolist()
 
     def close(self) -> None:
         if self.h:
@@ -163,6 +176,13 @@ class Engine:
     def protos_partial(self, success: Sequence[int], d_reduce_ptr: int) -> None:
         s = np.ascontiguousarray(success, dtype=np.uint32)
         self._chk(self.L.nemo_protos_partial(self.h, _p(s), len(s), ctypes.c_void_p(d_reduce_ptr)))
+
+    def reduce_vector(self) -> np.ndarray:
+        """nemo_fetch_reduce: the context's own reduction vector (after protos_partial(.., 0))."""
+        n = self.reduce_len()
+        out = np.zeros(n, np.uint32)
+        self._chk(self.L.nemo_fetch_reduce(self.h, _p(out), n))
+        return out
 
     def protos_finalize(self, d_reduce_ptr: int):
         T = self.corpus.n_tables

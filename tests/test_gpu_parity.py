@@ -457,3 +457,53 @@ def test_diff_label_set_mode(eng):
     assert np.array_equal(eng.missing(), orc.missing)
     with pytest.raises(E.NemoError):
         eng.goal_labels(f[0], 1, d.data_ptr(), cap - 1)  # capacity below the graph's nodes + 1
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0), (0, 0, 0)])
+def test_node_context(devices):
+    # nemo_ctx_create_node: the corpus LPT-sharded over the node context's
+    # shards, run 0 replicated, the prototype vector all-reduced (RCCL for one
+    # device, peer copies when shards share the device), the reference diff's
+    # failedRuns[0] label set broadcast from its owner; every result in the
+    # corpus' global numbering, bit-exact with the oracle
+    from tools import synth
+    corpus, _ = synth.generate(36, target_nodes=1500, p_fault=0.5)
+    e = E.Engine(devices=list(devices))
+    try:
+        assert e.devices() == list(devices)
+        e.set_timing(True)
+        for mode in (DIFF_REFERENCE, DIFF_PER_RUN):
+            _check(e, corpus, mode=mode, pulls=True)
+        s, f = corpus.success_iters(), corpus.failed_iters()
+        orc = O.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, skip_pulls=True)
+        e.diffprov(f, DIFF_REFERENCE)
+        assert np.array_equal(e.diff_masks_view(), orc.diff_mask)
+        # the staged hand-over, reassembled in global node / graph order
+        e.stage_simplified()
+        state, off, ht = e.simplified_view()
+        from nemo_amd.corpus import F_DELETED, F_HOLDS, F_KEPT
+        alive, holds = E.Engine.unpack_state(state, len(orc.flags))
+        assert np.array_equal(alive, (orc.flags & (F_KEPT | F_DELETED)) == F_KEPT)
+        assert np.array_equal(holds, (orc.flags & F_HOLDS) != 0)
+        G = corpus.n_graphs
+        g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
+        k = np.arange(len(ht)) - off[g].astype(np.int64)
+        got = np.stack([g, k, ht[:, 0].astype(np.int64), ht[:, 1].astype(np.int64)], 1)
+        assert np.array_equal(got, orc.chains[:, :4].astype(np.int64))
+        # diff-graph pulls by global entry
+        e.pull(2)
+        g0 = 2 * corpus.run_index(0) + 1
+        e0, e1 = int(corpus.edge_off[g0]), int(corpus.edge_off[g0 + 1])
+        src, dst = corpus.edge_src[e0:e1], corpus.edge_dst[e0:e1]
+        for i in range(len(f)):
+            m = orc.diff_mask[i]
+            want = sorted((int(a), int(b)) for a, b in zip(src, dst) if m[a] and m[b])
+            sp, dp = e.pulled(i)
+            assert sorted(zip(sp.tolist(), dp.tolist())) == want
+        tim = e.timings()
+        assert tim["k_chains"]["launches"] >= len(devices)
+        if len(devices) > 1:
+            with pytest.raises(E.NemoError):
+                e.set_stream(0)
+    finally:
+        e.close()

@@ -6,8 +6,8 @@ and compare with the CPU oracle, bit-exact:
 
   C3  the whole 10k-run corpus bench.py times (E ~ 1.5 V), every field incl.
       edge pulls, both diff modes
-  C5  graphs of 70k-1M nodes at the library's default thresholds: every graph
-      takes the deep tiers (k_chains_glob at V >= 65536, global CSR/Kahn, the
+  C5  graphs of 100k-1M nodes at the library's default thresholds: they take
+      the deep tiers (k_chains_glob at V >= 65536, global CSR/Kahn, the
       u32 wide_pairs hand-over of nemo_stage_simplified)
   C4  the 100k-run corpus on one context: the run-sharded partial reduction
       vectors (nemo_partition_runs' LPT shards, run 0 replicated) sum to the
@@ -85,7 +85,7 @@ def test_c3_full_corpus(eng):
 # (runs, nodes per graph, EOT, generator extras): Molly-density deep graphs and C5's ~4 edges per node
 DEEP = {
     "molly_200k": (4, 200_000, 400, {}),
-    "dense_70k": (2, 70_000, 140, {"body_extra": 6, "nval": 3, "nloc": 4}),
+    "dense_100k": (3, 100_000, 200, {"body_extra": 6, "nval": 3, "nloc": 4}),
     "molly_1m": (2, 1_000_000, 2000, {}),
 }
 
@@ -95,7 +95,10 @@ DEEP = {
 def test_c5_deep_graphs_default_tiers(eng, shape):
     n, nodes, eot, gen = DEEP[shape]
     corpus, _ = synth.generate(n, target_nodes=nodes, eot=eot, p_fault=1.0, threads=THREADS, **gen)
-    assert min(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 65536  # every graph on the deep tiers
+    sizes = [corpus.graph_size(g) for g in range(corpus.n_graphs)]
+    # run 0 and at least one more run on the deep tiers (>= 65536 nodes); dropped messages in failed runs
+    # leave smaller or empty graphs beside them, so the deep and LDS tiers share the launches
+    assert min(sizes[:2]) >= 65536 and sum(v >= 65536 for v in sizes) >= 3 and corpus.failed_iters()
     for mode in (DIFF_REFERENCE, DIFF_PER_RUN):
         s, f = corpus.success_iters(), corpus.failed_iters()
         res = E.analyze(corpus, s, f, diff_mode=mode, engine=eng, pulls=mode == DIFF_REFERENCE)
@@ -106,11 +109,8 @@ def test_c5_deep_graphs_default_tiers(eng, shape):
 
 
 def _reduce_vector(eng, success):
-    import torch
-    d = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda:0")
-    eng.protos_partial(success, d.data_ptr())
-    eng.synchronize()
-    return d.cpu().numpy().view(np.uint32).astype(np.int64)
+    eng.protos_partial(success, 0)  # the context's own vector
+    return eng.reduce_vector().astype(np.int64)
 
 
 @pytest.mark.timeout(900)
