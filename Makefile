@@ -30,7 +30,7 @@ $(LIB): $(OBJS)
 stamps: $(SRCS) $(HDRS)
 	@mkdir -p $(BUILD)/stamps
 	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -DNEMO_STAMPS -c -o $(BUILD)/stamps/$$(basename $$f .hip).o $$f || exit 1; done
-	$(HIPCC) $(HIPFLAGS) -shared -o nemo_amd/libnemohip_stamps.so $(BUILD)/stamps/*.o
+	$(HIPCC) $(HIPFLAGS) -shared -o nemo_amd/libnemohip_stamps.so $(BUILD)/stamps/*.o -pthread -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle

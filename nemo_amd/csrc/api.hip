@@ -59,6 +59,8 @@ struct nemo_ctx {
   uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
+  double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
+  uint32_t big_chunks = 1;           // k_csrb_* workgroups per big graph
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
   DevCorpus dc{};
@@ -608,7 +610,13 @@ static int device_load(nemo_ctx *c) {
   // order (4V) and per-node level (4V); the level offsets are per level
   if ((rc = timed(c, "k_build", 16 * Eb + 20 * Vb, 2 * Eb, [&] { nemo::launch_build(c->dc, c->stream); })))
     return rc;
-  if ((rc = timed(c, "k_csr", 16 * E + 12 * V, E, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
+  // graphs past k_build: k_csr (one workgroup per graph) below NEMO_CSR_BIG nodes, k_csrb_* above
+  const double Eg = std::max(0.0, E - c->bigE), Vg = std::max(0.0, V - c->bigV);
+  if ((rc = timed(c, "k_csr", 16 * Eg + 12 * Vg, Eg, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
+  if (c->dc.n_big &&
+      (rc = timed(c, "k_csrb", 16 * c->bigE + 12 * c->bigV, c->bigE,
+                  [&] { nemo::launch_csr_big(c->dc, c->big_chunks, c->stream); })))
+    return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
   return NEMO_OK;
 }
@@ -718,9 +726,56 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.chain, 5 * V);
   A(d.chain_tmp, 5 * V);
   A(d.nch, G);
-  A(d.sel, 3 * ((size_t)G + 1));
-  A(d.tail_first, V);
-  A(d.chain_nt, V);
+  A(d.sel, 4 * ((size_t)G + 1));
+  {
+    // graphs of NEMO_CSR_BIG nodes or more: the multi-workgroup CSR build's list
+    std::vector<uint32_t> big;
+    uint64_t emax = 0;
+    c->bigV = c->bigE = 0;
+    for (uint32_t g = 0; g < G; g++) {
+      const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+      if (v < NEMO_CSR_BIG) continue;
+      big.push_back(g);
+      emax = std::max(emax, e);
+      c->bigV += (double)v;
+      c->bigE += (double)e;
+    }
+    uint32_t *db = nullptr;
+    A(db, big.size());
+    if (!big.empty()) HIPCHK(c, hipMemcpy(db, big.data(), big.size() * 4, hipMemcpyHostToDevice));
+    d.big = db;
+    d.n_big = (uint32_t)big.size();
+    // the bucketed build's (bucket, chunk) count tables and (key, value) edge scratch
+    d.cb_hist = d.cb_key = d.cb_val = nullptr;
+    d.cb_hoff = nullptr;
+    d.cb_maxbk = d.cb_maxck = 0;
+    std::vector<uint64_t> hoff(big.size() + 1, 0);
+    bool fits = !big.empty();
+    for (size_t b = 0; b < big.size(); b++) {
+      const uint32_t g = big[b];
+      const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+      const uint64_t nbk = (v + 8191) / 8192, nck = (e + 8191) / 8192;
+      fits &= nbk <= CB_MAXB;
+      hoff[b + 1] = hoff[b] + std::max<uint64_t>(nbk * nck, 1);
+      d.cb_maxbk = std::max<uint32_t>(d.cb_maxbk, (uint32_t)nbk);
+      d.cb_maxck = std::max<uint32_t>(d.cb_maxck, (uint32_t)std::max<uint64_t>(nck, 1));
+    }
+    if (fits) {
+      uint64_t *dh = nullptr;
+      A(dh, hoff.size());
+      HIPCHK(c, hipMemcpy(dh, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice));
+      d.cb_hoff = dh;
+      A(d.cb_hist, hoff.back());
+      A(d.cb_key, E);
+      A(d.cb_val, E);
+    }
+    c->big_chunks = (uint32_t)std::min<uint64_t>(128, std::max<uint64_t>(1, (emax + 16383) / 16384));
+    uint64_t vpost = 0;  // k_pg_* chunks: the largest post graph
+    for (uint32_t g = 1; g < G; g += 2) vpost = std::max<uint64_t>(vpost, c->node_off[g + 1] - c->node_off[g]);
+    d.pg_chunks = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, vpost / 16384));
+  }
+  A(d.cl_first, V);
+  A(d.cl_next, V);
   A(d.proto_bits, R * c->W);
   A(d.graph_tables, R * c->W);
   A(d.gate, R);
@@ -1640,7 +1695,7 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "r0lab") base = c->d_r0lab;
   else if (n == "r0idx") base = c->d_r0idx;
   else if (n == "stamps") base = c->dc.stamps;
-  else if (n == "sel") base = c->dc.sel;  // worklists: [3][G+1] u32, count first (pulls, chains, load)
+  else if (n == "sel") base = c->dc.sel;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));

@@ -14,6 +14,8 @@
 #include "../../include/nemohip.h"
 
 #define NEMO_BLOCK 256
+#define NEMO_CSR_BIG 8192u  // graphs of at least this many nodes: multi-workgroup CSR build (k_csrb_*)
+#define CB_MAXB 4096u       // the bucketed CSR build's buckets per graph (of 8192 nodes): V <= 32M
 #define NEMO_WAVES (NEMO_BLOCK / 64)
 #define NEMO_NONE 0xFFFFFFFFu
 
@@ -168,6 +170,7 @@ struct DevCorpus {
   uint32_t lds_bytes;                    // dynamic LDS of k_proto_lds
   Tier t_ms, t_diff, t_pull;             // the LDS tiers of k_marksimp, k_diff_lds, k_pull_lds
   uint32_t gblock;                       // workgroup size of the global-tier kernels (256, or 1024 for deep corpora)
+  uint32_t pg_chunks;                    // k_pg_* workgroups per listed graph (by the largest post graph)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
   const uint32_t *esrc, *edst;
@@ -189,9 +192,16 @@ struct DevCorpus {
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
   uint32_t *chain_tmp;                   // [5*V]
   uint32_t *nch;                         // [G]
-  uint32_t *sel;                         // [3 (G + 1)] fallback-tier worklists (count first): k_pull's, k_chains', k_csr/k_topo's
-  uint32_t *tail_first;                  // [V] head of per-tail chain list
-  uint32_t *chain_nt;                    // [V] next chain with the same tail
+  uint32_t *sel;                         // [4 (G + 1)] fallback-tier worklists (count first): k_pull's, k_chains', k_csr/k_topo's, k_pg_*'s (runs)
+  const uint32_t *big;                   // graphs of >= 8192 nodes (host list): the multi-workgroup CSR build
+  uint32_t n_big;
+  // its bucketed form (null cb_hist: the atomic form): (bucket, chunk) counts per big graph at
+  // cb_hoff[b], (key, value) edge scratch, the largest bucket and chunk counts (the grid)
+  uint32_t *cb_hist, *cb_key, *cb_val;
+  const uint64_t *cb_hoff;
+  uint32_t cb_maxbk, cb_maxck;
+  uint32_t *cl_first;                    // [V] first chain of a tail (k_proto's global tier; scratch elsewhere)
+  uint32_t *cl_next;                     // [V] next chain with the same tail
   uint32_t *proto_bits, *graph_tables;   // [n_runs*words]
   uint8_t *gate;                         // [n_runs]
   unsigned long long *stamps;            // diagnostic builds only: [16*G] phase stamps

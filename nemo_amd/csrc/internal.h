@@ -50,6 +50,7 @@ __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e);
 void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
 void launch_topo(const DevCorpus &c, hipStream_t s);
+void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s);
 void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s);
 void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s);
 void launch_marksimp(const DevCorpus &c, hipStream_t s);

@@ -119,157 +119,251 @@ __global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier
   if (threadIdx.x == 0) c.holdany[g] = s_hold;
 }
 
-__device__ __forceinline__ void or8(uint8_t *b, uint32_t v, uint32_t bits) {
-  atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (v & 3u)));
-}
-
-// k_proto_lds takes the graphs within the LDS tier (and its chain cap)
-#define LCH_END 0x7FFFu
-__device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphView &gv) {
-  return lds_fits(c, gv.V, gv.E, gv.nlev) && c.nch[gv.g] <= lds_chain_cap(gv.V);
-}
-
 // extractProtos' per-run query (prototype.go:11-24) and missingFrom's table
 // set (:143-147) on the simplified post graph, without materialising it:
 // collapsed rule k is reached through its head (preds(r1) = goal parents of
 // the head) and leads to the goal children of its tail.
-template <int B>
-__global__ __launch_bounds__(B) void k_proto(DevCorpus c) {
-  __shared__ uint32_t s_s[NEMO_MAX_TABLES / 32];
-  __shared__ uint32_t s_t[NEMO_MAX_TABLES / 32];
-  __shared__ uint32_t s_gate;
-  const uint32_t r = blockIdx.x;
-  const uint32_t g = 2 * r + 1;
-  if (c.err[g] || c.err[g - 1]) return;
-  const GraphView gv = c.view(g);
-  if (proto_lds_fits(c, gv)) return;  // k_proto_lds's graph
-  const GraphView pre = c.view(g - 1);
-  const uint8_t *f = gv.flags;
-  uint8_t *sb = c.sb + gv.n0;
-  const uint32_t *ch = c.chain + 5 * gv.n0;
-  const uint32_t *tf = c.tail_first + gv.n0, *nt = c.chain_nt + gv.n0;
-  const uint32_t nch = c.nch[g];
-  for (uint32_t i = threadIdx.x; i < c.words; i += B) {
-    s_s[i] = 0;
-    s_t[i] = 0;
+//
+// Global tier (post graphs k_proto_lds does not take: the deep corpora's 1M-
+// node graphs), push form as k_proto_lds below.  The phases that are single
+// passes over a graph run as multi-workgroup kernels over a device list of
+// those runs (2D grid: x = chunk of the graph, y = list slot, kernel
+// boundaries between phases); only the Kahn-level sweep keeps one workgroup
+// per graph, and it issues a node's child pushes as independent
+// batched parent loads.  Per-node SB_* bits live in c.sb (HBM); a collapsed
+// rule's reach goes through per-tail chain lists built here (cl_first /
+// cl_next, the graph's chains only).
+#define PG_BLOCK 256
+#define PG_SWEEP 1024
+#define SB_NR 0x20u      // goal has a REG or TAIL parent (not a root)
+// byte v of a 4-aligned byte array (LDS, or a corpus-wide array with v the global index)
+__device__ __forceinline__ void or8(uint8_t *b, uint64_t v, uint32_t bits) {
+  atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (uint32_t)(v & 3u)));
+}
+
+// k_proto_lds takes the graphs within its LDS tier (and its chain cap)
+__device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphView &gv) {
+  return lds_fits(c, gv.V, gv.E, gv.nlev) && c.nch[gv.g] <= lds_chain_cap(gv.V);
+}
+__host__ __device__ __forceinline__ uint32_t *proto_list(const DevCorpus &c) { return c.sel + 3 * ((size_t)c.G + 1); }
+
+__global__ __launch_bounds__(NEMO_BLOCK) void k_proto_sel(DevCorpus c) {
+  const uint32_t r = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  bool need = false;
+  if (r < c.n_runs) {
+    const uint32_t g = 2 * r + 1;
+    need = !c.err[g] && !c.err[g - 1] && !proto_lds_fits(c, c.view(g));
   }
-  if (threadIdx.x == 0) s_gate = 0;
-  __syncthreads();
-  // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
-  for (uint32_t x = threadIdx.x; x < pre.V; x += B) {
-    const uint8_t fl = pre.flags[x];
-    if (!is_rule(pre.word[x]) && (fl & NEMO_F_HOLDS) && !(fl & NEMO_F_DELETED)) s_gate = 1;
+  uint32_t *lst = proto_list(c);
+  wave_append(need, r, lst + 1, lst);
+}
+
+// per-run table bitsets accumulated per workgroup in LDS, ORed out once
+struct PgBits {
+  uint32_t w[NEMO_MAX_TABLES / 32];
+};
+__device__ __forceinline__ void pg_bits_clear(PgBits &b, uint32_t W) {
+  for (uint32_t i = threadIdx.x; i < W; i += PG_BLOCK) b.w[i] = 0;
+}
+__device__ __forceinline__ void pg_bits_flush(PgBits &b, uint32_t *dst, uint32_t W) {
+  for (uint32_t i = threadIdx.x; i < W; i += PG_BLOCK)
+    if (b.w[i]) atomicOr(&dst[i], b.w[i]);
+}
+#define PG_LOOP(c, ...)                                                         \
+  const uint32_t *lst_ = proto_list(c);                                         \
+  const uint32_t nl_ = lst_[0];                                                 \
+  for (uint32_t b_ = blockIdx.y; b_ < nl_; b_ += gridDim.y) {                   \
+    const uint32_t r = lst_[1 + b_], g = 2 * r + 1;                             \
+    const GraphView gv = c.view(g);                                             \
+    __VA_ARGS__                                                                 \
   }
 #define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
 #define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
-#define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
-  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
-    const uint32_t w = gv.word[x];
-    uint8_t b = 0;
-    if (is_rule(w)) {
-      if (REG(x) || (f[x] & NEMO_F_HEAD)) ADD(s_t, table_of(w));
-    } else if (!DEL(x)) {
-      bool root = true, hasrc = false;
-      for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
-        const uint32_t p = gv.rc[j];
-        if (REG(p) || (f[p] & NEMO_F_TAIL)) root = false;
-      }
-      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) {
-        const uint32_t q = gv.fc[j];
-        if (REG(q) || (f[q] & NEMO_F_HEAD)) hasrc = true;
-      }
-      b = (root ? SB_ROOT : 0) | (hasrc ? SB_HASRC : 0);
+#define RULEISH(v) (REG(v) || (f[v] & NEMO_F_HEAD))
+
+// clear the graph's SB bytes, its bitset rows and its chains' head lists
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_init(DevCorpus c) {
+  PG_LOOP(c, {
+    uint8_t *sb = c.sb + gv.n0;
+    const uint32_t stride = gridDim.x * PG_BLOCK, t0 = blockIdx.x * PG_BLOCK + threadIdx.x;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      sb[x] = 0;
+      if (gv.flags[x] & NEMO_F_TAIL) c.cl_first[gv.n0 + x] = NEMO_NONE;  // every tail, linked below
     }
-    sb[x] = b;
-  }
-  __syncthreads();
-  // R1: rule children of roots (regular rules, and collapsed rules via their head)
-  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
-    const uint32_t w = gv.word[x];
-    if (!is_rule(w) || !(REG(x) || (f[x] & NEMO_F_HEAD))) continue;
-    bool r1 = false;
-    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
-      const uint32_t p = gv.rc[j];
-      if (!DEL(p) && (sb[p] & SB_ROOT)) r1 = true;
-    }
-    if (!r1) continue;
-    sb[x] |= SB_R1;
-    if (REG(x)) {
-      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) {
-        const uint32_t q = gv.fc[j];
-        if (!DEL(q) && (sb[q] & SB_HASRC)) {
-          ADD(s_s, table_of(w));
-          break;
-        }
+    if (blockIdx.x == 0)
+      for (uint32_t i = threadIdx.x; i < c.words; i += PG_BLOCK) {
+        c.proto_bits[(size_t)r * c.words + i] = 0;
+        c.graph_tables[(size_t)r * c.words + i] = 0;
       }
-    }
-  }
-  __syncthreads();
-  // G2: goal children of R1 rules; collapsed R1 rules that have a goal child with a rule child
-  for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
-    if (is_rule(gv.word[x]) || DEL(x)) continue;
-    bool g2 = false;
-    for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1] && !g2; j++) {
-      const uint32_t p = gv.rc[j];
-      if (REG(p)) {
-        g2 = (sb[p] & SB_R1) != 0;
-      } else if (f[p] & NEMO_F_TAIL) {
-        for (uint32_t k = tf[p]; k != NEMO_NONE; k = nt[k])
-          if (sb[ch[5 * k]] & SB_R1) g2 = true;
+  })
+}
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_link(DevCorpus c) {
+  PG_LOOP(c, {
+    const uint32_t *ch = c.chain + 5 * gv.n0;
+    for (uint32_t k = blockIdx.x * PG_BLOCK + threadIdx.x; k < c.nch[g]; k += gridDim.x * PG_BLOCK)
+      c.cl_next[gv.n0 + k] = atomicExch(&c.cl_first[gv.n0 + ch[5 * k + 1]], k);
+  })
+}
+// missingFrom's table set; not-root marks pushed from REG / TAIL rules; HASRC goals
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_a(DevCorpus c) {
+  __shared__ PgBits s_t;
+  PG_LOOP(c, {
+    const uint8_t *f = gv.flags;
+    uint8_t *sbg = c.sb;  // corpus-wide: or8 on n0 + x (n0 need not be 4-aligned)
+    pg_bits_clear(s_t, c.words);
+    __syncthreads();
+    for (uint32_t x = blockIdx.x * PG_BLOCK + threadIdx.x; x < gv.V; x += gridDim.x * PG_BLOCK) {
+      const uint32_t w = gv.word[x], j0 = gv.fp[x], j1 = gv.fp[x + 1];
+      if (is_rule(w)) {
+        if (RULEISH(x)) atomicOr(&s_t.w[table_of(w) >> 5], 1u << (table_of(w) & 31));
+        if (REG(x) || (f[x] & NEMO_F_TAIL))
+          for (uint32_t j = j0; j < j1; j++) or8(sbg, gv.n0 + gv.fc[j], SB_NR);
+      } else if (!DEL(x)) {
+        bool hasrc = false;
+        for (uint32_t j = j0; j < j1 && !hasrc; j++) hasrc = RULEISH(gv.fc[j]);
+        if (hasrc) or8(sbg, gv.n0 + x, SB_HASRC);
       }
-    }
-    if (g2) sb[x] |= SB_G2;
-  }
-  for (uint32_t k = threadIdx.x; k < nch; k += B) {
-    const uint32_t h = ch[5 * k], t = ch[5 * k + 1];
-    if (!(sb[h] & SB_R1)) continue;
-    for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) {
-      const uint32_t q = gv.fc[j];
-      if (!DEL(q) && (sb[q] & SB_HASRC)) {
-        ADD(s_s, table_of(gv.word[h]));
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  // rules reachable from G2 (forward level sweep over graph')
-  for (uint32_t l = 0; l < gv.nlev; l++) {
-    for (uint32_t i = gv.lvl[l] + threadIdx.x; i < gv.lvl[l + 1]; i += B) {
-      const uint32_t x = gv.topo[i];
-      const uint32_t w = gv.word[x];
-      bool rch = false;
-      if (!is_rule(w)) {
-        if (DEL(x)) continue;
-        for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1] && !rch; j++) {
-          const uint32_t p = gv.rc[j];
-          if (REG(p)) {
-            rch = (sb[p] & SB_RCH) != 0;
-          } else if (f[p] & NEMO_F_TAIL) {
-            for (uint32_t k = tf[p]; k != NEMO_NONE; k = nt[k])
-              if (sb[ch[5 * k]] & SB_RCH) rch = true;
-          }
-        }
-      } else if (REG(x) || (f[x] & NEMO_F_HEAD)) {
-        for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
-          const uint32_t p = gv.rc[j];
-          if (!DEL(p) && (sb[p] & (SB_G2 | SB_RCH))) rch = true;
-        }
-        if (rch) ADD(s_s, table_of(w));
-      }
-      if (rch) sb[x] |= SB_RCH;
     }
     __syncthreads();
+    pg_bits_flush(s_t, c.graph_tables + (size_t)r * c.words, c.words);
+    __syncthreads();
+  })
+}
+// R1: the rule children of roots (a push to a non-REG/HEAD rule is never read)
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_b(DevCorpus c) {
+  PG_LOOP(c, {
+    const uint8_t *f = gv.flags;
+    const uint8_t *sb = c.sb + gv.n0;
+    for (uint32_t x = blockIdx.x * PG_BLOCK + threadIdx.x; x < gv.V; x += gridDim.x * PG_BLOCK) {
+      if (is_rule(gv.word[x]) || DEL(x) || (sb[x] & SB_NR)) continue;
+      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) or8(c.sb, gv.n0 + gv.fc[j], SB_R1);
+    }
+  })
+}
+// G2 below R1 rules (regular, and collapsed through their chain's tail), with
+// the R1 tables whose rule has a live goal child that has a rule child
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_c(DevCorpus c) {
+  __shared__ PgBits s_s;
+  PG_LOOP(c, {
+    const uint8_t *f = gv.flags;
+    const uint8_t *sb = c.sb + gv.n0;
+    pg_bits_clear(s_s, c.words);
+    __syncthreads();
+    const uint32_t stride = gridDim.x * PG_BLOCK, t0 = blockIdx.x * PG_BLOCK + threadIdx.x;
+    auto below = [&](uint32_t src, uint32_t table) {
+      bool add = false;
+      for (uint32_t j = gv.fp[src]; j < gv.fp[src + 1]; j++) {
+        const uint32_t q = gv.fc[j];
+        if (DEL(q)) continue;
+        or8(c.sb, gv.n0 + q, SB_G2);
+        add |= (sb[q] & SB_HASRC) != 0;
+      }
+      if (add) atomicOr(&s_s.w[table >> 5], 1u << (table & 31));
+    };
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      const uint32_t w = gv.word[x];
+      if (is_rule(w) && REG(x) && (sb[x] & SB_R1)) below(x, table_of(w));
+    }
+    const uint32_t *ch = c.chain + 5 * gv.n0;
+    for (uint32_t k = t0; k < c.nch[g]; k += stride) {
+      const uint32_t h = ch[5 * k];
+      if (sb[h] & SB_R1) below(ch[5 * k + 1], table_of(gv.word[h]));
+    }
+    __syncthreads();
+    pg_bits_flush(s_s, c.proto_bits + (size_t)r * c.words, c.words);
+    __syncthreads();
+  })
+}
+// rules reachable from G2: one workgroup per graph, one barrier per Kahn level
+// (pull form: a node's parents lie on earlier levels, whose bits are final).
+// Deep graphs have ~20k levels of a few dozen nodes, so a level costs its
+// dependent-load chain: each node's parent ids, then their flag / SB bytes,
+// are fetched PG_BATCH at a time, independent of each other.
+#define PG_BATCH 4
+__global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
+  const uint32_t *lst = proto_list(c);
+  const uint32_t nl = lst[0];
+  for (uint32_t b = blockIdx.x; b < nl; b += gridDim.x) {
+    const uint32_t r = lst[1 + b], g = 2 * r + 1;
+    const GraphView gv = c.view(g);
+    const uint8_t *f = gv.flags;
+    uint8_t *sb = c.sb + gv.n0;
+    const uint32_t *ch = c.chain + 5 * gv.n0, nch = c.nch[g];
+    const uint32_t *clf = c.cl_first + gv.n0, *cln = c.cl_next + gv.n0;
+    for (uint32_t l = 0; l < gv.nlev; l++) {
+      const uint32_t e = gv.lvl[l + 1];
+      for (uint32_t i = gv.lvl[l] + threadIdx.x; i < e; i += PG_SWEEP) {
+        const uint32_t x = gv.topo[i];
+        const uint32_t w = gv.word[x], fx = f[x];
+        const bool rule = is_rule(w);
+        if (rule ? !((fx & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT || (fx & NEMO_F_HEAD))
+                 : (fx & NEMO_F_DELETED) != 0)
+          continue;
+        // a rule is reached from a live G2 / RCH goal parent; a goal from an RCH
+        // regular rule parent, or a tail parent one of whose chains has an RCH head
+        const uint32_t want = rule ? (SB_G2 | SB_RCH) : SB_RCH;
+        bool rch = false;
+        const uint32_t j1 = gv.rp[x + 1];
+        for (uint32_t j = gv.rp[x]; j < j1 && !rch; j += PG_BATCH) {
+          uint32_t p[PG_BATCH], fp_[PG_BATCH], bp[PG_BATCH];
+#pragma unroll
+          for (int q = 0; q < PG_BATCH; q++) p[q] = j + q < j1 ? gv.rc[j + q] : NEMO_NONE;
+#pragma unroll
+          for (int q = 0; q < PG_BATCH; q++) {
+            fp_[q] = p[q] != NEMO_NONE ? f[p[q]] : 0u;
+            bp[q] = p[q] != NEMO_NONE ? sb[p[q]] : 0u;
+          }
+#pragma unroll
+          for (int q = 0; q < PG_BATCH; q++) {
+            if (p[q] == NEMO_NONE) continue;
+            if (rule) {
+              rch |= !(fp_[q] & NEMO_F_DELETED) && (bp[q] & want);
+            } else if ((fp_[q] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT) {
+              rch |= (bp[q] & SB_RCH) != 0;
+            } else if (fp_[q] & NEMO_F_TAIL) {
+              uint32_t hops = 0;
+              for (uint32_t k = clf[p[q]]; k < nch && hops++ < nch && !rch; k = cln[k]) rch = (sb[ch[5 * k]] & SB_RCH) != 0;
+            }
+          }
+        }
+        if (rch) sb[x] |= SB_RCH;
+      }
+      __syncthreads();
+    }
   }
+}
+// tables of the reached rules; then extractProtos' gate (prototype.go:13)
+__global__ __launch_bounds__(PG_BLOCK) void k_pg_d(DevCorpus c) {
+  __shared__ PgBits s_s;
+  PG_LOOP(c, {
+    const uint8_t *f = gv.flags;
+    const uint8_t *sb = c.sb + gv.n0;
+    pg_bits_clear(s_s, c.words);
+    __syncthreads();
+    for (uint32_t x = blockIdx.x * PG_BLOCK + threadIdx.x; x < gv.V; x += gridDim.x * PG_BLOCK) {
+      const uint32_t w = gv.word[x];
+      if (is_rule(w) && RULEISH(x) && (sb[x] & SB_RCH)) atomicOr(&s_s.w[table_of(w) >> 5], 1u << (table_of(w) & 31));
+    }
+    __syncthreads();
+    pg_bits_flush(s_s, c.proto_bits + (size_t)r * c.words, c.words);
+    __syncthreads();
+  })
+}
+__global__ __launch_bounds__(NEMO_BLOCK) void k_pg_gate(DevCorpus c) {
+  const uint32_t *lst = proto_list(c);
+  for (uint32_t b = blockIdx.x * NEMO_BLOCK + threadIdx.x; b < lst[0]; b += gridDim.x * NEMO_BLOCK) {
+    const uint32_t r = lst[1 + b];
+    // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
+    const bool gt = c.holdany[2 * r] != 0;
+    c.gate[r] = gt ? 1 : 0;
+    if (!gt)
+      for (uint32_t i = 0; i < c.words; i++) c.proto_bits[(size_t)r * c.words + i] = 0;
+  }
+}
 #undef DEL
 #undef REG
-#undef ADD
-  const bool gate = s_gate != 0;
-  for (uint32_t i = threadIdx.x; i < c.words; i += B) {
-    c.proto_bits[(size_t)r * c.words + i] = gate ? s_s[i] : 0u;
-    c.graph_tables[(size_t)r * c.words + i] = s_t[i];
-  }
-  if (threadIdx.x == 0) c.gate[r] = gate ? 1 : 0;
-}
+#undef RULEISH
+#undef PG_LOOP
 
 // k_proto's LDS tier, push form: every phase propagates along forward rows
 // only, so LDS holds the forward u16 CSR, Kahn order + level offsets, the u16
@@ -287,7 +381,6 @@ __global__ __launch_bounds__(B) void k_proto(DevCorpus c) {
 // Per-node bits are ORed with LDS atomics (or8): pushes from different threads
 // meet in the same bytes.
 #define PROTO_BLOCK 512
-#define SB_NR 0x20u      // goal has a REG or TAIL parent (not a root)
 #define PCH_DONE 0x8000u // chain tail word: the head's reach was pushed
 __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
@@ -668,10 +761,18 @@ void launch_proto(const DevCorpus &c, hipStream_t s) {
     hipFuncSetAttribute((const void *)k_proto_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
     hipLaunchKernelGGL(k_proto_lds, dim3(c.n_runs), dim3(PROTO_BLOCK), c.lds_bytes, s, c);
   }
-  if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_proto<1024>, dim3(c.n_runs), dim3(1024), 0, s, c);
-  else
-    hipLaunchKernelGGL(k_proto<NEMO_BLOCK>, dim3(c.n_runs), dim3(NEMO_BLOCK), 0, s, c);
+  if (!c.n_runs) return;
+  launch_zero(proto_list(c), sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_proto_sel, dim3((c.n_runs + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
+  const dim3 grid(c.pg_chunks, std::min(c.n_runs, 256u));
+  hipLaunchKernelGGL(k_pg_init, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_link, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_a, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_b, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_c, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_sweep, dim3(std::min(c.n_runs, 2048u)), dim3(PG_SWEEP), 0, s, c);
+  hipLaunchKernelGGL(k_pg_d, grid, dim3(PG_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_pg_gate, dim3(std::min((c.n_runs + NEMO_BLOCK - 1) / NEMO_BLOCK, 64u)), dim3(NEMO_BLOCK), 0, s, c);
 }
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s) {

@@ -900,16 +900,6 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
   __syncthreads();
 #endif
   STAMP(8);
-  // tail lists: only F_TAIL nodes (= the tails of accepted chains) are ever read
-  __threadfence_block();
-  __syncthreads();  // out[] rows of other threads
-  for (uint32_t k = tid; k < nch; k += NEMO_BLOCK) c.tail_first[gv.n0 + out[5 * k + 1]] = NEMO_NONE;
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t k = tid; k < nch; k += NEMO_BLOCK) {
-    const uint32_t t = out[5 * k + 1];
-    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
-  }
   STAMP(9);
   if (tid == 0) {
     c.nch[g] = nch;
@@ -935,7 +925,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
   uint32_t *cnodes = c.s_g + gv.n0 + g;               // nodes bucketed by component
   uint32_t *coff = (uint32_t *)(c.s_e + gv.n0);       // [ncomp+1] bucket offsets, then cursors
   uint32_t *roots = c.chain + 5 * gv.n0;              // temp until the final sort
-  uint32_t *cidx = c.chain_nt + gv.n0;                // graph-local -> component-local
+  uint32_t *cidx = c.cl_next + gv.n0;                // graph-local -> component-local
   uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
   const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
@@ -1036,7 +1026,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
     // fallback for components beyond the LDS tile: workgroup-wide sweeps over
     // global memory; LDS-handled components are all FT_SEEN already.
     int32_t *down = c.s_d + gv.n0;
-    int32_t *du = (int32_t *)(c.tail_first + gv.n0);
+    int32_t *du = (int32_t *)(c.cl_first + gv.n0);
     unsigned long long *best = c.s_e + gv.n0;
     for (uint32_t l = gv.nlev; l-- > 0;) {
       for (uint32_t i = hl[l] + threadIdx.x; i < hl[l + 1]; i += NEMO_BLOCK) {
@@ -1134,17 +1124,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
 #pragma unroll
     for (int q = 0; q < 5; q++) out[5 * k + q] = tmp[5 * i + q];
   }
-  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) {
-    const uint32_t v = hs[i];
-    f[v] &= (uint8_t)~FT_SEEN;
-    c.tail_first[gv.n0 + v] = NEMO_NONE;
-  }
+  for (uint32_t i = threadIdx.x; i < nh; i += NEMO_BLOCK) f[hs[i]] &= (uint8_t)~FT_SEEN;
 #undef INH
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < n; k += NEMO_BLOCK) {
-    const uint32_t t = out[5 * k + 1];
-    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
-  }
   if (threadIdx.x == 0) c.nch[g] = n;
 }
 

@@ -423,13 +423,6 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     w[3] = gv.rank_of(w[0]);
     w[4] = 0;
   }
-  for (uint32_t i = tid; i < n; i += GB) c.tail_first[gv.n0 + hs[i]] = NEMO_NONE;
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t k = tid; k < nch; k += GB) {
-    const uint32_t t = out[5 * k + 1];
-    c.chain_nt[gv.n0 + k] = atomicExch(&c.tail_first[gv.n0 + t], k);
-  }
   STAMP(9);
   if (tid == 0) {
     c.nch[g] = nch;

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
 // are neither duplicates nor goal->goal / rule->rule (pre-post-prov.go:150-210).
 // Graphs with V < CSR_LDS count degrees, scan and hand out cursors in LDS;
 // larger ones do the same with global atomics.
-#define CSR_LDS 8192
+#define CSR_LDS NEMO_CSR_BIG
 template <int B>
 __device__ __forceinline__ void csr_graph(const DevCorpus c, const uint32_t g) {
   __shared__ uint32_t s_cnt[CSR_LDS];
@@ -274,6 +274,7 @@ __device__ __forceinline__ void csr_graph(const DevCorpus c, const uint32_t g) {
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   if (build_fits(c, V, E) && !c.redo[g]) return;  // k_build's graph
+  if (V >= CSR_LDS) return;                         // the multi-workgroup build (k_csrb_*)
   uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0, *rc = c.rc + e0;
   const uint32_t *es = c.esrc + e0, *ed = c.edst + e0, *word = c.word + n0;
   if (threadIdx.x == 0) s_created = 0;  // first read after the barrier below
@@ -344,6 +345,123 @@ __device__ __forceinline__ void csr_graph(const DevCorpus c, const uint32_t g) {
   }
 }
 
+// Graphs of CSR_LDS nodes or more (the deep corpora's 1M-node graphs): the
+// same CSR build spread over many workgroups per graph.  A 2D grid takes the
+// host's list of big graphs (y) and a chunk of each graph's edges or nodes
+// (x); kernel boundaries replace the barriers between the phases (count ->
+// per-graph scan -> scatter -> row sort + relationships-created).  Global
+// atomics on the row counters and cursors; one workgroup per graph only for
+// the scans.
+#define CSRB_BLOCK 256
+__device__ __forceinline__ bool csrb_take(const DevCorpus &c, uint32_t g, uint32_t V, uint32_t E) {
+  return V >= CSR_LDS && !(build_fits(c, V, E) && !c.redo[g]);
+}
+__global__ __launch_bounds__(CSRB_BLOCK) void k_csrb_count(DevCorpus c) {
+  for (uint32_t b = blockIdx.y; b < c.n_big; b += gridDim.y) {
+    const uint32_t g = c.big[b];
+    const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+    const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+    if (!csrb_take(c, g, V, E)) continue;
+    uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g;
+    const uint32_t *es = c.esrc + e0, *ed = c.edst + e0;
+    const uint32_t stride = gridDim.x * CSRB_BLOCK;
+    bool bad = false;
+    for (uint32_t e = blockIdx.x * CSRB_BLOCK + threadIdx.x; e < E; e += stride) {
+      const uint32_t x = es[e], y = ed[e];
+      if (x >= V || y >= V) {
+        bad = true;
+        continue;
+      }
+      atomicAdd(&fp[x], 1u);
+      atomicAdd(&rp[y], 1u);
+    }
+    if (__any(bad) && lane_id() == 0) atomicMax(&c.err[g], (uint32_t)NEMO_ERR_INVALID);
+  }
+}
+__global__ __launch_bounds__(CSRB_BLOCK) void k_csrb_zero(DevCorpus c) {
+  for (uint32_t b = blockIdx.y; b < c.n_big; b += gridDim.y) {
+    const uint32_t g = c.big[b];
+    const uint64_t n0 = c.node_off[g];
+    const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - c.edge_off[g]);
+    if (!csrb_take(c, g, V, E)) continue;
+    uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g;
+    for (uint32_t v = blockIdx.x * CSRB_BLOCK + threadIdx.x; v <= V; v += gridDim.x * CSRB_BLOCK) {
+      fp[v] = 0;
+      rp[v] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) c.created[g] = 0;
+  }
+}
+// one 1024-thread workgroup per big graph: row starts, and the scatter cursors
+__global__ __launch_bounds__(1024) void k_csrb_scan(DevCorpus c) {
+  __shared__ uint32_t s_lds[16];
+  const uint32_t g = c.big[blockIdx.x];
+  const uint64_t n0 = c.node_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - c.edge_off[g]);
+  if (!csrb_take(c, g, V, E) || c.err[g]) return;
+  uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *cf = c.s_a + n0 + g, *cr = c.s_b + n0 + g;
+  block_scan_inplace<1024, 16>(fp, V + 1, s_lds);
+  block_scan_inplace<1024, 16>(rp, V + 1, s_lds);
+  for (uint32_t v = threadIdx.x; v < V; v += 1024) {
+    cf[v] = fp[v];
+    cr[v] = rp[v];
+  }
+}
+__global__ __launch_bounds__(CSRB_BLOCK) void k_csrb_scatter(DevCorpus c) {
+  for (uint32_t b = blockIdx.y; b < c.n_big; b += gridDim.y) {
+    const uint32_t g = c.big[b];
+    const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+    const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+    if (!csrb_take(c, g, V, E) || c.err[g]) continue;
+    uint32_t *fc = c.fc + e0, *rc = c.rc + e0, *cf = c.s_a + n0 + g, *cr = c.s_b + n0 + g;
+    const uint32_t *es = c.esrc + e0, *ed = c.edst + e0;
+    for (uint32_t e = blockIdx.x * CSRB_BLOCK + threadIdx.x; e < E; e += gridDim.x * CSRB_BLOCK) {
+      const uint32_t x = es[e], y = ed[e];
+      fc[atomicAdd(&cf[x], 1u)] = y;
+      rc[atomicAdd(&cr[y], 1u)] = x;
+    }
+  }
+}
+// rows sorted (a merged duplicate DUETO edge is adjacent), relationships created
+__global__ __launch_bounds__(CSRB_BLOCK) void k_csrb_rows(DevCorpus c) {
+  __shared__ uint32_t s_cr;
+  for (uint32_t b = blockIdx.y; b < c.n_big; b += gridDim.y) {
+    const uint32_t g = c.big[b];
+    const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+    const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+    if (!csrb_take(c, g, V, E) || c.err[g]) continue;
+    const uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *word = c.word + n0;
+    uint32_t *fc = c.fc + e0, *rc = c.rc + e0;
+    if (threadIdx.x == 0) s_cr = 0;
+    __syncthreads();
+    uint32_t created = 0;
+    for (uint32_t v = blockIdx.x * CSRB_BLOCK + threadIdx.x; v < V; v += gridDim.x * CSRB_BLOCK) {
+      const uint32_t a = fp[v], bb = fp[v + 1];
+      sort_row(fc + a, bb - a);
+      sort_row(rc + rp[v], rp[v + 1] - rp[v]);
+      const bool rv = is_rule(word[v]);
+      for (uint32_t j = a; j < bb; j++) {
+        const uint32_t t = fc[j];
+        if (!(j > a && fc[j - 1] == t) && rv != is_rule(word[t])) created++;
+      }
+    }
+    for (int d = 32; d >= 1; d >>= 1) created += __shfl_xor(created, d);
+    if (lane_id() == 0 && created) atomicAdd(&s_cr, created);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cr) atomicAdd(&c.created[g], s_cr);
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(CSRB_BLOCK) void k_csrb_fin(DevCorpus c) {
+  const uint32_t b = blockIdx.x * CSRB_BLOCK + threadIdx.x;
+  if (b >= c.n_big) return;
+  const uint32_t g = c.big[b];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - c.node_off[g]), E = (uint32_t)(c.edge_off[g + 1] - c.edge_off[g]);
+  if (!csrb_take(c, g, V, E) || c.err[g]) return;
+  c.err[g] = c.created[g] == E ? 0u : (uint32_t)NEMO_ERR_LOAD;
+}
+
+#define TOPO_BATCH 4
 // Kahn levels: topo[] lists the graph's nodes level by level, lvl[l]..lvl[l+1]
 // is level l (longest path from a source).  A graph with a cycle is refused.
 template <int B>
@@ -376,15 +494,21 @@ __device__ __forceinline__ void topo_graph(const DevCorpus c, const uint32_t g) 
         j = fp[u];
         je = fp[u + 1];
       }
+      // children in batches of TOPO_BATCH: their loads and counter atomics are
+      // independent, so a batch costs one round trip instead of one per child
       while (__any(j < je)) {
-        bool p = false;
-        uint32_t ch = 0;
-        if (j < je) {
-          ch = fc[j++];
-          p = atomicSub(&cnt[ch], 1u) == 1u;
+        uint32_t ch[TOPO_BATCH], old[TOPO_BATCH];
+#pragma unroll
+        for (int q = 0; q < TOPO_BATCH; q++) ch[q] = j + q < je ? fc[j + q] : NEMO_NONE;
+#pragma unroll
+        for (int q = 0; q < TOPO_BATCH; q++) old[q] = ch[q] != NEMO_NONE ? atomicSub(&cnt[ch[q]], 1u) : 0u;
+        j = min(j + TOPO_BATCH, je);
+#pragma unroll
+        for (int q = 0; q < TOPO_BATCH; q++) {
+          const bool p = old[q] == 1u;
+          wave_append(p, ch[q], topo, &s_tail);
+          if (p) c.nlv[n0 + ch[q]] = nl + 1;
         }
-        wave_append(p, ch, topo, &s_tail);
-        if (p) c.nlv[n0 + ch] = nl + 1;
       }
     }
     __syncthreads();
@@ -448,6 +572,143 @@ void launch_load(const DevCorpus &c, hipStream_t s) {
     hipLaunchKernelGGL(k_csr<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
     hipLaunchKernelGGL(k_csr<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);
+}
+// Bucketed form of the same build (the default for big graphs): scattered
+// global atomics on 1M-entry row counters run at the memory-side atomic rate
+// (~20 G/s chip-wide, MI355X_MICROARCH.md "Global float atomics"), so the
+// counting happens in LDS instead.  Per direction: (1) every CB_CHUNK-edge
+// chunk histograms its keys by CB_NB-node bucket in LDS; (2) one workgroup per
+// graph scans the (bucket, chunk) counts; (3) each chunk partitions its edges
+// into their buckets' ranges (LDS cursors) as (key, value) pairs in HBM
+// scratch; (4) one workgroup per bucket counts its nodes' degrees, writes
+// their row pointers and scatters the values into their rows with LDS
+// cursors, then sorts the rows (and, forward, counts relationships created).
+// Every global write is then a streaming store into a contiguous range.
+#define CB_NB 8192u
+#define CB_CHUNK 8192u
+#define CB_BLOCK 1024
+__global__ __launch_bounds__(CB_BLOCK) void k_cb_hist(DevCorpus c, int dir) {
+  __shared__ uint32_t h[CB_MAXB];
+  const uint32_t b = blockIdx.y, g = c.big[b];
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  const uint32_t nbk = (V + CB_NB - 1) / CB_NB, nck = (E + CB_CHUNK - 1) / CB_CHUNK;
+  if (blockIdx.x >= nck || !csrb_take(c, g, V, E)) return;
+  for (uint32_t k = threadIdx.x; k < nbk; k += CB_BLOCK) h[k] = 0;
+  __syncthreads();
+  const uint32_t *key = (dir ? c.edst : c.esrc) + e0, *oth = (dir ? c.esrc : c.edst) + e0;
+  const uint32_t a = blockIdx.x * CB_CHUNK, z = min(E, a + CB_CHUNK);
+  bool bad = false;
+  for (uint32_t e = a + threadIdx.x; e < z; e += CB_BLOCK) {
+    const uint32_t k = key[e];
+    bad |= k >= V || oth[e] >= V;
+    if (k < V) atomicAdd(&h[k / CB_NB], 1u);
+  }
+  if (__any(bad) && lane_id() == 0) atomicMax(&c.err[g], (uint32_t)NEMO_ERR_INVALID);
+  __syncthreads();
+  uint32_t *out = c.cb_hist + c.cb_hoff[b];  // (bucket, chunk) counts, bucket-major
+  for (uint32_t k = threadIdx.x; k < nbk; k += CB_BLOCK) out[(uint64_t)k * nck + blockIdx.x] = h[k];
+}
+__global__ __launch_bounds__(1024) void k_cb_scan(DevCorpus c) {
+  __shared__ uint32_t s_lds[16];
+  const uint32_t b = blockIdx.x, g = c.big[b];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - c.node_off[g]), E = (uint32_t)(c.edge_off[g + 1] - c.edge_off[g]);
+  if (!csrb_take(c, g, V, E) || c.err[g]) return;
+  const uint32_t nbk = (V + CB_NB - 1) / CB_NB, nck = (E + CB_CHUNK - 1) / CB_CHUNK;
+  block_scan_inplace<1024, 16>(c.cb_hist + c.cb_hoff[b], nbk * nck, s_lds);
+}
+__global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
+  __shared__ uint32_t cur[CB_MAXB];
+  const uint32_t b = blockIdx.y, g = c.big[b];
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  const uint32_t nbk = (V + CB_NB - 1) / CB_NB, nck = (E + CB_CHUNK - 1) / CB_CHUNK;
+  if (blockIdx.x >= nck || !csrb_take(c, g, V, E) || c.err[g]) return;
+  const uint32_t *off = c.cb_hist + c.cb_hoff[b];
+  for (uint32_t k = threadIdx.x; k < nbk; k += CB_BLOCK) cur[k] = off[(uint64_t)k * nck + blockIdx.x];
+  __syncthreads();
+  const uint32_t *key = (dir ? c.edst : c.esrc) + e0, *oth = (dir ? c.esrc : c.edst) + e0;
+  uint32_t *ok = c.cb_key + e0, *ov = c.cb_val + e0;
+  const uint32_t a = blockIdx.x * CB_CHUNK, z = min(E, a + CB_CHUNK);
+  for (uint32_t e = a + threadIdx.x; e < z; e += CB_BLOCK) {
+    const uint32_t k = key[e], v = oth[e];
+    const uint32_t pos = atomicAdd(&cur[k / CB_NB], 1u);
+    ok[pos] = k;
+    ov[pos] = v;
+  }
+}
+__global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
+  __shared__ uint32_t cnt[CB_NB + 1];
+  __shared__ uint32_t s_lds[CB_BLOCK / 64];
+  __shared__ uint32_t s_cr;
+  const uint32_t b = blockIdx.y, g = c.big[b];
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  const uint32_t nbk = (V + CB_NB - 1) / CB_NB, nck = (E + CB_CHUNK - 1) / CB_CHUNK;
+  const uint32_t bk = blockIdx.x;
+  if (bk >= nbk || !csrb_take(c, g, V, E) || c.err[g]) return;
+  const uint32_t *off = c.cb_hist + c.cb_hoff[b];
+  const uint32_t lo = off[(uint64_t)bk * nck], hi = bk + 1 < nbk ? off[(uint64_t)(bk + 1) * nck] : E;
+  const uint32_t v0 = bk * CB_NB, nv = min(V, v0 + CB_NB) - v0;
+  const uint32_t *ek = c.cb_key + e0, *ev = c.cb_val + e0;
+  uint32_t *ptr = (dir ? c.rp : c.fp) + n0 + g, *col = (dir ? c.rc : c.fc) + e0;
+  for (uint32_t i = threadIdx.x; i <= nv; i += CB_BLOCK) cnt[i] = 0;
+  if (threadIdx.x == 0) s_cr = 0;
+  __syncthreads();
+  for (uint32_t j = lo + threadIdx.x; j < hi; j += CB_BLOCK) atomicAdd(&cnt[ek[j] - v0], 1u);
+  __syncthreads();
+  block_scan_inplace<CB_BLOCK>(cnt, nv + 1, s_lds);
+  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) ptr[v0 + i] = lo + cnt[i];
+  if (bk + 1 == nbk && threadIdx.x == 0) ptr[V] = E;
+  __syncthreads();
+  for (uint32_t j = lo + threadIdx.x; j < hi; j += CB_BLOCK) col[lo + atomicAdd(&cnt[ek[j] - v0], 1u)] = ev[j];
+  __threadfence_block();
+  __syncthreads();
+  // rows sorted (a merged duplicate DUETO edge is adjacent); forward rows count relationships created
+  const uint32_t *word = c.word + n0;
+  uint32_t created = 0;
+  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
+    const uint32_t v = v0 + i, a = ptr[v], z = v + 1 < V ? (i + 1 < nv ? ptr[v + 1] : hi) : E;
+    sort_row(col + a, z - a);
+    if (dir) continue;
+    const bool rv = is_rule(word[v]);
+    for (uint32_t j = a; j < z; j++) {
+      const uint32_t t = col[j];
+      if (!(j > a && col[j - 1] == t) && rv != is_rule(word[t])) created++;
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) created += __shfl_xor(created, d);
+  if (lane_id() == 0 && created) atomicAdd(&s_cr, created);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_cr) atomicAdd(&c.created[g], s_cr);
+}
+__global__ __launch_bounds__(CSRB_BLOCK) void k_cb_zero(DevCorpus c) {
+  const uint32_t b = blockIdx.x * CSRB_BLOCK + threadIdx.x;
+  if (b < c.n_big) c.created[c.big[b]] = 0;
+}
+
+void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s) {
+  if (!c.n_big) return;
+  if (c.cb_hist) {  // bucketed build (every big graph within CB_MAXB buckets)
+    hipLaunchKernelGGL(k_cb_zero, dim3((c.n_big + CSRB_BLOCK - 1) / CSRB_BLOCK), dim3(CSRB_BLOCK), 0, s, c);
+    for (int dir = 0; dir < 2; dir++) {
+      const dim3 gc(c.cb_maxck, c.n_big), gb(c.cb_maxbk, c.n_big);
+      hipLaunchKernelGGL(k_cb_hist, gc, dim3(CB_BLOCK), 0, s, c, dir);
+      hipLaunchKernelGGL(k_cb_scan, dim3(c.n_big), dim3(1024), 0, s, c);
+      hipLaunchKernelGGL(k_cb_part, gc, dim3(CB_BLOCK), 0, s, c, dir);
+      hipLaunchKernelGGL(k_cb_bucket, gb, dim3(CB_BLOCK), 0, s, c, dir);
+    }
+    hipLaunchKernelGGL(k_csrb_fin, dim3((c.n_big + CSRB_BLOCK - 1) / CSRB_BLOCK), dim3(CSRB_BLOCK), 0, s, c);
+    return;
+  }
+  if (!c.n_big) return;
+  const dim3 grid(chunks, std::min(c.n_big, 65535u));
+  hipLaunchKernelGGL(k_csrb_zero, grid, dim3(CSRB_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_csrb_count, grid, dim3(CSRB_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_csrb_scan, dim3(c.n_big), dim3(1024), 0, s, c);
+  hipLaunchKernelGGL(k_csrb_scatter, grid, dim3(CSRB_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_csrb_rows, grid, dim3(CSRB_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_csrb_fin, dim3((c.n_big + CSRB_BLOCK - 1) / CSRB_BLOCK), dim3(CSRB_BLOCK), 0, s, c);
 }
 void launch_topo(const DevCorpus &c, hipStream_t s) {  // after launch_load: its list
   if (!c.G) return;

@@ -1,6 +1,6 @@
 """Diagnostic: per-phase cycle shares of k_chains_glob (deep graphs) from the stamps build.
 
-usage: python tools/stamps_glob.py [RUNS] [NODES] [EOT]
+usage: python tools/stamps_glob.py [RUNS] [NODES] [EOT] [dense]
 """
 import os, sys
 import numpy as np
@@ -11,7 +11,9 @@ from tools import synth
 runs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 eot = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
-corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16)
+dense = len(sys.argv) > 4 and sys.argv[4] == "dense"  # C5's ~4 edges per node (tools/synth.py CONFIGS["c5"])
+extra = {"body_extra": 6, "nval": 3, "nloc": 4} if dense else {}
+corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16, **extra)
 eng = E.Engine(0)
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 G = corpus.n_graphs
