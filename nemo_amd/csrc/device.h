@@ -15,7 +15,7 @@
 
 #define NEMO_BLOCK 256
 #define NEMO_CSR_BIG 8192u  // graphs of at least this many nodes: multi-workgroup CSR build (k_csrb_*)
-#define CB_MAXB 4096u       // the bucketed CSR build's buckets per graph (of 8192 nodes): V <= 32M
+#define CB_MAXB 8192u       // the bucketed CSR build's buckets per graph (of 2048 nodes): V <= 16M
 #define NEMO_WAVES (NEMO_BLOCK / 64)
 #define NEMO_NONE 0xFFFFFFFFu
 

@@ -584,7 +584,7 @@ void launch_load(const DevCorpus &c, hipStream_t s) {
 // their row pointers and scatters the values into their rows with LDS
 // cursors, then sorts the rows (and, forward, counts relationships created).
 // Every global write is then a streaming store into a contiguous range.
-#define CB_NB 8192u
+#define CB_NB 2048u
 #define CB_CHUNK 8192u
 #define CB_BLOCK 1024
 __global__ __launch_bounds__(CB_BLOCK) void k_cb_hist(DevCorpus c, int dir) {
@@ -637,8 +637,13 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
     ov[pos] = v;
   }
 }
+// One bucket's rows built in LDS: degrees, row starts, the values scattered
+// by LDS cursors and each row sorted there, then written out coalesced.  A
+// bucket of more than CB_LDS_E edges (a hub-heavy one) sorts in HBM instead.
+#define CB_LDS_E 14336u
 __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   __shared__ uint32_t cnt[CB_NB + 1];
+  __shared__ uint32_t rows[CB_LDS_E];
   __shared__ uint32_t s_lds[CB_BLOCK / 64];
   __shared__ uint32_t s_cr;
   const uint32_t b = blockIdx.y, g = c.big[b];
@@ -649,34 +654,39 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   if (bk >= nbk || !csrb_take(c, g, V, E) || c.err[g]) return;
   const uint32_t *off = c.cb_hist + c.cb_hoff[b];
   const uint32_t lo = off[(uint64_t)bk * nck], hi = bk + 1 < nbk ? off[(uint64_t)(bk + 1) * nck] : E;
-  const uint32_t v0 = bk * CB_NB, nv = min(V, v0 + CB_NB) - v0;
-  const uint32_t *ek = c.cb_key + e0, *ev = c.cb_val + e0;
-  uint32_t *ptr = (dir ? c.rp : c.fp) + n0 + g, *col = (dir ? c.rc : c.fc) + e0;
+  const uint32_t v0 = bk * CB_NB, nv = min(V, v0 + CB_NB) - v0, ne = hi - lo;
+  const uint32_t *ek = c.cb_key + e0 + lo, *ev = c.cb_val + e0 + lo;
+  uint32_t *ptr = (dir ? c.rp : c.fp) + n0 + g, *col = (dir ? c.rc : c.fc) + e0 + lo;
+  const bool lds = ne <= CB_LDS_E;
+  uint32_t *dst = lds ? rows : col;  // where the rows are assembled and sorted
   for (uint32_t i = threadIdx.x; i <= nv; i += CB_BLOCK) cnt[i] = 0;
   if (threadIdx.x == 0) s_cr = 0;
   __syncthreads();
-  for (uint32_t j = lo + threadIdx.x; j < hi; j += CB_BLOCK) atomicAdd(&cnt[ek[j] - v0], 1u);
+  for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) atomicAdd(&cnt[ek[j] - v0], 1u);
   __syncthreads();
   block_scan_inplace<CB_BLOCK>(cnt, nv + 1, s_lds);
   for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) ptr[v0 + i] = lo + cnt[i];
   if (bk + 1 == nbk && threadIdx.x == 0) ptr[V] = E;
   __syncthreads();
-  for (uint32_t j = lo + threadIdx.x; j < hi; j += CB_BLOCK) col[lo + atomicAdd(&cnt[ek[j] - v0], 1u)] = ev[j];
+  for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) dst[atomicAdd(&cnt[ek[j] - v0], 1u)] = ev[j];
   __threadfence_block();
-  __syncthreads();
+  __syncthreads();  // cnt[i] = end of row i (local)
   // rows sorted (a merged duplicate DUETO edge is adjacent); forward rows count relationships created
   const uint32_t *word = c.word + n0;
   uint32_t created = 0;
   for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
-    const uint32_t v = v0 + i, a = ptr[v], z = v + 1 < V ? (i + 1 < nv ? ptr[v + 1] : hi) : E;
-    sort_row(col + a, z - a);
+    const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i];
+    sort_row(dst + a, z - a);
     if (dir) continue;
-    const bool rv = is_rule(word[v]);
+    const bool rv = is_rule(word[v0 + i]);
     for (uint32_t j = a; j < z; j++) {
-      const uint32_t t = col[j];
-      if (!(j > a && col[j - 1] == t) && rv != is_rule(word[t])) created++;
+      const uint32_t t = dst[j];
+      if (!(j > a && dst[j - 1] == t) && rv != is_rule(word[t])) created++;
     }
   }
+  __syncthreads();
+  if (lds)
+    for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) col[j] = rows[j];
   for (int d = 32; d >= 1; d >>= 1) created += __shfl_xor(created, d);
   if (lane_id() == 0 && created) atomicAdd(&s_cr, created);
   __syncthreads();
