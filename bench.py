@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU time budget of each baseline leg")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--e2e-runs", type=int, default=2000,
+                    help="end-to-end leg (rank 0, N=1): runs of the same shape written as a Molly directory, then "
+                         "streaming native ingest -> H2D -> analysis -> host results, pipelined by chunk (0: off)")
+    ap.add_argument("--e2e-chunk", type=int, default=500)
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                     help="off: the timed steps run without per-launch HIP events (two extra steps collect them)")
     ap.add_argument("--stage-blocks", type=int, default=0, help="bulk D2H staging by a k_to_host grid of this size (0: runtime copies)")
@@ -257,6 +261,11 @@ def main():
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_runs > 0 and not strong and args.config != "c5":
+        eng.close()
+        eng = Engine(local)
+        e2e = e2e_leg(args, gen, eng, threads, mode)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode)
@@ -299,6 +308,9 @@ def main():
                     for k, v in sorted(tim.items(), key=lambda kv: -kv[1]["ms"])},
         "gen_seconds_rank0": round(gen_s, 2),
     }
+    if e2e is not None:
+        out["e2e_runs_per_s"] = e2e["runs_per_s"]
+        out["e2e"] = e2e
     if "k_diff" in tim:  # all entries of a diffprov call run concurrently: the launch time is each entry's latency
         out["k_diff_entry_latency_ms"] = round(tim["k_diff"]["ms"] / tim["k_diff"]["launches"], 4)
     if rank == 0:
@@ -311,6 +323,42 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def e2e_leg(args, gen, eng, threads, mode):
+    """SURVEY.md 8d metric 1, second half: runs/s from a Molly-format directory on disk to host results.
+    nemo_amd/pipeline.py streams the directory through nemo_ingest_next (native JSON decode + interning,
+    `threads` threads) in chunks; chunk i is uploaded (nemo_load_corpus: H2D + CSR) and analysed while
+    chunk i+1 is decoded.  Best of 2 passes (the first also warms the page cache, as a re-analysis would)."""
+    import shutil
+    import tempfile
+
+    from nemo_amd import pipeline
+    from nemo_amd.ingest import load_molly_native
+    from tools import synth
+    corpus, info = synth.generate(args.e2e_runs, threads=threads, **gen)
+    d = tempfile.mkdtemp(prefix="nemo_e2e_")
+    try:
+        synth.write_molly(corpus, info, d, threads=threads)
+        del corpus
+        size = sum(os.path.getsize(os.path.join(d, x)) for x in os.listdir(d))
+        best = None
+        for _ in range(2):
+            r = pipeline.run(d, eng, chunk=args.e2e_chunk, threads=threads, diff_mode=mode, keep=False)
+            if best is None or r.timings["total_s"] < best.timings["total_s"]:
+                best = r
+        t = time.perf_counter()  # the decode alone, one shot (its rate bounds the pipeline)
+        c = load_molly_native(d, threads=threads)
+        t_ingest = time.perf_counter() - t
+        del c
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    tot = best.timings["total_s"]
+    return {"runs_per_s": round(args.e2e_runs / tot, 1), "runs": args.e2e_runs, "json_gb": round(size / 1e9, 3),
+            "chunk": args.e2e_chunk, "ingest_threads": threads, "total_s": round(tot, 3),
+            "device_and_handover_s": round(best.timings["device_s"], 3),
+            "ingest_only_s": round(t_ingest, 3), "ingest_gb_per_s": round(size / t_ingest / 1e9, 3),
+            "note": "JSON decode bound: the pipeline overlaps device work with the next chunk's decode"}
 
 
 def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):

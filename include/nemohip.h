@@ -235,6 +235,10 @@ int nemo_diffprov(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, 
 int nemo_goal_labels(nemo_ctx *ctx, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap);
 int nemo_diffprov_labels(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, const uint32_t *d_labels,
                          uint64_t labels_cap);
+/* The same with the label set in host memory (the caller interned it, e.g. a
+ * chunked pipeline whose failedRuns[0] was analysed with an earlier chunk). */
+int nemo_diffprov_host_labels(nemo_ctx *ctx, const uint32_t *failed_iters, size_t n_failed, const uint32_t *labels,
+                              uint64_t n_labels);
 /* D node mask over run 0's post graph for entry e (1 byte per node).        */
 int nemo_fetch_diff_mask(nemo_ctx *ctx, uint32_t entry, uint8_t *out, uint64_t cap);
 /* D masks of every entry, entry-major (n_entries * V0 bytes).               */
@@ -325,6 +329,25 @@ int nemo_ingest_corpus(const nemo_ingest *h, nemo_corpus *corpus);
 uint64_t nemo_ingest_count(const nemo_ingest *h, int kind);
 int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index, const char **s, size_t *len);
 void nemo_ingest_free(nemo_ingest *h);
+/* Streaming form: the same directory parsed chunk by chunk
+ * so that chunk i is loaded and analysed on the device while chunk i+1 is
+ * being parsed.  Interning is shared across chunks (ids in graph order, as the
+ * one-shot ingest assigns them); table "pre"/"post" ids are fixed by the first
+ * chunk.  nemo_ingest_next parses the next `chunk` runs into a corpus (arrays
+ * valid until the next call) and, with `with_run0`, prepends the run of
+ * iteration 0 as a replicated, not-owned run to every chunk after the one
+ * holding it (the good run of the diffs, differential-provenance.go:26).
+ * Returns NEMO_ERR_NOTFOUND when no run is left; validation failures as
+ * nemo_ingest_molly.  A chunk's arrays stay valid through the next call (two
+ * buffers), so one chunk can be uploaded while the next is parsed.          */
+typedef struct nemo_ingest_stream nemo_ingest_stream;
+int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
+                     nemo_ingest_stream **out);
+int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_run0, nemo_corpus *corpus, char *err,
+                     size_t err_cap);
+uint64_t nemo_ingest_stream_count(const nemo_ingest_stream *s, int kind);
+int nemo_ingest_stream_string(const nemo_ingest_stream *s, int kind, uint64_t index, const char **str, size_t *len);
+void nemo_ingest_close(nemo_ingest_stream *s);
 
 /* ---- instrumentation ------------------------------------------------------ */
 typedef struct nemo_timing {

@@ -113,6 +113,9 @@ struct nemo_ctx {
 
   // pinned upload staging (success flags, diff sources): reused once the
   // previous upload from the same buffer has landed (ev_up*)
+  uint32_t *d_hlab = nullptr, *h_hlab = nullptr;  // nemo_diffprov_host_labels' set [n, label...]
+  uint64_t hlab_cap = 0, h_hlab_cap = 0;
+  hipEvent_t ev_up_hlab = nullptr;
   uint8_t *h_succ = nullptr;
   uint32_t *h_dsrc = nullptr;
   uint64_t h_succ_cap = 0, h_dsrc_cap = 0;
@@ -356,6 +359,8 @@ static void release_corpus(nemo_ctx *c) {
   c->pull_slot_cap = 0;
   c->pull_which = -1;
   c->d_tcounts = c->d_tpre = c->d_tpost = c->d_tasync = nullptr;
+  c->d_hlab = nullptr;
+  c->hlab_cap = 0;
   c->trig_pending = false;
   c->d_chout = nullptr;
   c->d_choff = nullptr;
@@ -400,6 +405,8 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->ev_pull) hipEventDestroy(c->ev_pull);
   if (c->ev_trig) hipEventDestroy(c->ev_trig);
   if (c->ev_up_succ) hipEventDestroy(c->ev_up_succ);
+  if (c->ev_up_hlab) hipEventDestroy(c->ev_up_hlab);
+  if (c->h_hlab) hipHostFree(c->h_hlab);
   if (c->ev_up_dsrc) hipEventDestroy(c->ev_up_dsrc);
   if (c->h_succ) hipHostFree(c->h_succ);
   for (void *h : {(void *)c->h_red, (void *)c->h_tab, (void *)c->h_nmiss, (void *)c->h_mrows, (void *)c->h_mask,
@@ -1208,6 +1215,30 @@ int nemo_diffprov_labels(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   DISPATCH(node_diffprov_labels(c, failed_iters, n_failed, d_labels, labels_cap));
   if (!d_labels) return c ? fail(c, NEMO_ERR_INVALID, "no label set") : NEMO_ERR_INVALID;
   return diffprov_impl(c, failed_iters, n_failed, NEMO_DIFF_REFERENCE, d_labels, labels_cap);
+}
+
+int nemo_diffprov_host_labels(nemo_ctx *c, const uint32_t *failed_iters, size_t n_failed, const uint32_t *labels,
+                              uint64_t n_labels) {
+  DISPATCH(node_diffprov_host_labels(c, failed_iters, n_failed, labels, n_labels));
+  if (!c || (!labels && n_labels)) return NEMO_ERR_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if (n_labels + 1 > c->hlab_cap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(c, c->d_hlab);
+    c->d_hlab = nullptr;
+    c->hlab_cap = 0;
+    if ((rc = dalloc(c, &c->d_hlab, n_labels + 1))) return rc;
+    c->hlab_cap = n_labels + 1;
+  }
+  if (!c->ev_up_hlab) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_hlab, hipEventDisableTiming));
+  else HIPCHK(c, hipEventSynchronize(c->ev_up_hlab));  // the previous upload has landed
+  if ((rc = hgrow(c, &c->h_hlab, &c->h_hlab_cap, n_labels + 1))) return rc;
+  c->h_hlab[0] = (uint32_t)n_labels;
+  if (n_labels) memcpy(c->h_hlab + 1, labels, n_labels * 4);
+  nemo::launch_to_host(c->d_hlab, c->h_hlab, (n_labels + 1) * 4, c->stream);  // pinned -> device by a copy kernel
+  HIPCHK(c, hipEventRecord(c->ev_up_hlab, c->stream));
+  return diffprov_impl(c, failed_iters, n_failed, NEMO_DIFF_REFERENCE, c->d_hlab, n_labels + 1);
 }
 
 int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap) {

@@ -609,6 +609,197 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
   return NEMO_OK;
 }
 
+// ---- streaming ingest: chunk i is analysed on the device
+// while chunk i+1 is being parsed.  Interning is shared across chunks (ids are
+// assigned in graph order, as the one-shot ingest assigns them), so the
+// chunks' label and table ids agree with each other; the run of iteration 0
+// is replicated, not owned, into every chunk after the one holding it.
+struct nemo_ingest_stream {
+  std::string dir;
+  std::vector<uint32_t> iteration;
+  int threads = 1;
+  uint32_t next = 0;
+  std::unordered_map<std::string, uint32_t> tmap, lmap;
+  std::vector<std::string> tables, labels;
+  uint32_t table_pre = 0, table_post = 0;
+  bool pre_post = false;
+  int64_t run0 = -1;  // run index of iteration 0
+  bool have_run0 = false;
+  uint64_t r0_nv[2] = {0, 0}, r0_ne[2] = {0, 0};
+  std::vector<uint32_t> r0_word, r0_label, r0_rank, r0_src, r0_dst;
+  // the chunks' arrays, double-buffered: chunk i stays valid while chunk i+1 is parsed
+  struct Chunk {
+    std::vector<uint32_t> it, word, label, rank, src, dst;
+    std::vector<uint8_t> own;
+    std::vector<uint64_t> node_off, edge_off;
+  } buf[2];
+  uint32_t calls = 0;
+};
+
+extern "C" int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
+                                nemo_ingest_stream **out) {
+  if (!out_dir || !out || (n_runs && !iterations)) return NEMO_ERR_INVALID;
+  auto *s = new nemo_ingest_stream();
+  s->dir = out_dir;
+  s->iteration.assign(iterations, iterations + n_runs);
+  s->threads = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  for (uint32_t r = 0; r < n_runs && s->run0 < 0; r++)
+    if (iterations[r] == 0) s->run0 = r;
+  *out = s;
+  return NEMO_OK;
+}
+
+extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_run0, nemo_corpus *c, char *err,
+                                size_t err_cap) {
+  auto fail = [&](const std::string &m) {
+    if (err && err_cap) snprintf(err, err_cap, "%s", m.c_str());
+    return NEMO_ERR_LOAD;
+  };
+  if (!s || !c || chunk == 0) return NEMO_ERR_INVALID;
+  const uint32_t R = (uint32_t)s->iteration.size();
+  if (s->next >= R) return NEMO_ERR_NOTFOUND;
+  const uint32_t a = s->next, b = std::min<uint32_t>(R, a + chunk), G = 2 * (b - a);
+  s->next = b;
+  std::vector<Graph> gs(G);
+  int nt = std::max(1, std::min<int>(s->threads, (int)G));
+  std::atomic<uint32_t> nextg{0};
+  auto work = [&] {
+    for (uint32_t g; (g = nextg.fetch_add(1)) < G;) {
+      const uint32_t r = a + g / 2;
+      const char *cond = g % 2 ? "post" : "pre";
+      std::string path = s->dir + "/run_" + std::to_string(r) + "_" + cond + "_provenance.json";
+      parse_graph(path, s->iteration[r], cond, gs[g]);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; i++) pool.emplace_back(work);
+  work();
+  for (auto &t : pool) t.join();
+  for (uint32_t g = 0; g < G; g++)
+    if (!gs[g].err.empty()) return fail(gs[g].err);
+  std::vector<std::vector<uint32_t>> tre(G), lre(G);
+  for (uint32_t g = 0; g < G; g++) {
+    for (Str x : gs[g].tabs) {
+      auto it = s->tmap.emplace(std::string(gs[g].sv(x)), (uint32_t)s->tables.size());
+      if (it.second) s->tables.emplace_back(gs[g].sv(x));
+      tre[g].push_back(it.first->second);
+    }
+    for (Str x : gs[g].labs) {
+      auto it = s->lmap.emplace(std::string(gs[g].sv(x)), (uint32_t)s->labels.size());
+      if (it.second) s->labels.emplace_back(gs[g].sv(x));
+      lre[g].push_back(it.first->second);
+    }
+  }
+  if (!s->pre_post) {  // fixed from the first chunk on: every chunk's corpus names the same ids
+    for (const char *cn : {"pre", "post"}) {
+      auto it = s->tmap.emplace(cn, (uint32_t)s->tables.size());
+      if (it.second) s->tables.emplace_back(cn);
+      (cn[1] == 'r' ? s->table_pre : s->table_post) = it.first->second;
+    }
+    s->pre_post = true;
+  }
+  if (s->tables.size() > NEMO_MAX_TABLES) return fail("more than NEMO_MAX_TABLES distinct tables");
+  nemo_ingest_stream::Chunk &ck = s->buf[s->calls++ & 1];
+  const bool rep0 = with_run0 && s->have_run0 && !(s->run0 >= a && s->run0 < b);
+  const uint32_t Rc = (b - a) + (rep0 ? 1 : 0), Gc = 2 * Rc;
+  ck.it.clear();
+  ck.own.clear();
+  ck.node_off.assign(Gc + 1, 0);
+  ck.edge_off.assign(Gc + 1, 0);
+  uint32_t go = 0;
+  if (rep0) {
+    ck.it.push_back(0);
+    ck.own.push_back(0);
+    for (int k = 0; k < 2; k++) {
+      ck.node_off[go + 1] = ck.node_off[go] + s->r0_nv[k];
+      ck.edge_off[go + 1] = ck.edge_off[go] + s->r0_ne[k];
+      go++;
+    }
+  }
+  for (uint32_t r = a; r < b; r++) {
+    ck.it.push_back(s->iteration[r]);
+    ck.own.push_back(1);
+    for (int k = 0; k < 2; k++) {
+      const Graph &gr = gs[2 * (r - a) + k];
+      ck.node_off[go + 1] = ck.node_off[go] + gr.id.size();
+      ck.edge_off[go + 1] = ck.edge_off[go] + gr.src.size();
+      go++;
+    }
+  }
+  const uint64_t V = ck.node_off[Gc], E = ck.edge_off[Gc];
+  ck.word.resize(V), ck.label.resize(V), ck.rank.resize(V), ck.src.resize(E), ck.dst.resize(E);
+  if (rep0) {
+    std::copy(s->r0_word.begin(), s->r0_word.end(), ck.word.begin());
+    std::copy(s->r0_label.begin(), s->r0_label.end(), ck.label.begin());
+    std::copy(s->r0_rank.begin(), s->r0_rank.end(), ck.rank.begin());
+    std::copy(s->r0_src.begin(), s->r0_src.end(), ck.src.begin());
+    std::copy(s->r0_dst.begin(), s->r0_dst.end(), ck.dst.begin());
+  }
+  const uint32_t gbase = rep0 ? 2 : 0;
+  nextg = 0;
+  auto fill = [&] {
+    for (uint32_t g; (g = nextg.fetch_add(1)) < G;) {
+      const Graph &gr = gs[g];
+      const uint64_t n0 = ck.node_off[gbase + g], e0 = ck.edge_off[gbase + g];
+      for (size_t i = 0; i < gr.id.size(); i++) {
+        ck.word[n0 + i] = NEMO_WORD(i >= gr.n_goals, gr.tclass[i], tre[g][gr.ltab[i]]);
+        ck.label[n0 + i] = lre[g][gr.llab[i]];
+        ck.rank[n0 + i] = gr.rank[i];
+      }
+      std::copy(gr.src.begin(), gr.src.end(), ck.src.begin() + e0);
+      std::copy(gr.dst.begin(), gr.dst.end(), ck.dst.begin() + e0);
+    }
+  };
+  pool.clear();
+  for (int i = 1; i < nt; i++) pool.emplace_back(fill);
+  fill();
+  for (auto &t : pool) t.join();
+  if (s->run0 >= a && s->run0 < b) {  // keep run 0 for the chunks after this one
+    const uint32_t g0 = gbase + 2 * (uint32_t)(s->run0 - a);
+    const uint64_t n0 = ck.node_off[g0], n1 = ck.node_off[g0 + 2], e0 = ck.edge_off[g0], e1 = ck.edge_off[g0 + 2];
+    s->r0_nv[0] = ck.node_off[g0 + 1] - n0, s->r0_nv[1] = n1 - ck.node_off[g0 + 1];
+    s->r0_ne[0] = ck.edge_off[g0 + 1] - e0, s->r0_ne[1] = e1 - ck.edge_off[g0 + 1];
+    s->r0_word.assign(ck.word.begin() + n0, ck.word.begin() + n1);
+    s->r0_label.assign(ck.label.begin() + n0, ck.label.begin() + n1);
+    s->r0_rank.assign(ck.rank.begin() + n0, ck.rank.begin() + n1);
+    s->r0_src.assign(ck.src.begin() + e0, ck.src.begin() + e1);
+    s->r0_dst.assign(ck.dst.begin() + e0, ck.dst.begin() + e1);
+    s->have_run0 = true;
+  }
+  memset(c, 0, sizeof(*c));
+  c->n_runs = Rc;
+  c->n_tables = (uint32_t)s->tables.size();
+  c->table_pre = s->table_pre;
+  c->table_post = s->table_post;
+  c->iteration = ck.it.data();
+  c->owned = ck.own.data();
+  c->node_off = ck.node_off.data();
+  c->edge_off = ck.edge_off.data();
+  c->node_word = ck.word.data();
+  c->label = ck.label.data();
+  c->id_rank = ck.rank.data();
+  c->edge_src = ck.src.data();
+  c->edge_dst = ck.dst.data();
+  return NEMO_OK;
+}
+
+extern "C" uint64_t nemo_ingest_stream_count(const nemo_ingest_stream *s, int kind) {
+  if (!s) return 0;
+  return kind == NEMO_STR_TABLE ? s->tables.size() : kind == NEMO_STR_LABEL ? s->labels.size() : 0;
+}
+
+extern "C" int nemo_ingest_stream_string(const nemo_ingest_stream *s, int kind, uint64_t index, const char **str,
+                                         size_t *len) {
+  if (!s || !str || !len || (kind != NEMO_STR_TABLE && kind != NEMO_STR_LABEL)) return NEMO_ERR_INVALID;
+  const auto &v = kind == NEMO_STR_TABLE ? s->tables : s->labels;
+  if (index >= v.size()) return NEMO_ERR_INVALID;
+  *str = v[index].data();
+  *len = v[index].size();
+  return NEMO_OK;
+}
+
+extern "C" void nemo_ingest_close(nemo_ingest_stream *s) { delete s; }
+
 extern "C" int nemo_ingest_corpus(const nemo_ingest *h, nemo_corpus *c) {
   if (!h || !c) return NEMO_ERR_INVALID;
   memset(c, 0, sizeof(*c));

@@ -49,6 +49,7 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 // (redo) and rebuilt by k_csr + k_topo, which also take the graphs beyond
 // the caps; both tiers produce the same outputs and validations.
 #define BLD_EPT 32  // edges per thread held in registers (bld_e <= BLD_EPT * NEMO_BLOCK)
+#define BLD_KB 4    // Kahn: children of a node processed per round
 
 __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
   return lds_align(4u * ((v + 31u) / 32u)) + lds_align(2u * (v + 2u)) + lds_align(2u * e) + lds_align(v) +
@@ -231,16 +232,23 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
         j = u ? ptr[u - 1] : 0u;
         je = ptr[u];
       }
+      // children BLD_KB at a time: their LDS reads and counter atomics are independent
       while (__any(j < je)) {
-        bool p = false;
-        uint32_t ch = 0;
-        if (j < je) {
-          ch = col[j++];
-          const uint32_t sh = 8 * (ch & 3);
-          p = ((atomicSub(&cnt32[ch >> 2], 1u << sh) >> sh) & 0xFFu) == 1u;
+        uint32_t ch[BLD_KB], old[BLD_KB];
+#pragma unroll
+        for (int q = 0; q < BLD_KB; q++) ch[q] = j + q < je ? col[j + q] : 0xFFFFu;
+#pragma unroll
+        for (int q = 0; q < BLD_KB; q++) {
+          const uint32_t sh = 8 * (ch[q] & 3);
+          old[q] = ch[q] != 0xFFFFu ? (atomicSub(&cnt32[ch[q] >> 2], 1u << sh) >> sh) & 0xFFu : 0u;
         }
-        lds_append16(p, ch, q16 + hi, cur);
-        if (p) nlv[ch] = nl + 1;
+        j = min(j + BLD_KB, je);
+#pragma unroll
+        for (int q = 0; q < BLD_KB; q++) {
+          const bool p = old[q] == 1u;
+          lds_append16(p, ch[q], q16 + hi, cur);
+          if (p) nlv[ch[q]] = nl + 1;
+        }
       }
     }
     __syncthreads();

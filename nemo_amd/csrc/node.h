@@ -37,6 +37,7 @@ int node_missing_from(nemo_ctx *c, uint32_t failed_iter, const uint32_t *proto, 
                       uint32_t *n_out);
 int node_diffprov(nemo_ctx *c, const uint32_t *failed, size_t n, int mode);
 int node_diffprov_labels(nemo_ctx *c, const uint32_t *failed, size_t n, const uint32_t *d_labels, uint64_t cap);
+int node_diffprov_host_labels(nemo_ctx *c, const uint32_t *failed, size_t n, const uint32_t *labels, uint64_t n_labels);
 int node_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap);
 int node_fetch_diff_mask(nemo_ctx *c, uint32_t entry, uint8_t *out, uint64_t cap);
 int node_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap);

@@ -535,6 +535,30 @@ int node_diffprov_labels(nemo_ctx *c, const uint32_t *failed, size_t nf, const u
   if (!d_labels) return fail(c, NEMO_ERR_INVALID, "no label set");
   return node_diff(c, failed, nf, NEMO_DIFF_REFERENCE, d_labels, cap);
 }
+int node_diffprov_host_labels(nemo_ctx *c, const uint32_t *failed, size_t nf, const uint32_t *labels, uint64_t n_labels) {
+  Node *n = N(c);
+  NEED_LOADED(c, n);
+  // route the entries as node_diff does, every shard with the same host label set
+  const size_t P = n->sh.size();
+  std::vector<std::vector<uint32_t>> lists(P);
+  n->entry_shard.assign(nf, 0);
+  n->entry_local.assign(nf, 0);
+  for (auto &s : n->sh) s.entries.clear();
+  for (size_t e = 0; e < nf; e++) {
+    uint32_t r;
+    if (int rc = owner_of_iter(c, n, failed[e], &r)) return rc;
+    const uint32_t p = n->run_shard[r];
+    n->entry_shard[e] = p;
+    n->entry_local[e] = (uint32_t)lists[p].size();
+    lists[p].push_back(failed[e]);
+    n->sh[p].entries.push_back((uint32_t)e);
+  }
+  n->n_entries = n->run0 >= 0 ? (uint32_t)nf : 0;
+  for (size_t p = 0; p < P; p++)
+    SCHK(c, n->sh[p], nemo_diffprov_host_labels(n->sh[p].ctx, lists[p].data(), lists[p].size(), labels, n_labels));
+  return NEMO_OK;
+}
+
 int node_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap) {
   Node *n = N(c);
   if (n->sh.size() > 1) return fail(c, NEMO_ERR_INVALID, "nemo_goal_labels on a node context: its diffprov broadcasts");

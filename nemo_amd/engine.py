@@ -75,6 +75,7 @@ def lib():
             "nemo_missing_from": ([vp, u32, vp, u32, vp, P(u32)], i32),
             "nemo_diffprov": ([vp, vp, sz, i32], i32),
             "nemo_diffprov_labels": ([vp, vp, sz, vp, u64], i32),
+            "nemo_diffprov_host_labels": ([vp, vp, sz, vp, u64], i32),
             "nemo_goal_labels": ([vp, u32, i32, vp, u64], i32),
             "nemo_fetch_diff_mask": ([vp, u32, vp, u64], i32),
             "nemo_fetch_missing": ([vp, vp, u64, P(u64)], i32),
@@ -225,6 +226,12 @@ class Engine:
         """nemo_diffprov_labels: reference-mode diff with a (broadcast) device label set."""
         f = np.ascontiguousarray(failed, dtype=np.uint32)
         self._chk(self.L.nemo_diffprov_labels(self.h, _p(f), len(f), ctypes.c_void_p(d_labels_ptr), cap))
+
+    def diffprov_host_labels(self, failed: Sequence[int], labels: Sequence[int]) -> None:
+        """nemo_diffprov_host_labels: reference-mode diff with a host label set."""
+        f = np.ascontiguousarray(failed, dtype=np.uint32)
+        lab = np.ascontiguousarray(labels, dtype=np.uint32)
+        self._chk(self.L.nemo_diffprov_host_labels(self.h, _p(f), len(f), _p(lab), len(lab)))
 
     def triggers(self) -> None:
         self._chk(self.L.nemo_triggers(self.h))

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from nemo_amd.corpus import LoadError, load_molly
-from nemo_amd.ingest import load_molly_native
+from nemo_amd.ingest import STR_LABEL, STR_TABLE, load_molly_native
 from tests.small import random_prov
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -94,3 +94,76 @@ def test_null_and_empty_sections(tmp_path):
     write_dir(str(tmp_path), [(0, "success", {"goals": None, "rules": [], "edges": None}, {})])
     c = load_molly_native(str(tmp_path))
     assert int(c.node_off[-1]) == 0 and c.tables == ["pre", "post"]
+
+
+def _synth_dir(tmp_path, n_runs=40, nodes=300, body_extra=2):
+    from tools import synth
+    corpus, info = synth.generate(n_runs, target_nodes=nodes, body_extra=body_extra)
+    d = str(tmp_path / "molly")
+    synth.write_molly(corpus, info, d, threads=4)
+    return corpus, info, d
+
+
+def test_c_writer_matches_python_writer(tmp_path):
+    """synth.write_molly (C) writes the same files, byte for byte, as synth.to_molly."""
+    from tools import synth
+    corpus, info, d = _synth_dir(tmp_path, n_runs=6, nodes=200)
+    p = str(tmp_path / "py")
+    synth.to_molly(corpus, info, p)
+    names = sorted(os.listdir(p))
+    assert names == sorted(os.listdir(d))
+    for n in names:
+        assert open(os.path.join(p, n), "rb").read() == open(os.path.join(d, n), "rb").read(), n
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 16, 40, 100])
+def test_stream_chunks_match_one_shot(tmp_path, chunk):
+    """nemo_ingest_next's chunks, owned runs concatenated, equal nemo_ingest_molly's corpus; every chunk
+    after the one holding run 0 starts with run 0 replicated (not owned)."""
+    from nemo_amd.pipeline import IngestStream
+    _, _, d = _synth_dir(tmp_path)
+    one = load_molly_native(d, threads=4)
+    st = IngestStream(d, threads=3)
+    parts = {k: [] for k in ("node_word", "label", "id_rank", "edge_src", "edge_dst")}
+    sizes_v, sizes_e, its = [], [], []
+    seen0 = False
+    while True:
+        c = st.next(chunk)
+        if c is None:
+            break
+        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
+        if seen0 and chunk < one.n_runs:
+            assert int(c.iteration[0]) == 0 and own[0] == 0
+        for lr in range(c.n_runs):
+            if not own[lr]:
+                continue
+            its.append(int(c.iteration[lr]))
+            for g in (2 * lr, 2 * lr + 1):
+                n0, n1 = int(c.node_off[g]), int(c.node_off[g + 1])
+                e0, e1 = int(c.edge_off[g]), int(c.edge_off[g + 1])
+                for k in ("node_word", "label", "id_rank"):
+                    parts[k].append(np.asarray(getattr(c, k))[n0:n1].copy())
+                for k in ("edge_src", "edge_dst"):
+                    parts[k].append(np.asarray(getattr(c, k))[e0:e1].copy())
+                sizes_v.append(n1 - n0)
+                sizes_e.append(e1 - e0)
+        seen0 = seen0 or 0 in set(int(x) for x in c.iteration)
+        assert (c.table_pre, c.table_post) == (one.table_pre, one.table_post)
+    assert its == [int(x) for x in one.iteration]
+    assert np.array_equal(np.diff(one.node_off.astype(np.int64)), sizes_v)
+    assert np.array_equal(np.diff(one.edge_off.astype(np.int64)), sizes_e)
+    for k, v in parts.items():
+        assert np.array_equal(np.concatenate(v), np.asarray(getattr(one, k))), k
+    assert st.strings(STR_LABEL) == one.labels and st.strings(STR_TABLE) == one.tables
+    st.close()
+
+
+def test_stream_error_and_end(tmp_path):
+    from nemo_amd.pipeline import IngestStream
+    _, _, d = _synth_dir(tmp_path, n_runs=5, nodes=100)
+    open(os.path.join(d, "run_3_post_provenance.json"), "w").write('{"goals": [')
+    st = IngestStream(d)
+    assert st.next(3) is not None
+    with pytest.raises(LoadError):
+        st.next(3)
+    st.close()

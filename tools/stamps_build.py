@@ -10,7 +10,7 @@ import nemo_amd.engine as E  # noqa: E402
 E.LIB_PATH = os.path.join(os.path.dirname(E.LIB_PATH), "libnemohip_stamps.so")
 from tools import synth  # noqa: E402
 
-corpus, _ = synth.generate(int(sys.argv[1]) if len(sys.argv) > 1 else 500, threads=16)
+corpus, _ = synth.generate(int(sys.argv[1]) if len(sys.argv) > 1 else 500, threads=16, **synth.CONFIGS["c3"])
 eng = E.Engine(0)
 eng.load(corpus)
 eng.synchronize()

@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import nemo_amd.engine as E
 E.LIB_PATH = os.path.join(os.path.dirname(E.LIB_PATH), "libnemohip_stamps.so")
 from tools import synth
-corpus, _ = synth.generate(int(sys.argv[1]) if len(sys.argv) > 1 else 500, threads=16)
+corpus, _ = synth.generate(int(sys.argv[1]) if len(sys.argv) > 1 else 500, threads=16, **synth.CONFIGS["c3"])
 eng = E.Engine(0)
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 G = corpus.n_graphs

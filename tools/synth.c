@@ -16,6 +16,7 @@
  * graph the local node order equals the ID string order (id_rank = NULL).
  */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -573,4 +574,168 @@ void synth_free(synth_out *o) {
   free(o->edge_dst);
   free(o->base_id);
   memset(o, 0, sizeof *o);
+}
+
+/* ---- Molly-format writer (the e2e bench's input; tools/synth.py to_molly in C) ----
+ * runs.json + run_<i>_{pre,post}_provenance.json exactly as synth.to_molly
+ * writes them (json.dump's default separators), one file per OpenMP task. */
+typedef struct {
+  char *p;
+  size_t n, cap;
+} sbuf;
+static void sb_put(sbuf *b, const char *s, size_t n) {
+  if (b->n + n + 1 > b->cap) {
+    b->cap = (b->n + n + 1) * 2;
+    b->p = realloc(b->p, b->cap);
+  }
+  memcpy(b->p + b->n, s, n);
+  b->n += n;
+}
+static void sb_str(sbuf *b, const char *s) { sb_put(b, s, strlen(s)); }
+static void sb_u(sbuf *b, uint64_t v) {
+  char t[24];
+  int k = 0;
+  do t[k++] = (char)('0' + v % 10); while ((v /= 10));
+  while (k) sb_put(b, &t[--k], 1);
+}
+static void sb_i(sbuf *b, int64_t v) {
+  if (v < 0) {
+    sb_put(b, "-", 1);
+    v = -v;
+  }
+  sb_u(b, (uint64_t)v);
+}
+/* label text of an interned synthetic label (synth.py label_string) */
+static void sb_label(sbuf *b, uint32_t lab, const char *const *names, uint32_t eot, uint32_t nloc, uint32_t nval,
+                     int64_t *time_out) {
+  if (lab >= RULE_LABEL_BASE) {
+    sb_str(b, names[lab - RULE_LABEL_BASE]);
+    return;
+  }
+  const uint32_t t = lab % (eot + 2);
+  uint32_t rest = lab / (eot + 2);
+  const uint32_t val = rest % nval;
+  rest /= nval;
+  const uint32_t loc = rest % nloc, tab = rest / nloc;
+  const char *name = names[tab];
+  sb_str(b, name);
+  sb_str(b, "(n");
+  sb_u(b, loc);
+  if (!strcmp(name, "clock")) {
+    sb_str(b, ", n");
+    sb_u(b, val);
+    sb_str(b, ", ");
+    sb_i(b, (int64_t)t - 1);
+    sb_str(b, ", ");
+  } else if (!strcmp(name, "pre") || !strcmp(name, "post")) {
+    sb_str(b, ", ");
+  } else {
+    sb_str(b, ", v");
+    sb_u(b, val);
+    sb_str(b, ", ");
+  }
+  sb_u(b, t);
+  sb_str(b, ")");
+  if (time_out) *time_out = t;
+}
+static void sb_id(sbuf *b, int rule, uint32_t base) {
+  char t[16];
+  snprintf(t, sizeof t, "%08u", base);
+  sb_str(b, rule ? "rule" : "goal");
+  sb_str(b, t);
+}
+
+int synth_write_molly(const char *dir, uint32_t n_runs, const uint32_t *iteration, const uint8_t *status_ok,
+                      const uint64_t *node_off, const uint64_t *edge_off, const uint32_t *node_word,
+                      const uint32_t *label, const uint32_t *edge_src, const uint32_t *edge_dst,
+                      const uint32_t *base_id, uint32_t eot, uint32_t nloc, uint32_t nval, const char *const *names,
+                      int threads) {
+  static const char *types[3] = {"single", "next", "async"};
+  int bad = 0;
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : bad)
+  for (int64_t g = 0; g < 2 * (int64_t)n_runs; g++) {
+    const uint32_t r = (uint32_t)(g / 2);
+    const char *cond = g % 2 ? "post" : "pre";
+    const uint64_t n0 = node_off[g], n1 = node_off[g + 1], e0 = edge_off[g], e1 = edge_off[g + 1];
+    sbuf b = {0, 0, 0};
+    sb_str(&b, "{\"goals\": [");
+    int first = 1;
+    for (uint64_t v = n0; v < n1; v++) {
+      if (node_word[v] & NEMO_NODE_RULE) continue;
+      sb_str(&b, first ? "{\"id\": \"" : ", {\"id\": \"");
+      first = 0;
+      sb_id(&b, 0, base_id[v]);
+      sb_str(&b, "\", \"label\": \"");
+      int64_t t = 0;
+      sb_label(&b, label[v], names, eot, nloc, nval, &t);
+      sb_str(&b, "\", \"table\": \"");
+      sb_str(&b, names[node_word[v] & NEMO_TABLE_MASK]);
+      sb_str(&b, "\", \"time\": \"");
+      sb_i(&b, t);
+      sb_str(&b, "\"}");
+    }
+    sb_str(&b, "], \"rules\": [");
+    first = 1;
+    for (uint64_t v = n0; v < n1; v++) {
+      if (!(node_word[v] & NEMO_NODE_RULE)) continue;
+      sb_str(&b, first ? "{\"id\": \"" : ", {\"id\": \"");
+      first = 0;
+      sb_id(&b, 1, base_id[v]);
+      sb_str(&b, "\", \"label\": \"");
+      sb_label(&b, label[v], names, eot, nloc, nval, NULL);
+      sb_str(&b, "\", \"table\": \"");
+      sb_str(&b, names[node_word[v] & NEMO_TABLE_MASK]);
+      sb_str(&b, "\", \"type\": \"");
+      sb_str(&b, types[((node_word[v] >> NEMO_TYPE_SHIFT) & 7u) % 3]);
+      sb_str(&b, "\"}");
+    }
+    sb_str(&b, "], \"edges\": [");
+    for (uint64_t e = e0; e < e1; e++) {
+      const uint64_t s = n0 + edge_src[e], d = n0 + edge_dst[e];
+      sb_str(&b, e == e0 ? "{\"from\": \"" : ", {\"from\": \"");
+      sb_id(&b, (node_word[s] & NEMO_NODE_RULE) != 0, base_id[s]);
+      sb_str(&b, "\", \"to\": \"");
+      sb_id(&b, (node_word[d] & NEMO_NODE_RULE) != 0, base_id[d]);
+      sb_str(&b, "\"}");
+    }
+    sb_str(&b, "]}");
+    char path[4096];
+    snprintf(path, sizeof path, "%s/run_%u_%s_provenance.json", dir, r, cond);
+    FILE *f = fopen(path, "wb");
+    if (!f || fwrite(b.p, 1, b.n, f) != b.n) bad |= 1;
+    if (f) fclose(f);
+    free(b.p);
+  }
+  /* runs.json */
+  sbuf b = {0, 0, 0};
+  sb_str(&b, "[");
+  for (uint32_t r = 0; r < n_runs; r++) {
+    sb_str(&b, r ? ", {\"iteration\": " : "{\"iteration\": ");
+    sb_u(&b, iteration[r]);
+    sb_str(&b, status_ok[r] ? ", \"status\": \"success\"" : ", \"status\": \"failure\"");
+    sb_str(&b, ", \"failureSpec\": {\"eot\": ");
+    sb_u(&b, eot);
+    sb_str(&b, ", \"eff\": ");
+    sb_u(&b, eot > 3 ? eot - 2 : 1);
+    sb_str(&b, ", \"maxCrashes\": 0, \"nodes\": [");
+    for (uint32_t i = 0; i < nloc; i++) {
+      sb_str(&b, i ? ", \"n" : "\"n");
+      sb_u(&b, i);
+      sb_str(&b, "\"");
+    }
+    sb_str(&b, "], \"crashes\": [], \"omissions\": []}, \"model\": {\"tables\": {\"pre\": [[\"n0\", \"");
+    sb_u(&b, eot);
+    sb_str(&b, "\"]], \"post\": [[\"n0\", \"");
+    sb_u(&b, eot);
+    sb_str(&b, "\"]]}}, \"messages\": []}");
+  }
+  sb_str(&b, "]");
+  char path[4096];
+  snprintf(path, sizeof path, "%s/runs.json", dir);
+  FILE *f = fopen(path, "wb");
+  if (!f || fwrite(b.p, 1, b.n, f) != b.n) bad |= 1;
+  if (f) fclose(f);
+  free(b.p);
+  return bad ? -1 : 0;
 }

@@ -135,6 +135,27 @@ def label_string(lab: int, info: SynthInfo) -> str:
     return f"{name}(n{loc}, v{val}, {t})"
 
 
+def write_molly(corpus: Corpus, info: SynthInfo, out_dir: str, threads: Optional[int] = None) -> None:
+    """to_molly in C (libnemosynth synth_write_molly): the same files, byte for byte, one file per
+    OpenMP task -- fast enough to stage the bench's end-to-end input."""
+    L = lib()
+    if not getattr(L, "_wm", False):
+        vp = ctypes.c_void_p
+        L.synth_write_molly.argtypes = [ctypes.c_char_p, ctypes.c_uint32] + [vp] * 9 + \
+                                       [ctypes.c_uint32] * 3 + [vp, ctypes.c_int]
+        L.synth_write_molly.restype = ctypes.c_int
+        L._wm = True
+    os.makedirs(out_dir, exist_ok=True)
+    ok = np.ascontiguousarray([s == "success" for s in corpus.status], dtype=np.uint8)
+    names = (ctypes.c_char_p * len(TABLE_NAMES))(*[n.encode() for n in TABLE_NAMES])
+    arrs = [corpus.iteration, ok, corpus.node_off, corpus.edge_off, corpus.node_word, corpus.label,
+            corpus.edge_src, corpus.edge_dst, np.ascontiguousarray(info.base_id)]
+    rc = L.synth_write_molly(out_dir.encode(), corpus.n_runs, *[a.ctypes.data for a in arrs], info.eot, info.nloc,
+                             info.nval, ctypes.cast(names, ctypes.c_void_p), int(threads or min(16, os.cpu_count() or 1)))
+    if rc != 0:
+        raise OSError(f"synth_write_molly failed writing {out_dir}")
+
+
 def to_molly(corpus: Corpus, info: SynthInfo, out_dir: str) -> None:
     """Write a Molly-format output directory (runs.json + run_<i>_{pre,post}_provenance.json),
     the layout faultinjectors/molly.go:18,59-60 reads."""
