@@ -148,12 +148,40 @@ def mark_condition_holds(db: DB, run: int, C: str) -> None:
                 db.nodes[n].props["condition_holds"] = True
 
 
+class Namespaces:
+    """The `run` property values of the derived graphs and the numbers their IDs are printed with.
+
+    REFERENCE is the reference verbatim: the clean copy of run i is run 1000+i
+    (preprocessing.go:15,33,45), the diff graph of failed run f is run 2000+f
+    (differential-provenance.go:40) and the raw runs are those with run < 1000
+    (extensions.go:27); with >= 1000 runs these collide.
+    PER_RUN keeps every derived graph in a namespace of its own (the `run`
+    property is a (kind, iteration) pair) while IDs are still printed as
+    run_<1000+i> / run_<2000+f>: the semantics libnemohip implements."""
+
+    def __init__(self, tagged: bool):
+        self.tagged = tagged
+
+    def clean(self, it: int):
+        return ("clean", it) if self.tagged else 1000 + it
+
+    def diff(self, f: int):
+        return ("diff", f) if self.tagged else 2000 + f
+
+    def is_raw(self, run) -> bool:
+        return isinstance(run, int) if self.tagged else run < 1000
+
+
+REFERENCE = Namespaces(False)
+PER_RUN = Namespaces(True)
+
+
 def _rewrite_id(s: str, old: int, new: int) -> str:
     pfx = f"run_{old}"
     return f"run_{new}" + s[len(pfx):] if s.startswith(pfx) else s
 
 
-def clean_copy_prov(db: DB, it: int, C: str) -> Dict[int, int]:
+def clean_copy_prov(db: DB, it: int, C: str, ns: Namespaces = REFERENCE) -> Dict[int, int]:
     """preprocessing.go:13-63: export every (g1:Goal)-[*0..]->(g2:Goal) path, sed run/id, re-import."""
     nodes, rels = set(), set()
     for g1 in db.match("Goal", run=it, condition=C):
@@ -164,7 +192,7 @@ def clean_copy_prov(db: DB, it: int, C: str) -> Dict[int, int]:
     copy: Dict[int, int] = {}
     for n in sorted(nodes):
         props = dict(db.nodes[n].props)
-        props["run"] = 1000 + it
+        props["run"] = ns.clean(it)
         props["id"] = _rewrite_id(props["id"], it, 1000 + it)
         copy[n] = db.create(db.nodes[n].label, props)
     for a, b in sorted(rels):
@@ -173,9 +201,10 @@ def clean_copy_prov(db: DB, it: int, C: str) -> Dict[int, int]:
 
 
 def collapse_next_chains(db: DB, it: int, C: str,
-                         tie_key: Optional[Callable[[List[int]], object]] = None) -> List[dict]:
+                         tie_key: Optional[Callable[[List[int]], object]] = None,
+                         ns: Namespaces = REFERENCE) -> List[dict]:
     """preprocessing.go:66-348, literally (tie order of ORDER BY len DESC via tie_key)."""
-    run = 1000 + it
+    run = ns.clean(it)
     okn = lambda n: db.nodes[n].props.get("type") == "next" or "type" not in db.nodes[n].props
     groups: Dict[Tuple[int, ...], List[int]] = {}
     for r1 in db.match("Rule", run=run, condition=C, type="next"):
@@ -200,7 +229,7 @@ def collapse_next_chains(db: DB, it: int, C: str,
     for i, ch in enumerate(chains):
         table = db.prop(ch[0], "table")
         label = f"{table}_collapsed"
-        cid = f"run_{run}_{C}_{label}_{i}"
+        cid = f"run_{1000 + it}_{C}_{label}_{i}"
         c = db.create("Rule", {"run": run, "condition": C, "id": cid, "label": label, "table": table,
                                "type": "collapsed"})
         if not preds[i] or not succs[i]:
@@ -224,11 +253,11 @@ def collapse_next_chains(db: DB, it: int, C: str,
     return created
 
 
-def extract_protos_lists(db: DB, iters: Sequence[int], C: str) -> List[List[str]]:
+def extract_protos_lists(db: DB, iters: Sequence[int], C: str, ns: Namespaces = REFERENCE) -> List[List[str]]:
     """prototype.go:11-76: per success run, the list of distinct rule tables."""
     lists = []
     for it in iters:
-        run = 1000 + it
+        run = ns.clean(it)
         gate = len(db.match("Goal", run=run, condition="pre", condition_holds=True)) > 0
         paths = []
         for root in db.match("Goal", run=run, condition=C):
@@ -279,18 +308,18 @@ def protos_from_lists(iter_prov: List[List[str]], condition: str) -> Tuple[List[
     return inter, union
 
 
-def missing_from(db: DB, proto: List[str], failed_iter: int, C: str) -> List[str]:
+def missing_from(db: DB, proto: List[str], failed_iter: int, C: str, ns: Namespaces = REFERENCE) -> List[str]:
     """prototype.go:141-206."""
-    tabs = {db.prop(r, "table") for r in db.match("Rule", run=1000 + failed_iter, condition=C)}
+    tabs = {db.prop(r, "table") for r in db.match("Rule", run=ns.clean(failed_iter), condition=C)}
     return [f"<code>{p}</code>" for p in proto if p not in tabs]
 
 
-def naive_diff_prov(db: DB, failed_runs: Sequence[int]) -> List[dict]:
+def naive_diff_prov(db: DB, failed_runs: Sequence[int], ns: Namespaces = REFERENCE) -> List[dict]:
     """differential-provenance.go:18-146, including the in-place ###RUN### substitution (:43)."""
     res = []
     source = failed_runs[0] if failed_runs else None  # stale substitution: every export uses failedRuns[0]
     for f in failed_runs:
-        diff_run = 2000 + f
+        diff_run = ns.diff(f)
         fail_goals = [db.prop(n, "label") for n in db.match("Goal", run=source, condition="post")]
         nodes, rels = set(), set()
         for root in db.match("Goal", run=0, condition="post"):
@@ -304,7 +333,7 @@ def naive_diff_prov(db: DB, failed_runs: Sequence[int]) -> List[dict]:
         for n in sorted(nodes):
             props = dict(db.nodes[n].props)
             props["run"] = diff_run
-            props["id"] = _rewrite_id(props["id"], 0, diff_run)
+            props["id"] = _rewrite_id(props["id"], 0, 2000 + f)
             copy[n] = db.create(db.nodes[n].label, props)
         for a, b in sorted(rels):
             db.merge(copy[a], copy[b])
@@ -328,7 +357,7 @@ def naive_diff_prov(db: DB, failed_runs: Sequence[int]) -> List[dict]:
                 leaves = sorted(x for x in db.out[r] if db.is_(x, "Goal", run=diff_run, condition="post"))
                 missing.append({"rule": r, "goals": leaves})
         inv = {v: k for k, v in copy.items()}
-        res.append({"run": diff_run, "nodes": set(nodes), "copy": copy, "inv": inv, "missing": missing,
+        res.append({"run": diff_run, "id_run": 2000 + f, "nodes": set(nodes), "copy": copy, "inv": inv, "missing": missing,
                     "edges": {(a, b) for a in copy.values() for b in db.out[a]}})
     return res
 
@@ -363,10 +392,10 @@ def find_post_triggers(db: DB, run: int) -> List[Tuple[int, int]]:
     return rows
 
 
-def extensions(db: DB, n_runs: int) -> Tuple[bool, List[int]]:
+def extensions(db: DB, n_runs: int, ns: Namespaces = REFERENCE) -> Tuple[bool, List[int]]:
     """extensions.go:25-90 (rule list only; strings are built by the host)."""
     pres = [n for n in db.match("Goal", condition="pre", table="pre", condition_holds=True)
-            if db.prop(n, "run") < 1000]
+            if ns.is_raw(db.prop(n, "run"))]
     all_achieved = not (len(pres) < n_runs)
     rules = []
     for r in db.match("Rule", run=0, condition="pre", type="async"):
@@ -379,10 +408,12 @@ def extensions(db: DB, n_runs: int) -> Tuple[bool, List[int]]:
     return all_achieved, rules
 
 
-def run_reference_pipeline(runs: Sequence[Tuple[int, str, dict, dict]], tie_key=None) -> dict:
+def run_reference_pipeline(runs: Sequence[Tuple[int, str, dict, dict]], tie_key=None,
+                           ns: Namespaces = REFERENCE) -> dict:
     """main.go:106-177's call order over the literal evaluator.
 
-    `runs`: [(iteration, status, pre_prov, post_prov)] with Molly-prefixed IDs."""
+    `runs`: [(iteration, status, pre_prov, post_prov)] with Molly-prefixed IDs.
+    `ns`: the derived graphs' namespaces (REFERENCE, or PER_RUN for >= 1000 runs)."""
     db = DB()
     raw: Dict[Tuple[int, str], Dict[str, int]] = {}
     for it, _, pre, post in runs:
@@ -393,21 +424,21 @@ def run_reference_pipeline(runs: Sequence[Tuple[int, str, dict, dict]], tie_key=
     holds = {k: {i: db.prop(n, "condition_holds") for i, n in v.items()} for k, v in raw.items()}
     clean, chains = {}, {}
     for it, _, _, _ in runs:
-        clean[(it, "pre")] = clean_copy_prov(db, it, "pre")
-        clean[(it, "post")] = clean_copy_prov(db, it, "post")
-        chains[(it, "pre")] = collapse_next_chains(db, it, "pre", tie_key)
-        chains[(it, "post")] = collapse_next_chains(db, it, "post", tie_key)
+        clean[(it, "pre")] = clean_copy_prov(db, it, "pre", ns)
+        clean[(it, "post")] = clean_copy_prov(db, it, "post", ns)
+        chains[(it, "pre")] = collapse_next_chains(db, it, "pre", tie_key, ns)
+        chains[(it, "post")] = collapse_next_chains(db, it, "post", tie_key, ns)
     success = [it for it, st, _, _ in runs if st == "success"]
     failed = [it for it, st, _, _ in runs if st != "success"]
-    lists = extract_protos_lists(db, success, "post")
+    lists = extract_protos_lists(db, success, "post", ns)
     inter, union = protos_from_lists(lists, "post") if success else (None, None)
-    inter_miss = [missing_from(db, inter, f, "post") for f in failed] if success else None
-    union_miss = [missing_from(db, union, f, "post") for f in failed] if success else None
-    diffs = naive_diff_prov(db, failed)
+    inter_miss = [missing_from(db, inter, f, "post", ns) for f in failed] if success else None
+    union_miss = [missing_from(db, union, f, "post", ns) for f in failed] if success else None
+    diffs = naive_diff_prov(db, failed, ns)
     pre_trig = find_pre_triggers(db, 0)
     post_trig = find_post_triggers(db, 0)
-    all_pre, async_rules = extensions(db, len(runs))
-    return {"db": db, "raw": raw, "holds": holds, "clean": clean, "chains": chains, "lists": lists,
+    all_pre, async_rules = extensions(db, len(runs), ns)
+    return {"db": db, "ns": ns, "raw": raw, "holds": holds, "clean": clean, "chains": chains, "lists": lists,
             "success": success, "failed": failed, "inter": inter, "union": union, "inter_miss": inter_miss,
             "union_miss": union_miss, "diffs": diffs, "pre_trig": pre_trig, "post_trig": post_trig,
             "all_pre": all_pre, "async_rules": async_rules}

@@ -61,14 +61,15 @@ def create_dot(db: DB, edges: Sequence[Tuple[int, int]], graph_type: str) -> Can
     return nodes, out
 
 
-def pull_pre_post(db: DB, iters: Sequence[int]) -> List[Dict[str, Canon]]:
-    """PullPrePostProv (pre-post-prov.go:288-459)."""
+def pull_pre_post(db: DB, iters: Sequence[int], ns=None) -> List[Dict[str, Canon]]:
+    """PullPrePostProv (pre-post-prov.go:288-459); clean copies in `ns` (cypher_literal.Namespaces)."""
+    clean = ns.clean if ns is not None else (lambda it: 1000 + it)
     res = []
     for it in iters:
         res.append({"pre": create_dot(db, q24_edges(db, it, "pre"), "pre"),
                     "post": create_dot(db, q24_edges(db, it, "post"), "post"),
-                    "pre_clean": create_dot(db, q24_edges(db, 1000 + it, "pre"), "pre"),
-                    "post_clean": create_dot(db, q24_edges(db, 1000 + it, "post"), "post")})
+                    "pre_clean": create_dot(db, q24_edges(db, clean(it), "pre"), "pre"),
+                    "post_clean": create_dot(db, q24_edges(db, clean(it), "post"), "post")})
     return res
 
 
@@ -94,7 +95,7 @@ def create_diff_dot(db: DB, d: dict, failed_run: int, success_post: Canon) -> Tu
     for m in d["missing"]:
         missing.add(db.prop(m["rule"], "id"))
         missing.update(db.prop(x, "id") for x in m["goals"])
-    rn = lambda s: s.replace("run_0", f"run_{diff_run}")
+    rn = lambda s: s.replace("run_0", f"run_{d['id_run']}")
     views = []
     for _ in range(2):
         nodes = {rn(k): dict(v, style=_q("invis")) for k, v in success_post[0].items()}

@@ -165,12 +165,52 @@ def fixtures():
             and any("buffer_snd(y), ...)" in s for s in out) and not any("buffer_tick" in s for s in out)
             for out in x["corrections"]),
     }
+    # Q-NS-1000: 1002 runs.  The reference's derived
+    # graphs live at run 1000+i (clean copy, preprocessing.go:15) and 2000+f (diff
+    # graph, differential-provenance.go:40), so run 0's clean copy lands on raw run
+    # 1000 and extensions.go:27's `run < 1000` drops the raw runs >= 1000.  The build
+    # keeps every derived graph in its own namespace: the expected values are the
+    # literal evaluation with per-run namespaces, and the check shows (a) the
+    # reference namespaces give a different answer here, (b) runs 1000/1001 get
+    # exactly the results they get as runs 1/2 of a three-run corpus.
+    pre = prov(*cond_pattern("pre"))
+    good = prov([G(0, "post", "post(n, 3)", "3"), G(2, "log", "log(n, 2)", "2"), G(4, "ack", "ack(n, 1)", "1"),
+                 G(6, "vote", "vote(n, 1)", "1"), G(8, "commit", "commit(n, 1)", "1")],
+                [R(1, "post"), R(3, "log", "async"), R(7, "vote")],
+                [E("goal0", "rule1"), E("rule1", "goal2"), E("goal2", "rule3"), E("rule3", "goal4"),
+                 E("rule3", "goal6"), E("goal6", "rule7"), E("rule7", "goal8")])
+    f1 = prov([G(0, "post", "post(n, 3)", "3"), G(2, "log", "log(n, 2)", "2"), G(4, "ack", "ack(n, 1)", "1")],
+              [R(1, "post"), R(3, "log", "async")],
+              [E("goal0", "rule1"), E("rule1", "goal2"), E("goal2", "rule3"), E("rule3", "goal4")])
+    f2 = prov([G(0, "post", "post(n, 3)", "3")], [], [])
+    ns_runs = [(0, "success", pre, good)] + [(i, "success", EMPTY, EMPTY) for i in range(1, 1000)] + \
+              [(1000, "failure", pre, f1), (1001, "failure", pre, f2)]
+    fx["q_ns_1000"] = {"runs": ns_runs, "ns": CL.PER_RUN, "digests": True, "check": _check_ns(ns_runs)}
     return fx
 
 
-def expected(runs, digests=False):
+def _check_ns(runs):
+    def strip(ids):
+        return sorted("_".join(x.split("_")[2:]) for x in ids)
+
+    def check(x):
+        # the reference's own namespaces: cleanCopyProv of run 1000 also copies run 0's clean copy (run 1000)
+        ref = CL.run_reference_pipeline([(it, st, _molly_prefix(pre, it, "pre"), _molly_prefix(post, it, "post"))
+                                         for it, st, pre, post in runs])
+        raw1000 = set(ref["raw"][(1000, "post")].values())
+        differs = any(n not in raw1000 for n in ref["clean"][(1000, "post")])
+        small = expected([runs[0], (1,) + runs[1000][1:], (2,) + runs[1001][1:]], digests=True, ns=CL.PER_RUN)
+        same = (x["diff"] == small["diff"] and x["missing"] == small["missing"] and x["inter"] == small["inter"]
+                and strip(x["clean"][1000]) == strip(small["clean"][1]) and strip(x["clean"][1001]) ==
+                strip(small["clean"][2]) and x["lists"]["0"] == small["lists"]["0"] and x["pre_rows"] ==
+                small["pre_rows"] and x["post_rows"] == small["post_rows"])
+        return differs and same and len(x["clean"]) == 1002
+    return check
+
+
+def expected(runs, digests=False, ns=CL.REFERENCE):
     pruns = [(it, st, _molly_prefix(pre, it, "pre"), _molly_prefix(post, it, "post")) for it, st, pre, post in runs]
-    lit = CL.run_reference_pipeline(pruns)
+    lit = CL.run_reference_pipeline(pruns, ns=ns)
     db = lit["db"]
     out = {"holds": {}, "clean": [], "deleted": [], "chains": {}, "lists": {}}
     for it, _, _, _ in runs:
@@ -210,6 +250,8 @@ def expected(runs, digests=False):
         out["async"] = sorted(invp[r] for r in lit["async_rules"])
     out["all_pre"] = lit["all_pre"]
     out.update(host_expected(lit, runs, digests))
+    if ns is not CL.REFERENCE:
+        out["namespaces"] = "per_run"
     return out
 
 
@@ -230,13 +272,14 @@ def write(name, spec):
                           "failureSpec": {"eot": 4, "eff": 2, "maxCrashes": 0, "nodes": ["n"], "crashes": [],
                                           "omissions": []},
                           "model": {"tables": {"pre": [["n", "3"]], "post": [["n", "3"]]}}, "messages": []})
+        ind = None if len(spec["runs"]) > 100 else 1
         with open(os.path.join(d, f"run_{i}_pre_provenance.json"), "w") as fh:
-            json.dump(pre, fh, indent=1)
+            json.dump(pre, fh, indent=ind)
         with open(os.path.join(d, f"run_{i}_post_provenance.json"), "w") as fh:
-            json.dump(post, fh, indent=1)
+            json.dump(post, fh, indent=ind)
     with open(os.path.join(d, "runs.json"), "w") as fh:
-        json.dump(runs_json, fh, indent=1)
-    exp = expected(spec["runs"])
+        json.dump(runs_json, fh, indent=1 if len(spec["runs"]) <= 100 else None)
+    exp = expected(spec["runs"], spec.get("digests", False), spec.get("ns", CL.REFERENCE))
     assert spec["check"](exp), f"{name}: hand-derived property does not hold: {json.dumps(exp)[:400]}"
     with open(os.path.join(d, "expected.json"), "w") as fh:
         json.dump(exp, fh, indent=1, sort_keys=True)
@@ -244,6 +287,9 @@ def write(name, spec):
 
 
 if __name__ == "__main__":
+    only = sys.argv[1:]
     for name, spec in fixtures().items():
+        if only and name not in only:
+            continue
         write(name, spec)
         print("wrote", name)

@@ -61,7 +61,7 @@ def host_expected(lit, runs, digests: bool = False):
     With `digests`, the DOT views are stored as `<key>_sha256` digests."""
     db = lit["db"]
     iters = [it for it, _, _, _ in runs]
-    dots = HL.pull_pre_post(db, iters)
+    dots = HL.pull_pre_post(db, iters, lit.get("ns"))
     out = {"dots": [{k: _canon_json(v) for k, v in d.items()} for d in dots]}
     out["diff_dots"], out["failed_dots"], out["missing_events"] = [], [], []
     for f, d in zip(lit["failed"], lit["diffs"]):
