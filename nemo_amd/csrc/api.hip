@@ -559,7 +559,7 @@ static void set_lds_tier(nemo_ctx *c) {
 
 // k_build's LDS caps: the largest graphs, smallest first, whose build image
 // (k_load.hip build_tier_bytes) keeps four workgroups on a CU.
-#define BUILD_TIER_BUDGET (40u * 1024u - 64u)
+#define BUILD_TIER_BUDGET (160u * 1024u / 4u - 64u)
 static void set_build_tier(nemo_ctx *c) {
   std::vector<std::pair<uint32_t, uint32_t>> ve;
   ve.reserve(c->G);

@@ -51,6 +51,20 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 #define BLD_EPT 32  // edges per thread held in registers (bld_e <= BLD_EPT * NEMO_BLOCK)
 #define BLD_KB 4    // Kahn: children of a node processed per round
 
+#define BLD_RS 8    // row entries sorted in registers (longer rows: insertion sort in LDS)
+
+// 19-comparator sorting network for 8 keys (pads 0xFFFF sort last)
+__device__ __forceinline__ void sort_net8(uint32_t *x) {
+  constexpr int P[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
+                            {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+  for (int k = 0; k < 19; k++) {
+    const uint32_t a = x[P[k][0]], b = x[P[k][1]];
+    x[P[k][0]] = min(a, b);
+    x[P[k][1]] = max(a, b);
+  }
+}
+
 __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
   return lds_align(4u * ((v + 31u) / 32u)) + lds_align(2u * (v + 2u)) + lds_align(2u * e) + lds_align(v) +
          lds_align(2u * v);
@@ -71,7 +85,7 @@ __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint3
   return c.bld_bytes != 0u && V <= c.bld_v && E <= c.bld_e;
 }
 
-__global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
+__global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_bad, s_created, s_tail, s_cnt[3];
@@ -143,6 +157,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
     uint32_t *optr = dir ? c.fp + n0 + g : c.rp + n0 + g, *ocol = dir ? c.fc + e0 : c.rc + e0;
     for (uint32_t w = tid; w < (V + 2) / 2; w += NEMO_BLOCK) ptr32[w] = 0;
     __syncthreads();
+    if (dir == 0) STAMP(0);
 #pragma unroll
     for (int q = 0; q < BLD_EPT; q++)
       if (tid + q * NEMO_BLOCK < E) {
@@ -150,6 +165,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
         atomicAdd(&ptr32[k >> 1], 1u << (16 * (k & 1)));
       }
     __syncthreads();
+    if (dir == 0) STAMP(1);
     if (dir == 0) {  // in-degrees; a graph beyond the u8 counters goes to the global tier
       bool heavy = false;
       for (uint32_t w = tid; 4 * w < V; w += NEMO_BLOCK) {
@@ -169,9 +185,12 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
         return;
       }
     }
+    if (dir == 0) STAMP(2);
     block_scan_inplace(ptr, V + 1, s_lds);
+    if (dir == 0) STAMP(3);
     for (uint32_t v = tid; v <= V; v += NEMO_BLOCK) optr[v] = ptr[v];
     __syncthreads();
+    if (dir == 0) STAMP(4);
 #pragma unroll
     for (int q = 0; q < BLD_EPT; q++)
       if (tid + q * NEMO_BLOCK < E) {
@@ -179,27 +198,64 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
         col[(atomicAdd(&ptr32[k >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)((sd[q] >> vs) & 0xFFFFu);
       }
     __syncthreads();
-    for (uint32_t v = tid; v < V; v += NEMO_BLOCK) {
-      const uint32_t a = v ? ptr[v - 1] : 0u, b = ptr[v];
-      for (uint32_t i = a + 1; i < b; i++) {
-        const uint16_t x = col[i];
-        uint32_t j = i;
-        while (j > a && col[j - 1] > x) {
-          col[j] = col[j - 1];
-          j--;
-        }
-        col[j] = x;
+    if (dir == 0) STAMP(5);
+    // sort every row; two rows per thread at a time with all their LDS reads
+    // issued together, the entries sorted in registers (a latency chain of a
+    // few LDS round trips instead of one per entry)
+    for (uint32_t v0 = tid; v0 < V; v0 += 2 * NEMO_BLOCK) {
+      uint32_t a[2], n[2], x[2][BLD_RS];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t v = v0 + q * NEMO_BLOCK;
+        a[q] = v < V && v ? ptr[v - 1] : 0u;
+        n[q] = v < V ? ptr[v] - a[q] : 0u;
       }
-      if (dir == 0) {  // relationships created (pre-post-prov.go:150-210): distinct, goal<->rule
-        const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
-        for (uint32_t i = a; i < b; i++) {
-          const uint32_t t = col[i];
-          const bool rt = (s_rule[t >> 5] >> (t & 31)) & 1u;
-          if (!(i > a && col[i - 1] == t) && rv != rt) created++;
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int i = 0; i < BLD_RS; i++) x[q][i] = (uint32_t)i < n[q] ? col[a[q] + i] : 0xFFFFu;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t v = v0 + q * NEMO_BLOCK, b = a[q] + n[q];
+        if (n[q] <= BLD_RS) {
+          if (n[q] >= 2) {
+            sort_net8(x[q]);
+#pragma unroll
+            for (int i = 0; i < BLD_RS; i++)
+              if ((uint32_t)i < n[q]) col[a[q] + i] = (uint16_t)x[q][i];
+          }
+          if (dir == 0 && n[q]) {  // relationships created (pre-post-prov.go:150-210): distinct, goal<->rule
+            const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
+#pragma unroll
+            for (int i = 0; i < BLD_RS; i++) {
+              const uint32_t t = x[q][i];
+              if ((uint32_t)i < n[q] && !(i > 0 && x[q][i - 1] == t) && rv != ((s_rule[t >> 5] >> (t & 31)) & 1u))
+                created++;
+            }
+          }
+          continue;
+        }
+        for (uint32_t i = a[q] + 1; i < b; i++) {  // long row: insertion sort in LDS
+          const uint16_t y = col[i];
+          uint32_t j = i;
+          while (j > a[q] && col[j - 1] > y) {
+            col[j] = col[j - 1];
+            j--;
+          }
+          col[j] = y;
+        }
+        if (dir == 0) {
+          const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
+          for (uint32_t i = a[q]; i < b; i++) {
+            const uint32_t t = col[i];
+            const bool rt = (s_rule[t >> 5] >> (t & 31)) & 1u;
+            if (!(i > a[q] && col[i - 1] == t) && rv != rt) created++;
+          }
         }
       }
     }
     __syncthreads();
+    if (dir == 0) STAMP(6);
     for (uint32_t j = tid; j < E; j += NEMO_BLOCK) ocol[j] = col[j];
     __syncthreads();
     STAMP(12 + dir);
@@ -232,7 +288,9 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
         j = u ? ptr[u - 1] : 0u;
         je = ptr[u];
       }
-      // children BLD_KB at a time: their LDS reads and counter atomics are independent
+      // children BLD_KB at a time: their LDS reads and counter atomics are
+      // independent, and the ready ones of all BLD_KB slots take one append
+      // (ballots per slot, one counter atomic per wave)
       while (__any(j < je)) {
         uint32_t ch[BLD_KB], old[BLD_KB];
 #pragma unroll
@@ -243,11 +301,25 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_build(DevCorpus c) {
           old[q] = ch[q] != 0xFFFFu ? (atomicSub(&cnt32[ch[q] >> 2], 1u << sh) >> sh) & 0xFFu : 0u;
         }
         j = min(j + BLD_KB, je);
+        uint64_t m[BLD_KB];
+        uint32_t pre[BLD_KB], tot = 0;
 #pragma unroll
         for (int q = 0; q < BLD_KB; q++) {
-          const bool p = old[q] == 1u;
-          lds_append16(p, ch[q], q16 + hi, cur);
-          if (p) nlv[ch[q]] = nl + 1;
+          m[q] = __ballot(old[q] == 1u);
+          pre[q] = tot;
+          tot += (uint32_t)__popcll(m[q]);
+        }
+        if (tot) {
+          const int leader = __ffsll((long long)__ballot(1)) - 1;
+          uint32_t b = 0;
+          if ((int)lane_id() == leader) b = atomicAdd(cur, tot);
+          b = hi + __builtin_amdgcn_readlane(b, leader);
+#pragma unroll
+          for (int q = 0; q < BLD_KB; q++)
+            if (old[q] == 1u) {
+              q16[b + pre[q] + mbcnt(m[q])] = (uint16_t)ch[q];
+              nlv[ch[q]] = nl + 1;
+            }
         }
       }
     }

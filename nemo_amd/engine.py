@@ -47,6 +47,14 @@ def lib():
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libnemohip.so not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 under another file name,
+        # so loading libnemohip (which resolves /opt/rocm's libamdhip64.so.7) before torch would leave
+        # torch with a second runtime that cannot open the device ("No HIP GPUs are available").
+        # Loading torch first makes libnemohip bind to the runtime torch already holds (same soname).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u32, u64, sz, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int
         P = ctypes.POINTER

@@ -186,10 +186,33 @@ def test_build_tiers(eng, build_max):
         eng.set_option("build_lds_max", -1)
 
 
-def test_build_tiers_identical_device_arrays(eng):
-    # both tiers must produce the same CSR rows, Kahn order and level offsets
+def _long_graph(n, tag):
+    """goal0 -> rule0 -> goal1 -> ... (2n Kahn levels) with a side branch per step, as Molly JSON."""
+    goals = [{"id": f"goal{i}", "label": f"log(a, {i}, {tag})", "table": "log" if i else "post", "time": str(n - i)}
+             for i in range(n + 1)]
+    goals += [{"id": f"goals{i}", "label": f"ack(a, {i})", "table": "ack", "time": "1"} for i in range(0, n, 7)]
+    rules = [{"id": f"rule{i}", "label": "log", "table": "log", "type": "next" if i % 5 else "single"} for i in range(n)]
+    edges = []
+    for i in range(n):
+        edges += [{"from": f"goal{i}", "to": f"rule{i}"}, {"from": f"rule{i}", "to": f"goal{i + 1}"}]
+        if i % 7 == 0:
+            edges.append({"from": f"rule{i}", "to": f"goals{i}"})
+    return {"goals": goals, "rules": rules, "edges": edges}
+
+
+@pytest.mark.parametrize("shape", ["synthetic", "long"])
+def test_build_tiers_identical_device_arrays(eng, shape):
+    # both tiers must produce the same CSR rows, Kahn order and level offsets; the long graphs
+    # have more Kahn levels than k_build sweeps (BLD_MAXLV) and are redone by the global tier
     from tools import synth
-    corpus, _ = synth.generate(12, target_nodes=2500)
+    if shape == "long":
+        runs = [(0, "success", _long_graph(150, 0), _long_graph(400, 0)),
+                (1, "failure", _long_graph(90, 1), _long_graph(300, 1)),
+                (2, "success", _long_graph(20, 0), _long_graph(600, 0))]
+        corpus = corpus_from_graphs(runs)
+        _check(eng, corpus, mode=DIFF_REFERENCE, pulls=True)
+    else:
+        corpus, _ = synth.generate(12, target_nodes=2500)
     V, E, G = int(corpus.node_off[-1]), int(corpus.edge_off[-1]), corpus.n_graphs
     sizes = {"topo": 4 * V, "lvl": 4 * (V + G), "nlev": 4 * G, "fp": 4 * (V + G), "fc": 4 * E,
              "rp": 4 * (V + G), "rc": 4 * E}
@@ -203,6 +226,8 @@ def test_build_tiers_identical_device_arrays(eng):
             eng.set_option("build_lds_max", -1)
     for k in ("nlev", "fp", "fc", "rp", "rc"):
         assert np.array_equal(got[-1][k], got[0][k]), k
+    if shape == "long":
+        assert int(got[-1]["nlev"].max()) > 256
     # Kahn order inside a level depends on wave timing: compare level sets
     a, b, lv = got[-1]["topo"], got[0]["topo"], got[-1]["lvl"]
     for g in range(G):

@@ -25,3 +25,8 @@ print("graphs", ok.sum(), "cycles per graph: median", np.median(d.sum(1)), "p90"
 for i, nm in enumerate(names):
     print(f"{nm:14s} median {np.median(d[:, i]):10.0f}  share {d[:, i].sum() / d.sum():.3f}")
 print("levels per graph: median", np.median(nlev), "max", nlev.max())
+sub = ["zero ptr", "count atomics", "indeg pack", "scan", "row ptr store", "scatter", "row sort+dedupe", "col store"]
+b = np.concatenate([st[:, 11:12], st[:, 0:7], st[:, 12:13]], axis=1)[ok]
+db = np.diff(b, axis=1)
+for i, nm in enumerate(sub):
+    print(f"  rev {nm:16s} median {np.median(db[:, i]):9.0f}")
