@@ -89,6 +89,7 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lds[NEMO_WAVES];
   __shared__ uint32_t s_bad, s_created, s_tail, s_cnt[3];
+  __shared__ uint32_t s_sink[64];  // per-lane no-op atomic targets (one bank each: no same-address serialisation)
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
@@ -210,10 +211,14 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
         a[q] = v < V && v ? ptr[v - 1] : 0u;
         n[q] = v < V ? ptr[v] - a[q] : 0u;
       }
+      // unconditional reads at clamped addresses (no branch per entry, all in flight together)
 #pragma unroll
       for (int q = 0; q < 2; q++)
 #pragma unroll
-        for (int i = 0; i < BLD_RS; i++) x[q][i] = (uint32_t)i < n[q] ? col[a[q] + i] : 0xFFFFu;
+        for (int i = 0; i < BLD_RS; i++) {
+          const uint32_t y = col[min(a[q] + i, E - 1u)];
+          x[q][i] = (uint32_t)i < n[q] ? y : 0xFFFFu;
+        }
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const uint32_t v = v0 + q * NEMO_BLOCK, b = a[q] + n[q];
@@ -228,9 +233,9 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
             const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
 #pragma unroll
             for (int i = 0; i < BLD_RS; i++) {
-              const uint32_t t = x[q][i];
-              if ((uint32_t)i < n[q] && !(i > 0 && x[q][i - 1] == t) && rv != ((s_rule[t >> 5] >> (t & 31)) & 1u))
-                created++;
+              const uint32_t t = x[q][i], tw = min(t, V - 1u);
+              const bool rt = (s_rule[tw >> 5] >> (tw & 31)) & 1u;
+              created += (uint32_t)i < n[q] && !(i > 0 && x[q][i - 1] == t) && rv != rt;
             }
           }
           continue;
@@ -282,23 +287,27 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     if (tid == 0) s_cnt[(nl + 1) % 3] = 0;
     for (uint32_t base = lo; base < hi; base += NEMO_BLOCK) {
       const uint32_t i = base + tid;
-      uint32_t j = 0, je = 0;
-      if (i < hi) {
-        const uint32_t u = q16[i];
-        j = u ? ptr[u - 1] : 0u;
-        je = ptr[u];
-      }
+      // branch-free: reads and atomics at clamped / sink addresses, so the
+      // BLD_KB slots' round trips overlap instead of waiting one by one
+      const uint32_t u = q16[min(i, hi - 1u)];
+      const uint32_t pu = ptr[u ? u - 1u : 0u], pe = ptr[u];
+      uint32_t j = i < hi ? (u ? pu : 0u) : 0u, je = i < hi ? pe : 0u;
       // children BLD_KB at a time: their LDS reads and counter atomics are
       // independent, and the ready ones of all BLD_KB slots take one append
       // (ballots per slot, one counter atomic per wave)
       while (__any(j < je)) {
         uint32_t ch[BLD_KB], old[BLD_KB];
 #pragma unroll
-        for (int q = 0; q < BLD_KB; q++) ch[q] = j + q < je ? col[j + q] : 0xFFFFu;
+        for (int q = 0; q < BLD_KB; q++) {
+          const uint32_t y = col[min(j + q, E - 1u)];
+          ch[q] = j + q < je ? y : 0xFFFFu;
+        }
 #pragma unroll
         for (int q = 0; q < BLD_KB; q++) {
+          const bool ok = ch[q] != 0xFFFFu;
           const uint32_t sh = 8 * (ch[q] & 3);
-          old[q] = ch[q] != 0xFFFFu ? (atomicSub(&cnt32[ch[q] >> 2], 1u << sh) >> sh) & 0xFFu : 0u;
+          const uint32_t r = atomicSub(ok ? &cnt32[ch[q] >> 2] : &s_sink[lane_id()], ok ? 1u << sh : 0u);
+          old[q] = ok ? (r >> sh) & 0xFFu : 0u;
         }
         j = min(j + BLD_KB, je);
         uint64_t m[BLD_KB];
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     __syncthreads();
     nl++;
     lo = hi;
-    hi += *(volatile uint32_t *)cur;
+    hi += s_cnt[(nl - 1) % 3];  // after the barrier: plain LDS read
     if (tid == 0) lvl[nl] = lo;
   }
   for (uint32_t i = tid; i < hi; i += NEMO_BLOCK) topo[i] = q16[i];
