@@ -501,7 +501,8 @@ static void set_global_block(nemo_ctx *c) {
 #define LDS_TIER_BUDGET (78u * 1024u)
 #define NO_LEVEL_CAP 0xFFFFFFFFu
 typedef uint32_t (*TierBytes)(uint32_t v, uint32_t e, uint32_t l, uint32_t words);
-static Tier fit_tier(nemo_ctx *c, uint64_t vmax, uint64_t emax, uint32_t lcap, TierBytes bytes) {
+static Tier fit_tier(nemo_ctx *c, uint64_t vmax, uint64_t emax, uint32_t lcap, TierBytes bytes,
+                     uint32_t budget = LDS_TIER_BUDGET) {
   std::vector<std::pair<uint32_t, uint32_t>> ve;
   ve.reserve(c->G);
   for (uint32_t g = 0; g < c->G; g++) {
@@ -513,7 +514,7 @@ static Tier fit_tier(nemo_ctx *c, uint64_t vmax, uint64_t emax, uint32_t lcap, T
   for (auto &x : ve) {
     em = std::max(em, x.second);
     const uint32_t l = std::min(x.first, lcap);
-    if (bytes(x.first, em, l, c->W) > LDS_TIER_BUDGET) break;
+    if (bytes(x.first, em, l, c->W) > budget) break;
     cv = x.first;
     ce = em;
   }
@@ -527,10 +528,12 @@ static Tier fit_tier(nemo_ctx *c, uint64_t vmax, uint64_t emax, uint32_t lcap, T
 }
 
 static void set_lds_tier(nemo_ctx *c) {
-  // k_proto_lds: u16 CSR both ways, Kahn order + level offsets (<= 512 levels), node word, two node bytes, chains
-  const Tier tp = fit_tier(c, 16384, 65535, 512u, [](uint32_t v, uint32_t e, uint32_t l, uint32_t w) {
-    return lds_tier_bytes(v, e, l, w);
-  });
+  // k_proto_lds: edges in source Kahn order + level offsets (<= 512 levels), node bytes, chains; three
+  // 512-thread workgroups per CU
+  const Tier tp = fit_tier(
+      c, 16384, 65535, 512u,
+      [](uint32_t v, uint32_t e, uint32_t l, uint32_t w) { return lds_tier_bytes(v, e, l, w); },
+      160u * 1024u / 3u - 256u);
   c->dc.lds_v = tp.v;
   c->dc.lds_e = tp.e;
   c->dc.lds_l = tp.l;
@@ -603,19 +606,25 @@ static int device_load(nemo_ctx *c) {
   int rc;
   nemo::launch_zero(c->dc.err, c->G * sizeof(uint32_t), c->stream);
   // graphs within k_build's LDS caps vs the global tier
-  double Vb = 0, Eb = 0;
+  double Vb = 0, Eb = 0, Vp = 0, Ep = 0;
   for (uint32_t g = 0; g < c->G && c->dc.bld_bytes; g++) {
     const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
     if (v <= c->dc.bld_v && e <= c->dc.bld_e) {
       Vb += (double)v;
       Eb += (double)e;
+      if (g & 1) {
+        Vp += (double)v;
+        Ep += (double)e;
+      }
     }
   }
   const double V = (double)c->V - Vb, E = (double)c->E - Eb;
   // k_build, HBM lower bound: read the edge list (8E) and node words (4V);
   // write both column arrays (8E), both row-pointer arrays (8V), the Kahn
-  // order (4V) and per-node level (4V); the level offsets are per level
-  if ((rc = timed(c, "k_build", 16 * Eb + 20 * Vb, 2 * Eb, [&] { nemo::launch_build(c->dc, c->stream); })))
+  // order (4V) and per-node level (4V); the level offsets are per level; post
+  // graphs also their edges in source Kahn order (4E) and position offsets (4V)
+  if ((rc = timed(c, "k_build", 16 * Eb + 20 * Vb + 4 * Ep + 4 * Vp, 2 * Eb,
+                  [&] { nemo::launch_build(c->dc, c->stream); })))
     return rc;
   // graphs past k_build: k_csr (one workgroup per graph) below NEMO_CSR_BIG nodes, k_csrb_* above
   const double Eg = std::max(0.0, E - c->bigE), Vg = std::max(0.0, V - c->bigV);
@@ -697,6 +706,8 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   A(d.topo, V);
   A(d.lvl, V + G);
   A(d.nlv, V);
+  A(d.e2, E);
+  A(d.posoff, V);
   A(d.nlev, G);
   A(d.flags, V);
   A(d.sb, V);
@@ -985,9 +996,9 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   // k_proto first: it is what the analysis stream has ready when a bulk
   // staging copy starts beside it (a kernel queued behind the copy's start
   // waits for the copy's blit to drain); the reduction's inputs follow it
-  // post graphs only: both CSR directions 8(V+1) + 8E, Kahn order + level offsets 4V, node word 4V, flags 1V
+  // post graphs only (HBM lower bound): edges in source Kahn order 4E, node word 4V, flags 1V
   const double V = c->postV, E = c->postE;
-  int rc = timed(c, "k_proto", 8 * E + 17 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
+  int rc = timed(c, "k_proto", 4 * E + 5 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
   if (rc) return rc;
   nemo::launch_to_host(c->d_is_success, succ, c->n_runs, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_succ, s));

@@ -177,6 +177,8 @@ struct DevCorpus {
   uint32_t *fp, *fc, *rp, *rc;           // fp/rp: V+G entries (graph g at n0+g)
   uint32_t *topo, *lvl, *nlev;           // lvl: V+G entries
   uint32_t *nlv;                         // [V] Kahn level of every node
+  uint32_t *e2, *posoff;                 // post graphs built by k_build: forward edges in source Kahn order
+                                         // (src << 16 | dst, [E]) and each Kahn position's first edge ([V])
   uint8_t *flags, *sb;                   // V
   uint32_t *s_a, *s_b, *s_c;             // V+G scratch
   int32_t *s_d;                          // V scratch
@@ -244,13 +246,13 @@ __host__ __device__ __forceinline__ uint32_t hash_label(uint32_t x) {
   x *= 0x9E3779B1u;
   return x ^ (x >> 15);
 }
-// accepted @next chains of a tier graph held in LDS as (head, tail) u16 pairs
-__host__ __device__ __forceinline__ uint32_t lds_chain_cap(uint32_t v) { return v / 4u < 32766u ? v / 4u : 32766u; }
-// k_proto_lds's image: forward u16 CSR, Kahn order, level offsets, u16 node
-// word, flags + SB bytes, table bitsets, chain (head, tail) pairs
+// k_proto_lds's chains (head, tail) held in LDS: graphs with more run the global tier
+__host__ __device__ __forceinline__ uint32_t proto_chain_cap(uint32_t v) { return v / 8u + 16u; }
+// k_proto_lds's image: chain (head, tail) pairs, table bitsets, u16 node bytes,
+// per-level edge offsets, the forward edges in source Kahn order (u32 pairs)
 __host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t e, uint32_t l, uint32_t words) {
-  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + 2u * lds_align(2u * v) + lds_align(2u * (l + 1u)) +
-         2u * lds_align(v) + lds_align(8u * words) + 2u * lds_align(2u * lds_chain_cap(v));
+  return 2u * lds_align(2u * proto_chain_cap(v)) + lds_align(8u * words) + lds_align(2u * (v + 1u)) +
+         lds_align(2u * (l + 1u)) + lds_align(4u * e);
 }
 
 __device__ __forceinline__ bool lds_fits(const DevCorpus &c, uint32_t V, uint32_t E, uint32_t nlev) {
@@ -271,10 +273,11 @@ __host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t
 }
 
 struct ProtoLds {
-  uint16_t *fp, *fc, *topo, *lv, *nw;
   uint16_t *chd, *ctl;  // chain head, chain tail (bit 15: reach pushed)
-  uint8_t *a, *b;       // flags, SB_* bits
   uint32_t *words;      // 2 * c.words u32 of table bitsets
+  uint16_t *ab;         // per node: flags byte | PB_* byte << 8 (u32-packed pairs for atomics)
+  uint16_t *elo;        // per Kahn level: first edge of e2[] whose source is on it
+  uint32_t *e2;         // forward edges in source Kahn order: src << 16 | dst
 };
 
 // Carve k_proto_lds's dynamic LDS for a graph of V nodes / E edges / L levels.
@@ -288,19 +291,11 @@ __device__ __forceinline__ ProtoLds proto_carve(void *base, uint32_t V, uint32_t
   p += lds_align(2u * chain_cap);
   g.words = (uint32_t *)p;
   p += lds_align(8u * words);
-  g.fp = (uint16_t *)p;
+  g.ab = (uint16_t *)p;
   p += lds_align(2u * (V + 1u));
-  g.fc = (uint16_t *)p;
-  p += lds_align(2u * E);
-  g.topo = (uint16_t *)p;
-  p += lds_align(2u * V);
-  g.nw = (uint16_t *)p;
-  p += lds_align(2u * V);
-  g.lv = (uint16_t *)p;
+  g.elo = (uint16_t *)p;
   p += lds_align(2u * (L + 1u));
-  g.a = p;
-  p += lds_align(V);
-  g.b = p;
+  g.e2 = (uint32_t *)p;
   return g;
 }
 
@@ -309,7 +304,7 @@ __device__ __forceinline__ ProtoLds proto_carve(void *base, uint32_t V, uint32_t
 // page-granular allocations and the extra lanes are dropped), and each thread
 // keeps STAGE_DEPTH chunks in flight, so a whole ~5k-node graph arrives in a
 // handful of HBM round trips instead of one per loop iteration.
-enum StageKind : uint32_t { ST_U16 = 0, ST_U8 = 1, ST_WORD = 2 };
+enum StageKind : uint32_t { ST_U16 = 0, ST_U8 = 1, ST_WORD = 2, ST_U32 = 3 };
 struct StageDesc {
   const void *src;
   void *dst;
@@ -365,6 +360,12 @@ __device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
 #pragma unroll
           for (int b = 0; b < 16; b++)
             if (e0 + b >= 0 && e0 + b < n) o[e0 + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        } else if (d[i].kind == ST_U32) {
+          const int32_t e0 = 4 * (int32_t)(k - first[i]) - (int32_t)skip[i];
+          uint32_t *o = (uint32_t *)d[i].dst;
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (e0 + b >= 0 && e0 + b < n) o[e0 + b] = w[b];
         } else {
           const int32_t e0 = 4 * (int32_t)(k - first[i]) - (int32_t)skip[i];
           uint16_t *o = (uint16_t *)d[i].dst;

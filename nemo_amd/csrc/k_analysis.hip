@@ -141,9 +141,11 @@ __device__ __forceinline__ void or8(uint8_t *b, uint64_t v, uint32_t bits) {
   atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (uint32_t)(v & 3u)));
 }
 
-// k_proto_lds takes the graphs within its LDS tier (and its chain cap)
+// k_proto_lds takes the graphs within its LDS tier (and its chain cap) that
+// k_build built: their edges in source Kahn order are in c.e2 / c.posoff
 __device__ __forceinline__ bool proto_lds_fits(const DevCorpus &c, const GraphView &gv) {
-  return lds_fits(c, gv.V, gv.E, gv.nlev) && c.nch[gv.g] <= lds_chain_cap(gv.V);
+  return lds_fits(c, gv.V, gv.E, gv.nlev) && c.nch[gv.g] <= proto_chain_cap(gv.V) && c.bld_bytes &&
+         gv.V <= c.bld_v && gv.E <= c.bld_e && !c.redo[gv.g];
 }
 __host__ __device__ __forceinline__ uint32_t *proto_list(const DevCorpus &c) { return c.sel + 3 * ((size_t)c.G + 1); }
 
@@ -365,23 +367,34 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_pg_gate(DevCorpus c) {
 #undef RULEISH
 #undef PG_LOOP
 
-// k_proto's LDS tier, push form: every phase propagates along forward rows
-// only, so LDS holds the forward u16 CSR, Kahn order + level offsets, the u16
-// node word, the flags byte, an SB_* byte per node and the graph's chains as
-// (head, tail) u16 pairs -- no reverse CSR and no per-tail chain lists
-// (device.h proto_lds_bytes, ~11 B/node + 2 B/edge).  The same predicates as
-// k_proto's pull form:
-//   ROOT  goal, not deleted, no REG or TAIL parent        (push SB_NR from REG/TAIL rules)
+// k_proto's LDS tier, edge-parallel push form.  The graph's forward edges are
+// laid out in LDS in the Kahn order of their source (e2[]: src << 16 | dst,
+// built from the HBM CSR + Kahn order by one degree scan), so every phase is
+// one pass over a contiguous edge range with one edge per thread -- no
+// per-node child loops -- and the reachability sweep touches, per Kahn level,
+// exactly the edges leaving that level (elo[] offsets).  Per node one u16:
+// low byte = flags (NEMO_F_* | PAB_RULE), high byte = PB_* bits ORed by LDS
+// atomics.  LDS ~2 B/node + 4 B/edge (device.h lds_tier_bytes).  Same
+// predicates as k_proto's global tier:
+//   ROOT  goal, not deleted, no REG or TAIL parent        (push PB_NR from REG/TAIL rules)
 //   R1    REG/HEAD rule with a ROOT parent                  (push from ROOT goals)
 //   G2    live goal below an R1 REG rule or below the tail of a chain with an R1 head
+//         (tails of chains with an R1 head carry PB_R1T and push like R1 REG rules)
 //   RCH   Kahn-level sweep: live G2/RCH goals reach their REG/HEAD rule children,
-//         RCH REG rules their live goal children, an RCH head its chain's tail's
-//         live goal children (chains are rescanned each level until their head is
-//         reached; the tail's children lie two levels below the head or deeper)
-// Per-node bits are ORed with LDS atomics (or8): pushes from different threads
-// meet in the same bytes.
+//         RCH REG rules their live goal children; a chain whose head is RCH marks
+//         its tail PB_RCHT (the tail lies two levels below the head or deeper)
+//         and the tail pushes RCH to its live goal children at its own level.
 #define PROTO_BLOCK 512
-#define PCH_DONE 0x8000u // chain tail word: the head's reach was pushed
+#define PCH_DONE 0x8000u  // chain tail word: the head's reach was pushed
+#define PAB_RULE 0x80u    // rule bit in the flags byte (NEMO_F_* use bits 0-4)
+#define PB_NR 0x01u
+#define PB_HASRC 0x02u
+#define PB_R1 0x04u
+#define PB_G2 0x08u
+#define PB_RCH 0x10u
+#define PB_R1T 0x20u
+#define PB_ADDT 0x40u
+#define PB_RCHT 0x80u
 __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   extern __shared__ __align__(16) uint8_t dyn[];
   const uint32_t r = blockIdx.x;
@@ -389,123 +402,125 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
   if (c.err[g] || c.err[g - 1]) return;
   const GraphView gv = c.view(g);
   if (!proto_lds_fits(c, gv)) return;
-  const uint32_t V = gv.V, W = c.words, tid = threadIdx.x;
+  const uint32_t V = gv.V, E = gv.E, L = gv.nlev, W = c.words, tid = threadIdx.x;
   STAMP(0);
   const uint32_t nch = c.nch[g];
-  ProtoLds L = proto_carve(dyn, V, gv.E, gv.nlev, W, lds_chain_cap(V));
-  uint32_t *s_s = L.words, *s_t = L.words + W;
-  const uint32_t *ch = c.chain + 5 * gv.n0;
-  for (uint32_t i = tid; i < 2 * W; i += PROTO_BLOCK) L.words[i] = 0;
+  ProtoLds P = proto_carve(dyn, V, E, L, W, proto_chain_cap(V));
+  uint32_t *s_s = P.words, *s_t = P.words + W;
+  uint16_t *ab = P.ab;
+  uint32_t *ab32 = (uint32_t *)P.ab;
+  for (uint32_t i = tid; i < 2 * W; i += PROTO_BLOCK) P.words[i] = 0;
+  // the forward edges in source Kahn order (k_build's e2) staged; each level's
+  // first edge from the Kahn position its level starts at
   {
-    const StageDesc d[6] = {{gv.fp, L.fp, V + 1, ST_U16},         {gv.fc, L.fc, gv.E, ST_U16},
-                            {gv.topo, L.topo, V, ST_U16},         {gv.lvl, L.lv, gv.nlev + 1, ST_U16},
-                            {gv.word, L.nw, V, ST_WORD},          {gv.flags, L.a, V, ST_U8}};
-    stage_lds<6, PROTO_BLOCK>(d);
+    const StageDesc d[1] = {{c.e2 + gv.e0, P.e2, E, ST_U32}};
+    stage_lds<1, PROTO_BLOCK>(d);
   }
+  for (uint32_t l = tid; l <= L; l += PROTO_BLOCK) P.elo[l] = l < L ? (uint16_t)c.posoff[gv.n0 + gv.lvl[l]] : (uint16_t)E;
   for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-    L.chd[k] = (uint16_t)ch[5 * k];
-    L.ctl[k] = (uint16_t)ch[5 * k + 1];
+    P.chd[k] = (uint16_t)c.chain[5 * (gv.n0 + k)];
+    P.ctl[k] = (uint16_t)c.chain[5 * (gv.n0 + k) + 1];
   }
-  for (uint32_t x4 = tid; x4 < (V + 3) / 4; x4 += PROTO_BLOCK) ((uint32_t *)L.b)[x4] = 0;
+  // node bytes; missingFrom's table set (prototype.go:143-147): the tables of the REG / HEAD rules
+  for (uint32_t v = tid; v < V; v += PROTO_BLOCK) {
+    const uint32_t w = gv.word[v], f = gv.flags[v];
+    const bool rule = is_rule(w);
+    ab[v] = (uint16_t)(f | (rule ? PAB_RULE : 0u));
+    if (rule && (((f & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT) || (f & NEMO_F_HEAD)))
+      atomicOr(&s_t[table_of(w) >> 5], 1u << (table_of(w) & 31));
+  }
   // OPTIONAL MATCH (g:Goal{run:1000+i, condition:"pre", condition_holds:true}) on the simplified pre graph
   const bool gt = c.holdany[g - 1] != 0;
   __syncthreads();
   STAMP(1);
-  const uint8_t *f = L.a;
-  uint8_t *sb = L.b;
-#define LRULE(v) ((L.nw[v] & NW_RULE) != 0)
-#define LTAB(v) (L.nw[v] & NW_TABLE)
-#define DEL(v) ((f[v] & NEMO_F_DELETED) != 0)
-#define REG(v) ((f[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
-#define RULEISH(v) (REG(v) || (f[v] & NEMO_F_HEAD))
-#define ADD(bits, t) atomicOr(&bits[(t) >> 5], 1u << ((t) & 31))
-#define SET(v, bit) or8(sb, (v), (bit))
-  // missingFrom's table set; not-root marks; goals with a rule child (HASRC)
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
-    const uint32_t j0 = L.fp[x], j1 = L.fp[x + 1];
-    if (LRULE(x)) {
-      if (RULEISH(x)) ADD(s_t, LTAB(x));
-      if (REG(x) || (f[x] & NEMO_F_TAIL))
-        for (uint32_t j = j0; j < j1; j++) SET(L.fc[j], SB_NR);
-    } else if (!DEL(x)) {
-      bool hasrc = false;
-      for (uint32_t j = j0; j < j1 && !hasrc; j++) hasrc = RULEISH(L.fc[j]);
-      if (hasrc) SET(x, SB_HASRC);
-    }
+#define XRULE(x) (((x) & PAB_RULE) != 0)
+#define XDEL(x) (((x) & NEMO_F_DELETED) != 0)
+#define XREG(x) (((x) & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT)
+#define XRULEISH(x) (XREG(x) || ((x) & NEMO_F_HEAD))
+#define XSB(x) ((x) >> 8)
+#define SET(v, bits) atomicOr(&ab32[(v) >> 1], (uint32_t)(bits) << (8u + 16u * ((v) & 1u)))
+#define EDGES(lo, hi, BODY)                                    \
+  for (uint32_t e = (lo) + tid; e < (hi); e += PROTO_BLOCK) {  \
+    const uint32_t sd_ = P.e2[e], s = sd_ >> 16, d = sd_ & 0xFFFFu; \
+    const uint32_t as = ab[s], ad = ab[d];                     \
+    BODY                                                       \
   }
+  // not-root marks from REG / TAIL rules; goals with a REG / HEAD rule child
+  EDGES(0, E, {
+    if (XRULE(as)) {
+      if (XREG(as) || (as & NEMO_F_TAIL)) SET(d, PB_NR);
+    } else if (!XDEL(as) && XRULEISH(ad)) {
+      SET(s, PB_HASRC);
+    }
+  })
   __syncthreads();
   STAMP(2);
-  // R1: REG/HEAD rule children of roots
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
-    if (LRULE(x) || DEL(x) || (sb[x] & SB_NR)) continue;
-    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
-      if (RULEISH(L.fc[j])) SET(L.fc[j], SB_R1);
-  }
+  // R1: REG / HEAD rule children of roots
+  EDGES(0, E, {
+    if (!XRULE(as) && !XDEL(as) && !(XSB(as) & PB_NR) && XRULEISH(ad)) SET(d, PB_R1);
+  })
+  __syncthreads();
+  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK)
+    if (XSB(ab[P.chd[k]]) & PB_R1) SET(P.ctl[k], PB_R1T);
   __syncthreads();
   STAMP(3);
-  // G2 below R1 rules (regular, and collapsed through their chain's tail), with
-  // the R1 tables whose rule has a goal child that has a rule child
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK) {
-    if (!LRULE(x) || !REG(x) || !(sb[x] & SB_R1)) continue;
-    bool add = false;
-    for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++) {
-      const uint32_t q = L.fc[j];
-      if (DEL(q)) continue;
-      SET(q, SB_G2);
-      add |= (sb[q] & SB_HASRC) != 0;
+  // G2 below R1 REG rules and below the tails of chains with an R1 head; the
+  // pushing rule is marked PB_ADDT when such a goal has a rule child
+  EDGES(0, E, {
+    if (XRULE(as) && ((XREG(as) && (XSB(as) & PB_R1)) || (XSB(as) & PB_R1T)) && !XDEL(ad)) {
+      SET(d, PB_G2);
+      if (XSB(ad) & PB_HASRC) SET(s, PB_ADDT);
     }
-    if (add) ADD(s_s, LTAB(x));
-  }
-  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-    const uint32_t h = L.chd[k], t = L.ctl[k];
-    if (!(sb[h] & SB_R1)) continue;
-    bool add = false;
-    for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) {
-      const uint32_t q = L.fc[j];
-      if (DEL(q)) continue;
-      SET(q, SB_G2);
-      add |= (sb[q] & SB_HASRC) != 0;
-    }
-    if (add) ADD(s_s, LTAB(h));
-  }
+  })
   __syncthreads();
   STAMP(4);
-  // rules reachable from G2: one barrier per Kahn level; a node's own bits are
-  // final when its level starts (every parent lies on an earlier level)
-  for (uint32_t l = 0; l < gv.nlev; l++) {
-    const uint32_t e = L.lv[l + 1];
-    for (uint32_t i = L.lv[l] + tid; i < e; i += PROTO_BLOCK) {
-      const uint32_t x = L.topo[i];
-      const uint32_t bx = sb[x];
-      if (!LRULE(x)) {
-        if (DEL(x) || !(bx & (SB_G2 | SB_RCH))) continue;
-        for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
-          if (RULEISH(L.fc[j])) SET(L.fc[j], SB_RCH);
-      } else if (REG(x) && (bx & SB_RCH)) {
-        for (uint32_t j = L.fp[x]; j < L.fp[x + 1]; j++)
-          if (!DEL(L.fc[j])) SET(L.fc[j], SB_RCH);
-      }
+  for (uint32_t v = tid; v < V; v += PROTO_BLOCK) {
+    const uint32_t x = ab[v];
+    if (XRULE(x) && XREG(x) && (XSB(x) & PB_ADDT)) {
+      const uint32_t t = table_of(gv.word[v]);
+      atomicOr(&s_s[t >> 5], 1u << (t & 31));
     }
+  }
+  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
+    const uint32_t h = P.chd[k];
+    if ((XSB(ab[h]) & PB_R1) && (XSB(ab[P.ctl[k]]) & PB_ADDT)) {
+      const uint32_t t = table_of(gv.word[h]);
+      atomicOr(&s_s[t >> 5], 1u << (t & 31));
+    }
+  }
+  STAMP(5);
+  // rules reachable from G2: per Kahn level, the edges leaving it (a node's
+  // bits are final when its level starts: every parent lies on an earlier level)
+  for (uint32_t l = 0; l < L; l++) {
+    EDGES(P.elo[l], P.elo[l + 1], {
+      const uint32_t sb = XSB(as);
+      const bool act = XRULE(as) ? ((XREG(as) && (sb & PB_RCH)) || (sb & PB_RCHT)) : (!XDEL(as) && (sb & (PB_G2 | PB_RCH)));
+      if (act && (XRULE(as) ? !XDEL(ad) : XRULEISH(ad))) SET(d, PB_RCH);
+    })
     for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-      const uint32_t t = L.ctl[k];
-      if ((t & PCH_DONE) || !(sb[L.chd[k]] & SB_RCH)) continue;
-      L.ctl[k] = (uint16_t)(t | PCH_DONE);
-      for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++)
-        if (!DEL(L.fc[j])) SET(L.fc[j], SB_RCH);
+      const uint32_t t = P.ctl[k];
+      if ((t & PCH_DONE) || !(XSB(ab[P.chd[k]]) & PB_RCH)) continue;
+      P.ctl[k] = (uint16_t)(t | PCH_DONE);
+      SET(t, PB_RCHT);
     }
     __syncthreads();
   }
   STAMP(6);
   // tables of the reached rules (RCH is only ever set on REG / HEAD rules and live goals)
-  for (uint32_t x = tid; x < V; x += PROTO_BLOCK)
-    if (LRULE(x) && (sb[x] & SB_RCH)) ADD(s_s, LTAB(x));
-#undef LRULE
-#undef LTAB
-#undef DEL
-#undef REG
-#undef RULEISH
-#undef ADD
+  for (uint32_t v = tid; v < V; v += PROTO_BLOCK) {
+    const uint32_t x = ab[v];
+    if (XRULE(x) && (XSB(x) & PB_RCH)) {
+      const uint32_t t = table_of(gv.word[v]);
+      atomicOr(&s_s[t >> 5], 1u << (t & 31));
+    }
+  }
+#undef XRULE
+#undef XDEL
+#undef XREG
+#undef XRULEISH
+#undef XSB
 #undef SET
+#undef EDGES
   __syncthreads();
   for (uint32_t i = tid; i < W; i += PROTO_BLOCK) {
     c.proto_bits[(size_t)r * W + i] = gt ? s_s[i] : 0u;

@@ -339,6 +339,51 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     if (tid == 0) lvl[nl] = lo;
   }
   for (uint32_t i = tid; i < hi; i += NEMO_BLOCK) topo[i] = q16[i];
+  if ((g & 1u) && hi == V) {
+    // post graphs: the forward edges in source Kahn order for k_proto_lds (e2:
+    // src << 16 | dst) and each Kahn position's first edge (posoff).  Every
+    // thread copies the rows of a contiguous chunk of Kahn positions, four at a
+    // time with their LDS reads issued together (rows past four entries loop).
+    const uint32_t chunk = (V + NEMO_BLOCK - 1) / NEMO_BLOCK, i0 = min(V, tid * chunk), i1 = min(V, i0 + chunk);
+    uint32_t sum = 0;
+    for (uint32_t i = i0; i < i1; i += 4) {
+      uint32_t u[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) u[q] = q16[min(i + q, i1 - 1u)];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t a = ptr[u[q] ? u[q] - 1u : 0u], b = ptr[u[q]];
+        sum += i + q < i1 ? b - (u[q] ? a : 0u) : 0u;
+      }
+    }
+    uint32_t tot;
+    uint32_t off = block_exscan(sum, &tot, s_lds);
+    uint32_t *e2 = c.e2 + e0, *po = c.posoff + n0;
+    for (uint32_t i = i0; i < i1; i += 4) {
+      uint32_t u[4], a[4], n[4], y[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) u[q] = q16[min(i + q, i1 - 1u)];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t pa = ptr[u[q] ? u[q] - 1u : 0u], pb = ptr[u[q]];
+        a[q] = u[q] ? pa : 0u;
+        n[q] = i + q < i1 ? pb - a[q] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) y[q][k] = col[min(a[q] + k, E - 1u)];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (i + q < i1) po[i + q] = off;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if ((uint32_t)k < n[q]) e2[off + k] = (u[q] << 16) | y[q][k];
+        for (uint32_t k = 4; k < n[q]; k++) e2[off + k] = (u[q] << 16) | col[a[q] + k];
+        off += n[q];
+      }
+    }
+  }
   STAMP(15);
   if (tid == 0) {
     c.created[g] = s_created;
