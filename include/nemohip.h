@@ -156,7 +156,11 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *   "global_block"      workgroup size of the global-memory tiers: 256 or 1024
  *                       (default: 1024 when >= 1/8 of the graphs have >= 64k nodes)
  *   "stage_blocks"      nemo_stage_simplified's bulk copies: 0 = runtime copies
- *                       (default), else a copy kernel on this many workgroups   */
+ *                       (default), else a copy kernel on this many workgroups
+ *   "stage_sdma"        request nemo_stage_simplified's runtime copies as NoCU
+ *                       (SDMA) copies (1) or plain D2H copies (0, default)
+ *   "stage_cus"         CUs the copy stream's blit kernels may use (default 8,
+ *                       0 = all); set before the first nemo_stage_simplified */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);

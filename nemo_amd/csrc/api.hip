@@ -132,6 +132,8 @@ struct nemo_ctx {
   uint64_t staged_n = 0, staged_cap = 0, chht_hint = 0;
   bool pairs_wide = false;    // some graph has >= 65536 nodes: u32 pairs
   uint32_t stage_blocks = 0;  // bulk staging: 0 = runtime copies, else k_to_host on this many blocks
+  bool stage_sdma = false;    // runtime copies requested as NoCU (SDMA) copies
+  uint32_t stage_cus = 8;     // CUs of the copy stream (hipExtStreamCreateWithCUMask); 0 = unmasked
   uint32_t *d_state = nullptr;  // 2-bit node state (k_pack_state)
   uint32_t *d_chht = nullptr;
   uint64_t d_chht_cap = 0;
@@ -449,6 +451,14 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     }
     c->lds_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     if (c->loaded) set_lds_tier(c);
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "stage_sdma")) {
+    c->stage_sdma = value > 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "stage_cus")) {  // takes effect when the copy stream is created (first stage)
+    c->stage_cus = value < 0 ? 8u : (uint32_t)value;
     return NEMO_OK;
   }
   if (!strcmp(name, "stage_blocks")) {
@@ -1490,9 +1500,18 @@ static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
   if (c->stage_blocks) {  // CU stores into pinned memory from a small grid beside the analysis
     nemo::launch_to_host(c->h_flags, c->d_state, sbytes, c->copy, c->stage_blocks);
     nemo::launch_to_host(c->h_chht, c->d_chht, pw * cap * 4, c->copy, c->stage_blocks);
-  } else {  // runtime copies
-    if (sbytes) HIPCHK(c, hipMemcpyAsync(c->h_flags, c->d_state, sbytes, hipMemcpyDeviceToHost, c->copy));
-    if (cap) HIPCHK(c, hipMemcpyAsync(c->h_chht, c->d_chht, pw * cap * 4, hipMemcpyDeviceToHost, c->copy));
+  } else {  // runtime copies: SDMA (the pinned buffers are device-addressable), else the runtime's blit kernel
+    auto copy = [&](void *dst, const void *src, size_t n) -> hipError_t {
+      if (!n) return hipSuccess;
+      if (c->stage_sdma) {
+        if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->copy) == hipSuccess) return hipSuccess;
+        (void)hipGetLastError();
+        c->stage_sdma = false;
+      }
+      return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->copy);
+    };
+    HIPCHK(c, copy(c->h_flags, c->d_state, sbytes));
+    HIPCHK(c, copy(c->h_chht, c->d_chht, pw * cap * 4));
   }
   HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
   c->staged_cap = cap;
@@ -1507,7 +1526,18 @@ int nemo_stage_simplified(nemo_ctx *c) {
   int rc;
   hipStream_t s = c->stream;
   if (!c->copy) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    // the bulk D2H copies run as the runtime's blit kernel, PCIe-bound for ~0.5 ms
+    // per step: confined to a few CUs, they no longer hold workgroup slots of
+    // the LDS-tier kernel running beside them (stage_cus, default 8; 0 = any CU)
+    if (c->stage_cus) {
+      uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t k = 0; k < std::min(c->stage_cus, 256u); k++) mask[k >> 5] |= 1u << (k & 31);
+      if (hipExtStreamCreateWithCUMask(&c->copy, 8, mask) != hipSuccess) {
+        (void)hipGetLastError();
+        c->copy = nullptr;
+      }
+    }
+    if (!c->copy) HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));
   }
