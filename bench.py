@@ -178,8 +178,10 @@ def main():
         eng.rebuild()
         eng.mark()
         eng.simplify()
-        eng.stage_simplified()  # flags + chain pairs -> pinned host, overlapping the rest
         eng.protos_partial(success, d_red.data_ptr())
+        # flags + chain pairs -> pinned host on the copy stream, overlapping the diffs and pulls (queued
+        # after k_proto_lds, the LDS-heaviest kernel, which a concurrent PCIe blit slows most)
+        eng.stage_simplified()
         if world > 1:
             dist.all_reduce(d_red)
         if label_bcast:

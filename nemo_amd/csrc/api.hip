@@ -1767,7 +1767,8 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "r0lab") base = c->d_r0lab;
   else if (n == "r0idx") base = c->d_r0idx;
   else if (n == "stamps") base = c->dc.stamps;
-  else if (n == "sel") base = c->dc.sel;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
+  else if (n == "sel") base = c->dc.sel;
+  else if (n == "redo") base = c->dc.redo;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));
