@@ -53,6 +53,17 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 
 #define BLD_RS 8    // row entries sorted in registers (longer rows: insertion sort in LDS)
 
+// 5-comparator sorting network for 4 keys
+__device__ __forceinline__ void sort_net4(uint32_t *x) {
+  constexpr int P[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t a = x[P[k][0]], b = x[P[k][1]];
+    x[P[k][0]] = min(a, b);
+    x[P[k][1]] = max(a, b);
+  }
+}
+
 // 19-comparator sorting network for 8 keys (pads 0xFFFF sort last)
 __device__ __forceinline__ void sort_net8(uint32_t *x) {
   constexpr int P[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
@@ -63,6 +74,65 @@ __device__ __forceinline__ void sort_net8(uint32_t *x) {
     x[P[k][0]] = min(a, b);
     x[P[k][1]] = max(a, b);
   }
+}
+
+// k_build's row sort: rows v0 and v0 + NEMO_BLOCK ([a, a + n) in col), both
+// rows' LDS reads issued together and the entries sorted in registers (a row
+// longer than RS: insertion sort in LDS); reverse rows (dir 0) also count the
+// relationships created (pre-post-prov.go:150-210: distinct, goal<->rule).
+template <int RS>
+__device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t *s_rule, uint32_t E, uint32_t V,
+                                                  int dir, uint32_t v0, const uint32_t (&a)[2],
+                                                  const uint32_t (&n)[2]) {
+  uint32_t x[2][RS], created = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+#pragma unroll
+    for (int i = 0; i < RS; i++) {
+      const uint32_t y = col[min(a[q] + i, E - 1u)];  // clamped, unconditional: all reads in flight together
+      x[q][i] = (uint32_t)i < n[q] ? y : 0xFFFFu;
+    }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t v = v0 + q * NEMO_BLOCK, b = a[q] + n[q];
+    if (n[q] <= (uint32_t)RS) {
+      if (n[q] >= 2) {
+        if (RS == 4) sort_net4(x[q]);
+        else sort_net8(x[q]);
+#pragma unroll
+        for (int i = 0; i < RS; i++)
+          if ((uint32_t)i < n[q]) col[a[q] + i] = (uint16_t)x[q][i];
+      }
+      if (dir == 0 && n[q]) {
+        const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
+#pragma unroll
+        for (int i = 0; i < RS; i++) {
+          const uint32_t t = x[q][i], tw = min(t, V - 1u);
+          const bool rt = (s_rule[tw >> 5] >> (tw & 31)) & 1u;
+          created += (uint32_t)i < n[q] && !(i > 0 && x[q][i - 1] == t) && rv != rt;
+        }
+      }
+      continue;
+    }
+    for (uint32_t i = a[q] + 1; i < b; i++) {  // long row: insertion sort in LDS
+      const uint16_t y = col[i];
+      uint32_t j = i;
+      while (j > a[q] && col[j - 1] > y) {
+        col[j] = col[j - 1];
+        j--;
+      }
+      col[j] = y;
+    }
+    if (dir == 0) {
+      const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
+      for (uint32_t i = a[q]; i < b; i++) {
+        const uint32_t t = col[i];
+        const bool rt = (s_rule[t >> 5] >> (t & 31)) & 1u;
+        if (!(i > a[q] && col[i - 1] == t) && rv != rt) created++;
+      }
+    }
+  }
+  return created;
 }
 
 __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
@@ -204,60 +274,19 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     // issued together, the entries sorted in registers (a latency chain of a
     // few LDS round trips instead of one per entry)
     for (uint32_t v0 = tid; v0 < V; v0 += 2 * NEMO_BLOCK) {
-      uint32_t a[2], n[2], x[2][BLD_RS];
+      uint32_t a[2], n[2];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const uint32_t v = v0 + q * NEMO_BLOCK;
         a[q] = v < V && v ? ptr[v - 1] : 0u;
         n[q] = v < V ? ptr[v] - a[q] : 0u;
       }
-      // unconditional reads at clamped addresses (no branch per entry, all in flight together)
-#pragma unroll
-      for (int q = 0; q < 2; q++)
-#pragma unroll
-        for (int i = 0; i < BLD_RS; i++) {
-          const uint32_t y = col[min(a[q] + i, E - 1u)];
-          x[q][i] = (uint32_t)i < n[q] ? y : 0xFFFFu;
-        }
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const uint32_t v = v0 + q * NEMO_BLOCK, b = a[q] + n[q];
-        if (n[q] <= BLD_RS) {
-          if (n[q] >= 2) {
-            sort_net8(x[q]);
-#pragma unroll
-            for (int i = 0; i < BLD_RS; i++)
-              if ((uint32_t)i < n[q]) col[a[q] + i] = (uint16_t)x[q][i];
-          }
-          if (dir == 0 && n[q]) {  // relationships created (pre-post-prov.go:150-210): distinct, goal<->rule
-            const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
-#pragma unroll
-            for (int i = 0; i < BLD_RS; i++) {
-              const uint32_t t = x[q][i], tw = min(t, V - 1u);
-              const bool rt = (s_rule[tw >> 5] >> (tw & 31)) & 1u;
-              created += (uint32_t)i < n[q] && !(i > 0 && x[q][i - 1] == t) && rv != rt;
-            }
-          }
-          continue;
-        }
-        for (uint32_t i = a[q] + 1; i < b; i++) {  // long row: insertion sort in LDS
-          const uint16_t y = col[i];
-          uint32_t j = i;
-          while (j > a[q] && col[j - 1] > y) {
-            col[j] = col[j - 1];
-            j--;
-          }
-          col[j] = y;
-        }
-        if (dir == 0) {
-          const bool rv = (s_rule[v >> 5] >> (v & 31)) & 1u;
-          for (uint32_t i = a[q]; i < b; i++) {
-            const uint32_t t = col[i];
-            const bool rt = (s_rule[t >> 5] >> (t & 31)) & 1u;
-            if (!(i > a[q] && col[i - 1] == t) && rv != rt) created++;
-          }
-        }
-      }
+      // rows of at most four entries everywhere in the wave (most reverse rows,
+      // goals' forward rows): the 4-key network; else the 8-key one
+      if (!__any(n[0] > 4u || n[1] > 4u))
+        created += sort_row_pair<4>(col, s_rule, E, V, dir, v0, a, n);
+      else
+        created += sort_row_pair<BLD_RS>(col, s_rule, E, V, dir, v0, a, n);
     }
     __syncthreads();
     if (dir == 0) STAMP(6);
