@@ -389,6 +389,9 @@ __device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
       c.stamps[16 * (size_t)blockIdx.x + (k)] = t_;                                       \
     }                                                                                     \
   } while (0)
+// phase accumulators: TICK waits for the wave's outstanding memory operations,
+// so a phase is charged with the latency of the loads it issued
+#define TICK(t) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory")
 #else
 #define STAMP(k) \
   do {           \

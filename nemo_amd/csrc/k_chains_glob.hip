@@ -78,6 +78,21 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
   return s;
 }
 
+#define GS_RING 8192u  // values kept in LDS (power of two)
+#define GS_WN 2048u    // nodes per window
+#define GS_E 4096u     // extra in-ring links per window (past the packed ones)
+struct GSweepLds {
+  int32_t rv[GS_RING];   // up / down by ring slot (index & (GS_RING - 1))
+  uint32_t rc[GS_RING];  // down: crank by ring slot
+  int32_t init[GS_WN];   // up: value over the parents outside the ring; down: best such child's down
+  uint32_t ibc[GS_WN], ibr[GS_WN];  // down: that child and its crank; ibc then nxt
+  uint32_t lev[GS_WN];   // Kahn level
+  uint64_t lk[GS_WN][2]; // first GS_KEEP in-ring links (u16 offsets from the ring base)
+  uint16_t aoff[GS_WN], acnt[GS_WN];  // GS_MORE: link t in [GS_KEEP, acnt) at adj[aoff + t - GS_KEEP]
+  uint16_t adj[GS_E];    // extra in-ring links
+  uint8_t flg[GS_WN];    // bit 0 rule, GS_MORE, GS_SPILL
+};
+
 __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
@@ -89,9 +104,286 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
   return m;
 }
 
+
+// up / down of the chain subgraph H* as windowed sweeps.  The compact index
+// orders H* by Kahn level, so a node's H* parents have smaller indices and its
+// children larger ones.  Deep graphs have ~20k levels of a few dozen H* nodes:
+// a level-synchronous sweep over HBM scratch pays a chain of dependent HBM
+// round trips and a 16-wave barrier per level.  Here the index range is cut
+// into GS_WN-node windows; the whole workgroup stages a window (coalesced):
+// links that leave the ring of the last GS_RING values are resolved from HBM
+// (their values are final), the others become an LDS adjacency list of ring
+// offsets.  Then ONE wave walks the window's levels with every value in LDS:
+// a level costs a few LDS round trips and no barrier (a wave's LDS operations
+// complete in order).  A window whose in-ring links overflow GS_E leaves its
+// last nodes' rows in HBM (re-read in the sweep).
+//   up   (forward):  up(i)   = max(rule ? 0 : -1, up(p) + 1 over H* parents p)
+//   down (backward): the child w of greatest (down(w), -crank(w)); down(i) =
+//                    down(w) + 1, or rule ? 0 : -1 without children; nxt(i) = w
+#define GS_MORE 0x2u   // more than GS_KEEP in-ring links: the rest in the window's list
+#define GS_SPILL 0x4u  // ... or, past the list's capacity, in HBM
+#define GS_KEEP 8      // in-ring links packed per node (u16 each, GS_NOLINK = none)
+#define GS_NOLINK 0xFFFFu
+template <bool UP>
+__device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, const uint32_t *hs, const uint32_t *nlv,
+                                           uint32_t *s_fail, GSweepLds &L, uint32_t *s_red, unsigned long long *st) {
+#ifdef NEMO_STAMPS
+  unsigned long long acc_s = 0, acc_w = 0, t_a = 0, t_b = 0, iters = 0, spills = 0;
+#endif
+  constexpr uint32_t M = GS_RING - 1u;
+  constexpr uint32_t PT = GS_WN / GB;  // window nodes per thread
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t *off = UP ? S.pcoff : S.ccoff, *col = UP ? S.par : S.child;
+  const uint32_t nwin = (n + GS_WN - 1) / GS_WN;
+  for (uint32_t wi = 0; wi < nwin; wi++) {
+    const uint32_t w0 = UP ? wi * GS_WN : (n > (wi + 1) * GS_WN ? n - (wi + 1) * GS_WN : 0u);
+    const uint32_t w1 = UP ? min(n, w0 + GS_WN) : n - wi * GS_WN;
+    const uint32_t nw = w1 - w0;
+    // ring = [base, base + GS_RING) around the window; link offsets relative to base
+    const uint32_t base = UP ? (w1 > GS_RING ? w1 - GS_RING : 0u) : w0;
+#ifdef NEMO_STAMPS
+    TICK(t_a);
+#endif
+    // ---- stage (whole workgroup): node k = tid + q * GB ----
+    uint32_t r0[PT], r1[PT], cnt[PT], keep[PT][GS_KEEP];
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * GB, i = w0 + k;
+      const bool in = k < nw;
+      r0[q] = in ? off[i] : 0u;
+      r1[q] = in ? off[i + 1] : 0u;
+      cnt[q] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * GB, i = w0 + k;
+      if (k >= nw) continue;
+      const uint32_t rule = S.rule[i];
+      L.lev[k] = nlv[hs[i]];
+      L.flg[k] = (uint8_t)rule;
+      if (UP) {
+        int32_t d = rule ? 0 : -1;
+        for (uint32_t j = r0[q]; j < r1[q]; j++) {
+          const uint32_t p = col[j];
+          if (p >= base) {
+            if (cnt[q] < GS_KEEP) keep[q][min(cnt[q], (uint32_t)GS_KEEP - 1u)] = p - base;
+            cnt[q]++;
+          } else {
+            d = max(d, S.up[p] + 1);
+          }
+        }
+        L.init[k] = d;
+      } else {
+        int32_t best = -1;
+        uint32_t bc = GNIL, br = GNIL;
+        for (uint32_t j = r0[q]; j < r1[q]; j++) {
+          const uint32_t w = col[j];
+          if (w < base + GS_RING) {
+            if (cnt[q] < GS_KEEP) keep[q][min(cnt[q], (uint32_t)GS_KEEP - 1u)] = w - base;
+            cnt[q]++;
+          } else {
+            const int32_t dw = S.down[w];
+            const uint32_t rw = S.crank[w];
+            if (dw > best || (dw == best && rw < br)) {
+              best = dw;
+              bc = w;
+              br = rw;
+            }
+          }
+        }
+        L.init[k] = best;
+        L.ibc[k] = bc;
+        L.ibr[k] = br;
+        L.rc[i & M] = S.crank[i];
+      }
+    }
+    // first GS_KEEP links packed per node; the rest in the window's list
+    // (offsets by a block scan of the extra counts), past its capacity in HBM
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PT; q++) sum += cnt[q] > GS_KEEP ? cnt[q] - GS_KEEP : 0u;
+    uint32_t tot;
+    uint32_t o = block_exscan<GB>(sum, &tot, s_red);
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * GB;
+      if (k >= nw) continue;
+      uint64_t lk[2] = {0, 0};
+#pragma unroll
+      for (int t = 0; t < GS_KEEP; t++)
+        lk[t >> 2] |= (uint64_t)((uint32_t)t < cnt[q] ? keep[q][t] : GS_NOLINK) << (16 * (t & 3));
+      L.lk[k][0] = lk[0];
+      L.lk[k][1] = lk[1];
+      if (cnt[q] <= GS_KEEP) continue;
+      const uint32_t extra = cnt[q] - GS_KEEP;
+      const bool fits = o + extra <= GS_E;
+      L.flg[k] |= fits ? GS_MORE : (GS_MORE | GS_SPILL);
+      L.aoff[k] = (uint16_t)(fits ? o : 0u);  // adj index of link t = aoff + t - GS_KEEP
+      L.acnt[k] = (uint16_t)(fits ? cnt[q] : GS_KEEP);
+      if (fits) {
+        uint32_t x = 0;
+        for (uint32_t j = r0[q]; j < r1[q]; j++) {
+          const uint32_t p = col[j];
+          if (UP ? p >= base : p < base + GS_RING) {
+            if (x >= GS_KEEP) L.adj[o + x - GS_KEEP] = (uint16_t)(p - base);
+            x++;
+          }
+        }
+      }
+      o += extra;
+    }
+    __syncthreads();
+#ifdef NEMO_STAMPS
+    TICK(t_b);
+    acc_s += t_b - t_a;
+    t_a = t_b;
+#endif
+    // ---- sweep (wave 0): the window's nodes level by level ----
+    // Everything but the ring values is static, so the next batch's node data
+    // (level, first links, staged far value) is read while the current batch
+    // waits on its ring reads: a level's critical path is one LDS round trip
+    // for the links' values and the write of its own.
+    if (tid < 64) {
+      uint32_t k = 0;
+      auto fetch = [&](uint32_t k0, uint32_t &lv, uint64_t (&lk)[2], int32_t &ini, uint32_t &bc, uint32_t &br,
+                       uint32_t &fl) {
+        const uint32_t q = k0 + lane, kk = UP ? q : nw - 1u - q;
+        const bool in = q < nw;
+        const uint32_t kc = in ? kk : 0u;
+        lv = in ? L.lev[kc] : GNIL;
+        lk[0] = L.lk[kc][0];
+        lk[1] = L.lk[kc][1];
+        ini = L.init[kc];
+        fl = L.flg[kc];
+        if (!UP) {
+          bc = L.ibc[kc];
+          br = L.ibr[kc];
+        }
+      };
+      uint32_t lv, bc = 0, br = 0, fl;
+      uint64_t lk[2];
+      int32_t ini;
+      fetch(0, lv, lk, ini, bc, br, fl);
+      while (k < nw) {
+        const uint32_t q = k + lane, kk = UP ? q : nw - 1u - q;
+        const uint32_t l = __builtin_amdgcn_readfirstlane(lv);
+        const bool mine = q < nw && lv == l;
+        const uint64_t m = __ballot(mine);  // contiguous from lane 0: nodes are sorted by level
+        const uint32_t kn = k + (uint32_t)__popcll(m);
+        uint32_t lv2, bc2 = 0, br2 = 0, fl2;
+        uint64_t lk2[2];
+        int32_t ini2;
+        fetch(kn, lv2, lk2, ini2, bc2, br2, fl2);
+        if (mine) {
+          const uint32_t i = w0 + kk;
+          uint32_t u[GS_KEEP];
+#pragma unroll
+          for (int h = 0; h < GS_KEEP; h++) u[h] = (uint32_t)(lk[h >> 2] >> (16 * (h & 3))) & 0xFFFFu;
+          if (UP) {
+            int32_t d = ini, v[GS_KEEP];
+#pragma unroll
+            for (int h = 0; h < GS_KEEP; h++) v[h] = L.rv[(base + u[h]) & M];
+#pragma unroll
+            for (int h = 0; h < GS_KEEP; h++)
+              if (u[h] != GS_NOLINK) d = max(d, v[h] + 1);
+            if (fl & GS_MORE) {  // links past the first four: the window's list, or HBM
+              const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
+              for (uint32_t t = GS_KEEP; t < ac; t++) d = max(d, L.rv[(base + L.adj[ao + t - GS_KEEP]) & M] + 1);
+              if (fl & GS_SPILL)
+                for (uint32_t j = off[i]; j < off[i + 1]; j++) {
+                  const uint32_t p = col[j];
+                  d = max(d, (p >= base ? L.rv[p & M] : S.up[p]) + 1);
+                }
+            }
+            L.rv[i & M] = d;
+          } else {
+            int32_t best = ini;
+            auto take = [&](uint32_t w, int32_t dw, uint32_t rw) {
+              if (dw > best || (dw == best && rw < br)) {
+                best = dw;
+                bc = w;
+                br = rw;
+              }
+            };
+            int32_t dv[GS_KEEP];
+            uint32_t rr[GS_KEEP];
+#pragma unroll
+            for (int h = 0; h < GS_KEEP; h++) {
+              dv[h] = L.rv[(base + u[h]) & M];
+              rr[h] = L.rc[(base + u[h]) & M];
+            }
+#pragma unroll
+            for (int h = 0; h < GS_KEEP; h++)
+              if (u[h] != GS_NOLINK) take(base + u[h], dv[h], rr[h]);
+            if (fl & GS_MORE) {
+              const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
+              for (uint32_t t = GS_KEEP; t < ac; t++) {
+                const uint32_t w = base + L.adj[ao + t - GS_KEEP];
+                take(w, L.rv[w & M], L.rc[w & M]);
+              }
+              if (fl & GS_SPILL)
+                for (uint32_t j = off[i]; j < off[i + 1]; j++) {
+                  const uint32_t w = col[j];
+                  if (w < base + GS_RING) take(w, L.rv[w & M], L.rc[w & M]);
+                  else take(w, S.down[w], S.crank[w]);
+                }
+            }
+            int32_t d = best >= 0 ? best + 1 : ((fl & 1u) ? 0 : -1);
+            L.rv[i & M] = d;
+            L.ibc[kk] = d > 0 ? bc : GNIL;  // nxt (the staged far best is consumed)
+            if (d < 0) *s_fail = 1;  // a goal without a chain continuation: impossible on H*
+          }
+        }
+#ifdef NEMO_STAMPS
+        iters++;
+        spills += __ballot(mine && (fl & GS_SPILL)) != 0 ? 1u : 0u;
+#endif
+        k = kn;
+        lv = lv2;
+        lk[0] = lk2[0];
+        lk[1] = lk2[1];
+        ini = ini2;
+        bc = bc2;
+        br = br2;
+        fl = fl2;
+        wsync();
+      }
+    }
+    __syncthreads();
+    // ---- the window's values to HBM (no global store inside the sweep: a later
+    // load there would wait for it), performed before the next window stages ----
+    for (uint32_t k = tid; k < nw; k += GB) {
+      const uint32_t i = w0 + k;
+      if (UP) {
+        S.up[i] = L.rv[i & M];
+      } else {
+        S.down[i] = L.rv[i & M];
+        S.nxt[i] = L.ibc[k];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#ifdef NEMO_STAMPS
+    TICK(t_b);
+    acc_w += t_b - t_a;
+#endif
+  }
+#ifdef NEMO_STAMPS
+  if (threadIdx.x == 0 && st) {
+    st[UP ? 10 : 12] = acc_s;
+    st[UP ? 11 : 13] = acc_w;
+    if (UP) {
+      st[14] = iters | (spills << 32);
+      st[15] = n;
+    }
+  }
+#endif
+}
+
 __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __shared__ uint32_t s_lds[GB / 64];
   __shared__ uint32_t s_nch, s_fail;
+  __shared__ GSweepLds s_gs;
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   if (c.err[g] || c.gs_off[g] == ~0ull) return;
   const GraphView gv = c.view(g);
@@ -173,44 +465,14 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
 #undef INH
   __syncthreads();
   STAMP(2);
-  // ---- up (forward) and down/nxt (backward), half the workgroup each -------------
-  {
-    constexpr uint32_t HALF = GB / 2;
-    const bool upper = tid < HALF;
-    const uint32_t ht = upper ? tid : tid - HALF;
-    for (uint32_t s = 0; s < ns; s++) {
-      if (upper) {
-        for (uint32_t i = S.seg[s] + ht; i < S.seg[s + 1]; i += HALF) {
-          int32_t d = S.rule[i] ? 0 : -1;
-          for (uint32_t j = S.pcoff[i]; j < S.pcoff[i + 1]; j++) d = max(d, S.up[S.par[j]] + 1);
-          S.up[i] = d;
-        }
-      } else {
-        const uint32_t sd = ns - 1 - s;
-        for (uint32_t i = S.seg[sd] + ht; i < S.seg[sd + 1]; i += HALF) {
-          int32_t best = -1;
-          uint32_t bc = GNIL, br = GNIL;
-          for (uint32_t j = S.ccoff[i]; j < S.ccoff[i + 1]; j++) {
-            const uint32_t w = S.child[j];
-            const int32_t dw = S.down[w];
-            const uint32_t rw = S.crank[w];
-            if (dw > best || (dw == best && rw < br)) {
-              best = dw;
-              bc = w;
-              br = rw;
-            }
-          }
-          int32_t d = best >= 0 ? best + 1 : (S.rule[i] ? 0 : -1);
-          if (S.rule[i] && d < 0) d = 0;
-          if (d > 0 && best < 0) bc = GNIL;
-          S.down[i] = d;
-          S.nxt[i] = d > 0 ? bc : GNIL;
-          if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
-        }
-      }
-      __syncthreads();
-    }
-  }
+  // ---- up (forward) and down/nxt (backward): windowed single-wave sweeps -----------
+#ifdef NEMO_STAMPS
+  unsigned long long *gst = c.stamps ? c.stamps + 16 * (size_t)blockIdx.x : nullptr;
+#else
+  unsigned long long *gst = nullptr;
+#endif
+  glob_sweep<true>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
+  glob_sweep<false>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
   STAMP(3);
   uint32_t mu = 0, ml = 0;
   for (uint32_t i = tid; i < n; i += GB) {

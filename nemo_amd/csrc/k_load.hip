@@ -634,6 +634,7 @@ __device__ __forceinline__ void topo_graph(const DevCorpus c, const uint32_t g) 
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0);
   if (build_fits(c, V, (uint32_t)(c.edge_off[g + 1] - e0)) && !c.redo[g]) return;  // k_build's graph
+  if (V >= CSR_LDS) return;  // k_topo_deep's graph
   const uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0;
   uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g, *cnt = c.s_a + n0 + g;
   if (threadIdx.x == 0) s_tail = 0;
@@ -719,6 +720,139 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
     __syncthreads();
   }
 }
+// Kahn levels of the big graphs (V >= CSR_LDS: the deep corpora's 1M-node
+// graphs, ~22k levels of a few dozen nodes).  A level is a chain of dependent
+// HBM round trips (the frontier's row pointers, their children, the in-degree
+// atomics), so the kernel is built to keep that chain short:
+//   - the frontier lives in LDS (the level's nodes are not re-read from topo[]
+//     unless the level outgrows TD_Q);
+//   - every lane issues up to TD_BATCH child loads and then as many counter
+//     atomics at once, so a node of out-degree <= TD_BATCH costs one round
+//     trip of each, not one per child;
+//   - the ready children of a lane are appended with one wave scan and one LDS
+//     atomic per wave;
+//   - 256 threads: four waves meet at the two barriers of a level.
+#define TD_B 256
+#define TD_Q 4096u
+#define TD_BATCH 16
+__global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
+  __shared__ uint32_t s_q[2][TD_Q];
+  // appends of level L go to s_n[(L + 1) % 3]: read after the level's barrier,
+  // reset during level L + 2, so one barrier per level orders everything
+  __shared__ uint32_t s_n[3];
+  const uint32_t g = c.big[blockIdx.x];
+  if (c.err[g]) return;
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  if ((build_fits(c, V, E) && !c.redo[g]) || V < CSR_LDS) return;
+  const uint32_t *fp = c.fp + n0 + g, *rp = c.rp + n0 + g, *fc = c.fc + e0;
+  uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g, *cnt = c.s_a + n0 + g, *nlv = c.nlv + n0;
+  const uint32_t tid = threadIdx.x;
+  if (tid < 3) s_n[tid] = 0;
+  if (tid == 0) lvl[0] = 0;
+  __syncthreads();
+  // level 0: the sources
+  for (uint32_t b = 0; b < V; b += TD_B) {
+    const uint32_t v = b + tid;
+    const uint32_t d = v < V ? rp[v + 1] - rp[v] : 1u;
+    if (v < V) cnt[v] = d;
+    const bool p = d == 0u;
+    const uint64_t m = __ballot(p);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&s_n[1], (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, 0);
+    if (p) {
+      const uint32_t i = base + mbcnt(m);
+      topo[i] = v;
+      nlv[v] = 0;
+      if (i < TD_Q) s_q[0][i] = v;
+    }
+  }
+  __syncthreads();
+  uint32_t lo = 0, hi = s_n[1], nl = 0, cur = 0, k3 = 1;  // k3 = (nl + 1) % 3
+#ifdef NEMO_STAMPS
+  unsigned long long acc[5] = {0, 0, 0, 0, 0}, ta, tb;
+#define TD_T(k) \
+  do {          \
+    TICK(tb);   \
+    acc[k] += tb - ta; \
+    ta = tb;    \
+  } while (0)
+  TICK(ta);
+#else
+#define TD_T(k) \
+  do {          \
+  } while (0)
+#endif
+  while (lo < hi) {
+    const uint32_t n = hi - lo, kn = k3 == 2 ? 0u : k3 + 1u;  // this level's append counter
+    if (tid == 0) s_n[kn == 2 ? 0u : kn + 1u] = 0;            // = (nl + 3) % 3: free since level nl - 1
+    uint32_t *qn = s_q[cur ^ 1];
+    for (uint32_t b = 0; b < n; b += TD_B) {
+      const uint32_t i = b + tid;
+      uint32_t j = 0, je = 0;
+      if (i < n) {
+        const uint32_t u = i < TD_Q ? s_q[cur][i] : topo[lo + i];
+        j = fp[u];
+        je = fp[u + 1];
+      }
+      TD_T(0);
+      while (__any(j < je)) {
+        uint32_t ch[TD_BATCH];
+        bool rdy[TD_BATCH];
+#pragma unroll
+        for (int k = 0; k < TD_BATCH; k++) ch[k] = j + k < je ? fc[j + k] : NEMO_NONE;
+        TD_T(1);
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < TD_BATCH; k++) {
+          const uint32_t old = ch[k] != NEMO_NONE ? atomicSub(&cnt[ch[k]], 1u) : 0u;
+          rdy[k] = old == 1u;
+          r += rdy[k] ? 1u : 0u;
+        }
+        TD_T(2);
+        uint32_t tot;
+        const uint32_t ex = wave_exscan(r, &tot);
+        if (tot) {
+          uint32_t base = 0;
+          if (lane_id() == 0) base = atomicAdd(&s_n[kn], tot);
+          uint32_t at = __builtin_amdgcn_readlane(base, 0) + ex;
+#pragma unroll
+          for (int k = 0; k < TD_BATCH; k++) {
+            if (!rdy[k]) continue;
+            topo[hi + at] = ch[k];
+            nlv[ch[k]] = nl + 1;
+            if (at < TD_Q) qn[at] = ch[k];
+            at++;
+          }
+        }
+        j = min(j + TD_BATCH, je);
+        TD_T(3);
+      }
+    }
+    __syncthreads();
+    TD_T(4);
+    const uint32_t m = s_n[kn];
+    nl++;
+    lo = hi;
+    hi += m;
+    cur ^= 1;
+    k3 = kn;
+    if (tid == 0) lvl[nl] = lo;
+  }
+  if (tid == 0) {
+    c.nlev[g] = nl;
+    if (hi != V) c.err[g] = NEMO_ERR_CYCLE;
+  }
+#ifdef NEMO_STAMPS
+  if (tid == 0 && c.stamps)
+    for (int k = 0; k < 5; k++) c.stamps[16 * (size_t)g + k] = acc[k];
+#endif
+#undef TD_T
+}
+
+
 #define LOAD_GRID 2048u
 
 void launch_build(const DevCorpus &c, hipStream_t s) {
@@ -890,6 +1024,7 @@ void launch_topo(const DevCorpus &c, hipStream_t s) {  // after launch_load: its
     hipLaunchKernelGGL(k_topo<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
     hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);
+  if (c.n_big) hipLaunchKernelGGL(k_topo_deep, dim3(c.n_big), dim3(TD_B), 0, s, c);
 }
 
 }  // namespace nemo

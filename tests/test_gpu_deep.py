@@ -1,0 +1,98 @@
+"""GPU parity of the deep tier's edge cases (graphs of >= 8192 nodes: the
+multi-workgroup CSR build, k_topo_deep and the global-tier sweeps), against
+the CPU oracle.
+
+- a Kahn level wider than k_topo_deep's LDS frontier (TD_Q = 4096 nodes), so
+  the level's tail is read back from topo[];
+- a cycle inside a big graph (loadProv's refusal, NEMO_ERR_CYCLE);
+- a hub goal whose out-degree exceeds one batch of child loads (TD_BATCH).
+"""
+import random
+
+import pytest
+
+from nemo_amd import engine as E
+from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE, corpus_from_graphs
+from oracle import oracle as O
+from tests.compare import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def _check(eng, corpus, mode=DIFF_REFERENCE):
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, diff_mode=mode)
+    res = E.analyze(corpus, s, f, diff_mode=mode, engine=eng, pulls=True)
+    assert_same(corpus, res, orc, len(f), check_pulls=True)
+
+
+def wide_prov(cond: str, width: int, seed: int, hub: int = 0, cycle: bool = False) -> dict:
+    """Three wide levels (root goals -> rules -> goals) plus a @next chain per
+    column and a few cross edges; `hub` extra rule children hang off goal 0."""
+    rng = random.Random(seed)
+    goals, rules, edges = [], [], []
+
+    def goal(name, table, t):
+        goals.append({"id": "goal_" + name, "label": f"{table}({name})", "table": table, "time": str(t)})
+
+    def rule(name, table, typ):
+        rules.append({"id": "rule_" + name, "label": table, "table": table, "type": typ})
+
+    goal("c0", cond, 1)
+    rule("c1", cond, "single")
+    edges += [{"from": "c0", "to": "c1"}]
+    for i in range(width):
+        t = ["t1", "t2", cond][i % 3]
+        goal(f"a{i}", t, 1)
+        rule(f"r{i}", t, "next" if i % 2 else "single")
+        goal(f"b{i}", t, 2)
+        rule(f"n{i}", t, "next")
+        goal(f"d{i}", t, 3)
+        edges += [{"from": f"a{i}", "to": f"r{i}"}, {"from": f"r{i}", "to": f"b{i}"},
+                  {"from": f"b{i}", "to": f"n{i}"}, {"from": f"n{i}", "to": f"d{i}"}]
+        if i and rng.random() < 0.3:
+            edges.append({"from": f"a{rng.randrange(i)}", "to": f"r{i}"})
+    edges.append({"from": "c1", "to": "a0"})
+    for k in range(hub):
+        rule(f"h{k}", "t1", "single")
+        goal(f"hg{k}", "t1", 2)
+        edges += [{"from": "a0", "to": f"h{k}"}, {"from": f"h{k}", "to": f"hg{k}"}]
+    gset = {g["id"][5:] for g in goals}
+    edges = [{"from": ("goal_" if e["from"] in gset else "rule_") + e["from"],
+              "to": ("goal_" if e["to"] in gset else "rule_") + e["to"]} for e in edges]
+    if cycle:
+        edges.append({"from": "goal_d7", "to": "rule_r7"})  # r7 -> b7 -> n7 -> d7 -> r7
+    return {"goals": goals, "rules": rules, "edges": edges}
+
+
+def test_wide_level_past_lds_frontier(eng):
+    graphs = [(it, "success" if it != 2 else "failure", wide_prov("pre", 5000, it), wide_prov("post", 5000, 10 + it))
+              for it in range(3)]
+    corpus = corpus_from_graphs(graphs)
+    assert min(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 8192
+    _check(eng, corpus)
+    _check(eng, corpus, mode=DIFF_PER_RUN)
+
+
+def test_hub_out_degree(eng):
+    graphs = [(it, "success" if it != 1 else "failure", wide_prov("pre", 2000, it, hub=300),
+               wide_prov("post", 2000, 20 + it, hub=37)) for it in range(2)]
+    corpus = corpus_from_graphs(graphs)
+    assert min(corpus.graph_size(g) for g in range(corpus.n_graphs)) >= 8192
+    _check(eng, corpus)
+
+
+def test_cycle_in_big_graph_refused(eng):
+    graphs = [(0, "success", wide_prov("pre", 3000, 1), wide_prov("post", 3000, 2, cycle=True))]
+    corpus = corpus_from_graphs(graphs)
+    assert corpus.graph_size(1) >= 8192
+    with pytest.raises(E.NemoError) as ei:
+        eng.load(corpus)
+    assert ei.value.code == 4

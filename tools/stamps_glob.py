@@ -25,6 +25,9 @@ d = np.diff(st[ok][:, :10], axis=1)
 print("graphs", int(ok.sum()), "total ticks per graph: median", np.median(d.sum(1)))
 for i, nm in enumerate(names):
     print(f"{nm:22s} median {np.median(d[:, i]):12.0f}  share {d[:, i].sum() / d.sum():.3f}")
+for i, nm in enumerate(["up stage", "up sweep", "down stage", "down sweep"]):
+    print(f"{nm:22s} median {np.median(st[ok][:, 10 + i]):12.0f}")
+print("sweep iterations (up)", np.median(st[ok][:, 14] & 0xFFFFFFFF), "with a spilled node", np.median(st[ok][:, 14] >> 32), "H* nodes", np.median(st[ok][:, 15]))
 ch = eng.chains()
 print("chains per graph", len(ch) / G, "max chain length", int(np.max(ch[:, 4])) if len(ch) else 0)
 eng.close()
