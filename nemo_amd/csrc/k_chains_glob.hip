@@ -283,9 +283,11 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
             int32_t d = ini, v[GS_KEEP];
 #pragma unroll
             for (int h = 0; h < GS_KEEP; h++) v[h] = L.rv[(base + u[h]) & M];
+            // keep the reads issued together: sunk into the conditional uses
+            // below, each would be its own LDS round trip
+            asm volatile("" ::: "memory");
 #pragma unroll
-            for (int h = 0; h < GS_KEEP; h++)
-              if (u[h] != GS_NOLINK) d = max(d, v[h] + 1);
+            for (int h = 0; h < GS_KEEP; h++) d = max(d, u[h] != GS_NOLINK ? v[h] + 1 : d);
             if (fl & GS_MORE) {  // links past the first four: the window's list, or HBM
               const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
               for (uint32_t t = GS_KEEP; t < ac; t++) d = max(d, L.rv[(base + L.adj[ao + t - GS_KEEP]) & M] + 1);
@@ -312,6 +314,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
               dv[h] = L.rv[(base + u[h]) & M];
               rr[h] = L.rc[(base + u[h]) & M];
             }
+            asm volatile("" ::: "memory");
 #pragma unroll
             for (int h = 0; h < GS_KEEP; h++)
               if (u[h] != GS_NOLINK) take(base + u[h], dv[h], rr[h]);
@@ -336,7 +339,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
         }
 #ifdef NEMO_STAMPS
         iters++;
-        spills += __ballot(mine && (fl & GS_SPILL)) != 0 ? 1u : 0u;
+        spills += __ballot(mine && (fl & GS_MORE)) != 0 ? 1u : 0u;
 #endif
         k = kn;
         lv = lv2;

@@ -27,7 +27,7 @@ for i, nm in enumerate(names):
     print(f"{nm:22s} median {np.median(d[:, i]):12.0f}  share {d[:, i].sum() / d.sum():.3f}")
 for i, nm in enumerate(["up stage", "up sweep", "down stage", "down sweep"]):
     print(f"{nm:22s} median {np.median(st[ok][:, 10 + i]):12.0f}")
-print("sweep iterations (up)", np.median(st[ok][:, 14] & 0xFFFFFFFF), "with a spilled node", np.median(st[ok][:, 14] >> 32), "H* nodes", np.median(st[ok][:, 15]))
+print("sweep iterations (up)", np.median(st[ok][:, 14] & 0xFFFFFFFF), "with a node of > 8 in-ring links", np.median(st[ok][:, 14] >> 32), "H* nodes", np.median(st[ok][:, 15]))
 ch = eng.chains()
 print("chains per graph", len(ch) / G, "max chain length", int(np.max(ch[:, 4])) if len(ch) else 0)
 eng.close()
