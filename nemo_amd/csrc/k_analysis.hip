@@ -1,5 +1,7 @@
 // k_analysis.hip — markConditionHolds, cleanCopyProv, collapseNextChains and
 // extractProtos as per-graph workgroup kernels (one graph per workgroup).
+#include <algorithm>
+
 #include "device.h"
 #include "internal.h"
 
@@ -19,6 +21,7 @@ __global__ __launch_bounds__(B) void k_mark(DevCorpus c, int skip_tier) {
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
   if (skip_tier && tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
+  if (gv.V >= NEMO_CSR_BIG) return;                                      // k_mw_mark_*'s graph
   const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
   for (uint32_t i = threadIdx.x; i < c.words; i += B) s_tq[i] = 0;
   if (threadIdx.x == 0) {
@@ -72,6 +75,7 @@ __global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
   if (skip_tier && tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;  // k_marksimp's graph
+  if (gv.V >= NEMO_CSR_BIG) return;                                      // k_mw_simplify_*'s graph
   uint8_t *f = gv.flags;
   for (uint32_t x = threadIdx.x; x < gv.V; x += B) {
     uint8_t fl = f[x] & NEMO_F_HOLDS;
@@ -118,6 +122,147 @@ __global__ __launch_bounds__(B) void k_simplify_flags(DevCorpus c, int skip_tier
   __syncthreads();
   if (threadIdx.x == 0) c.holdany[g] = s_hold;
 }
+
+// The same two kernels for the big graphs (V >= NEMO_CSR_BIG: the deep
+// corpora's 1M-node graphs, few per corpus): one workgroup per graph leaves
+// the chip latency-bound on dependent row reads, so each phase runs as its own
+// multi-workgroup kernel over the host's list of big graphs (2D grid: x =
+// chunk of the graph, y = list slot; kernel boundaries replace the barriers).
+// markConditionHolds' table set Tq and its any-flag are ORed per graph into
+// scratch (c.s_c at the graph's V+G slice: [0] any, [1 + w] Tq words).
+#define MW_BLOCK 256
+#define MW_LOOP(c, skip, ...)                                                              \
+  for (uint32_t b_ = blockIdx.y; b_ < c.n_big; b_ += gridDim.y) {                          \
+    const uint32_t g = c.big[b_];                                                          \
+    if (c.err[g]) continue;                                                                \
+    const GraphView gv = c.view(g);                                                        \
+    if (skip && tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) continue;                          \
+    const uint32_t t0 = blockIdx.x * MW_BLOCK + threadIdx.x, stride = gridDim.x * MW_BLOCK; \
+    uint32_t *tqg = c.s_c + gv.n0 + g;                                                     \
+    (void)t0, (void)stride, (void)tqg;                                                     \
+    __VA_ARGS__                                                                            \
+  }
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_mark_z(DevCorpus c, int skip) {
+  MW_LOOP(c, skip, {
+    if (blockIdx.x == 0) {
+      for (uint32_t i = threadIdx.x; i <= c.words; i += MW_BLOCK) tqg[i] = 0;
+      if (threadIdx.x == 0) c.prehold[g] = 0;
+    }
+  })
+}
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_mark_a(DevCorpus c, int skip) {
+  __shared__ uint32_t s_tq[NEMO_MAX_TABLES / 32];
+  __shared__ uint32_t s_any;
+  MW_LOOP(c, skip, {
+    const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
+    for (uint32_t i = threadIdx.x; i < c.words; i += MW_BLOCK) s_tq[i] = 0;
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      const uint32_t w = gv.word[x];
+      if (is_rule(w) || gv.outdeg(x) == 0) continue;
+      bool pos = false, neg = false;
+      for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) {
+        const uint32_t rcn = gv.rc[j];
+        if (table_of(gv.word[rcn]) != C) continue;
+        for (uint32_t i = gv.rp[rcn]; i < gv.rp[rcn + 1]; i++) {
+          const uint32_t t = gv.rc[i];
+          if (table_of(gv.word[t]) != C) continue;
+          pos = true;
+          neg |= gv.indeg(t) > 0;
+        }
+      }
+      if (pos && !neg) {
+        atomicOr(&s_tq[table_of(w) >> 5], 1u << (table_of(w) & 31));
+        s_any = 1;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < c.words; i += MW_BLOCK)
+      if (s_tq[i]) atomicOr(&tqg[1 + i], s_tq[i]);
+    if (threadIdx.x == 0 && s_any) atomicOr(&tqg[0], 1u);
+    __syncthreads();
+  })
+}
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_mark_b(DevCorpus c, int skip) {
+  __shared__ uint32_t s_tq[NEMO_MAX_TABLES / 32 + 1];
+  MW_LOOP(c, skip, {
+    const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
+    for (uint32_t i = threadIdx.x; i <= c.words; i += MW_BLOCK) s_tq[i] = tqg[i];
+    __syncthreads();
+    const bool any = s_tq[0] != 0;
+    uint32_t pre = 0;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      const uint32_t w = gv.word[x];
+      const uint32_t t = table_of(w);
+      const bool h = any && !is_rule(w) && (t == C || ((s_tq[1 + (t >> 5)] >> (t & 31)) & 1u));
+      gv.flags[x] = h ? (uint8_t)NEMO_F_HOLDS : (uint8_t)0;
+      pre += (h && t == c.table_pre) ? 1u : 0u;
+    }
+    for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);
+    if (lane_id() == 0 && pre) atomicAdd(&c.prehold[g], pre);
+    __syncthreads();
+  })
+}
+// cleanCopyProv + collapseNextChains' local flags, one kernel per phase
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_1(DevCorpus c, int skip) {
+  MW_LOOP(c, skip, {
+    uint8_t *f = gv.flags;
+    if (t0 == 0) c.holdany[g] = 0;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      uint8_t fl = f[x] & NEMO_F_HOLDS;
+      if (!is_rule(gv.word[x]) || (gv.indeg(x) > 0 && gv.outdeg(x) > 0)) fl |= NEMO_F_KEPT;
+      f[x] = fl;
+    }
+  })
+}
+#define ISNEXT(v) (is_rule(gv.word[v]) && type_of(gv.word[v]) == NEMO_TYPE_NEXT && (f[v] & NEMO_F_KEPT))
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_2(DevCorpus c, int skip) {
+  MW_LOOP(c, skip, {
+    uint8_t *f = gv.flags;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      if (is_rule(gv.word[x])) continue;
+      uint8_t b = 0;
+      for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++)
+        if (ISNEXT(gv.rc[j])) b |= FT_NP;
+      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++)
+        if (ISNEXT(gv.fc[j])) b |= FT_NC;
+      f[x] |= b;
+    }
+  })
+}
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_3(DevCorpus c, int skip) {
+  MW_LOOP(c, skip, {
+    uint8_t *f = gv.flags;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      if (!ISNEXT(x)) continue;
+      bool gp = false, gc = false;
+      for (uint32_t j = gv.rp[x]; j < gv.rp[x + 1]; j++) gp |= (f[gv.rc[j]] & FT_NP) != 0;
+      for (uint32_t j = gv.fp[x]; j < gv.fp[x + 1]; j++) gc |= (f[gv.fc[j]] & FT_NC) != 0;
+      uint8_t fl = f[x];
+      if (gp || gc) fl |= NEMO_F_DELETED;
+      if (!gp && gc) fl |= NEMO_F_HEAD;
+      if (gp && !gc) fl |= NEMO_F_TAIL;
+      f[x] = fl;
+    }
+  })
+}
+#undef ISNEXT
+__global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_4(DevCorpus c, int skip) {
+  MW_LOOP(c, skip, {
+    uint8_t *f = gv.flags;
+    bool hold = false;
+    for (uint32_t x = t0; x < gv.V; x += stride) {
+      if (is_rule(gv.word[x])) continue;
+      uint8_t fl = f[x];
+      if ((fl & FT_NP) && (fl & FT_NC)) fl |= NEMO_F_DELETED;
+      f[x] = fl & (uint8_t)~(FT_NP | FT_NC);
+      hold |= (fl & (NEMO_F_HOLDS | NEMO_F_DELETED)) == NEMO_F_HOLDS;
+    }
+    if (__any(hold) && lane_id() == 0) c.holdany[g] = 1;  // extractProtos' gate (prototype.go:13)
+  })
+}
+#undef MW_LOOP
 
 // extractProtos' per-run query (prototype.go:11-24) and missingFrom's table
 // set (:143-147) on the simplified post graph, without materialising it:
@@ -753,17 +898,29 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_
   }
 }
 
+static dim3 mw_grid(const DevCorpus &c) { return dim3(std::max(1u, c.pg_chunks), std::min(c.n_big, 65535u)); }
 void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+  const int sk = skip_tier ? 1 : 0;
   if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_mark<1024>, dim3(c.G), dim3(1024), 0, s, c, skip_tier ? 1 : 0);
+    hipLaunchKernelGGL(k_mark<1024>, dim3(c.G), dim3(1024), 0, s, c, sk);
   else
-    hipLaunchKernelGGL(k_mark<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
+    hipLaunchKernelGGL(k_mark<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, sk);
+  if (!c.n_big) return;
+  hipLaunchKernelGGL(k_mw_mark_z, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
+  hipLaunchKernelGGL(k_mw_mark_a, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
+  hipLaunchKernelGGL(k_mw_mark_b, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
 }
 void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+  const int sk = skip_tier ? 1 : 0;
   if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_simplify_flags<1024>, dim3(c.G), dim3(1024), 0, s, c, skip_tier ? 1 : 0);
+    hipLaunchKernelGGL(k_simplify_flags<1024>, dim3(c.G), dim3(1024), 0, s, c, sk);
   else
-    hipLaunchKernelGGL(k_simplify_flags<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, skip_tier ? 1 : 0);
+    hipLaunchKernelGGL(k_simplify_flags<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, sk);
+  if (!c.n_big) return;
+  hipLaunchKernelGGL(k_mw_simplify_1, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
+  hipLaunchKernelGGL(k_mw_simplify_2, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
+  hipLaunchKernelGGL(k_mw_simplify_3, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
+  hipLaunchKernelGGL(k_mw_simplify_4, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
 }
 void launch_marksimp(const DevCorpus &c, hipStream_t s) {
   if (!c.t_ms.bytes) return;
