@@ -60,6 +60,7 @@ struct nemo_ctx {
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
+  uint64_t bigVmax = 0;              // the largest of them
   uint32_t big_chunks = 1;           // k_csrb_* workgroups per big graph
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
 
@@ -82,6 +83,8 @@ struct nemo_ctx {
   // memory asynchronously; the first fetch waits for them
   int pull_which = -1;
   uint32_t pull_slots = 0, pull_slot_cap = 0;
+  uint32_t *d_pck = nullptr;          // big graphs' pull chunk table
+  size_t pull_ck_cap = 0;
   uint32_t *d_pcnt = nullptr, *d_psrc = nullptr, *d_pdst = nullptr;
   uint64_t *d_poff = nullptr, pull_cap = 0;
   unsigned long long *d_pcur = nullptr;
@@ -359,6 +362,8 @@ static void release_corpus(nemo_ctx *c) {
   c->pull_hint[0] = c->pull_hint[1] = c->pull_hint[2] = 0;
   c->pull_cap = 0;
   c->pull_slot_cap = 0;
+  c->d_pck = nullptr;
+  c->pull_ck_cap = 0;
   c->pull_which = -1;
   c->d_tcounts = c->d_tpre = c->d_tpost = c->d_tasync = nullptr;
   c->d_hlab = nullptr;
@@ -760,12 +765,14 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     std::vector<uint32_t> big;
     uint64_t emax = 0;
     c->bigV = c->bigE = 0;
+    c->bigVmax = 0;
     for (uint32_t g = 0; g < G; g++) {
       const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
       if (v < NEMO_CSR_BIG) continue;
       big.push_back(g);
       emax = std::max(emax, e);
       c->bigV += (double)v;
+      c->bigVmax = std::max<uint64_t>(c->bigVmax, v);
       c->bigE += (double)e;
     }
     uint32_t *db = nullptr;
@@ -1692,6 +1699,23 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   a.cnt = c->d_pcnt;
   a.off = c->d_poff;
   a.cursor = c->d_pcur;
+  // big graphs' chunk table (k_diff.hip MWP_CH = 4096 nodes or chains per chunk)
+  a.ccnt = nullptr;
+  a.maxck = 0;
+  const uint64_t vg0 = c->node_off[g0 + 1] - c->node_off[g0];
+  const uint32_t rows = which == 2 ? (vg0 >= NEMO_CSR_BIG ? slots : 0u) : c->dc.n_big;
+  if (rows) {
+    a.maxck = (uint32_t)(2 * ((c->bigVmax + 4095) / 4096));
+    const size_t need = (size_t)rows * a.maxck;
+    if (need > c->pull_ck_cap) {
+      dfree(c, c->d_pck);
+      c->d_pck = nullptr;
+      c->pull_ck_cap = 0;
+      if ((rc = dalloc(c, &c->d_pck, need))) return rc;
+      c->pull_ck_cap = need;
+    }
+    a.ccnt = c->d_pck;
+  }
   c->pull_args = a;
   if ((rc = pull_grow(c, std::max<uint64_t>(cap, 1)))) return rc;
   return pull_launch(c);

@@ -38,6 +38,10 @@ struct PullArgs {
   unsigned long long *cursor;  // region allocator (zeroed before the launch)
   uint64_t cap;             // capacity of src/dst
   uint32_t *src, *dst;      // output
+  // big slots (graph of >= NEMO_CSR_BIG nodes): multi-workgroup pull over
+  // MWP_CH-node chunks, [row slots][maxck] chunk counts -> offsets (null: none)
+  uint32_t *ccnt;
+  uint32_t maxck;
 };
 
 struct TrigArgs {

@@ -619,6 +619,7 @@ __device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, c
   }
   const GraphView gv = c.view(g);
   if (tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph or diff entry
+  if (a.ccnt && gv.V >= NEMO_CSR_BIG) return;             // k_mwp_*'s graph
   const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
@@ -692,6 +693,142 @@ __device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, c
       }
     }
     pos += tot;
+  }
+}
+
+// The same pull for big graphs (V >= NEMO_CSR_BIG), spread over MWP_CH-node
+// chunks: one workgroup per graph walked ~1M rows as a latency-bound loop.
+// Three kernels: each chunk counts its edges (node chunks, then chain
+// chunks); one workgroup per slot scans its chunk counts into offsets and
+// claims the slot's region; each chunk writes its edges from its offset in
+// the same order as pull_slot (rows in node order, each row in CSR order,
+// then collapsed edges by k).  Slot rows: the big-graph list (raw /
+// simplified) or the diff entries.
+#define MWP_CH 4096u
+#define MWP_BLOCK 256
+struct MwpSlot {
+  uint32_t slot, g, nnc, nt;
+  const uint8_t *m;
+};
+__device__ __forceinline__ bool mwp_slot(const DevCorpus &c, const PullArgs &a, uint32_t y, MwpSlot &s,
+                                         GraphView &gv) {
+  if (a.which == 2) {
+    s.slot = y;
+    s.g = a.g0;
+  } else {
+    if (y >= c.n_big) return false;
+    s.g = s.slot = c.big[y];
+  }
+  if (c.err[s.g]) return false;
+  gv = c.view(s.g);
+  if (tier_fits(c.t_pull, gv.V, gv.E, gv.nlev) || gv.V < NEMO_CSR_BIG) return false;
+  const uint32_t nch = a.which == 1 ? c.nch[s.g] : 0u;
+  s.nnc = (gv.V + MWP_CH - 1) / MWP_CH;
+  s.nt = s.nnc + (nch + MWP_CH - 1) / MWP_CH;
+  s.m = a.mask ? a.mask + (size_t)s.slot * a.mask_stride : nullptr;
+  return true;
+}
+// edges of node u (raw / simplified / diff row) or of chain k (collapsed edges)
+__device__ __forceinline__ uint32_t mwp_row_count(const PullArgs &a, const GraphView &gv, const uint8_t *m,
+                                                  uint32_t u) {
+  uint32_t n = 0;
+  if (pull_alive(a.which, gv.flags, m, u))
+    for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) n += pull_alive(a.which, gv.flags, m, gv.fc[j]);
+  return n;
+}
+__device__ __forceinline__ uint32_t mwp_chain_count(const GraphView &gv, const uint8_t *m, uint32_t h, uint32_t t) {
+  uint32_t n = 0;
+  for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) n += pull_alive(1, gv.flags, m, gv.rc[j]);
+  for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) n += pull_alive(1, gv.flags, m, gv.fc[j]);
+  return n;
+}
+__global__ __launch_bounds__(MWP_BLOCK) void k_mwp_count(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_n;
+  MwpSlot s;
+  GraphView gv;
+  if (!mwp_slot(c, a, blockIdx.y, s, gv) || blockIdx.x >= s.nt) return;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  uint32_t n = 0;
+  if (blockIdx.x < s.nnc) {
+    const uint32_t u0 = blockIdx.x * MWP_CH, u1 = min(gv.V, u0 + MWP_CH);
+    for (uint32_t u = u0 + threadIdx.x; u < u1; u += MWP_BLOCK) n += mwp_row_count(a, gv, s.m, u);
+  } else {
+    const uint32_t *ch = c.chain + 5 * gv.n0, nch = c.nch[s.g];
+    const uint32_t k0 = (blockIdx.x - s.nnc) * MWP_CH, k1 = min(nch, k0 + MWP_CH);
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += MWP_BLOCK) n += mwp_chain_count(gv, s.m, ch[5 * k], ch[5 * k + 1]);
+  }
+  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
+  if (lane_id() == 0 && n) atomicAdd(&s_n, n);
+  __syncthreads();
+  if (threadIdx.x == 0) a.ccnt[(size_t)blockIdx.y * a.maxck + blockIdx.x] = s_n;
+}
+__global__ __launch_bounds__(MWP_BLOCK) void k_mwp_scan(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_lds[MWP_BLOCK / 64];
+  MwpSlot s;
+  GraphView gv;
+  if (!mwp_slot(c, a, blockIdx.x, s, gv)) return;
+  const uint32_t tot = block_scan_inplace<MWP_BLOCK>(a.ccnt + (size_t)blockIdx.x * a.maxck, s.nt, s_lds);
+  if (threadIdx.x == 0) {
+    a.off[s.slot] = atomicAdd(a.cursor, (unsigned long long)tot);
+    a.cnt[s.slot] = tot;
+  }
+}
+__global__ __launch_bounds__(MWP_BLOCK) void k_mwp_write(DevCorpus c, PullArgs a) {
+  __shared__ uint32_t s_lds[MWP_BLOCK / 64];
+  MwpSlot s;
+  GraphView gv;
+  if (!mwp_slot(c, a, blockIdx.y, s, gv) || blockIdx.x >= s.nt) return;
+  if (a.off[s.slot] + a.cnt[s.slot] > a.cap) return;  // the host re-runs the pull with room
+  uint64_t pos = a.off[s.slot] + a.ccnt[(size_t)blockIdx.y * a.maxck + blockIdx.x];
+  if (blockIdx.x < s.nnc) {
+    const uint32_t u0 = blockIdx.x * MWP_CH, u1 = min(gv.V, u0 + MWP_CH);
+    for (uint32_t base = u0; base < u1; base += MWP_BLOCK) {
+      const uint32_t u = base + threadIdx.x;
+      const uint32_t n = u < u1 ? mwp_row_count(a, gv, s.m, u) : 0u;
+      uint32_t tot;
+      uint64_t o = pos + block_exscan<MWP_BLOCK>(n, &tot, s_lds);
+      if (n)
+        for (uint32_t j = gv.fp[u]; j < gv.fp[u + 1]; j++) {
+          const uint32_t v = gv.fc[j];
+          if (!pull_alive(a.which, gv.flags, s.m, v)) continue;
+          a.src[o] = u;
+          a.dst[o] = v;
+          o++;
+        }
+      pos += tot;
+    }
+  } else {
+    const uint32_t *ch = c.chain + 5 * gv.n0, nch = c.nch[s.g];
+    const uint32_t k0 = (blockIdx.x - s.nnc) * MWP_CH, k1 = min(nch, k0 + MWP_CH);
+    for (uint32_t base = k0; base < k1; base += MWP_BLOCK) {
+      const uint32_t k = base + threadIdx.x;
+      uint32_t h = 0, t = 0, n = 0;
+      if (k < k1) {
+        h = ch[5 * k];
+        t = ch[5 * k + 1];
+        n = mwp_chain_count(gv, s.m, h, t);
+      }
+      uint32_t tot;
+      uint64_t o = pos + block_exscan<MWP_BLOCK>(n, &tot, s_lds);
+      if (n) {
+        for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) {
+          const uint32_t p = gv.rc[j];
+          if (!pull_alive(1, gv.flags, s.m, p)) continue;
+          a.src[o] = p;
+          a.dst[o] = gv.V + k;
+          o++;
+        }
+        for (uint32_t j = gv.fp[t]; j < gv.fp[t + 1]; j++) {
+          const uint32_t q = gv.fc[j];
+          if (!pull_alive(1, gv.flags, s.m, q)) continue;
+          a.src[o] = gv.V + k;
+          a.dst[o] = q;
+          o++;
+        }
+      }
+      pos += tot;
+    }
   }
 }
 
@@ -1065,6 +1202,12 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
     hipLaunchKernelGGL(k_pull<1024>, dim3(grid), dim3(1024), 0, s, c, a);
   else
     hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c, a);
+  if (!a.ccnt) return;
+  const uint32_t rows = a.which == 2 ? slots : c.n_big;
+  if (!rows) return;
+  hipLaunchKernelGGL(k_mwp_count, dim3(a.maxck, rows), dim3(MWP_BLOCK), 0, s, c, a);
+  hipLaunchKernelGGL(k_mwp_scan, dim3(rows), dim3(MWP_BLOCK), 0, s, c, a);
+  hipLaunchKernelGGL(k_mwp_write, dim3(a.maxck, rows), dim3(MWP_BLOCK), 0, s, c, a);
 }
 // failGoals' label set of one graph (differential-provenance.go:23-24) into
 // device memory as [n, label...]: the hand-over a sharded reference-mode
