@@ -122,7 +122,7 @@ struct DiffWin {
   uint16_t adj[DW_E];     // window-local index of each extra in-window link
   uint16_t u0[DW_N], u1[DW_N];  // first two in-window links (DW_SPILL = none)
   uint8_t val[DW_N];      // F / B bit (modes 0, 1), D bit (mode 2)
-  uint32_t l0, l1;        // first and last Kahn level in the window
+  uint32_t lv[DW_N];      // Kahn level
 };
 
 // g0 in Kahn order, pass 1 (one thread per position): inverse order, row
@@ -206,8 +206,6 @@ __device__ __noinline__ void diff_window_sweep(uint32_t V, const DiffArgs &a, ui
       x[q] = MODE == 2 ? 0 : (good ? 1 : 0);
       if (MODE == 2 && !(ob[q] & DB_D)) r1[q] = r0[q];  // only D nodes get a depth
       if (MODE != 2 && good) r1[q] = r0[q];             // Good: set regardless of neighbours
-      if (in && k == 0) W.l0 = lev[q];
-      if (in && k == n - 1) W.l1 = lev[q];
     }
 #pragma unroll
     for (int q = 0; q < PT; q++) {
@@ -277,6 +275,8 @@ __device__ __noinline__ void diff_window_sweep(uint32_t V, const DiffArgs &a, ui
       } else {
         W.val[k] = (uint8_t)x[q];
       }
+      W.lv[k] = lev[q];
+      W.ln[k] = 0;
       if (!cx[q]) continue;
       const bool spill = base + cx[q] > DW_E;
       W.off[k] = base;
@@ -297,57 +297,68 @@ __device__ __noinline__ void diff_window_sweep(uint32_t V, const DiffArgs &a, ui
     acc_s += t_b - t_a;
     t_a = t_b;
 #endif
-    const uint32_t l0 = W.l0, nl = W.l1 - l0 + 1u;
-    for (uint32_t i = 0; i < nl; i++) {
-      const uint32_t li = l0 + (FWD ? i : nl - 1 - i);
-#pragma unroll
-      for (int q = 0; q < PT; q++) {
-        if (lev[q] != li) continue;
-        const uint32_t k = tid + q * B;
-        const uint32_t v0 = W.u0[k], v1 = W.u1[k];
-        if (MODE != 2) {
-          if (x[q]) continue;
-          // plain ORs, no short-circuit: the ROCm 7.2 compiler mis-evaluated
-          // `(u0 && val[u0]) || (u1 && val[u1])` in the 1024-thread instance
-          uint32_t hv = 0;
-          if (v0 != DW_SPILL) hv |= W.val[v0];
-          if (v1 != DW_SPILL) hv |= W.val[v1];
-          if (!hv && cx[q]) {
-            if (W.ln[k] != DW_SPILL) {
-              const uint32_t o = W.off[k], m = W.ln[k];
-              for (uint32_t t = 0; t < m; t++) hv |= W.val[W.adj[o + t]];
-            } else {
-              for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
-                const uint32_t p = col[j];
-                if (FWD ? p >= w0 : p < w1) hv |= W.val[p - w0];
+    // the window's levels, walked by ONE wave: a level is a few LDS round trips
+    // and no workgroup barrier (a wave's LDS operations complete in order);
+    // positions are level-sorted, so a level is a contiguous run
+    if (tid < 64) {
+      const uint32_t lane = lane_id();
+      uint32_t k = 0;
+      while (k < n) {
+        const uint32_t q = k + lane, kk = FWD ? q : n - 1u - q;
+        const bool in = q < n;
+        const uint32_t lv = in ? W.lv[kk] : NIL;
+        const uint32_t l = __builtin_amdgcn_readfirstlane(lv);
+        const bool mine = in && lv == l;
+        const uint64_t m = __ballot(mine);
+        if (mine) {
+          const uint32_t v0 = W.u0[kk], v1 = W.u1[kk], ln = W.ln[kk];
+          if (MODE != 2) {
+            if (!W.val[kk]) {
+              const uint32_t a0 = W.val[v0 != DW_SPILL ? v0 : kk], a1 = W.val[v1 != DW_SPILL ? v1 : kk];
+              uint32_t hv = (v0 != DW_SPILL ? a0 : 0u) | (v1 != DW_SPILL ? a1 : 0u);
+              if (!hv && ln) {
+                if (ln != DW_SPILL) {
+                  const uint32_t o = W.off[kk];
+                  for (uint32_t t = 0; t < ln; t++) hv |= W.val[W.adj[o + t]];
+                } else {
+                  const uint32_t i = w0 + kk;
+                  for (uint32_t j = ptr[i] + 2; j < ptr[i + 1]; j++) {
+                    const uint32_t p = col[j];
+                    if (FWD ? p >= w0 : p < w1) hv |= W.val[p - w0];
+                  }
+                }
+              }
+              if (hv) W.val[kk] = 1;
+            }
+          } else if (W.val[kk]) {  // D nodes get a depth
+            const int32_t a0 = W.dep[v0 != DW_SPILL ? v0 : kk], a1 = W.dep[v1 != DW_SPILL ? v1 : kk];
+            int32_t d = W.dep[kk];
+            if (v0 != DW_SPILL) d = max(d, a0 + 1);
+            if (v1 != DW_SPILL) d = max(d, a1 + 1);
+            if (ln) {
+              if (ln != DW_SPILL) {
+                const uint32_t o = W.off[kk];
+                for (uint32_t t = 0; t < ln; t++) d = max(d, W.dep[W.adj[o + t]] + 1);
+              } else {
+                const uint32_t i = w0 + kk;
+                for (uint32_t j = ptr[i] + 2; j < ptr[i + 1]; j++) {
+                  const uint32_t p = col[j];
+                  if (p >= w0 && (bits[p] & DB_D)) d = max(d, W.dep[p - w0] + 1);
+                }
               }
             }
+            W.dep[kk] = d;
           }
-          if (hv) {
-            x[q] = 1;
-            W.val[k] = 1;
-          }
-        } else {
-          if (!(ob[q] & DB_D)) continue;
-          int32_t d = x[q];
-          if (v0 != DW_SPILL) d = max(d, W.dep[v0] + 1);
-          if (v1 != DW_SPILL) d = max(d, W.dep[v1] + 1);
-          if (cx[q]) {
-            if (W.ln[k] != DW_SPILL) {
-              const uint32_t o = W.off[k], m = W.ln[k];
-              for (uint32_t t = 0; t < m; t++) d = max(d, W.dep[W.adj[o + t]] + 1);
-            } else {
-              for (uint32_t j = r0[q] + 2; j < r1[q]; j++) {
-                const uint32_t p = col[j];
-                if (p >= w0 && (bits[p] & DB_D)) d = max(d, W.dep[p - w0] + 1);
-              }
-            }
-          }
-          x[q] = d;
-          W.dep[k] = d;
         }
+        k += (uint32_t)__popcll(m);
+        wsync();
       }
-      __syncthreads();
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * B;
+      if (k < n) x[q] = MODE == 2 ? W.dep[k] : (int32_t)W.val[k];
     }
 #ifdef NEMO_STAMPS
     DW_T(t_b);
@@ -402,6 +413,20 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   uint8_t *bits = a.bits + (size_t)e * V;     // by Kahn position
   int32_t *depth = a.depth + (size_t)e * V;   // by Kahn position
   uint8_t *mask = a.mask + (size_t)e * V;     // by node
+#ifdef NEMO_STAMPS
+  unsigned long long *st = c.stamps ? c.stamps + 16 * (size_t)e : nullptr, tk;
+#define DK_T(slot)                      \
+  do {                                  \
+    TICK(tk);                           \
+    if (threadIdx.x == 0 && st) st[slot] = tk; \
+  } while (0)
+#else
+  unsigned long long *st = nullptr;
+#define DK_T(slot) \
+  do {             \
+  } while (0)
+#endif
+  DK_T(9);
   if (threadIdx.x == 0) s_max = -1;
   for (uint32_t i = threadIdx.x; i < V; i += B) bits[i] = 0;
   __threadfence();
@@ -409,14 +434,11 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
   diff_fail_goals<B>(a, src, bits, a.r0pos);
   __threadfence();
   __syncthreads();
-#ifdef NEMO_STAMPS
-  unsigned long long *st = c.stamps ? c.stamps + 16 * (size_t)e : nullptr;
-#else
-  unsigned long long *st = nullptr;
-#endif
+  DK_T(10);
   diff_window_sweep<B, 0>(V, a, bits, depth, W, s_red, st);
   diff_window_sweep<B, 1>(V, a, bits, depth, W, s_red, st);
   diff_window_sweep<B, 2>(V, a, bits, depth, W, s_red, st);
+  DK_T(11);
   // D mask (by node); goal leaves of D (no D child)
   for (uint32_t i = threadIdx.x; i < V; i += B) {
     const uint8_t b = bits[i];
@@ -449,6 +471,8 @@ __global__ __launch_bounds__(B) void k_diff(DevCorpus c, DiffArgs a) {
       a.missing[2 * k + 1] = gv.topo[i];
     }
   }
+  DK_T(12);
+#undef DK_T
 }
 
 // k_diff over the LDS graph tier: the same three level sweeps (Fwd*, Bwd*,

@@ -12,8 +12,10 @@ from tools import synth
 runs = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 eot = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
-corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16)
+corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16, body_extra=6, nval=3, nloc=4)
 s, f = corpus.success_iters(), corpus.failed_iters()
+if not f:  # entries only need a label source: take successful runs
+    f = [i for i in s if i != 0][:4]
 eng = E.Engine(0)
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 eng.set_timing(True)
@@ -25,4 +27,7 @@ tot = st[:, :9].sum(1)
 print("ticks per entry: median", np.median(tot))
 for i, nm in enumerate(names):
     print(f"{nm:10s} median {np.median(st[:, i]):12.0f}  share {st[:, i].sum() / tot.sum():.3f}")
+d = np.diff(st[:, 9:13], axis=1)
+for i, nm in enumerate(["clear + failGoals", "three sweeps", "mask + leaves + missing"]):
+    print(f"{nm:24s} median {np.median(d[:, i]):12.0f}")
 eng.close()
