@@ -938,8 +938,10 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
 // by LDS cursors and each row sorted there, then written out coalesced.  A
 // bucket of more than CB_LDS_E edges (a hub-heavy one) sorts in HBM instead.
 #define CB_LDS_E 14336u
+#define CB_WSORT_MIN 12u
 __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   __shared__ uint32_t cnt[CB_NB + 1];
+  __shared__ uint32_t s_long[CB_NB], s_nlong;
   __shared__ uint32_t rows[CB_LDS_E];
   __shared__ uint32_t s_lds[CB_BLOCK / 64];
   __shared__ uint32_t s_cr;
@@ -968,12 +970,39 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) dst[atomicAdd(&cnt[ek[j] - v0], 1u)] = ev[j];
   __threadfence_block();
   __syncthreads();  // cnt[i] = end of row i (local)
-  // rows sorted (a merged duplicate DUETO edge is adjacent); forward rows count relationships created
+  // rows sorted (a merged duplicate DUETO edge is adjacent): short rows by
+  // their thread, rows of CB_WSORT_MIN..64 entries by a whole wave (bitonic
+  // network over shuffles) -- one thread heap-sorting a 60-entry row in LDS
+  // held the workgroup for most of its time
+  if (threadIdx.x == 0) s_nlong = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
+    const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i], n = z - a;
+    const bool wide = n >= CB_WSORT_MIN && n <= 64u;
+    wave_append(wide, i, s_long, &s_nlong);
+    if (!wide) sort_row(dst + a, n);
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x >> 6; q < s_nlong; q += CB_BLOCK / 64) {
+    const uint32_t i = s_long[q], a = i ? cnt[i - 1] : 0u, n = cnt[i] - a, l = lane_id();
+    uint32_t x = l < n ? dst[a + l] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, (int)j);
+        const bool up = (l & k) == 0, low = (l & j) == 0;
+        x = (low == up) ? min(x, y) : max(x, y);
+      }
+    if (l < n) dst[a + l] = x;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // forward rows count relationships created (pre-post-prov.go:150-210)
   const uint32_t *word = c.word + n0;
   uint32_t created = 0;
   for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
     const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i];
-    sort_row(dst + a, z - a);
     if (dir) continue;
     const bool rv = is_rule(word[v0 + i]);
     for (uint32_t j = a; j < z; j++) {
