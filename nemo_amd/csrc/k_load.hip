@@ -938,7 +938,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
 // by LDS cursors and each row sorted there, then written out coalesced.  A
 // bucket of more than CB_LDS_E edges (a hub-heavy one) sorts in HBM instead.
 #define CB_LDS_E 14336u
-#define CB_WSORT_MIN 12u
+#define CB_WSORT_MIN 20u
 __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   __shared__ uint32_t cnt[CB_NB + 1];
   __shared__ uint32_t s_long[CB_NB], s_nlong;
