@@ -726,20 +726,23 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
 // atomics), so the kernel is built to keep that chain short:
 //   - the frontier lives in LDS (the level's nodes are not re-read from topo[]
 //     unless the level outgrows TD_Q);
-//   - every lane issues up to TD_BATCH child loads and then as many counter
-//     atomics at once, so a node of out-degree <= TD_BATCH costs one round
-//     trip of each, not one per child;
-//   - the ready children of a lane are appended with one wave scan and one LDS
-//     atomic per wave;
-//   - 256 threads: four waves meet at the two barriers of a level.
+//   - edge-parallel: the frontier's rows are published with one block scan of
+//     their degrees, and each thread takes edges (a binary search over the
+//     row offsets in LDS), so a lane has ~one child load and one counter
+//     atomic in flight.  A returning device-scope atomic costs ~3k cycles
+//     under load; a lane queueing a whole row of them (one node per lane)
+//     spent ~60 % of each level there (135 -> 115 -> 73 ms per C5 launch);
+//   - ready children are appended with one wave scan and one LDS atomic per
+//     wave; 256 threads, so the barriers of a level are four waves'.
 #define TD_B 256
 #define TD_Q 4096u
-#define TD_BATCH 16
+#define TD_EPT 4  // frontier edges per thread per round
 __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   __shared__ uint32_t s_q[2][TD_Q];
   // appends of level L go to s_n[(L + 1) % 3]: read after the level's barrier,
   // reset during level L + 2, so one barrier per level orders everything
   __shared__ uint32_t s_n[3];
+  __shared__ uint32_t s_eo[TD_B], s_j0[TD_B], s_red[TD_B / 64];
   const uint32_t g = c.big[blockIdx.x];
   if (c.err[g]) return;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
@@ -771,55 +774,59 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   }
   __syncthreads();
   uint32_t lo = 0, hi = s_n[1], nl = 0, cur = 0, k3 = 1;  // k3 = (nl + 1) % 3
-#ifdef NEMO_STAMPS
-  unsigned long long acc[5] = {0, 0, 0, 0, 0}, ta, tb;
-#define TD_T(k) \
-  do {          \
-    TICK(tb);   \
-    acc[k] += tb - ta; \
-    ta = tb;    \
-  } while (0)
-  TICK(ta);
-#else
-#define TD_T(k) \
-  do {          \
-  } while (0)
-#endif
   while (lo < hi) {
     const uint32_t n = hi - lo, kn = k3 == 2 ? 0u : k3 + 1u;  // this level's append counter
     if (tid == 0) s_n[kn == 2 ? 0u : kn + 1u] = 0;            // = (nl + 3) % 3: free since level nl - 1
     uint32_t *qn = s_q[cur ^ 1];
+    // edge-parallel: a chunk of TD_B frontier nodes publishes its rows (start,
+    // exclusive degree offset); every thread then takes edges of the chunk, so
+    // each lane has ~one child load and one counter atomic in flight instead of
+    // a whole row's worth (a lane's 16 queued atomics were ~60 % of a level)
     for (uint32_t b = 0; b < n; b += TD_B) {
-      const uint32_t i = b + tid;
-      uint32_t j = 0, je = 0;
+      const uint32_t i = b + tid, nc = min((uint32_t)TD_B, n - b);
+      uint32_t j0 = 0, d = 0;
       if (i < n) {
         const uint32_t u = i < TD_Q ? s_q[cur][i] : topo[lo + i];
-        j = fp[u];
-        je = fp[u + 1];
+        j0 = fp[u];
+        d = fp[u + 1] - j0;
       }
-      TD_T(0);
-      while (__any(j < je)) {
-        uint32_t ch[TD_BATCH];
-        bool rdy[TD_BATCH];
+      uint32_t tot;
+      const uint32_t eo = block_exscan<TD_B>(d, &tot, s_red);
+      s_eo[tid] = eo;
+      s_j0[tid] = j0;
+      __syncthreads();
+      for (uint32_t e0 = 0; e0 < tot; e0 += TD_B * TD_EPT) {
+        uint32_t ch[TD_EPT];
+        bool rdy[TD_EPT];
 #pragma unroll
-        for (int k = 0; k < TD_BATCH; k++) ch[k] = j + k < je ? fc[j + k] : NEMO_NONE;
-        TD_T(1);
+        for (int k = 0; k < TD_EPT; k++) {
+          const uint32_t e = e0 + k * TD_B + tid;
+          ch[k] = NEMO_NONE;
+          if (e < tot) {
+            uint32_t lo2 = 0, hi2 = nc;  // the last row starting at or before e
+            while (hi2 - lo2 > 1) {
+              const uint32_t mid = (lo2 + hi2) >> 1;
+              if (s_eo[mid] <= e) lo2 = mid;
+              else hi2 = mid;
+            }
+            ch[k] = fc[s_j0[lo2] + (e - s_eo[lo2])];
+          }
+        }
         uint32_t r = 0;
 #pragma unroll
-        for (int k = 0; k < TD_BATCH; k++) {
+        for (int k = 0; k < TD_EPT; k++) {
           const uint32_t old = ch[k] != NEMO_NONE ? atomicSub(&cnt[ch[k]], 1u) : 0u;
           rdy[k] = old == 1u;
           r += rdy[k] ? 1u : 0u;
         }
-        TD_T(2);
-        uint32_t tot;
-        const uint32_t ex = wave_exscan(r, &tot);
-        if (tot) {
+        uint32_t wt;
+        const uint32_t ex = wave_exscan(r, &wt);
+        if (wt) {
           uint32_t base = 0;
-          if (lane_id() == 0) base = atomicAdd(&s_n[kn], tot);
+          if (lane_id() == 0) base = atomicAdd(&s_n[kn], wt);
           uint32_t at = __builtin_amdgcn_readlane(base, 0) + ex;
 #pragma unroll
-          for (int k = 0; k < TD_BATCH; k++) {
+          for (int k = 0; k < TD_EPT; k++) {
             if (!rdy[k]) continue;
             topo[hi + at] = ch[k];
             nlv[ch[k]] = nl + 1;
@@ -827,12 +834,9 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
             at++;
           }
         }
-        j = min(j + TD_BATCH, je);
-        TD_T(3);
       }
+      __syncthreads();  // s_eo / s_j0 are rewritten by the next chunk
     }
-    __syncthreads();
-    TD_T(4);
     const uint32_t m = s_n[kn];
     nl++;
     lo = hi;
@@ -845,11 +849,6 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
     c.nlev[g] = nl;
     if (hi != V) c.err[g] = NEMO_ERR_CYCLE;
   }
-#ifdef NEMO_STAMPS
-  if (tid == 0 && c.stamps)
-    for (int k = 0; k < 5; k++) c.stamps[16 * (size_t)g + k] = acc[k];
-#endif
-#undef TD_T
 }
 
 
