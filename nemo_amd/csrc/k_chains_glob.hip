@@ -15,6 +15,7 @@
 namespace nemo {
 
 #define GB 1024  // threads per workgroup
+#define GA_B 4   // row entries loaded together while building the H* adjacency
 #define GNIL 0xFFFFFFFFu
 
 // Scratch layout (u32 units) for a graph of V nodes and E edges.
@@ -437,33 +438,51 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(1);
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
-  for (uint32_t i = tid; i <= n; i += GB) {
-    S.ccoff[i] = 0;
-    S.pcoff[i] = 0;
-  }
-  __syncthreads();
-  const uint32_t *es = c.esrc + gv.e0, *ed = c.edst + gv.e0;
+  // From the graph's own CSR rows, one H* node per thread: a row's children
+  // (or parents) in batches of GA_B with their loads in flight together, no
+  // atomics.  (Counting and scattering the whole edge list with cursor
+  // atomics cost a latency-bound pass over all E edges per direction.)
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
-  for (uint32_t e = tid; e < E; e += GB) {
-    const uint32_t a = es[e], b = ed[e];
-    if (!INH(a) || !INH(b)) continue;
-    atomicAdd(&S.ccoff[hidx[a]], 1u);
-    atomicAdd(&S.pcoff[hidx[b]], 1u);
+  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
+    uint32_t k = 0;
+    const uint32_t j1 = ptr[x + 1];
+    for (uint32_t j = ptr[x]; j < j1; j += GA_B) {
+      uint32_t y[GA_B];
+      bool h[GA_B];
+#pragma unroll
+      for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
+#pragma unroll
+      for (int q = 0; q < GA_B; q++) h[q] = j + q < j1 && INH(y[q]);
+      if (out) {
+        uint32_t hy[GA_B];
+#pragma unroll
+        for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GA_B; q++)
+          if (h[q]) out[k++] = hy[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < GA_B; q++) k += h[q] ? 1u : 0u;
+      }
+    }
+    return k;
+  };
+  for (uint32_t i = tid; i < n; i += GB) {
+    const uint32_t x = hs[i];
+    S.ccoff[i] = hrow(gv.fp, gv.fc, x, nullptr);
+    S.pcoff[i] = hrow(gv.rp, gv.rc, x, nullptr);
+  }
+  if (tid == 0) {
+    S.ccoff[n] = 0;
+    S.pcoff[n] = 0;
   }
   __syncthreads();
   block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
   block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
   for (uint32_t i = tid; i < n; i += GB) {
-    S.ccur[i] = S.ccoff[i];
-    S.pcur[i] = S.pcoff[i];
-  }
-  __syncthreads();
-  for (uint32_t e = tid; e < E; e += GB) {
-    const uint32_t a = es[e], b = ed[e];
-    if (!INH(a) || !INH(b)) continue;
-    const uint32_t ia = hidx[a], ib = hidx[b];
-    S.child[atomicAdd(&S.ccur[ia], 1u)] = ib;
-    S.par[atomicAdd(&S.pcur[ib], 1u)] = ia;
+    const uint32_t x = hs[i];
+    hrow(gv.fp, gv.fc, x, S.child + S.ccoff[i]);
+    hrow(gv.rp, gv.rc, x, S.par + S.pcoff[i]);
   }
 #undef INH
   __syncthreads();
