@@ -16,6 +16,7 @@ namespace nemo {
 
 #define GB 1024  // threads per workgroup
 #define GA_B 4   // row entries loaded together while building the H* adjacency
+#define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bitonic)
 #define GNIL 0xFFFFFFFFu
 
 // Scratch layout (u32 units) for a graph of V nodes and E edges.
@@ -594,10 +595,31 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     t0[i] = S.nxt[i] != GNIL ? S.nxt[i] : i;
   }
   __syncthreads();
+  // (HBM passes below take GU elements per thread per round, every load of
+  // the round issued before its stores: one dependent chain per round, not
+  // one per element)
   for (uint32_t span = 1; span <= maxlen; span <<= 1) {
-    for (uint32_t i = tid; i < n; i += GB) {
-      h1[i] = h0[h0[i]];
-      t1[i] = t0[t0[i]];
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      uint32_t a[GU], b[GU];
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB;
+        a[q] = i < n ? h0[i] : 0u;
+        b[q] = i < n ? t0[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        a[q] = h0[a[q]];
+        b[q] = t0[b[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB;
+        if (i < n) {
+          h1[i] = a[q];
+          t1[i] = b[q];
+        }
+      }
     }
     __syncthreads();
     uint32_t *x = h0;
@@ -645,14 +667,26 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   }
   __syncthreads();
   for (uint32_t r = 1; r <= maxup; r <<= 1) {
-    for (uint32_t i = tid; i < n; i += GB) {
-      const uint32_t p = pa[i];
-      if (p != GNIL) {
-        vb[i] = va[i] + va[p];
-        pb[i] = pa[p];
-      } else {
-        vb[i] = va[i];
-        pb[i] = GNIL;
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      uint32_t p[GU], v[GU], vp[GU], pp[GU];
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB;
+        p[q] = i < n ? pa[i] : GNIL;
+        v[q] = i < n ? va[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t pq = p[q] != GNIL ? p[q] : 0u;
+        vp[q] = va[pq];
+        pp[q] = pa[pq];
+      }
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB;
+        if (i >= n) continue;
+        vb[i] = p[q] != GNIL ? v[q] + vp[q] : v[q];
+        pb[i] = p[q] != GNIL ? pp[q] : GNIL;
       }
     }
     __syncthreads();
@@ -683,13 +717,21 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   for (uint32_t k = 2; k <= N2; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < N2; i += GB) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long x = S.key[i], y = S.key[ixj];
-          if ((x > y) == ((i & k) == 0)) {
-            S.key[i] = y;
-            S.key[ixj] = x;
+      for (uint32_t i0 = tid; i0 < N2; i0 += GB * GU) {
+        unsigned long long x[GU], y[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          const uint32_t i = i0 + q * GB, ixj = i ^ j;
+          const bool act = i < N2 && ixj > i;
+          x[q] = act ? S.key[i] : 0ull;
+          y[q] = act ? S.key[ixj] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          const uint32_t i = i0 + q * GB, ixj = i ^ j;
+          if (i < N2 && ixj > i && (x[q] > y[q]) == ((i & k) == 0)) {
+            S.key[i] = y[q];
+            S.key[ixj] = x[q];
           }
         }
       }
