@@ -505,26 +505,76 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   const uint32_t maxup = gmax_u32(mu, s_lds);
   const uint32_t maxlen = gmax_u32(ml, s_lds);
   // ---- bucket by up -----------------------------------------------------------------
-  for (uint32_t k = tid; k <= maxup + 1; k += GB) S.uoff[k] = 0;
-  __syncthreads();
-  for (uint32_t i = tid; i < n; i += GB) atomicAdd(&S.uoff[S.up[i]], 1u);
-  __syncthreads();
-  block_scan_inplace<GB, 16>(S.uoff, maxup + 2, s_lds);
-  for (uint32_t k = tid; k <= maxup + 1; k += GB) S.cnt[k] = S.uoff[k];
-  __syncthreads();
-  for (uint32_t i = tid; i < n; i += GB) S.ub[atomicAdd(&S.cnt[S.up[i]], 1u)] = i;
+  // (counters in LDS -- the sweeps' ring, free now -- when the up range fits)
+  if (maxup + 2 <= GS_RING) {
+    uint32_t *lc = reinterpret_cast<uint32_t *>(s_gs.rv);
+    for (uint32_t k = tid; k <= maxup + 1; k += GB) lc[k] = 0;
+    __syncthreads();
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      int32_t u[GU];
+#pragma unroll
+      for (int q = 0; q < GU; q++) u[q] = i0 + q * GB < n ? S.up[i0 + q * GB] : -1;
+#pragma unroll
+      for (int q = 0; q < GU; q++)
+        if (u[q] >= 0) atomicAdd(&lc[u[q]], 1u);
+    }
+    __syncthreads();
+    block_scan_inplace<GB>(lc, maxup + 2, s_lds);
+    for (uint32_t k = tid; k <= maxup + 1; k += GB) S.uoff[k] = lc[k];
+    __syncthreads();
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      int32_t u[GU];
+#pragma unroll
+      for (int q = 0; q < GU; q++) u[q] = i0 + q * GB < n ? S.up[i0 + q * GB] : -1;
+#pragma unroll
+      for (int q = 0; q < GU; q++)
+        if (u[q] >= 0) S.ub[atomicAdd(&lc[u[q]], 1u)] = i0 + q * GB;
+    }
+  } else {
+    for (uint32_t k = tid; k <= maxup + 1; k += GB) S.uoff[k] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += GB) atomicAdd(&S.uoff[S.up[i]], 1u);
+    __syncthreads();
+    block_scan_inplace<GB, 16>(S.uoff, maxup + 2, s_lds);
+    for (uint32_t k = tid; k <= maxup + 1; k += GB) S.cnt[k] = S.uoff[k];
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += GB) S.ub[atomicAdd(&S.cnt[S.up[i]], 1u)] = i;
+  }
   // best parent fixed up front where only one parent has up == up(v) - 1
   constexpr uint32_t MULTI = 0xFFFFFFFEu;
-  for (uint32_t i = tid; i < n; i += GB) {
-    const int32_t k = S.up[i];
-    uint32_t cand = GNIL, cn = 0;
-    if (k > 0)
-      for (uint32_t q = S.pcoff[i]; q < S.pcoff[i + 1]; q++)
-        if (S.up[S.par[q]] == k - 1) {
-          cn++;
-          cand = S.par[q];
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+    int32_t k[GU];
+    uint32_t r0[GU], r1[GU], p0[GU], cand[GU], cn[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB;
+      const bool in = i < n;
+      k[q] = in ? S.up[i] : 0;
+      r0[q] = in ? S.pcoff[i] : 0u;
+      r1[q] = in ? S.pcoff[i + 1] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) p0[q] = k[q] > 0 && r1[q] > r0[q] ? S.par[r0[q]] : GNIL;
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const int32_t u0 = p0[q] != GNIL ? S.up[p0[q]] : -2;
+      cn[q] = p0[q] != GNIL && u0 == k[q] - 1 ? 1u : 0u;
+      cand[q] = cn[q] ? p0[q] : GNIL;
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB;
+      if (i >= n) continue;
+      if (k[q] > 0)
+        for (uint32_t j = r0[q] + 1; j < r1[q]; j++) {  // the rest of the row (rare)
+          const uint32_t pj = S.par[j];
+          if (S.up[pj] == k[q] - 1) {
+            cn[q]++;
+            cand[q] = pj;
+          }
         }
-    S.bp[i] = cn > 1 ? MULTI : cand;
+      S.bp[i] = cn[q] > 1 ? MULTI : cand[q];
+    }
   }
   __syncthreads();
   STAMP(4);
