@@ -602,6 +602,44 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       continue;
     }
     const uint32_t mp = a - S.uoff[k - 1];  // size of level k-1: po(bp) < mp
+    if (b - a <= GB && mp + 1 <= GS_RING) {
+      // one node per thread, its (node, crank, po(bp)) kept in registers; the
+      // group counters and the groups' cranks in LDS (the sweeps' ring)
+      uint32_t *lcnt = reinterpret_cast<uint32_t *>(s_gs.rv), *lgrp = s_gs.rc;
+      const uint32_t j = a + tid;
+      const bool act = j < b;
+      for (uint32_t w = tid; w <= mp; w += GB) lcnt[w] = 0;
+      const uint32_t i = act ? S.ub[j] : 0u;
+      uint32_t bpi = act ? S.bp[i] : 0u;
+      const uint32_t cr = act ? S.crank[i] : 0u;
+      if (act && bpi == MULTI) {
+        uint32_t bpo = GNIL;
+        for (uint32_t q = S.pcoff[i]; q < S.pcoff[i + 1]; q++) {
+          const uint32_t p = S.par[q];
+          if ((uint32_t)S.up[p] == k - 1 && S.po[p] < bpo) {
+            bpi = p;
+            bpo = S.po[p];
+          }
+        }
+        S.bp[i] = bpi;
+      }
+      const uint32_t bpo = act ? S.po[bpi] : 0u;
+      __syncthreads();
+      if (act) atomicAdd(&lcnt[bpo], 1u);
+      __syncthreads();
+      block_scan_inplace<GB>(lcnt, mp + 1, s_lds);  // group bases
+      if (act) lgrp[atomicAdd(&lcnt[bpo], 1u)] = cr;
+      __syncthreads();  // lcnt[q] = end of group q = base of group q + 1
+      if (act) {
+        const uint32_t base = bpo ? lcnt[bpo - 1] : 0u, end = lcnt[bpo];
+        uint32_t r = 0;
+        for (uint32_t q = base; q < end; q++) r += lgrp[q] < cr;
+        S.po[i] = base + r;
+        S.fpos[i] = base;
+      }
+      __syncthreads();
+      continue;
+    }
     for (uint32_t w = tid; w <= mp; w += GB) S.cnt[w] = 0;
     __syncthreads();
     for (uint32_t j = a + tid; j < b; j += GB) {
