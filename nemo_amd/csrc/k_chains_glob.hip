@@ -83,6 +83,7 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
 #define GS_RING 8192u  // values kept in LDS (power of two)
 #define GS_WN 2048u    // nodes per window
 #define GS_E 4096u     // extra in-ring links per window (past the packed ones)
+#define GS_SORT_CH 16384u  // keys per LDS chunk of the chain sort (128 KB of the sweeps' memory)
 struct GSweepLds {
   int32_t rv[GS_RING];   // up / down by ring slot (index & (GS_RING - 1))
   uint32_t rc[GS_RING];  // down: crank by ring slot
@@ -388,7 +389,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   __shared__ uint32_t s_lds[GB / 64];
   __shared__ uint32_t s_nch, s_fail;
-  __shared__ GSweepLds s_gs;
+  __shared__ __align__(16) GSweepLds s_gs;
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   if (c.err[g] || c.gs_off[g] == ~0ull) return;
   const GraphView gv = c.view(g);
@@ -803,28 +804,60 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     S.grp[va[rep] + (uint32_t)S.up[rep]] = q;
   }
   __syncthreads();
-  for (uint32_t k = 2; k <= N2; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i0 = tid; i0 < N2; i0 += GB * GU) {
-        unsigned long long x[GU], y[GU];
+  // Bitonic network over N2 keys: the passes with j < GS_SORT_CH run on
+  // GS_SORT_CH-key chunks staged in LDS (the sweeps' memory, free by now), so
+  // only the passes with j >= GS_SORT_CH sweep the HBM array.
+  static_assert(sizeof(GSweepLds) >= GS_SORT_CH * sizeof(unsigned long long), "sort chunk fits the sweeps' LDS");
+  unsigned long long *lk = reinterpret_cast<unsigned long long *>(&s_gs);
+  auto hbm_pass = [&](uint32_t k, uint32_t j) {
+    for (uint32_t i0 = tid; i0 < N2; i0 += GB * GU) {
+      unsigned long long x[GU], y[GU];
 #pragma unroll
-        for (int q = 0; q < GU; q++) {
-          const uint32_t i = i0 + q * GB, ixj = i ^ j;
-          const bool act = i < N2 && ixj > i;
-          x[q] = act ? S.key[i] : 0ull;
-          y[q] = act ? S.key[ixj] : 0ull;
-        }
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB, ixj = i ^ j;
+        const bool act = i < N2 && ixj > i;
+        x[q] = act ? S.key[i] : 0ull;
+        y[q] = act ? S.key[ixj] : 0ull;
+      }
 #pragma unroll
-        for (int q = 0; q < GU; q++) {
-          const uint32_t i = i0 + q * GB, ixj = i ^ j;
-          if (i < N2 && ixj > i && (x[q] > y[q]) == ((i & k) == 0)) {
-            S.key[i] = y[q];
-            S.key[ixj] = x[q];
-          }
+      for (int q = 0; q < GU; q++) {
+        const uint32_t i = i0 + q * GB, ixj = i ^ j;
+        if (i < N2 && ixj > i && (x[q] > y[q]) == ((i & k) == 0)) {
+          S.key[i] = y[q];
+          S.key[ixj] = x[q];
         }
       }
+    }
+    __syncthreads();
+  };
+  // every pass of stages k in [k0, k1] with j < min(k, CH), chunk by chunk
+  auto lds_passes = [&](uint32_t k0, uint32_t k1) {
+    const uint32_t ch = min(N2, (uint32_t)GS_SORT_CH);
+    for (uint32_t cb = 0; cb < N2; cb += ch) {
+      for (uint32_t t = tid; t < ch; t += GB) lk[t] = S.key[cb + t];
+      __syncthreads();
+      for (uint32_t k = k0; k <= k1; k <<= 1)
+        for (uint32_t j = min(k, ch) >> 1; j > 0; j >>= 1) {
+          for (uint32_t t = tid; t < ch; t += GB) {
+            const uint32_t u = t ^ j;
+            if (u > t) {
+              const unsigned long long x = lk[t], y = lk[u];
+              if ((x > y) == (((cb + t) & k) == 0)) {
+                lk[t] = y;
+                lk[u] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      for (uint32_t t = tid; t < ch; t += GB) S.key[cb + t] = lk[t];
       __syncthreads();
     }
+  };
+  lds_passes(2, min(N2, (uint32_t)GS_SORT_CH));
+  for (uint32_t k = 2 * GS_SORT_CH; k <= N2; k <<= 1) {
+    for (uint32_t j = k >> 1; j >= GS_SORT_CH; j >>= 1) hbm_pass(k, j);
+    lds_passes(k, k);
   }
   STAMP(8);
   uint32_t *out = c.chain + 5 * gv.n0;
