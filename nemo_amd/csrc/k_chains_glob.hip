@@ -17,6 +17,7 @@ namespace nemo {
 #define GB 1024  // threads per workgroup
 #define GA_B 4   // row entries loaded together while building the H* adjacency
 #define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bitonic)
+#define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
 
 // Scratch layout (u32 units) for a graph of V nodes and E edges.
@@ -407,29 +408,48 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(0);
   // ---- H* in level order, compact ID ranks ------------------------------------
-  for (uint32_t l = tid; l <= ns; l += GB) S.seg[l] = 0;
+  // a stream compaction of the Kahn order (level-sorted already) by the H*
+  // flag: block scans over CP positions per thread, no counter atomics; the
+  // per-level starts are the compaction's running count at each level's first
+  // position (cpos: S.va, free until the preorder phase)
   for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
   __syncthreads();
-  for (uint32_t x = tid; x < V; x += GB)
-    if (f[x] & NEMO_F_DELETED) atomicAdd(&S.seg[nlv[x]], 1u);
+  uint32_t *cpos = S.va;
+  uint32_t n = 0;
+  for (uint32_t base = 0; base < V; base += GB * CP) {
+    const uint32_t p0 = base + tid * CP;
+    uint32_t x[CP], cl = 0;
+    bool h[CP];
+#pragma unroll
+    for (int q = 0; q < CP; q++) x[q] = p0 + q < V ? gv.topo[p0 + q] : 0u;
+#pragma unroll
+    for (int q = 0; q < CP; q++) {
+      h[q] = p0 + q < V && (f[x[q]] & NEMO_F_DELETED);
+      cl += h[q] ? 1u : 0u;
+    }
+    uint32_t tot;
+    uint32_t i = block_exscan<GB>(cl, &tot, s_lds) + n;
+#pragma unroll
+    for (int q = 0; q < CP; q++) {
+      if (p0 + q >= V) continue;
+      cpos[p0 + q] = i;
+      if (!h[q]) continue;
+      hs[i] = x[q];
+      hidx[x[q]] = i;
+      S.rule[i] = is_rule(gv.word[x[q]]) ? 1u : 0u;
+      const uint32_t r = gv.rank_of(x[q]);
+      S.crank[i] = r;
+      atomicOr(&S.bm[r >> 5], 1u << (r & 31));
+      i++;
+    }
+    n += tot;
+  }
   __syncthreads();
-  const uint32_t n = block_scan_inplace<GB, 16>(S.seg, ns + 1, s_lds);
   if (n == 0) {
     if (tid == 0) c.nch[g] = 0;
     return;
   }
-  for (uint32_t l = tid; l <= ns; l += GB) S.cur[l] = S.seg[l];
-  __syncthreads();
-  for (uint32_t x = tid; x < V; x += GB) {
-    if (!(f[x] & NEMO_F_DELETED)) continue;
-    const uint32_t i = atomicAdd(&S.cur[nlv[x]], 1u);
-    hs[i] = x;
-    hidx[x] = i;
-    S.rule[i] = is_rule(gv.word[x]) ? 1u : 0u;
-    const uint32_t r = gv.rank_of(x);
-    S.crank[i] = r;
-    atomicOr(&S.bm[r >> 5], 1u << (r & 31));
-  }
+  for (uint32_t l = tid; l <= ns; l += GB) S.seg[l] = l < ns ? cpos[gv.lvl[l]] : n;
   __syncthreads();
   for (uint32_t w = tid; w < nw; w += GB) S.bmpre[w] = __popc(S.bm[w]);
   __syncthreads();
