@@ -94,9 +94,19 @@ def cpu_info():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    omp = os.environ.get("OMP_NUM_THREADS")
-    threads = min(usable, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else usable
-    return {"nproc": os.cpu_count(), "usable_cores": usable, "threads": threads, "model": model}
+    # a cgroup CPU quota (cgroup v2 cpu.max "<quota> <period>") caps what all threads together can
+    # run, whatever the affinity mask says: it, not OMP_NUM_THREADS, is the real limit when present
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = usable if quota is None else max(1, min(usable, int(quota + 0.999)))
+    return {"nproc": os.cpu_count(), "usable_cores": usable, "cgroup_cpu_quota": quota, "threads": threads,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "model": model}
 
 
 def main():
@@ -124,7 +134,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    threads = min(16, cpu_info()["threads"])
+    threads = cpu_info()["threads"]  # host generation / e2e ingest: every core the quota allows
     t0 = time.time()
     if strong:  # C4: one fixed corpus, LPT-sharded by Σ(V+E) (nemo_partition_runs), run 0 replicated
         R_total = args.runs_per_gpu * world if args.runs_per_gpu else cfg["runs_total"]
@@ -365,7 +375,8 @@ def e2e_leg(args, gen, eng, threads, mode):
 
 def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):
     """oracle/nemo_oracle.c timed on the host (rank 0, N=1): OpenMP over graphs on every usable core
-    (capped by OMP_NUM_THREADS) and on one core, each leg for about --cpu-seconds of a bounded sample."""
+    (or the cgroup quota's worth when one is set) and on one core, each leg for about --cpu-seconds of a
+    bounded sample."""
     from oracle import oracle as O
     from tools import synth
     info = cpu_info()
@@ -375,7 +386,7 @@ def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):
     if cfg["cpu_runs"]:  # deep graphs / huge corpora: a bounded sample of the same shape
         g = dict(gen)
         g.update(cfg.get("cpu_sample", {}))
-        sample, _ = synth.generate(cfg["cpu_runs"], threads=min(16, threads), **g)
+        sample, _ = synth.generate(cfg["cpu_runs"], threads=threads, **g)
         s_succ, s_fail, s_runs = sample.success_iters(), sample.failed_iters(), sample.n_runs
         desc = f"{s_runs} runs of the same shape" + (f" at {g['target_nodes']}-node graphs (EOT {g['eot']})"
                                                     if "cpu_sample" in cfg else "")
@@ -399,6 +410,9 @@ def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):
     v_one, reps1, t_one = leg(1, one, su1, fa1, int(own1.sum()))
     return {"value": round(v_all, 4), "unit": "runs/s", "cores": threads, "kind": "port",
             "value_1core": round(v_one, 4), "nproc": info["nproc"], "usable_cores": info["usable_cores"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"], "omp_num_threads_env": info["omp_num_threads_env"],
+            "cores_rule": "every usable core, or the cgroup cpu.max quota when one is set (OMP_NUM_THREADS "
+                          "is not a cap)",
             "cpu_model": info["model"],
             "sample": f"oracle/nemo_oracle.c (OpenMP over graphs, {threads} threads) on {desc}, {reps} full pass(es) "
                       f"in {t_all:.1f}s, the same phases incl. the edge-list materialisation; 1-core leg: the "

@@ -337,13 +337,15 @@ void nemo_ingest_free(nemo_ingest *h);
  * so that chunk i is loaded and analysed on the device while chunk i+1 is
  * being parsed.  Interning is shared across chunks (ids in graph order, as the
  * one-shot ingest assigns them); table "pre"/"post" ids are fixed by the first
- * chunk.  nemo_ingest_next parses the next `chunk` runs into a corpus (arrays
- * valid until the next call) and, with `with_run0`, prepends the run of
- * iteration 0 as a replicated, not-owned run to every chunk after the one
- * holding it (the good run of the diffs, differential-provenance.go:26).
- * Returns NEMO_ERR_NOTFOUND when no run is left; validation failures as
- * nemo_ingest_molly.  A chunk's arrays stay valid through the next call (two
- * buffers), so one chunk can be uploaded while the next is parsed.          */
+ * chunk.  nemo_ingest_next parses the next `chunk` runs into a corpus and,
+ * with `with_run0`, prepends the run of iteration 0 as a replicated, not-owned
+ * run to every chunk after the one holding it (the good run of the diffs,
+ * differential-provenance.go:26).  Run 0 is parsed first, into the first
+ * chunk, wherever runs.json lists it, so every chunk that holds a failed run
+ * also holds the good run.  Returns NEMO_ERR_NOTFOUND when no run is left;
+ * validation failures as nemo_ingest_molly.  Lifetime: the ingest keeps two
+ * buffers, so the arrays of chunk i stay valid until the call that returns
+ * chunk i+2; chunk i can be uploaded while chunk i+1 is parsed.             */
 typedef struct nemo_ingest_stream nemo_ingest_stream;
 int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
                      nemo_ingest_stream **out);

@@ -617,13 +617,14 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
 struct nemo_ingest_stream {
   std::string dir;
   std::vector<uint32_t> iteration;
+  std::vector<uint32_t> order;  // parse order: run 0 first, then runs.json order
   int threads = 1;
-  uint32_t next = 0;
+  uint32_t next = 0;  // next position in `order`
   std::unordered_map<std::string, uint32_t> tmap, lmap;
   std::vector<std::string> tables, labels;
   uint32_t table_pre = 0, table_post = 0;
   bool pre_post = false;
-  int64_t run0 = -1;  // run index of iteration 0
+  int64_t run0 = -1;  // position of iteration 0 in `order` (0, or -1: absent)
   bool have_run0 = false;
   uint64_t r0_nv[2] = {0, 0}, r0_ne[2] = {0, 0};
   std::vector<uint32_t> r0_word, r0_label, r0_rank, r0_src, r0_dst;
@@ -643,8 +644,17 @@ extern "C" int nemo_ingest_open(const char *out_dir, const uint32_t *iterations,
   s->dir = out_dir;
   s->iteration.assign(iterations, iterations + n_runs);
   s->threads = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  for (uint32_t r = 0; r < n_runs && s->run0 < 0; r++)
-    if (iterations[r] == 0) s->run0 = r;
+  // run 0 is the good run of every diff (differential-provenance.go:26): it is
+  // parsed first, so every chunk that holds a failed run also holds run 0
+  int64_t r0 = -1;
+  for (uint32_t r = 0; r < n_runs && r0 < 0; r++)
+    if (iterations[r] == 0) r0 = r;
+  if (r0 >= 0) {
+    s->order.push_back((uint32_t)r0);
+    s->run0 = 0;
+  }
+  for (uint32_t r = 0; r < n_runs; r++)
+    if ((int64_t)r != r0) s->order.push_back(r);
   *out = s;
   return NEMO_OK;
 }
@@ -665,7 +675,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
   std::atomic<uint32_t> nextg{0};
   auto work = [&] {
     for (uint32_t g; (g = nextg.fetch_add(1)) < G;) {
-      const uint32_t r = a + g / 2;
+      const uint32_t r = s->order[a + g / 2];  // file names use the run index (molly.go:59-60)
       const char *cond = g % 2 ? "post" : "pre";
       std::string path = s->dir + "/run_" + std::to_string(r) + "_" + cond + "_provenance.json";
       parse_graph(path, s->iteration[r], cond, gs[g]);
@@ -717,7 +727,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
     }
   }
   for (uint32_t r = a; r < b; r++) {
-    ck.it.push_back(s->iteration[r]);
+    ck.it.push_back(s->iteration[s->order[r]]);
     ck.own.push_back(1);
     for (int k = 0; k < 2; k++) {
       const Graph &gr = gs[2 * (r - a) + k];

@@ -22,7 +22,7 @@ namespace nemo {
 
 // Scratch layout (u32 units) for a graph of V nodes and E edges.
 struct GlobScratch {
-  uint32_t *seg, *cur, *bm, *bmpre, *crank, *rule;
+  uint32_t *cur, *bm, *bmpre, *crank, *rule;
   uint32_t *ccoff, *pcoff, *ccur, *pcur, *child, *par;
   int32_t *up, *down;
   uint32_t *nxt, *bp, *po, *fpos, *ub, *uoff, *cnt, *grp;
@@ -33,7 +33,7 @@ struct GlobScratch {
 
 uint64_t glob_words(uint64_t V, uint64_t E) {
   const uint64_t w = (V + 31) / 32 + 2;
-  return 2 * (V + 1) + 2 * w + 4 * (V + 1) + 2 * E + 2 * (V + 2) + 20 * V + 4 * V + 64;
+  return (V + 1) + 2 * w + 4 * (V + 1) + 2 * E + 2 * (V + 2) + 20 * V + 4 * V + 64;
 }
 
 __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
@@ -44,7 +44,6 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
     p += n;
     return q;
   };
-  s.seg = take(V + 1);
   s.cur = take(V + 1);
   s.bm = take(w);
   s.bmpre = take(w);
@@ -394,7 +393,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   if (c.err[g] || c.gs_off[g] == ~0ull) return;
   const GraphView gv = c.view(g);
-  const uint32_t V = gv.V, E = gv.E, ns = gv.nlev;
+  const uint32_t V = gv.V, E = gv.E;
   GlobScratch S = glob_carve(c.gscratch + c.gs_off[g], V, E);
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
   uint32_t *hidx = c.s_f + gv.n0 + g;  // graph-local node -> compact index
@@ -409,12 +408,9 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   STAMP(0);
   // ---- H* in level order, compact ID ranks ------------------------------------
   // a stream compaction of the Kahn order (level-sorted already) by the H*
-  // flag: block scans over CP positions per thread, no counter atomics; the
-  // per-level starts are the compaction's running count at each level's first
-  // position (cpos: S.va, free until the preorder phase)
+  // flag: block scans over CP positions per thread, no counter atomics
   for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
   __syncthreads();
-  uint32_t *cpos = S.va;
   uint32_t n = 0;
   for (uint32_t base = 0; base < V; base += GB * CP) {
     const uint32_t p0 = base + tid * CP;
@@ -431,9 +427,7 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     uint32_t i = block_exscan<GB>(cl, &tot, s_lds) + n;
 #pragma unroll
     for (int q = 0; q < CP; q++) {
-      if (p0 + q >= V) continue;
-      cpos[p0 + q] = i;
-      if (!h[q]) continue;
+      if (p0 + q >= V || !h[q]) continue;
       hs[i] = x[q];
       hidx[x[q]] = i;
       S.rule[i] = is_rule(gv.word[x[q]]) ? 1u : 0u;
@@ -449,8 +443,6 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
     if (tid == 0) c.nch[g] = 0;
     return;
   }
-  for (uint32_t l = tid; l <= ns; l += GB) S.seg[l] = l < ns ? cpos[gv.lvl[l]] : n;
-  __syncthreads();
   for (uint32_t w = tid; w < nw; w += GB) S.bmpre[w] = __popc(S.bm[w]);
   __syncthreads();
   block_scan_inplace<GB, 16>(S.bmpre, nw, s_lds);

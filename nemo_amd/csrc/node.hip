@@ -25,10 +25,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -52,10 +55,67 @@ struct Shard {
   std::vector<uint64_t> no, eo;
 };
 
+// One persistent host thread per shard.  The per-shard entry points block on
+// their own stream or events (a fetch waits for its kernel), so a serial loop
+// over shards would serialise the devices behind those waits; the pool runs
+// every shard's call at once and joins (the caller stays synchronous, as the
+// reference's single goroutine expects, main.go:106-177).
+class Pool {
+ public:
+  explicit Pool(size_t n) : slot_(n) {
+    for (size_t i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  // run f(i) for every i on its own thread; returns when all have finished
+  void run(const std::function<void(size_t)> &f) {
+    std::unique_lock<std::mutex> g(m_);
+    job_ = &f;
+    pending_ = slot_.size();
+    gen_++;
+    cv_.notify_all();
+    done_.wait(g, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(size_t i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(size_t)> *f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<char> slot_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t)> *job_ = nullptr;
+  size_t pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct Node {
   std::vector<Shard> sh;
+  Pool *pool = nullptr;  // one thread per shard (P > 1)
   bool rccl = false;
   std::vector<ncclComm_t> comms;
   // peer-copy reduction (shards sharing a device)
@@ -124,6 +184,20 @@ __global__ void k_sum_u32(uint32_t *acc, const uint32_t *parts, uint32_t n_parts
 
 static Node *N(const nemo_ctx *c) { return ctx_node(c); }
 
+// f(shard, p) on every shard, one host thread per shard; the first failing
+// shard's status and message are reported
+static int fanout(nemo_ctx *c, Node *n, const std::function<int(Shard &, size_t)> &f) {
+  const size_t P = n->sh.size();
+  std::vector<int> rcs(P, 0);
+  if (P == 1 || !n->pool) {
+    for (size_t p = 0; p < P; p++) rcs[p] = f(n->sh[p], p);
+  } else {
+    n->pool->run([&](size_t p) { rcs[p] = f(n->sh[p], p); });
+  }
+  for (size_t p = 0; p < P; p++) SCHK(c, n->sh[p], rcs[p]);
+  return NEMO_OK;
+}
+
 extern "C" int nemo_ctx_create_node(int ndev, const int *devices, nemo_ctx **out) {
   if (!out) return NEMO_ERR_INVALID;
   *out = nullptr;
@@ -164,19 +238,25 @@ extern "C" int nemo_ctx_create_node(int ndev, const int *devices, nemo_ctx **out
     hipSetDevice(devs[i]);
     hipEventCreateWithFlags(&n->ev[i], hipEventDisableTiming);
   }
+  if (ndev > 1) n->pool = new Pool((size_t)ndev);
   *out = ctx_new_facade(n);
   return NEMO_OK;
 }
 
 extern "C" int nemo_node_devices(const nemo_ctx *c, int *devices, int cap) {
   const Node *n = c ? N(c) : nullptr;
-  if (!n) return c ? 1 : 0;
+  if (!n) {  // a single-device context
+    if (c && devices && cap > 0) devices[0] = ctx_device(c);
+    return c ? 1 : 0;
+  }
   for (int i = 0; i < (int)n->sh.size() && devices && i < cap; i++) devices[i] = n->sh[i].device;
   return (int)n->sh.size();
 }
 
 void node_destroy(Node *n) {
   if (!n) return;
+  delete n->pool;
+  n->pool = nullptr;
   for (auto &s : n->sh) {
     if (!s.ctx) continue;
     hipSetDevice(s.device);
@@ -335,19 +415,16 @@ int node_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
 int node_rebuild(nemo_ctx *c) {
   Node *n = N(c);
   NEED_LOADED(c, n);
-  for (auto &s : n->sh) SCHK(c, s, nemo_rebuild(s.ctx));
-  return NEMO_OK;
+  return fanout(c, n, [](Shard &s, size_t) { return nemo_rebuild(s.ctx); });
 }
 int node_mark_holds(nemo_ctx *c) {
   Node *n = N(c);
   NEED_LOADED(c, n);
-  for (auto &s : n->sh) SCHK(c, s, nemo_mark_holds(s.ctx));
-  return NEMO_OK;
+  return fanout(c, n, [](Shard &s, size_t) { return nemo_mark_holds(s.ctx); });
 }
 int node_simplify(nemo_ctx *c) {
   Node *n = N(c);
-  for (auto &s : n->sh) SCHK(c, s, nemo_simplify(s.ctx));
-  return NEMO_OK;
+  return fanout(c, n, [](Shard &s, size_t) { return nemo_simplify(s.ctx); });
 }
 
 // ---- cross-shard exchanges -----------------------------------------------------
@@ -409,6 +486,15 @@ static int broadcast_labels(nemo_ctx *c, Node *n, uint32_t root, uint64_t count)
   }
   Shard &o = n->sh[root];
   hipStream_t so = ctx_stream(o.ctx);
+  // a destination's d_lab may still be read by its previous k_diff: the copy
+  // waits for everything queued on that shard's stream so far
+  for (size_t p = 0; p < P; p++) {
+    if (p == root) continue;
+    HCHK(c, hipSetDevice(n->sh[p].device));
+    HCHK(c, hipEventRecord(n->ev[p], ctx_stream(n->sh[p].ctx)));
+    HCHK(c, hipSetDevice(o.device));
+    HCHK(c, hipStreamWaitEvent(so, n->ev[p], 0));
+  }
   HCHK(c, hipSetDevice(o.device));
   for (size_t p = 0; p < P; p++)
     if (p != root) HCHK(c, hipMemcpyPeerAsync(n->sh[p].d_lab, n->sh[p].device, o.d_lab, o.device, count * 4, so));
@@ -428,7 +514,11 @@ int node_protos_partial(nemo_ctx *c, const uint32_t *success, size_t ns, uint32_
     return fail(c, NEMO_ERR_INVALID, "a node context reduces across its devices itself: pass d_reduce = NULL");
   // success iterations stay global: each shard ignores the runs it does not hold, and the first
   // one (Q-PROTO-FIRST) counts on the shard that owns it (k_reduce gates on ownership)
-  for (auto &s : n->sh) SCHK(c, s, nemo_protos_partial(s.ctx, success, ns, n->sh.size() > 1 ? nullptr : d_red));
+  const bool multi = n->sh.size() > 1;
+  if (int rc = fanout(c, n, [&](Shard &s, size_t) {
+        return nemo_protos_partial(s.ctx, success, ns, multi ? nullptr : d_red);
+      }))
+    return rc;
   return allreduce_sum(c, n, node_reduce_len(c));
 }
 
@@ -451,14 +541,13 @@ int node_fetch_run_tables(nemo_ctx *c, int which, uint32_t *out, uint64_t cap) {
   if (!out) return fail(c, NEMO_ERR_INVALID, "null output");
   const uint32_t W = (n->T + 31) / 32;
   if (cap < (uint64_t)n->n_runs * W) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  for (uint32_t p = 0; p < n->sh.size(); p++) {
-    Shard &s = n->sh[p];
+  return fanout(c, n, [&](Shard &s, size_t p) {
     std::vector<uint32_t> t((size_t)s.runs.size() * W + 1);
-    SCHK(c, s, nemo_fetch_run_tables(s.ctx, which, t.data(), (uint64_t)s.runs.size() * W));
+    if (int rc = nemo_fetch_run_tables(s.ctx, which, t.data(), (uint64_t)s.runs.size() * W)) return rc;
     for (size_t i = 0; i < s.runs.size(); i++)
       if (n->run_shard[s.runs[i]] == p) memcpy(out + (size_t)s.runs[i] * W, &t[i * W], W * 4);
-  }
-  return NEMO_OK;
+    return NEMO_OK;
+  });
 }
 
 static int owner_of_iter(nemo_ctx *c, Node *n, uint32_t it, uint32_t *run) {
@@ -505,10 +594,8 @@ static int node_diff(nemo_ctx *c, const uint32_t *failed, size_t nf, int mode, c
     SCHK(c, n->sh[0], nemo_diffprov_labels(n->sh[0].ctx, lists[0].data(), lists[0].size(), d_labels, lab_cap));
     return NEMO_OK;
   }
-  if (mode == NEMO_DIFF_PER_RUN || nf == 0 || P == 1 || n->run0 < 0) {
-    for (size_t p = 0; p < P; p++) SCHK(c, n->sh[p], nemo_diffprov(n->sh[p].ctx, lists[p].data(), lists[p].size(), mode));
-    return NEMO_OK;
-  }
+  if (mode == NEMO_DIFF_PER_RUN || nf == 0 || P == 1 || n->run0 < 0)
+    return fanout(c, n, [&](Shard &s, size_t p) { return nemo_diffprov(s.ctx, lists[p].data(), lists[p].size(), mode); });
   // reference mode over shards: failedRuns[0]'s label set from its owner, broadcast
   uint32_t r0f;
   if (int rc = owner_of_iter(c, n, failed[0], &r0f)) return rc;
@@ -524,9 +611,9 @@ static int node_diff(nemo_ctx *c, const uint32_t *failed, size_t nf, int mode, c
     }
   SCHK(c, n->sh[root], nemo_goal_labels(n->sh[root].ctx, failed[0], 1, n->sh[root].d_lab, cap));
   if (int rc = broadcast_labels(c, n, root, cap)) return rc;
-  for (size_t p = 0; p < P; p++)
-    SCHK(c, n->sh[p], nemo_diffprov_labels(n->sh[p].ctx, lists[p].data(), lists[p].size(), n->sh[p].d_lab, cap));
-  return NEMO_OK;
+  return fanout(c, n, [&](Shard &s, size_t p) {
+    return nemo_diffprov_labels(s.ctx, lists[p].data(), lists[p].size(), s.d_lab, cap);
+  });
 }
 int node_diffprov(nemo_ctx *c, const uint32_t *failed, size_t nf, int mode) {
   return node_diff(c, failed, nf, mode, nullptr, 0);
@@ -554,9 +641,9 @@ int node_diffprov_host_labels(nemo_ctx *c, const uint32_t *failed, size_t nf, co
     n->sh[p].entries.push_back((uint32_t)e);
   }
   n->n_entries = n->run0 >= 0 ? (uint32_t)nf : 0;
-  for (size_t p = 0; p < P; p++)
-    SCHK(c, n->sh[p], nemo_diffprov_host_labels(n->sh[p].ctx, lists[p].data(), lists[p].size(), labels, n_labels));
-  return NEMO_OK;
+  return fanout(c, n, [&](Shard &s, size_t p) {
+    return nemo_diffprov_host_labels(s.ctx, lists[p].data(), lists[p].size(), labels, n_labels);
+  });
 }
 
 int node_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out, uint64_t cap) {
@@ -582,14 +669,14 @@ int node_fetch_diff_masks(nemo_ctx *c, uint8_t *out, uint64_t cap) {
   const uint64_t V0 = v0_of(n);
   if (!out) return fail(c, NEMO_ERR_INVALID, "null output");
   if (cap < n->n_entries * V0) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  for (auto &s : n->sh) {
-    if (s.entries.empty()) continue;
+  return fanout(c, n, [&](Shard &s, size_t) {
+    if (s.entries.empty()) return (int)NEMO_OK;
     const uint8_t *m = nullptr;
     uint64_t ne = 0, v0 = 0;
-    SCHK(c, s, nemo_diff_masks_view(s.ctx, &m, &ne, &v0));
+    if (int rc = nemo_diff_masks_view(s.ctx, &m, &ne, &v0)) return rc;
     for (size_t i = 0; i < s.entries.size() && m; i++) memcpy(out + s.entries[i] * V0, m + i * V0, V0);
-  }
-  return NEMO_OK;
+    return (int)NEMO_OK;
+  });
 }
 int node_diff_masks_view(nemo_ctx *c, const uint8_t **masks, uint64_t *n_entries, uint64_t *v0) {
   Node *n = N(c);
@@ -610,14 +697,19 @@ int node_diff_masks_view(nemo_ctx *c, const uint8_t **masks, uint64_t *n_entries
 }
 int node_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n_out) {
   Node *n = N(c);
+  std::vector<std::vector<nemo_missing>> per(n->sh.size());
+  if (int rc = fanout(c, n, [&](Shard &s, size_t p) {
+        uint64_t k = 0;
+        if (int r = nemo_fetch_missing(s.ctx, nullptr, 0, &k)) return r;
+        per[p].resize(k + 1);
+        if (int r = nemo_fetch_missing(s.ctx, per[p].data(), k, &k)) return r;
+        per[p].resize(k);
+        return (int)NEMO_OK;
+      }))
+    return rc;
   std::vector<nemo_missing> all;
-  for (auto &s : n->sh) {
-    uint64_t k = 0;
-    SCHK(c, s, nemo_fetch_missing(s.ctx, nullptr, 0, &k));
-    std::vector<nemo_missing> v(k + 1);
-    SCHK(c, s, nemo_fetch_missing(s.ctx, v.data(), k, &k));
-    for (uint64_t i = 0; i < k; i++) all.push_back({s.entries[v[i].entry], v[i].rule});
-  }
+  for (size_t p = 0; p < n->sh.size(); p++)
+    for (const auto &m : per[p]) all.push_back({n->sh[p].entries[m.entry], m.rule});
   std::sort(all.begin(), all.end(), [](const nemo_missing &a, const nemo_missing &b) {
     return a.entry != b.entry ? a.entry < b.entry : a.rule < b.rule;
   });
@@ -668,20 +760,25 @@ static uint32_t global_graph(const Node *n, const Shard &s, uint32_t lg, bool *o
 
 int node_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_out) {
   Node *n = N(c);
+  std::vector<std::vector<nemo_chain>> per(n->sh.size());
+  if (int rc = fanout(c, n, [&](Shard &s, size_t p) {
+        uint64_t k = 0;
+        if (int r = nemo_fetch_chains(s.ctx, nullptr, 0, &k)) return r;
+        per[p].resize(k + 1);
+        if (int r = nemo_fetch_chains(s.ctx, per[p].data(), k, &k)) return r;
+        per[p].resize(k);
+        return (int)NEMO_OK;
+      }))
+    return rc;
   std::vector<nemo_chain> all;
-  for (auto &s : n->sh) {
-    uint64_t k = 0;
-    SCHK(c, s, nemo_fetch_chains(s.ctx, nullptr, 0, &k));
-    std::vector<nemo_chain> v(k + 1);
-    SCHK(c, s, nemo_fetch_chains(s.ctx, v.data(), k, &k));
-    for (uint64_t i = 0; i < k; i++) {
+  for (size_t p = 0; p < n->sh.size(); p++)
+    for (auto v : per[p]) {
       bool mine;
-      const uint32_t g = global_graph(n, s, v[i].graph, &mine);
+      const uint32_t g = global_graph(n, n->sh[p], v.graph, &mine);
       if (!mine) continue;  // run 0's replica
-      v[i].graph = g;
-      all.push_back(v[i]);
+      v.graph = g;
+      all.push_back(v);
     }
-  }
   std::sort(all.begin(), all.end(), [](const nemo_chain &a, const nemo_chain &b) {
     return a.graph != b.graph ? a.graph < b.graph : a.k < b.k;
   });
@@ -693,8 +790,7 @@ int node_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
 }
 
 int node_stage_simplified(nemo_ctx *c) {
-  for (auto &s : N(c)->sh) SCHK(c, s, nemo_stage_simplified(s.ctx));
-  return NEMO_OK;
+  return fanout(c, N(c), [](Shard &s, size_t) { return nemo_stage_simplified(s.ctx); });
 }
 
 int node_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **chain_off, const uint32_t **chain_ht,
@@ -713,10 +809,11 @@ int node_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **ch
   };
   std::vector<V> v(n->sh.size());
   bool wide = false;
-  for (size_t p = 0; p < n->sh.size(); p++) {
-    SCHK(c, n->sh[p], nemo_simplified_view(n->sh[p].ctx, &v[p].st, &v[p].off, &v[p].ht, &v[p].n, &v[p].wide));
-    wide |= v[p].wide != 0;
-  }
+  if (int rc = fanout(c, n, [&](Shard &s, size_t p) {
+        return nemo_simplified_view(s.ctx, &v[p].st, &v[p].off, &v[p].ht, &v[p].n, &v[p].wide);
+      }))
+    return rc;
+  for (size_t p = 0; p < n->sh.size(); p++) wide |= v[p].wide != 0;
   // 2-bit node states in global node order; chain pairs in global graph order
   n->state.assign((n->V + 3) / 4 + 16, 0);
   n->choff.assign((size_t)n->G + 1, 0);
@@ -767,7 +864,7 @@ int node_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **ch
 int node_pull_edges(nemo_ctx *c, int which) {
   Node *n = N(c);
   NEED_LOADED(c, n);
-  for (auto &s : n->sh) SCHK(c, s, nemo_pull_edges(s.ctx, which));
+  if (int rc = fanout(c, n, [&](Shard &s, size_t) { return nemo_pull_edges(s.ctx, which); })) return rc;
   n->pull_which = which;
   return NEMO_OK;
 }
@@ -807,13 +904,14 @@ int node_fetch_pulled_all(nemo_ctx *c, uint64_t *off, uint32_t *cnt, uint32_t *s
   std::vector<uint64_t> used(n->sh.size()), base(n->sh.size() + 1, 0);
   std::vector<std::vector<uint64_t>> so(n->sh.size());
   std::vector<std::vector<uint32_t>> sc(n->sh.size());
-  for (size_t p = 0; p < n->sh.size(); p++) {
-    const uint32_t ls = n->pull_which == 2 ? (uint32_t)n->sh[p].entries.size() : 2 * (uint32_t)n->sh[p].runs.size();
-    so[p].assign(ls + 1, 0);
-    sc[p].assign(ls + 1, 0);
-    SCHK(c, n->sh[p], nemo_fetch_pulled_all(n->sh[p].ctx, so[p].data(), sc[p].data(), nullptr, nullptr, 0, &used[p]));
-    base[p + 1] = base[p] + used[p];
-  }
+  if (int rc = fanout(c, n, [&](Shard &s, size_t p) {
+        const uint32_t ls = n->pull_which == 2 ? (uint32_t)s.entries.size() : 2 * (uint32_t)s.runs.size();
+        so[p].assign(ls + 1, 0);
+        sc[p].assign(ls + 1, 0);
+        return nemo_fetch_pulled_all(s.ctx, so[p].data(), sc[p].data(), nullptr, nullptr, 0, &used[p]);
+      }))
+    return rc;
+  for (size_t p = 0; p < n->sh.size(); p++) base[p + 1] = base[p] + used[p];
   if (n_used) *n_used = base[n->sh.size()];
   for (uint32_t s = 0; s < slots; s++) {
     uint32_t p, ls;
@@ -823,10 +921,10 @@ int node_fetch_pulled_all(nemo_ctx *c, uint64_t *off, uint32_t *cnt, uint32_t *s
   }
   if (!src && !dst) return NEMO_OK;
   if (cap < base[n->sh.size()]) return fail(c, NEMO_ERR_INVALID, "capacity too small");
-  for (size_t p = 0; p < n->sh.size(); p++)
-    SCHK(c, n->sh[p], nemo_fetch_pulled_all(n->sh[p].ctx, nullptr, nullptr, src ? src + base[p] : nullptr,
-                                            dst ? dst + base[p] : nullptr, used[p], &used[p]));
-  return NEMO_OK;
+  return fanout(c, n, [&](Shard &s, size_t p) {
+    return nemo_fetch_pulled_all(s.ctx, nullptr, nullptr, src ? src + base[p] : nullptr, dst ? dst + base[p] : nullptr,
+                                 used[p], &used[p]);
+  });
 }
 
 int node_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, uint64_t bytes) {
@@ -834,8 +932,7 @@ int node_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   return NEMO_OK;
 }
 int node_synchronize(nemo_ctx *c) {
-  for (auto &s : N(c)->sh) SCHK(c, s, nemo_synchronize(s.ctx));
-  return NEMO_OK;
+  return fanout(c, N(c), [](Shard &s, size_t) { return nemo_synchronize(s.ctx); });
 }
 int node_timings(nemo_ctx *c, nemo_timing *out, uint32_t cap, uint32_t *n_out) {
   std::map<std::string, nemo_timing> acc;

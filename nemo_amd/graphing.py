@@ -231,8 +231,14 @@ class Neo4J:
     def _rule(self, p: ProvNode) -> Rule:
         return Rule(p.id, p.label, p.table, p.type or "")
 
-    def _edges(self, slot: int, g: int, run: Optional[int] = None) -> List[Tuple[ProvNode, ProvNode]]:
-        s, d = self.eng.pulled(slot)
+    def _edges(self, slot: Optional[int], g: int, run: Optional[int] = None) -> List[Tuple[ProvNode, ProvNode]]:
+        """Edge rows of a pulled slot, or (slot None) of raw graph g: the raw graph's relationships
+        are exactly the loaded edges, which the host holds, so no device pull is made for them."""
+        if slot is None:
+            e0, e1 = int(self.Runs.edge_off[g]), int(self.Runs.edge_off[g + 1])
+            s, d = self.Runs.edge_src[e0:e1], self.Runs.edge_dst[e0:e1]
+        else:
+            s, d = self.eng.pulled(slot)
         order = np.lexsort((d, s))
         cache: Dict[int, ProvNode] = {}
 
@@ -267,10 +273,9 @@ class Neo4J:
         c = self.Runs
         n = c.n_runs
         pre, post, pre_c, post_c = [None] * n, [None] * n, [None] * n, [None] * n
-        self.eng.pull(0)
-        for r in range(n):
-            pre[r] = create_dot(self._edges(2 * r, 2 * r), "pre")
-            post[r] = create_dot(self._edges(2 * r + 1, 2 * r + 1), "post")
+        for r in range(n):  # raw graphs: the loaded edges (host-held), no device pull
+            pre[r] = create_dot(self._edges(None, 2 * r), "pre")
+            post[r] = create_dot(self._edges(None, 2 * r + 1), "post")
         self.eng.pull(1)
         for r in range(n):
             it = int(c.iteration[r])
@@ -335,11 +340,10 @@ class Neo4J:
             missing[entry].append(m)
         self.eng.pull(2)
         diff_edges = [self._edges(e, g0, 2000 + int(f)) for e, f in enumerate(failedRuns)]
-        self.eng.pull(0)
         diffs, faileds = [], []
         for e, f in enumerate(failedRuns):
             gf = self._g(int(f), "post")
-            failed_edges = self._edges(gf, gf)
+            failed_edges = self._edges(None, gf)
             ids = set()
             for m in missing[e]:
                 ids.add(m.Rule.ID)

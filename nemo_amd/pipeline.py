@@ -144,8 +144,12 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
     if 0 in success:
         success = [0] + [x for x in success if x != 0]
     failed = [it for it in its if not ok[it]]
+    if failed and 0 not in ok:
+        raise LoadError("failed runs but no run of iteration 0: the diffs need the good run "
+                        "(differential-provenance.go:26)")
     f0 = failed[0] if failed else None
     f0_labels = None
+    run_of = {it: r for r, it in enumerate(its)}  # the stream parses run 0 first, then runs.json order
     res = PipelineResult(n_runs=len(its))
     acc = np.zeros(0, np.int64)  # summed [cnt[T], first[T], achvd, first_nonempty, prehold, nruns]
     T_seen = 0
@@ -159,7 +163,6 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
 
     th = threading.Thread(target=parse)
     th.start()
-    base = 0  # run index of the chunk's first own run
     t_dev = 0.0
     while True:
         th.join()
@@ -190,7 +193,7 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
         chunk_its = [int(x) for x, o in zip(c.iteration, own) if o]
         cf = [f for f in failed if f in set(chunk_its)]
         if cf and diff_mode == DIFF_REFERENCE:
-            if f0_labels is None:  # failedRuns[0] is the first failed run: it is in this chunk
+            if f0_labels is None:  # failedRuns[0] is the first failed run in parse order: it is in this chunk
                 g = 2 * c.run_index(f0) + 1
                 n0, n1 = int(c.node_off[g]), int(c.node_off[g + 1])
                 f0_labels = c.label[n0:n1][(c.node_word[n0:n1] & NODE_RULE) == 0].copy()
@@ -213,7 +216,7 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
             for lr, it in enumerate(int(x) for x in c.iteration):
                 if not own[lr]:
                     continue
-                r = its.index(it) if lr == 0 and not own[0] else base + (lr - (0 if own[0] else 1))
+                r = run_of[it]
                 for k in (0, 1):
                     g = 2 * lr + k
                     res.flags[2 * r + k] = flags[int(c.node_off[g]) - int(c.node_off[0]):
@@ -228,7 +231,6 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
             if trig is not None:
                 res.triggers = tuple(np.asarray(x).copy() for x in trig)
         t_dev += time.perf_counter() - td
-        base += len(chunk_its)
     st_tables = st.strings(STR_TABLE)
     st.close()
     T = T_seen

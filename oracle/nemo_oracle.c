@@ -183,6 +183,245 @@ static int cmp_chain(const void *a, const void *b) {
   return x->iter < y->iter ? -1 : x->iter > y->iter;
 }
 
+/* The greedy of collapseNextChains (preprocessing.go:108-138), literally: per
+ * weakly connected component of H*, recompute du (longest H*-path from v to a
+ * rule that contains an unseen node; down[] while v itself is unseen) over the
+ * whole component, accept the longest such path (canonical tie-break), mark
+ * it seen, repeat.  O(chains x component): kept as the cross-check of
+ * greedy_incremental (tests/test_oracle_greedy.py, NEMO_ORACLE_RESCAN=1). */
+#define INH(v) ((g->flags[v] & NEMO_F_DELETED) != 0)
+static uint32_t greedy_rescan(graph_t *g, const uint32_t *order, const uint32_t *cnt, uint32_t ncomp,
+                              const int32_t *down, int32_t *du, uint8_t *unseen, chain_rec *ch) {
+  uint32_t nch = 0;
+  for (uint32_t c = 0; c < ncomp; c++) {
+    const uint32_t *cn = order + cnt[c];
+    uint32_t m = cnt[c + 1] - cnt[c];
+    for (uint32_t iter = 0;; iter++) {
+      for (uint32_t i = m; i-- > 0;) {
+        uint32_t v = cn[i];
+        if (unseen[v]) {
+          du[v] = down[v];
+          continue;
+        }
+        int32_t d = -1;
+        for (uint32_t j = g->fp[v]; j < g->fp[v + 1]; j++) {
+          uint32_t w = g->fc[j];
+          if (INH(w) && du[w] >= 0 && du[w] + 1 > d) d = du[w] + 1;
+        }
+        du[v] = d;
+      }
+      int32_t lmax = -1;
+      uint32_t s = NONE;
+      for (uint32_t i = 0; i < m; i++) {
+        uint32_t v = cn[i];
+        if (!IS_RULE(g->word[v])) continue;
+        if (du[v] > lmax || (du[v] == lmax && s != NONE && rank_of(g, v) < rank_of(g, s))) {
+          lmax = du[v];
+          s = v;
+        }
+      }
+      if (lmax < 2) break;
+      uint32_t v = s;
+      int u = unseen[s];
+      unseen[s] = 0;
+      for (int32_t rem = lmax; rem > 0; rem--) {
+        uint32_t best = NONE;
+        for (uint32_t j = g->fp[v]; j < g->fp[v + 1]; j++) {
+          uint32_t w = g->fc[j];
+          if (!INH(w)) continue;
+          int32_t val = u ? down[w] : du[w];
+          if (val == rem - 1 && (best == NONE || rank_of(g, w) < rank_of(g, best))) best = w;
+        }
+        if (best == NONE) { /* impossible by construction of du/down */
+          gerr(g, NEMO_ERR_INVALID, "internal: chain walk lost its path");
+          break;
+        }
+        v = best;
+        u |= unseen[v];
+        unseen[v] = 0;
+      }
+      ch[nch].head = s;
+      ch[nch].tail = v;
+      ch[nch].len = (uint32_t)lmax;
+      ch[nch].rank = rank_of(g, s);
+      ch[nch].iter = iter;
+      nch++;
+    }
+  }
+  return nch;
+}
+
+/* Selection entries are u64 snapshots: du at push time (high word), then the
+ * complement of the ID rank, so the max is the longest and, among equals, the
+ * smallest rank (cmp_chain's tie-break).  The key never changes once pushed. */
+static void sel_push(uint64_t **a, size_t *n, size_t *cap, uint64_t x) {
+  if (*n == *cap) {
+    *cap = *cap * 2 + 64;
+    *a = realloc(*a, *cap * sizeof **a);
+  }
+  size_t i = (*n)++;
+  while (i > 0 && (*a)[(i - 1) / 2] < x) {
+    (*a)[i] = (*a)[(i - 1) / 2];
+    i = (i - 1) / 2;
+  }
+  (*a)[i] = x;
+}
+static uint64_t sel_pop(uint64_t *a, size_t *n) {
+  uint64_t top = a[0], x = a[--*n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    uint64_t best = x;
+    if (l < *n && a[l] > best) m = l, best = a[l];
+    if (r < *n && a[r] > best) m = r;
+    if (m == i) break;
+    a[i] = a[m];
+    i = m;
+  }
+  if (*n) a[i] = x;
+  return top;
+}
+#define SEL_KEY(d, r) (((uint64_t)(uint32_t)(d) << 32) | (uint64_t)(0xFFFFFFFFu - (r)))
+
+/* Max-heap of node indices by H* topological position (greedy_incremental's
+ * propagation order: children before parents). */
+typedef struct {
+  uint32_t *a;
+  size_t n, cap;
+  const uint32_t *pos;
+} pos_heap;
+static void pos_push(pos_heap *h, uint32_t x) {
+  if (h->n == h->cap) {
+    h->cap = h->cap * 2 + 64;
+    h->a = realloc(h->a, h->cap * sizeof *h->a);
+  }
+  size_t i = h->n++;
+  while (i > 0 && h->pos[h->a[(i - 1) / 2]] < h->pos[x]) {
+    h->a[i] = h->a[(i - 1) / 2];
+    i = (i - 1) / 2;
+  }
+  h->a[i] = x;
+}
+static uint32_t pos_pop(pos_heap *h) {
+  uint32_t top = h->a[0], x = h->a[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    uint32_t best = x;
+    if (l < h->n && h->pos[h->a[l]] > h->pos[best]) m = l, best = h->a[l];
+    if (r < h->n && h->pos[h->a[r]] > h->pos[best]) m = r;
+    if (m == i) break;
+    h->a[i] = h->a[m];
+    i = m;
+  }
+  if (h->n) h->a[i] = x;
+  return top;
+}
+
+/* The same greedy without the rescans.  du only decreases as nodes become
+ * seen, and only a seen node's du is recursive (an unseen node's du is its
+ * down[]), so accepting a chain changes du on the chain's nodes and, through
+ * seen parents only, above them: those are re-evaluated children-first from a
+ * heap keyed by topological position.  The next chain's head (max du, then min
+ * rank, over rules) comes from a max-heap of (du, rank) snapshots whose stale
+ * entries (du changed since the push) are skipped.  Components need no
+ * separate loops: a chain only changes du inside its own component, so each
+ * component sees the same sequence of acceptances as greedy_rescan, and
+ * `iter` (a global acceptance counter here) only breaks ties between chains
+ * of the same head, i.e. of the same component, in the same relative order.
+ * Cost: the re-evaluations above each chain (the seen ancestors whose length
+ * drops), superlinear on deep graphs (~15 min for a C5-shape 1M-node graph)
+ * but far below the rescan's O(chains x component). */
+static uint32_t greedy_incremental(graph_t *g, const uint32_t *hs, uint32_t nh, const int32_t *down, int32_t *du,
+                                   uint8_t *unseen, chain_rec *ch) {
+  const uint32_t V = g->V;
+  uint32_t *pos = malloc((size_t)V * sizeof *pos);
+  uint32_t *of_rank = malloc((size_t)V * sizeof *of_rank); /* ID rank -> node */
+  uint8_t *queued = calloc(V, 1);
+  uint32_t *path = malloc(((size_t)nh + 1) * sizeof *path);
+  pos_heap prop = {NULL, 0, 0, pos};
+  uint64_t *sel = NULL;
+  size_t nsel = 0, capsel = 0;
+  for (uint32_t v = 0; v < V; v++) of_rank[rank_of(g, v)] = v;
+  for (uint32_t i = 0; i < nh; i++) {
+    const uint32_t v = hs[i];
+    pos[v] = i;
+    du[v] = down[v];
+    if (IS_RULE(g->word[v]) && du[v] >= 2) sel_push(&sel, &nsel, &capsel, SEL_KEY(du[v], rank_of(g, v)));
+  }
+  uint32_t nch = 0;
+  while (nsel) {
+    const uint64_t e = sel_pop(sel, &nsel);
+    const uint32_t s = of_rank[0xFFFFFFFFu - (uint32_t)e];
+    if (du[s] != (int32_t)(e >> 32)) continue; /* stale: du[s] dropped since (re-pushed then if >= 2) */
+    const int32_t lmax = du[s];
+    uint32_t v = s, np = 0;
+    int u = unseen[s];
+    unseen[s] = 0;
+    path[np++] = s;
+    for (int32_t rem = lmax; rem > 0; rem--) {
+      uint32_t best = NONE;
+      for (uint32_t j = g->fp[v]; j < g->fp[v + 1]; j++) {
+        uint32_t w = g->fc[j];
+        if (!INH(w)) continue;
+        int32_t val = u ? down[w] : du[w];
+        if (val == rem - 1 && (best == NONE || rank_of(g, w) < rank_of(g, best))) best = w;
+      }
+      if (best == NONE) {
+        gerr(g, NEMO_ERR_INVALID, "internal: chain walk lost its path");
+        break;
+      }
+      v = best;
+      u |= unseen[v];
+      unseen[v] = 0;
+      path[np++] = v;
+    }
+    ch[nch].head = s;
+    ch[nch].tail = v;
+    ch[nch].len = (uint32_t)lmax;
+    ch[nch].rank = rank_of(g, s);
+    ch[nch].iter = nch;
+    nch++;
+    if (g->err) break;
+    /* du of the newly seen nodes and of their seen ancestors, children first */
+    for (uint32_t i = 0; i < np; i++)
+      if (!queued[path[i]]) {
+        queued[path[i]] = 1;
+        pos_push(&prop, path[i]);
+      }
+    while (prop.n) {
+      const uint32_t x = pos_pop(&prop);
+      queued[x] = 0;
+      int32_t d = -1;
+      for (uint32_t j = g->fp[x]; j < g->fp[x + 1]; j++) {
+        uint32_t w = g->fc[j];
+        if (INH(w) && du[w] >= 0 && du[w] + 1 > d) d = du[w] + 1;
+      }
+      if (d == du[x]) continue;
+      du[x] = d;
+      if (IS_RULE(g->word[x]) && d >= 2) sel_push(&sel, &nsel, &capsel, SEL_KEY(d, rank_of(g, x)));
+      for (uint32_t j = g->rp[x]; j < g->rp[x + 1]; j++) {
+        uint32_t p = g->rc[j];
+        if (INH(p) && !unseen[p] && !queued[p]) {
+          queued[p] = 1;
+          pos_push(&prop, p);
+        }
+      }
+    }
+    /* the head's own entry was consumed: it stays a candidate at an unchanged
+     * length (a changed one was pushed above) */
+    if (du[s] == lmax) sel_push(&sel, &nsel, &capsel, SEL_KEY(du[s], rank_of(g, s)));
+  }
+  free(sel);
+  free(prop.a);
+  free(pos);
+  free(of_rank);
+  free(queued);
+  free(path);
+  return nch;
+}
+#undef INH
+
 /* collapseNextChains (graphing/preprocessing.go:66-348) on the clean copy.
  * Q13 (:70-78) lists every path r1(next)-[*1..]->(g)-[*1..]->r2(next) whose
  * nodes are goals or next rules, longest first; the Go loop (:108-138) accepts
@@ -273,61 +512,10 @@ static void collapse(graph_t *g) {
   for (uint32_t i = 0; i < nh; i++) order[cur[cid[hs[i]]]++] = hs[i];
   chain_rec *ch = malloc(((size_t)nh + 1) * sizeof *ch);
   uint32_t nch = 0;
-  for (uint32_t c = 0; c < ncomp; c++) {
-    const uint32_t *cn = order + cnt[c];
-    uint32_t m = cnt[c + 1] - cnt[c];
-    for (uint32_t iter = 0;; iter++) {
-      for (uint32_t i = m; i-- > 0;) {
-        uint32_t v = cn[i];
-        if (unseen[v]) {
-          du[v] = down[v];
-          continue;
-        }
-        int32_t d = -1;
-        for (uint32_t j = g->fp[v]; j < g->fp[v + 1]; j++) {
-          uint32_t w = g->fc[j];
-          if (INH(w) && du[w] >= 0 && du[w] + 1 > d) d = du[w] + 1;
-        }
-        du[v] = d;
-      }
-      int32_t lmax = -1;
-      uint32_t s = NONE;
-      for (uint32_t i = 0; i < m; i++) {
-        uint32_t v = cn[i];
-        if (!IS_RULE(g->word[v])) continue;
-        if (du[v] > lmax || (du[v] == lmax && s != NONE && rank_of(g, v) < rank_of(g, s))) {
-          lmax = du[v];
-          s = v;
-        }
-      }
-      if (lmax < 2) break;
-      uint32_t v = s;
-      int u = unseen[s];
-      unseen[s] = 0;
-      for (int32_t rem = lmax; rem > 0; rem--) {
-        uint32_t best = NONE;
-        for (uint32_t j = g->fp[v]; j < g->fp[v + 1]; j++) {
-          uint32_t w = g->fc[j];
-          if (!INH(w)) continue;
-          int32_t val = u ? down[w] : du[w];
-          if (val == rem - 1 && (best == NONE || rank_of(g, w) < rank_of(g, best))) best = w;
-        }
-        if (best == NONE) { /* impossible by construction of du/down */
-          gerr(g, NEMO_ERR_INVALID, "internal: chain walk lost its path");
-          break;
-        }
-        v = best;
-        u |= unseen[v];
-        unseen[v] = 0;
-      }
-      ch[nch].head = s;
-      ch[nch].tail = v;
-      ch[nch].len = (uint32_t)lmax;
-      ch[nch].rank = rank_of(g, s);
-      ch[nch].iter = iter;
-      nch++;
-    }
-  }
+  if (getenv("NEMO_ORACLE_RESCAN"))
+    nch = greedy_rescan(g, order, cnt, ncomp, down, du, unseen, ch);
+  else
+    nch = greedy_incremental(g, hs, nh, down, du, unseen, ch);
   qsort(ch, nch, sizeof *ch, cmp_chain);
   g->ch = ch;
   g->nch = nch;

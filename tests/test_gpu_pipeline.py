@@ -69,3 +69,28 @@ def test_pipeline_matches_oracle(eng, molly_dir, chunk, mode):
     pre, post, asy = res.triggers
     assert np.array_equal(pre, orc.pre_rows) and np.array_equal(post, orc.post_rows)
     assert np.array_equal(np.sort(asy), np.sort(orc.async_rules))
+
+
+@pytest.mark.timeout(300)
+def test_pipeline_run0_not_first(eng, tmp_path):
+    """runs.json lists run 0 in the middle: the stream parses it first, so the chunks before its old
+    position still have the good run for their diffs (differential-provenance.go:26)."""
+    from tests.test_ingest import rotate_dir
+    corpus, info = synth.generate(120, target_nodes=700, body_extra=3, p_fault=0.3)
+    d = str(tmp_path / "molly")
+    synth.write_molly(corpus, info, d)
+    rotate_dir(d, 50)
+    one = load_molly_native(d, threads=8)
+    assert int(one.iteration[0]) == 50
+    s = [0] + [x for x in one.success_iters() if x != 0]
+    f = one.failed_iters()
+    assert f and min(one.run_index(x) for x in f) < one.run_index(0)
+    orc = O.analyze(one, s, f, diff_mode=DIFF_REFERENCE, threads=8, skip_pulls=True)
+    res = P.run(d, eng, chunk=32, threads=8, diff_mode=DIFF_REFERENCE, keep=True)
+    for g in range(one.n_graphs):
+        a, b = int(one.node_off[g]), int(one.node_off[g + 1])
+        assert np.array_equal(res.flags[g], orc.flags[a:b]), f"flags of graph {g}"
+    assert _names(res.inter, res.tables) == _names(orc.inter, one.tables)
+    for e, it in enumerate(f):
+        assert np.array_equal(res.diff_mask[it], orc.diff_mask[e]), f"D mask of failed run {it}"
+        assert np.array_equal(res.missing[it], np.sort(orc.missing[orc.missing[:, 0] == e][:, 1])), it

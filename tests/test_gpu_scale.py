@@ -74,12 +74,60 @@ def test_c3_full_corpus(eng):
     _say("c3 compared")
     del res
     _check_staged(eng, corpus, orc)
+    # raw pulls (run i: the loaded edges, pre-post-prov.go:298-301) and diff-graph pulls (Q24, run 2000+f:
+    # D's induced edges, differential-provenance.go:159-222) of every graph / entry
+    _check_raw_pulls(eng, corpus)
+    eng.diffprov(f, DIFF_REFERENCE)
+    _check_diff_pulls(eng, corpus, orc.diff_mask)
     del orc
     # the bench's per-run diff mode on the same resident corpus
     eng.diffprov(f, DIFF_PER_RUN)
     orc = O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN, threads=THREADS, skip_pulls=True)
     assert np.array_equal(eng.diff_masks(len(f)), orc.diff_mask)
     assert np.array_equal(eng.missing(), orc.missing)
+
+
+def _edge_keys(g, s, d):
+    """The multiset of (graph, src, dst) rows as sorted packed u64 keys (one sort instead of a lexsort)."""
+    g, s, d = (np.asarray(x, np.uint64) for x in (g, s, d))
+    bs = max(int(s.max()).bit_length() if len(s) else 1, int(d.max()).bit_length() if len(d) else 1)
+    bg = int(g.max()).bit_length() if len(g) else 1
+    assert bg + 2 * bs <= 64
+    k = (g << np.uint64(2 * bs)) | (s << np.uint64(bs)) | d
+    k.sort()
+    return k
+
+
+def _pulled_rows(eng, slots):
+    off, cnt, src, dst = eng.pulled_all(slots)
+    gi = np.repeat(np.arange(slots, dtype=np.int64), np.asarray(cnt, np.int64))
+    idx = np.concatenate([np.arange(int(o), int(o) + int(n), dtype=np.int64) for o, n in zip(off, cnt)]
+                         + [np.zeros(0, np.int64)])
+    return _edge_keys(gi, src[idx], dst[idx])
+
+
+def _check_raw_pulls(eng, corpus):
+    """nemo_pull_edges(0) == every graph's loaded edges, as a multiset per graph."""
+    eng.pull(0)
+    G = corpus.n_graphs
+    got = _pulled_rows(eng, G)
+    eg = np.repeat(np.arange(G, dtype=np.int64), np.diff(corpus.edge_off.astype(np.int64)))
+    want = _edge_keys(eg, corpus.edge_src, corpus.edge_dst)
+    assert np.array_equal(got, want), "raw pulls differ from the loaded edges"
+
+
+def _check_diff_pulls(eng, corpus, masks):
+    """nemo_pull_edges(2) == for every diff entry, run 0's post edges with both endpoints in the oracle's D."""
+    eng.pull(2)
+    n = len(masks)
+    got = _pulled_rows(eng, n)
+    g0 = 2 * corpus.run_index(0) + 1
+    e0, e1 = int(corpus.edge_off[g0]), int(corpus.edge_off[g0 + 1])
+    src, dst = corpus.edge_src[e0:e1].astype(np.int64), corpus.edge_dst[e0:e1].astype(np.int64)
+    keep = (masks[:, src] != 0) & (masks[:, dst] != 0)  # [entries, E0]
+    ent, j = np.nonzero(keep)
+    want = _edge_keys(ent, src[j], dst[j])
+    assert np.array_equal(got, want), f"diff pulls differ ({len(got)} vs {len(want)} edges)"
 
 
 # (runs, nodes per graph, EOT, generator extras): Molly-density deep graphs and C5's ~4 edges per node
@@ -113,13 +161,19 @@ def _reduce_vector(eng, success):
     return eng.reduce_vector().astype(np.int64)
 
 
+@pytest.fixture(scope="module")
+def c4():
+    corpus, _ = synth.generate(100_000, threads=THREADS, **synth.CONFIGS["c3"])
+    _say("c4 generated", int(corpus.node_off[-1]))
+    return corpus
+
+
 @pytest.mark.timeout(900)
-def test_c4_sharded_partials_and_sample(eng):
+def test_c4_sharded_partials_and_sample(eng, c4):
     from nemo_amd.shard import shard_layout
     R, parts = 100_000, 8
-    corpus, _ = synth.generate(R, threads=THREADS, **synth.CONFIGS["c3"])
+    corpus = c4
     s, f = corpus.success_iters(), corpus.failed_iters()
-    _say("c4 generated", int(corpus.node_off[-1]))
     eng.load(corpus)
     eng.mark()
     eng.simplify()
@@ -169,3 +223,39 @@ def test_c4_sharded_partials_and_sample(eng):
         total += _reduce_vector(eng, succ)
         _say("c4 shard", rank)
     assert np.array_equal(total, full)
+
+
+def _results(e, corpus, s, f):
+    """Every host-facing result of one analysis (main.go:106-177's calls), pulls of the diff graphs
+    and the staged simplification included."""
+    res = E.analyze(corpus, s, f, diff_mode=DIFF_REFERENCE, engine=e, pulls=False)
+    e.stage_simplified()
+    state, off, ht = e.simplified_view()
+    res.staged = (np.array(state, copy=True), np.array(off, copy=True), np.array(ht, copy=True))
+    e.pull(2)
+    res.diff_pulls = _pulled_rows(e, len(f))
+    res.run0 = corpus.run_index(0)
+    return res
+
+
+@pytest.mark.timeout(900)
+def test_c4_node_context_8_shards(eng, c4):
+    """nemo_ctx_create_node with 8 shards (all on device 0: the one-GPU layout of an 8-GPU node) over the
+    100k-run C4 corpus equals one single-device context on every field: flags, chains, proto lists,
+    table sets, inter/union, D masks, missing events, trigger rows, diff pulls, the staged view.  The
+    shards' calls run on one host thread each (main.go:95's single Neo4J value drives the whole node)."""
+    corpus = c4
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    one = _results(eng, corpus, s, f)
+    _say("c4 single context")
+    eng.load(synth.generate(2, target_nodes=100)[0])  # release the single context's corpus
+    node = E.Engine(devices=[0] * 8)
+    try:
+        got = _results(node, corpus, s, f)
+        _say("c4 node context")
+    finally:
+        node.close()
+    assert_same(corpus, got, one, len(f), check_pulls=False)
+    assert np.array_equal(got.diff_pulls, one.diff_pulls), "diff pulls differ"
+    for a, b, name in zip(got.staged, one.staged, ("state", "chain_off", "chain_ht")):
+        assert np.array_equal(a, b), f"staged {name} differs"

@@ -167,3 +167,56 @@ def test_stream_error_and_end(tmp_path):
     with pytest.raises(LoadError):
         st.next(3)
     st.close()
+
+
+def rotate_dir(d, k):
+    """Rewrite a Molly directory so that runs.json lists its runs rotated by k (run 0 no longer first);
+    provenance files follow their run's new index (molly.go:59-60 names them by index)."""
+    runs = json.load(open(os.path.join(d, "runs.json")))
+    R = len(runs)
+    tmp = {}
+    for j in range(R):
+        old = (j + k) % R
+        for cond in ("pre", "post"):
+            tmp[(j, cond)] = open(os.path.join(d, f"run_{old}_{cond}_provenance.json"), "rb").read()
+    for (j, cond), data in tmp.items():
+        open(os.path.join(d, f"run_{j}_{cond}_provenance.json"), "wb").write(data)
+    json.dump(runs[k:] + runs[:k], open(os.path.join(d, "runs.json"), "w"))
+
+
+@pytest.mark.parametrize("chunk", [4, 11])
+def test_stream_parses_run0_first(tmp_path, chunk):
+    """runs.json with run 0 in the middle: the stream parses run 0 into the first chunk (owned) and
+    replicates it into every later chunk, so each chunk with a failed run holds the good run; every run's
+    arrays equal the one-shot ingest's for the same iteration."""
+    from nemo_amd.pipeline import IngestStream
+    _, _, d = _synth_dir(tmp_path, n_runs=30, nodes=200)
+    rotate_dir(d, 17)
+    one = load_molly_native(d, threads=4)
+    assert int(one.iteration[0]) == 17 and int(one.iteration[13]) == 0
+    st = IngestStream(d, threads=2)
+    first, its = True, []
+    while True:
+        c = st.next(chunk)
+        if c is None:
+            break
+        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
+        assert int(c.iteration[0]) == 0 and bool(own[0]) == first
+        first = False
+        for lr in range(c.n_runs):
+            if not own[lr]:
+                continue
+            it = int(c.iteration[lr])
+            its.append(it)
+            r = one.run_index(it)
+            for k in (0, 1):
+                g, go = 2 * lr + k, 2 * r + k
+                a, b = int(c.node_off[g]), int(c.node_off[g + 1])
+                oa, ob = int(one.node_off[go]), int(one.node_off[go + 1])
+                assert np.array_equal(np.asarray(c.node_word)[a:b], np.asarray(one.node_word)[oa:ob])
+                assert np.array_equal(np.asarray(c.id_rank)[a:b], np.asarray(one.id_rank)[oa:ob])
+                ea, eb = int(c.edge_off[g]), int(c.edge_off[g + 1])
+                oea, oeb = int(one.edge_off[go]), int(one.edge_off[go + 1])
+                assert np.array_equal(np.asarray(c.edge_src)[ea:eb], np.asarray(one.edge_src)[oea:oeb])
+    assert its == [0] + [int(x) for x in one.iteration if int(x) != 0]
+    st.close()
