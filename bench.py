@@ -163,6 +163,7 @@ def main():
     eng.set_option("stage_blocks", args.stage_blocks)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
+    free0 = torch.cuda.mem_get_info()[0]
     eng.load(corpus)
     d_red = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda")
     V0 = corpus.graph_size(2 * corpus.run_index(0) + 1)
@@ -187,13 +188,9 @@ def main():
         # every device phase is enqueued first; host-side retrieval (which syncs) comes last
         eng.rebuild()
         eng.mark()
-        eng.simplify()
-        eng.protos_partial(success, d_red.data_ptr())
-        # flags + chain pairs -> pinned host on the copy stream, overlapping the diffs and pulls (queued
-        # after k_proto_lds, the LDS-heaviest kernel, which a concurrent PCIe blit slows most)
-        eng.stage_simplified()
-        if world > 1:
-            dist.all_reduce(d_red)
+        # CreateNaiveDiffProv reads only the raw run-0 graph and the label source
+        # (differential-provenance.go:22-98): issued here, its kernels run on the library's second
+        # stream beside the simplification; pull(2) and the mask views wait for them
         if label_bcast:
             if rank == lab_owner:
                 eng.goal_labels(f0, 1, d_lab.data_ptr(), lab_cap)
@@ -201,6 +198,13 @@ def main():
             eng.diffprov_labels(failed, d_lab.data_ptr(), lab_cap)
         else:
             eng.diffprov(failed, mode)
+        eng.simplify()
+        eng.protos_partial(success, d_red.data_ptr())
+        # flags + chain pairs -> pinned host on the copy stream, overlapping the pulls (queued
+        # after k_proto_lds, the LDS-heaviest kernel, which a concurrent PCIe blit slows most)
+        eng.stage_simplified()
+        if world > 1:
+            dist.all_reduce(d_red)
         if has_run0:
             eng.triggers()
         eng.pull(1)
@@ -222,6 +226,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    hbm_used = free0 - torch.cuda.mem_get_info()[0]  # the resident corpus + every buffer a step grew
     eng.set_timing(args.kernel_timing == "on")
     eng.reset_timings()
     if world > 1:
@@ -319,6 +324,9 @@ def main():
                         "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
                     for k, v in sorted(tim.items(), key=lambda kv: -kv[1]["ms"])},
         "gen_seconds_rank0": round(gen_s, 2),
+        "hbm_used_gb_rank0": round(hbm_used / 1e9, 2),
+        "diff_dedupe": "entries sharing a label source share one computation (reference mode: failedRuns[0] "
+                       "for every entry, differential-provenance.go:22-43)",
     }
     if e2e is not None:
         out["e2e_runs_per_s"] = e2e["runs_per_s"]

@@ -78,6 +78,18 @@ struct nemo_ctx {
   int32_t *d_ddepth = nullptr;
   uint32_t *d_dtopo = nullptr;       // g0 in Kahn order (DiffArgs::tpos ...)
   uint64_t miss_cap = 0;
+  // entries that share a label source share one computation: n_uniq distinct
+  // sources, entry e's result is unique result dmap[e] (d_dmap on the device)
+  uint32_t n_uniq = 0, *d_dmap = nullptr;
+  uint8_t *d_dumask = nullptr;       // [n_uniq * V0] when n_uniq < n_entries
+  std::vector<uint32_t> dmap;
+  // CreateNaiveDiffProv reads only the raw run-0 graph and the label sources
+  // (differential-provenance.go:22-98), so its kernels run on `aux`, beside
+  // the simplification on `stream`; whatever rewrites the graphs' structure,
+  // or reads the D masks on `stream`, first waits for ev_diff (join_aux)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  bool aux_pending = false;
 
   // pulls: per-slot (offset, count) and the region cursor come back to pinned
   // memory asynchronously; the first fetch waits for them
@@ -218,21 +230,21 @@ static int guard_staged(nemo_ctx *c) {
 }
 
 template <class F>
-static int timed(nemo_ctx *c, const char *name, double bytes, double edges, F &&f) {
+static int timed_on(nemo_ctx *c, hipStream_t st, const char *name, double bytes, double edges, F &&f) {
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
     a = get_event(c);
     b = get_event(c);
-    hipEventRecord(a, c->stream);
+    hipEventRecord(a, st);
   }
   f();
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(c, NEMO_ERR_HIP, "launch %s: %s", name, hipGetErrorString(e));
   if (c->timing) {
-    hipEventRecord(b, c->stream);
+    hipEventRecord(b, st);
     c->pending.push_back({name, a, b, bytes, edges});
-    if (c->pending.size() > 4096) {  // bound outstanding events
-      hipEventSynchronize(c->pending.back().b);
+    if (c->pending.size() > 4096) {  // bound outstanding events (they may be on two streams)
+      for (auto &p : c->pending) hipEventSynchronize(p.b);
       for (auto &p : c->pending) {
         float ms = 0;
         hipEventElapsedTime(&ms, p.a, p.b);
@@ -250,8 +262,21 @@ static int timed(nemo_ctx *c, const char *name, double bytes, double edges, F &&
   return NEMO_OK;
 }
 
+template <class F>
+static int timed(nemo_ctx *c, const char *name, double bytes, double edges, F &&f) {
+  return timed_on(c, c->stream, name, bytes, edges, f);
+}
+
 static int ensure_event(nemo_ctx *c, hipEvent_t *e) {
   if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  return NEMO_OK;
+}
+
+// `stream` waits for the diff kernels queued on `aux` (see nemo_ctx::aux)
+static int join_aux(nemo_ctx *c) {
+  if (!c->aux_pending) return NEMO_OK;
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_diff, 0));
+  c->aux_pending = false;
   return NEMO_OK;
 }
 
@@ -286,6 +311,7 @@ int ctx_fail(nemo_ctx *c, int code, const char *msg) {
 }
 uint32_t *ctx_reduce_buf(nemo_ctx *c) { return c->d_red; }
 hipStream_t ctx_stream(nemo_ctx *c) { return c->stream; }
+int ctx_join_aux(nemo_ctx *c) { return join_aux(c); }
 int ctx_device(const nemo_ctx *c) { return c->device; }
 
 #define DISPATCH(call)              \
@@ -353,6 +379,11 @@ static void release_corpus(nemo_ctx *c) {
   c->d_dbits = c->d_dmask = nullptr;
   c->d_ddepth = nullptr;
   c->d_dtopo = nullptr;
+  c->d_dmap = nullptr;
+  c->d_dumask = nullptr;
+  c->n_uniq = 0;
+  c->dmap.clear();
+  c->aux_pending = false;
   c->n_entries = c->diff_cap = 0;
   c->miss_cap = 0;
   c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
@@ -391,6 +422,7 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   if (c->copy) hipStreamSynchronize(c->copy);
+  if (c->aux) hipStreamSynchronize(c->aux);
   release_corpus(c);
   for (auto &p : c->pending) {
     hipEventDestroy(p.a);
@@ -423,6 +455,8 @@ void nemo_ctx_destroy(nemo_ctx *c) {
     if (e) hipEventDestroy(e);
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
+  if (c->aux) hipStreamDestroy(c->aux);
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -658,6 +692,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->copy) HIPCHK(c, hipStreamSynchronize(c->copy));
+  if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
   release_corpus(c);
   if (in->n_tables > NEMO_MAX_TABLES)
     return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
@@ -924,6 +959,7 @@ int nemo_rebuild(nemo_ctx *c) {
   HIPCHK(c, hipSetDevice(c->device));
   int rc = guard_staged(c);
   if (rc) return rc;
+  if ((rc = join_aux(c))) return rc;  // the diff kernels read the graphs rebuilt here
   rc = device_load(c);
   if (rc) return rc;
   c->marked = c->simplified = c->protos_done = c->trig_done = false;
@@ -1152,18 +1188,31 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
   if (!c->ev_up_dsrc) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_dsrc, hipEventDisableTiming));
   else HIPCHK(c, hipEventSynchronize(c->ev_up_dsrc));  // the previous upload has landed
-  if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, n_failed)) return rg;
-  uint32_t *src = c->h_dsrc;
+  if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, 2 * n_failed)) return rg;
+  // D_f depends on run 0 and on the label source alone (differential-provenance.go:22-43):
+  // entries with the same source share one computation.  In the reference mode every
+  // entry's source is failedRuns[0] (the in-place ###RUN### substitution of :43), so
+  // the whole call is one computation; in the per-run mode each distinct failed run is.
+  uint32_t *src = c->h_dsrc, *emap = c->h_dsrc + n_failed;
+  c->dmap.assign(n_failed, 0);
+  std::unordered_map<uint32_t, uint32_t> uniq;
+  uint32_t nu = 0;
   double src_bytes = 0;  // the label sources' HBM reads (word + label per node, or the label set)
   for (size_t e = 0; e < n_failed; e++) {
     uint32_t r;
     const uint32_t it = mode == NEMO_DIFF_PER_RUN && !d_labels ? failed_iters[e] : failed_iters[0];
     int rc = run_index(c, d_labels ? failed_iters[e] : it, &r);
     if (rc) return rc;
-    src[e] = 2 * r + 1;
-    src_bytes += d_labels ? 0.0 : 8.0 * (double)(c->node_off[2 * r + 2] - c->node_off[2 * r + 1]);
+    const uint32_t key = d_labels ? 0u : 2 * r + 1;  // label mode: one set for every entry
+    auto ins = uniq.emplace(key, nu);
+    if (ins.second) {
+      src[nu++] = 2 * r + 1;
+      src_bytes += d_labels ? 0.0 : 8.0 * (double)(c->node_off[2 * r + 2] - c->node_off[2 * r + 1]);
+    }
+    c->dmap[e] = emap[e] = ins.first->second;
   }
-  if (d_labels) src_bytes = 4.0 * (double)labels_cap;  // read once, then L2-resident for every entry
+  if (d_labels) src_bytes = 4.0 * (double)labels_cap;  // read once, then L2-resident
+  const bool expand = nu < n_failed;
   const uint32_t g0 = 2 * c->run0 + 1;
   const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
   const uint64_t E0 = c->edge_off[g0 + 1] - c->edge_off[g0];
@@ -1172,11 +1221,14 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     dfree(c, c->d_dsrc);
     dfree(c, c->d_dbits);
     dfree(c, c->d_dmask);
+    dfree(c, c->d_dumask);
     dfree(c, c->d_ddepth);
     dfree(c, c->d_miss);
-    if ((rc = dalloc(c, &c->d_dsrc, n_failed))) return rc;
+    c->d_dumask = nullptr;
+    if ((rc = dalloc(c, &c->d_dsrc, 2 * n_failed))) return rc;
     if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dumask, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
     dfree(c, c->d_dtopo);
     if ((rc = dalloc(c, &c->d_dtopo, 4 * V0 + 2 * E0 + 2 + c->n_r0lab))) return rc;
@@ -1184,8 +1236,16 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->diff_cap = (uint32_t)n_failed;
   }
   if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;
-  hipStream_t s = c->stream;
-  nemo::launch_to_host(c->d_dsrc, src, n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
+  c->d_dmap = c->d_dsrc + n_failed;
+  c->n_uniq = nu;
+  // the diff kernels go on `aux` once `stream` has reached this point (the load /
+  // rebuild of the graphs they read is queued there)
+  if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  if ((rc = ensure_event(c, &c->ev_fork))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  hipStream_t s = c->aux;
+  nemo::launch_to_host(c->d_dsrc, src, 2 * n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
   nemo::launch_zero(c->d_nmiss, 4, s);
   nemo::DiffArgs a;
@@ -1207,20 +1267,21 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   a.trc = a.tfp + V0 + 1;
   a.tfc = a.trc + E0;
   a.r0pos = a.tfc + E0;
-  a.mask = c->d_dmask;
+  a.mask = expand ? c->d_dumask : c->d_dmask;
   a.missing = c->d_miss;
   a.n_missing = c->d_nmiss;
   // HBM lower bound: run 0's post graph once (rows both ways, node word, Kahn
-  // order: 8E0 + 16V0 -- every entry re-reads it from L2), each entry's label
-  // source and its D mask (V0); the three reachability sweeps per entry are
-  // counted as traversed edges, not as HBM bytes
+  // order: 8E0 + 16V0 -- every entry re-reads it from L2), each distinct label
+  // source and each entry's D mask (V0); the three reachability sweeps per
+  // computed entry are counted as traversed edges, not as HBM bytes
   const double bytes = 8.0 * E0 + 16.0 * V0 + src_bytes + (double)n_failed * V0;
-  rc = timed(c, "k_diff", bytes, (double)n_failed * 3 * E0,
-             [&] {
-               // the Kahn-order relayout only when g0 may fall outside the LDS tier
-               const bool lds = c->dc.t_diff.bytes && V0 <= c->dc.t_diff.v && E0 <= c->dc.t_diff.e;
-               nemo::launch_diff(c->dc, a, (uint32_t)n_failed, lds ? 0u : (uint32_t)V0, s);
-             });
+  rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0,
+                [&] {
+                  // the Kahn-order relayout only when g0 may fall outside the LDS tier
+                  const bool lds = c->dc.t_diff.bytes && V0 <= c->dc.t_diff.v && E0 <= c->dc.t_diff.e;
+                  nemo::launch_diff(c->dc, a, nu, lds ? 0u : (uint32_t)V0, s);
+                  if (expand) nemo::launch_diff_expand(c->d_dmask, c->d_dumask, c->d_dmap, V0, (uint32_t)n_failed, s);
+                });
   if (rc) return rc;
   // D masks and the missing-event count -> pinned host
   if ((rc = ensure_event(c, &c->ev_diff))) return rc;
@@ -1229,6 +1290,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   nemo::launch_to_host(c->h_mask, c->d_dmask, n_failed * V0, s);
   nemo::launch_to_host(c->h_nmiss, c->d_nmiss, 4, s);
   HIPCHK(c, hipEventRecord(c->ev_diff, s));
+  c->aux_pending = true;
   c->n_entries = (uint32_t)n_failed;
   return NEMO_OK;
 }
@@ -1251,6 +1313,7 @@ int nemo_diffprov_host_labels(nemo_ctx *c, const uint32_t *failed_iters, size_t 
   if (!c || (!labels && n_labels)) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if ((rc = join_aux(c))) return rc;  // the previous diff may still read d_hlab
   if (n_labels + 1 > c->hlab_cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     dfree(c, c->d_hlab);
@@ -1281,6 +1344,7 @@ int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out,
   if (cap < V + 1) return fail(c, NEMO_ERR_INVALID, "label capacity %llu < %llu", (unsigned long long)cap,
                                (unsigned long long)(V + 1));
   HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = join_aux(c))) return rc;  // d_out may be the label set a previous diff still reads
   return timed(c, "k_goal_labels", 8.0 * (double)V, 0, [&] { nemo::launch_goal_labels(c->dc, g, d_out, c->stream); });
 }
 
@@ -1328,30 +1392,36 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
   DISPATCH(node_fetch_missing(c, out, cap, n_out));
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
-  uint32_t n = 0;
+  uint32_t nu_rows = 0;
   if (c->n_entries) {
     HIPCHK(c, hipEventSynchronize(c->ev_diff));
-    n = *c->h_nmiss;
+    nu_rows = *c->h_nmiss;
   }
-  if (n_out) *n_out = n;
-  if (!out) return NEMO_OK;
-  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  // rows of the distinct computations (unique index, rule), then one copy per entry
   int rc;
   if ((rc = ensure_event(c, &c->ev_misc))) return rc;
-  if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * (uint64_t)n + 2))) return rc;
+  if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * (uint64_t)nu_rows + 2))) return rc;
   const uint32_t *rows = c->h_mrows;
-  if (n) {
-    nemo::launch_to_host(c->h_mrows, c->d_miss, 8ull * n, c->stream);
+  if (nu_rows) {
+    nemo::launch_to_host(c->h_mrows, c->d_miss, 8ull * nu_rows, c->stream);
     HIPCHK(c, hipEventRecord(c->ev_misc, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev_misc));
   }
-  std::vector<std::pair<uint32_t, uint32_t>> v(n);
-  for (uint32_t i = 0; i < n; i++) v[i] = {rows[2 * i], rows[2 * i + 1]};
-  std::sort(v.begin(), v.end());
-  for (uint32_t i = 0; i < n; i++) {
-    out[i].entry = v[i].first;
-    out[i].rule = v[i].second;
-  }
+  std::vector<std::vector<uint32_t>> per(c->n_uniq);
+  for (uint32_t i = 0; i < nu_rows; i++) per[rows[2 * i]].push_back(rows[2 * i + 1]);
+  uint64_t n = 0;
+  for (auto &v : per) std::sort(v.begin(), v.end());
+  for (uint32_t e = 0; e < c->n_entries; e++) n += per[c->dmap[e]].size();
+  if (n_out) *n_out = n;
+  if (!out) return NEMO_OK;
+  if (cap < n) return fail(c, NEMO_ERR_INVALID, "capacity too small");
+  uint64_t k = 0;
+  for (uint32_t e = 0; e < c->n_entries; e++)
+    for (uint32_t r : per[c->dmap[e]]) {
+      out[k].entry = e;
+      out[k].rule = r;
+      k++;
+    }
   return NEMO_OK;
 }
 
@@ -1655,6 +1725,7 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   int rc;
   if (!c->pull_synced) HIPCHK(c, hipEventSynchronize(c->ev_pull));  // pinned slot table still in flight
   c->pull_synced = true;
+  if (which == 2 && (rc = join_aux(c))) return rc;  // the D masks
   const uint32_t slots = which == 2 ? c->n_entries : c->G;
   if (!c->ev_pull) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pull, hipEventDisableTiming));
   if (!c->h_pcur) HIPCHK(c, hipHostMalloc((void **)&c->h_pcur, sizeof(unsigned long long)));
@@ -1805,6 +1876,7 @@ int nemo_synchronize(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
   return NEMO_OK;
 }
 

@@ -65,6 +65,9 @@ void launch_proto(const DevCorpus &c, hipStream_t s);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s);
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint32_t V0, hipStream_t s);
+// entry e's D mask = unique result map[e]'s ([n_entries][V0] from [n_uniq][V0])
+void launch_diff_expand(uint8_t *mask, const uint8_t *umask, const uint32_t *map, uint64_t V0, uint32_t n_entries,
+                        hipStream_t s);
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
 void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
                         hipStream_t s);

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_4(DevCorpus c, int ski
 // rule's reach goes through per-tail chain lists built here (cl_first /
 // cl_next, the graph's chains only).
 #define PG_BLOCK 256
-#define PG_SWEEP 1024
+#define PG_SWEEP 64  // one wave per graph: a level has a few dozen nodes
 #define SB_NR 0x20u      // goal has a REG or TAIL parent (not a root)
 // byte v of a 4-aligned byte array (LDS, or a corpus-wide array with v the global index)
 __device__ __forceinline__ void or8(uint8_t *b, uint64_t v, uint32_t bits) {
@@ -421,11 +421,13 @@ __global__ __launch_bounds__(PG_BLOCK) void k_pg_c(DevCorpus c) {
     __syncthreads();
   })
 }
-// rules reachable from G2: one workgroup per graph, one barrier per Kahn level
+// rules reachable from G2: one wave per graph, one wave barrier per Kahn level
 // (pull form: a node's parents lie on earlier levels, whose bits are final).
 // Deep graphs have ~20k levels of a few dozen nodes, so a level costs its
 // dependent-load chain: each node's parent ids, then their flag / SB bytes,
-// are fetched PG_BATCH at a time, independent of each other.
+// are fetched PG_BATCH at a time, independent of each other.  The graph is a
+// chain of latencies, so it is one wave: many graphs then share a CU (a
+// 1024-thread workgroup had 15 idle waves per level and one graph per CU).
 #define PG_BATCH 4
 __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
   const uint32_t *lst = proto_list(c);

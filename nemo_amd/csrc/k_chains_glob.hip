@@ -14,7 +14,11 @@
 
 namespace nemo {
 
-#define GB 1024  // threads per workgroup
+// One workgroup per deep graph, sized so that four share a CU (256 threads,
+// ~37 KB of LDS): each graph's level walks are latency chains run by one wave,
+// so a CU makes progress on four graphs at once instead of one (a 1024-thread,
+// 146 KB workgroup held a whole CU for one graph).
+#define GB 256   // threads per workgroup
 #define GA_B 4   // row entries loaded together while building the H* adjacency
 #define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bitonic)
 #define CP 16    // Kahn positions per thread per round of the H* compaction
@@ -80,10 +84,10 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
   return s;
 }
 
-#define GS_RING 8192u  // values kept in LDS (power of two)
-#define GS_WN 2048u    // nodes per window
-#define GS_E 4096u     // extra in-ring links per window (past the packed ones)
-#define GS_SORT_CH 16384u  // keys per LDS chunk of the chain sort (128 KB of the sweeps' memory)
+#define GS_RING 2048u  // values kept in LDS (power of two)
+#define GS_WN 512u     // nodes per window
+#define GS_E 1024u     // extra in-ring links per window (past the packed ones)
+#define GS_SORT_CH 4096u   // keys per LDS chunk of the chain sort (32 KB of the sweeps' memory)
 struct GSweepLds {
   int32_t rv[GS_RING];   // up / down by ring slot (index & (GS_RING - 1))
   uint32_t rc[GS_RING];  // down: crank by ring slot
@@ -386,7 +390,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 #endif
 }
 
-__global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
+__global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
   __shared__ uint32_t s_lds[GB / 64];
   __shared__ uint32_t s_nch, s_fail;
   __shared__ __align__(16) GSweepLds s_gs;
@@ -518,9 +522,11 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
   const uint32_t maxup = gmax_u32(mu, s_lds);
   const uint32_t maxlen = gmax_u32(ml, s_lds);
   // ---- bucket by up -----------------------------------------------------------------
-  // (counters in LDS -- the sweeps' ring, free now -- when the up range fits)
-  if (maxup + 2 <= GS_RING) {
-    uint32_t *lc = reinterpret_cast<uint32_t *>(s_gs.rv);
+  // (counters in LDS -- the sweeps' memory, free now -- when the up range fits)
+  constexpr uint32_t LW = sizeof(GSweepLds) / 4;
+  uint32_t *const lw = reinterpret_cast<uint32_t *>(&s_gs);
+  if (maxup + 2 <= LW) {
+    uint32_t *lc = lw;
     for (uint32_t k = tid; k <= maxup + 1; k += GB) lc[k] = 0;
     __syncthreads();
     for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
@@ -615,10 +621,10 @@ __global__ __launch_bounds__(GB) void k_chains_glob(DevCorpus c) {
       continue;
     }
     const uint32_t mp = a - S.uoff[k - 1];  // size of level k-1: po(bp) < mp
-    if (b - a <= GB && mp + 1 <= GS_RING) {
+    if (b - a <= GB && mp + 1 + GB <= LW) {
       // one node per thread, its (node, crank, po(bp)) kept in registers; the
-      // group counters and the groups' cranks in LDS (the sweeps' ring)
-      uint32_t *lcnt = reinterpret_cast<uint32_t *>(s_gs.rv), *lgrp = s_gs.rc;
+      // group counters and the groups' cranks in LDS (the sweeps' memory)
+      uint32_t *lcnt = lw, *lgrp = lw + LW - GB;
       const uint32_t j = a + tid;
       const bool act = j < b;
       for (uint32_t w = tid; w <= mp; w += GB) lcnt[w] = 0;

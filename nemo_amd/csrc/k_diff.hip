@@ -1209,6 +1209,21 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint
   else
     hipLaunchKernelGGL(k_diff<NEMO_BLOCK>, dim3(n_entries), dim3(NEMO_BLOCK), 0, s, c, a);
 }
+// entries sharing a label source: copy the shared mask to each entry's row, 16 B per lane
+__global__ __launch_bounds__(NEMO_BLOCK) void k_diff_expand(uint8_t *__restrict__ mask, const uint8_t *__restrict__ umask,
+                                                         const uint32_t *__restrict__ map, uint64_t V0) {
+  const uint32_t e = blockIdx.y;
+  const uint8_t *src = umask + (uint64_t)map[e] * V0;
+  uint8_t *dst = mask + (uint64_t)e * V0;
+  for (uint64_t i = blockIdx.x * (uint64_t)NEMO_BLOCK + threadIdx.x; i < V0; i += (uint64_t)gridDim.x * NEMO_BLOCK)
+    dst[i] = src[i];
+}
+void launch_diff_expand(uint8_t *mask, const uint8_t *umask, const uint32_t *map, uint64_t V0, uint32_t n_entries,
+                        hipStream_t s) {
+  if (!V0 || !n_entries) return;
+  const uint32_t gx = (uint32_t)std::min<uint64_t>(64, (V0 + NEMO_BLOCK - 1) / NEMO_BLOCK);
+  hipLaunchKernelGGL(k_diff_expand, dim3(gx, n_entries), dim3(NEMO_BLOCK), 0, s, mask, umask, map, V0);
+}
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
   if (c.t_pull.bytes && slots) {
     const uint32_t bytes = c.t_pull.bytes;

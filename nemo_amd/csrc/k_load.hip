@@ -735,7 +735,7 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
 //   - ready children are appended with one wave scan and one LDS atomic per
 //     wave; 256 threads, so the barriers of a level are four waves'.
 #define TD_B 256
-#define TD_Q 4096u
+#define TD_Q 2048u
 #define TD_EPT 4  // frontier edges per thread per round
 __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   __shared__ uint32_t s_q[2][TD_Q];

@@ -15,6 +15,7 @@ int ctx_fail(nemo_ctx *c, int code, const char *msg);
 uint32_t *ctx_reduce_buf(nemo_ctx *c);  // the context's own reduction vector (device)
 hipStream_t ctx_stream(nemo_ctx *c);
 int ctx_device(const nemo_ctx *c);
+int ctx_join_aux(nemo_ctx *c);  // the context's stream waits for its queued diff kernels
 
 // node.hip: the node context's entry points (same contracts as nemohip.h)
 void node_destroy(Node *n);

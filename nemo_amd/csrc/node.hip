@@ -609,6 +609,9 @@ static int node_diff(nemo_ctx *c, const uint32_t *failed, size_t nf, int mode, c
       HCHK(c, hipMalloc(&s.d_lab, cap * 4));
       s.lab_cap = cap;
     }
+  // every shard's stream first waits for its previous diff (on the shard's aux
+  // stream), which may still read the d_lab this broadcast overwrites
+  for (auto &s : n->sh) SCHK(c, s, ctx_join_aux(s.ctx));
   SCHK(c, n->sh[root], nemo_goal_labels(n->sh[root].ctx, failed[0], 1, n->sh[root].d_lab, cap));
   if (int rc = broadcast_labels(c, n, root, cap)) return rc;
   return fanout(c, n, [&](Shard &s, size_t p) {

@@ -2,7 +2,7 @@
 multi-workgroup CSR build, k_topo_deep and the global-tier sweeps), against
 the CPU oracle.
 
-- a Kahn level wider than k_topo_deep's LDS frontier (TD_Q = 4096 nodes), so
+- a Kahn level wider than k_topo_deep's LDS frontier (TD_Q = 2048 nodes), so
   the level's tail is read back from topo[];
 - a cycle inside a big graph (loadProv's refusal, NEMO_ERR_CYCLE);
 - a hub goal whose out-degree exceeds one batch of child loads (TD_BATCH).
