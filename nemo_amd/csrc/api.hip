@@ -792,7 +792,22 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     if (words) A(d.gscratch, words);
   }
   A(d.chain, 5 * V);
-  A(d.chain_tmp, 5 * V);
+  {
+    // k_chains' per-graph scratch (5 words per node), for the graphs k_chains_glob
+    // does not take (those keep theirs in the glob scratch)
+    std::vector<uint64_t> off(G, 0);
+    uint64_t words = 0;
+    for (uint32_t g = 0; g < G; g++) {
+      const uint64_t v = c->node_off[g + 1] - c->node_off[g];
+      off[g] = words;
+      if (!(v >= c->glob_min_v && v > 0)) words += 5 * v;
+    }
+    uint64_t *toff;
+    A(toff, G);
+    HIPCHK(c, hipMemcpy(toff, off.data(), G * 8, hipMemcpyHostToDevice));
+    d.tmp_off = toff;
+    A(d.chain_tmp, words);
+  }
   A(d.nch, G);
   A(d.sel, 4 * ((size_t)G + 1));
   {
@@ -836,7 +851,9 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       HIPCHK(c, hipMemcpy(dh, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice));
       d.cb_hoff = dh;
       A(d.cb_hist, hoff.back());
-      A(d.cb_key, E);
+      // keys: e2's slots (k_build writes e2 only for the graphs it builds, the
+      // bucketed build takes only the others: disjoint edge ranges)
+      d.cb_key = d.e2;
       A(d.cb_val, E);
     }
     c->big_chunks = (uint32_t)std::min<uint64_t>(128, std::max<uint64_t>(1, (emax + 16383) / 16384));
@@ -1182,7 +1199,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   if (!c || (!failed_iters && n_failed)) return NEMO_ERR_INVALID;
   if (mode != NEMO_DIFF_REFERENCE && mode != NEMO_DIFF_PER_RUN) return fail(c, NEMO_ERR_INVALID, "unknown diff mode %d", mode);
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_diffprov before nemo_mark_holds");
-  if (int rm = ensure_marked(c)) return rm;
+  // (the diff kernels read no holds flags: a deferred mark stays fused with the simplification)
   HIPCHK(c, hipSetDevice(c->device));
   c->n_entries = 0;
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing

@@ -192,7 +192,8 @@ struct DevCorpus {
   uint32_t *gscratch;                    // k_chains_glob scratch (deep graphs), null if none
   const uint64_t *gs_off;                // [G] u32 offset of the graph's region, ~0 = not deep
   uint32_t *chain;                       // [5*V] sorted chains (head, tail, len, rank, iter) at n0
-  uint32_t *chain_tmp;                   // [5*V]
+  uint32_t *chain_tmp;                   // [5*V of the graphs k_chains_glob does not take]
+  const uint64_t *tmp_off;               // [G] u32 offset of the graph's chain_tmp region
   uint32_t *nch;                         // [G]
   uint32_t *sel;                         // [4 (G + 1)] fallback-tier worklists (count first): k_pull's, k_chains', k_csr/k_topo's, k_pg_*'s (runs)
   const uint32_t *big;                   // graphs of >= 8192 nodes (host list): the multi-workgroup CSR build

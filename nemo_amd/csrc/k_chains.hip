@@ -249,7 +249,7 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
   const uint8_t *f = gv.flags;
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
   uint32_t *hidx = c.s_f + gv.n0 + g;  // graph-local node -> compact index
-  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  uint32_t *tmp = c.chain_tmp + c.tmp_off[g];
   const uint32_t tid = threadIdx.x;
   const uint32_t cap = min((uint32_t)HCAP, c.hcap_limit);
   STAMP(0);
@@ -926,7 +926,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_big(DevCorpus c) {
   uint32_t *coff = (uint32_t *)(c.s_e + gv.n0);       // [ncomp+1] bucket offsets, then cursors
   uint32_t *roots = c.chain + 5 * gv.n0;              // temp until the final sort
   uint32_t *cidx = c.cl_next + gv.n0;                // graph-local -> component-local
-  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  uint32_t *tmp = c.chain_tmp + c.tmp_off[g];
   const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     s_n = 0;

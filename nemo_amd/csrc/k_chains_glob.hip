@@ -9,6 +9,8 @@
 // jumping, the final order a bitonic sort of 64-bit keys.  The graphs are the
 // ones the host gave a scratch region (DevCorpus::gs_off, V >= glob_min_v);
 // k_chains and k_chains_big skip them.
+#include <algorithm>
+
 #include "device.h"
 #include "internal.h"
 
@@ -24,20 +26,28 @@ namespace nemo {
 #define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
 
-// Scratch layout (u32 units) for a graph of V nodes and E edges.
+// Scratch layout (u32 units) for a graph of V nodes and E edges.  The
+// preorder's buffers (va, vb, pa, pb) reuse the pointer-jumping buffers
+// (ha, hb, ta, tb): the heads and tails are read for the last time when the
+// representatives are recorded, before the preorder starts.  The
+// representatives themselves (5 words each, at most V) go where the H*
+// adjacency was (child, par: dead once the prefix ranks are done), padded to
+// 5V words when 2E is less.
 struct GlobScratch {
-  uint32_t *cur, *bm, *bmpre, *crank, *rule;
-  uint32_t *ccoff, *pcoff, *ccur, *pcur, *child, *par;
+  uint32_t *bm, *bmpre, *crank, *rule;
+  uint32_t *ccoff, *pcoff, *child, *par;
   int32_t *up, *down;
   uint32_t *nxt, *bp, *po, *fpos, *ub, *uoff, *cnt, *grp;
   uint32_t *ha, *hb, *ta, *tb;  // pointer-jumping buffers (heads, tails)
   uint32_t *S, *A, *va, *vb, *pa, *pb;
+  uint32_t *tmp;                // [5 * V] representatives (over child / par)
   unsigned long long *key;      // up to 2V keys (power-of-two padded chain count)
 };
 
 uint64_t glob_words(uint64_t V, uint64_t E) {
   const uint64_t w = (V + 31) / 32 + 2;
-  return (V + 1) + 2 * w + 4 * (V + 1) + 2 * E + 2 * (V + 2) + 20 * V + 4 * V + 64;
+  const uint64_t adj = std::max<uint64_t>(2 * E, 5 * V);  // child + par, or the representatives
+  return 2 * w + 2 * (V + 1) + adj + 2 * (V + 2) + 16 * V + 4 * V + 64;
 }
 
 __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
@@ -48,17 +58,16 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
     p += n;
     return q;
   };
-  s.cur = take(V + 1);
   s.bm = take(w);
   s.bmpre = take(w);
   s.crank = take(V);
   s.rule = take(V);
   s.ccoff = take(V + 1);
   s.pcoff = take(V + 1);
-  s.ccur = take(V + 1);
-  s.pcur = take(V + 1);
   s.child = take(E);
   s.par = take(E);
+  s.tmp = s.child;
+  if (5ull * V > 2ull * E) take(5ull * V - 2ull * E);
   s.up = (int32_t *)take(V);
   s.down = (int32_t *)take(V);
   s.nxt = take(V);
@@ -75,10 +84,10 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
   s.tb = take(V);
   s.S = take(V);
   s.A = take(V);
-  s.va = take(V);
-  s.vb = take(V);
-  s.pa = take(V);
-  s.pb = take(V);
+  s.va = s.ha;
+  s.vb = s.hb;
+  s.pa = s.ta;
+  s.pb = s.tb;
   p = (uint32_t *)(((uintptr_t)p + 7) & ~(uintptr_t)7);
   s.key = (unsigned long long *)p;
   return s;
@@ -401,7 +410,7 @@ __global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
   GlobScratch S = glob_carve(c.gscratch + c.gs_off[g], V, E);
   uint32_t *hs = c.s_a + gv.n0 + g;    // compact index -> graph-local node
   uint32_t *hidx = c.s_f + gv.n0 + g;  // graph-local node -> compact index
-  uint32_t *tmp = c.chain_tmp + 5 * gv.n0;
+  uint32_t *tmp = S.tmp;
   const uint8_t *f = gv.flags;
   const uint32_t *nlv = c.nlv + gv.n0;
   const uint32_t nw = (V + 31) / 32;
