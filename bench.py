@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                     help="off: the timed steps run without per-launch HIP events (two extra steps collect them)")
     ap.add_argument("--stage-blocks", type=int, default=0, help="bulk D2H staging by a k_to_host grid of this size (0: runtime copies)")
+    ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
+                    help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
     return ap.parse_args()
 
 
@@ -161,6 +163,9 @@ def main():
 
     eng = Engine(local)
     eng.set_option("stage_blocks", args.stage_blocks)
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        eng.set_option(k, int(v))
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
     free0 = torch.cuda.mem_get_info()[0]

@@ -4,9 +4,10 @@
 // desc then the preorder of the representatives in the best-prefix forest)
 // with every per-node array in a global scratch region, so it scales to
 // chain subgraphs of hundreds of thousands of nodes and thousands of levels
-// (1M-node graphs, EOT ~ 2000).  One 1024-thread workgroup per
-// graph; long walks (chain heads and tails, ancestor sums) use pointer
-// jumping, the final order a bitonic sort of 64-bit keys.  The graphs are the
+// (1M-node graphs, EOT ~ 2000).  One 256- or 512-thread
+// workgroup per graph; long walks (chain heads and tails, ancestor sums) use
+// pointer jumping, the final order a stable counting sort of the
+// preorder-ordered chains by length.  The graphs are the
 // ones the host gave a scratch region (DevCorpus::gs_off, V >= glob_min_v);
 // k_chains and k_chains_big skip them.
 #include <algorithm>
@@ -16,13 +17,13 @@
 
 namespace nemo {
 
-// One workgroup per deep graph, sized so that four share a CU (256 threads,
-// ~37 KB of LDS): each graph's level walks are latency chains run by one wave,
-// so a CU makes progress on four graphs at once instead of one (a 1024-thread,
-// 146 KB workgroup held a whole CU for one graph).
-#define GB 256   // threads per workgroup
+// One workgroup per deep graph of GB threads (256 or 512, the kernel's
+// template argument) and ~37 KB of LDS, so that two to four share a CU: each
+// graph's level walks are latency chains run by one wave, so a CU makes
+// progress on several graphs at once (a 1024-thread, 146 KB workgroup held a
+// whole CU for one graph).
 #define GA_B 4   // row entries loaded together while building the H* adjacency
-#define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bitonic)
+#define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bucketing)
 #define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
 
@@ -96,7 +97,6 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
 #define GS_RING 2048u  // values kept in LDS (power of two)
 #define GS_WN 512u     // nodes per window
 #define GS_E 1024u     // extra in-ring links per window (past the packed ones)
-#define GS_SORT_CH 4096u   // keys per LDS chunk of the chain sort (32 KB of the sweeps' memory)
 struct GSweepLds {
   int32_t rv[GS_RING];   // up / down by ring slot (index & (GS_RING - 1))
   uint32_t rc[GS_RING];  // down: crank by ring slot
@@ -109,6 +109,7 @@ struct GSweepLds {
   uint8_t flg[GS_WN];    // bit 0 rule, GS_MORE, GS_SPILL
 };
 
+template <int GB>
 __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
@@ -140,7 +141,7 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #define GS_SPILL 0x4u  // ... or, past the list's capacity, in HBM
 #define GS_KEEP 8      // in-ring links packed per node (u16 each, GS_NOLINK = none)
 #define GS_NOLINK 0xFFFFu
-template <bool UP>
+template <bool UP, int GB>
 __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, const uint32_t *hs, const uint32_t *nlv,
                                            uint32_t *s_fail, GSweepLds &L, uint32_t *s_red, unsigned long long *st) {
 #ifdef NEMO_STAMPS
@@ -399,7 +400,9 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 #endif
 }
 
-__global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
+template <int GB>
+__global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
+  static_assert(GS_WN % GB == 0, "whole window nodes per thread");
   __shared__ uint32_t s_lds[GB / 64];
   __shared__ uint32_t s_nch, s_fail;
   __shared__ __align__(16) GSweepLds s_gs;
@@ -520,16 +523,16 @@ __global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
 #else
   unsigned long long *gst = nullptr;
 #endif
-  glob_sweep<true>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
-  glob_sweep<false>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
+  glob_sweep<true, GB>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
+  glob_sweep<false, GB>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
   STAMP(3);
   uint32_t mu = 0, ml = 0;
   for (uint32_t i = tid; i < n; i += GB) {
     mu = max(mu, (uint32_t)max(S.up[i], 0));
     ml = max(ml, (uint32_t)max(S.up[i] + S.down[i], 0));
   }
-  const uint32_t maxup = gmax_u32(mu, s_lds);
-  const uint32_t maxlen = gmax_u32(ml, s_lds);
+  const uint32_t maxup = gmax_u32<GB>(mu, s_lds);
+  const uint32_t maxlen = gmax_u32<GB>(ml, s_lds);
   // ---- bucket by up -----------------------------------------------------------------
   // (counters in LDS -- the sweeps' memory, free now -- when the up range fits)
   constexpr uint32_t LW = sizeof(GSweepLds) / 4;
@@ -814,82 +817,61 @@ __global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
     pb = x;
   }
   STAMP(7);
-  // ---- acceptance order: keys (len desc, preorder asc) are unique; bitonic sort -------
-  uint32_t N2 = 1;
-  while (N2 < nch) N2 <<= 1;
-  for (uint32_t q = tid; q < N2; q += GB) {
-    unsigned long long key = ~0ull;
-    if (q < nch) {
-      const uint32_t len = tmp[5 * q + 2], rep = tmp[5 * q + 4];
-      key = ((unsigned long long)(0xFFFFFFFFu - len) << 32) | (va[rep] + (uint32_t)S.up[rep]);
-    }
-    S.key[q] = key;
-  }
-  // chain of each preorder index (grp is free again)
+  // ---- acceptance order (len desc, preorder asc) -------------------------------------
+  // pre = va + up is the representative's preorder index (unique, < n): the chains
+  // laid out by it are already in preorder; a stable LSD counting sort by
+  // (maxlen - len), 4 bits a pass, each thread a contiguous chunk, then orders them
+  // by length.  (A bitonic network over the padded key array made ~190 passes.)
+  for (uint32_t i = tid; i < n; i += GB) S.grp[i] = GNIL;
+  __syncthreads();
   for (uint32_t q = tid; q < nch; q += GB) {
     const uint32_t rep = tmp[5 * q + 4];
-    S.grp[va[rep] + (uint32_t)S.up[rep]] = q;
+    S.grp[va[rep] + (uint32_t)S.up[rep]] = q;  // chain of each preorder index
   }
   __syncthreads();
-  // Bitonic network over N2 keys: the passes with j < GS_SORT_CH run on
-  // GS_SORT_CH-key chunks staged in LDS (the sweeps' memory, free by now), so
-  // only the passes with j >= GS_SORT_CH sweep the HBM array.
-  static_assert(sizeof(GSweepLds) >= GS_SORT_CH * sizeof(unsigned long long), "sort chunk fits the sweeps' LDS");
-  unsigned long long *lk = reinterpret_cast<unsigned long long *>(&s_gs);
-  auto hbm_pass = [&](uint32_t k, uint32_t j) {
-    for (uint32_t i0 = tid; i0 < N2; i0 += GB * GU) {
-      unsigned long long x[GU], y[GU];
+  unsigned long long *ka = S.key, *kb = S.key + nch;  // nch <= n <= V: both fit the 2V keys
+  {
+    uint32_t o = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += GB * CP) {
+      const uint32_t p0 = b0 + tid * CP;
+      uint32_t qv[CP], cl = 0;
 #pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB, ixj = i ^ j;
-        const bool act = i < N2 && ixj > i;
-        x[q] = act ? S.key[i] : 0ull;
-        y[q] = act ? S.key[ixj] : 0ull;
+      for (int q = 0; q < CP; q++) {
+        qv[q] = p0 + q < n ? S.grp[p0 + q] : GNIL;
+        cl += qv[q] != GNIL ? 1u : 0u;
       }
+      uint32_t tot;
+      uint32_t i = block_exscan<GB>(cl, &tot, s_lds) + o;
 #pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB, ixj = i ^ j;
-        if (i < N2 && ixj > i && (x[q] > y[q]) == ((i & k) == 0)) {
-          S.key[i] = y[q];
-          S.key[ixj] = x[q];
-        }
-      }
+      for (int q = 0; q < CP; q++)
+        if (qv[q] != GNIL)
+          ka[i++] = ((unsigned long long)(maxlen - tmp[5 * qv[q] + 2]) << 32) | (p0 + (uint32_t)q);
+      o += tot;
+    }
+  }
+  __syncthreads();
+  static_assert(16 * 512 <= sizeof(GSweepLds) / 4, "per-thread digit counters fit the sweeps' LDS");
+  const uint32_t kbits = 32u - (uint32_t)__clz((int)max(maxlen, 1u));
+  for (uint32_t sh = 32; sh < 32 + kbits; sh += 4) {
+    const uint32_t per = (nch + GB - 1) / GB, a = min(nch, tid * per), z = min(nch, a + per);
+#pragma unroll
+    for (int d = 0; d < 16; d++) lw[d * GB + tid] = 0;  // thread tid's column: no conflicts, no atomics
+    for (uint32_t i = a; i < z; i++) lw[((uint32_t)(ka[i] >> sh) & 15u) * GB + tid]++;
+    __syncthreads();
+    block_scan_inplace<GB>(lw, 16 * GB, s_lds);  // digit-major: bases in (digit, thread) order
+    for (uint32_t i = a; i < z; i++) {
+      const unsigned long long x = ka[i];
+      kb[lw[((uint32_t)(x >> sh) & 15u) * GB + tid]++] = x;
     }
     __syncthreads();
-  };
-  // every pass of stages k in [k0, k1] with j < min(k, CH), chunk by chunk
-  auto lds_passes = [&](uint32_t k0, uint32_t k1) {
-    const uint32_t ch = min(N2, (uint32_t)GS_SORT_CH);
-    for (uint32_t cb = 0; cb < N2; cb += ch) {
-      for (uint32_t t = tid; t < ch; t += GB) lk[t] = S.key[cb + t];
-      __syncthreads();
-      for (uint32_t k = k0; k <= k1; k <<= 1)
-        for (uint32_t j = min(k, ch) >> 1; j > 0; j >>= 1) {
-          for (uint32_t t = tid; t < ch; t += GB) {
-            const uint32_t u = t ^ j;
-            if (u > t) {
-              const unsigned long long x = lk[t], y = lk[u];
-              if ((x > y) == (((cb + t) & k) == 0)) {
-                lk[t] = y;
-                lk[u] = x;
-              }
-            }
-          }
-          __syncthreads();
-        }
-      for (uint32_t t = tid; t < ch; t += GB) S.key[cb + t] = lk[t];
-      __syncthreads();
-    }
-  };
-  lds_passes(2, min(N2, (uint32_t)GS_SORT_CH));
-  for (uint32_t k = 2 * GS_SORT_CH; k <= N2; k <<= 1) {
-    for (uint32_t j = k >> 1; j >= GS_SORT_CH; j >>= 1) hbm_pass(k, j);
-    lds_passes(k, k);
+    unsigned long long *t = ka;
+    ka = kb;
+    kb = t;
   }
   STAMP(8);
   uint32_t *out = c.chain + 5 * gv.n0;
   for (uint32_t pos = tid; pos < nch; pos += GB) {
-    const uint32_t q = S.grp[(uint32_t)(S.key[pos] & 0xFFFFFFFFu)];
+    const uint32_t q = S.grp[(uint32_t)(ka[pos] & 0xFFFFFFFFu)];
     uint32_t *w = out + 5 * pos;
     w[0] = hs[tmp[5 * q]];
     w[1] = hs[tmp[5 * q + 1]];
@@ -906,7 +888,10 @@ __global__ __launch_bounds__(GB, 4) void k_chains_glob(DevCorpus c) {
 
 void launch_chains_glob(const DevCorpus &c, hipStream_t s) {
   if (!c.gscratch) return;
-  hipLaunchKernelGGL(k_chains_glob, dim3(c.G), dim3(GB), 0, s, c);
+  if (c.glob_block == 512)
+    hipLaunchKernelGGL(k_chains_glob<512>, dim3(c.G), dim3(512), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_chains_glob<256>, dim3(c.G), dim3(256), 0, s, c);
 }
 
 }  // namespace nemo

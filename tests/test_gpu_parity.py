@@ -286,14 +286,17 @@ def test_build_heavy_indegree_redo(eng):
     _check(eng, corpus)
 
 
+@pytest.mark.parametrize("block", [256, 512])
 @pytest.mark.parametrize("kind", ["random", "synthetic", "branchy"])
-def test_chains_glob_tier(kind):
-    # k_chains_glob (deep-graph tier, scratch in HBM) on every graph of small corpora
+def test_chains_glob_tier(kind, block):
+    # k_chains_glob (deep-graph tier, scratch in HBM) on every graph of small corpora, at both
+    # workgroup sizes
     import random as _r
     from tests.small import random_prov
     e = E.Engine(0)
     try:
         e.set_option("chains_glob_min_v", 0)
+        e.set_option("chains_glob_block", block)
         if kind == "random":
             for seed in range(12):
                 corpus, _ = random_corpus(300 + seed, max_nodes=16)
