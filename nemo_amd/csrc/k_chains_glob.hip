@@ -22,7 +22,6 @@ namespace nemo {
 // graph's level walks are latency chains run by one wave, so a CU makes
 // progress on several graphs at once (a 1024-thread, 146 KB workgroup held a
 // whole CU for one graph).
-#define GA_B 4   // row entries loaded together while building the H* adjacency
 #define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bucketing)
 #define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
@@ -140,6 +139,7 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #define GS_MORE 0x2u   // more than GS_KEEP in-ring links: the rest in the window's list
 #define GS_SPILL 0x4u  // ... or, past the list's capacity, in HBM
 #define GS_KEEP 8      // in-ring links packed per node (u16 each, GS_NOLINK = none)
+#define GS_SB 4        // row entries per row and step while staging a window
 #define GS_NOLINK 0xFFFFu
 template <bool UP, int GB>
 __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, const uint32_t *hs, const uint32_t *nlv,
@@ -171,47 +171,72 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       r1[q] = in ? off[i + 1] : 0u;
       cnt[q] = 0;
     }
+    // the PT rows walked together, GS_SB entries of each per step: every load of
+    // a step (columns, then the far values) in flight at once
+    uint32_t rl[PT], lv[PT], cr[PT];
+    int32_t dd[PT];
+    uint32_t bc[PT], br[PT];
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * GB, i = w0 + k;
+      const bool in = k < nw;
+      rl[q] = in ? S.rule[i] : 0u;
+      lv[q] = in ? nlv[hs[i]] : 0u;
+      cr[q] = in && !UP ? S.crank[i] : 0u;
+      dd[q] = UP ? (rl[q] ? 0 : -1) : -1;
+      bc[q] = br[q] = GNIL;
+    }
+    bool more = false;
+#pragma unroll
+    for (int q = 0; q < PT; q++) more |= r0[q] < r1[q];
+    for (uint32_t t = 0; more; t += GS_SB) {
+      uint32_t p[PT][GS_SB];
+      bool far[PT][GS_SB];
+#pragma unroll
+      for (int q = 0; q < PT; q++)
+#pragma unroll
+        for (int h = 0; h < GS_SB; h++) p[q][h] = r0[q] + t + h < r1[q] ? col[r0[q] + t + h] : GNIL;
+      int32_t fv[PT][GS_SB];
+      uint32_t fr[PT][GS_SB];
+#pragma unroll
+      for (int q = 0; q < PT; q++)
+#pragma unroll
+        for (int h = 0; h < GS_SB; h++) {
+          far[q][h] = p[q][h] != GNIL && (UP ? p[q][h] < base : p[q][h] >= base + GS_RING);
+          fv[q][h] = far[q][h] ? (UP ? S.up[p[q][h]] : S.down[p[q][h]]) : 0;
+          fr[q][h] = far[q][h] && !UP ? S.crank[p[q][h]] : 0u;
+        }
+      more = false;
+#pragma unroll
+      for (int q = 0; q < PT; q++) {
+#pragma unroll
+        for (int h = 0; h < GS_SB; h++) {  // in row order: the kept links' order is the row's
+          if (p[q][h] == GNIL) continue;
+          if (!far[q][h]) {
+            if (cnt[q] < GS_KEEP) keep[q][min(cnt[q], (uint32_t)GS_KEEP - 1u)] = p[q][h] - base;
+            cnt[q]++;
+          } else if (UP) {
+            dd[q] = max(dd[q], fv[q][h] + 1);
+          } else if (fv[q][h] > dd[q] || (fv[q][h] == dd[q] && fr[q][h] < br[q])) {
+            dd[q] = fv[q][h];
+            bc[q] = p[q][h];
+            br[q] = fr[q][h];
+          }
+        }
+        more |= r0[q] + t + GS_SB < r1[q];
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PT; q++) {
       const uint32_t k = tid + q * GB, i = w0 + k;
       if (k >= nw) continue;
-      const uint32_t rule = S.rule[i];
-      L.lev[k] = nlv[hs[i]];
-      L.flg[k] = (uint8_t)rule;
-      if (UP) {
-        int32_t d = rule ? 0 : -1;
-        for (uint32_t j = r0[q]; j < r1[q]; j++) {
-          const uint32_t p = col[j];
-          if (p >= base) {
-            if (cnt[q] < GS_KEEP) keep[q][min(cnt[q], (uint32_t)GS_KEEP - 1u)] = p - base;
-            cnt[q]++;
-          } else {
-            d = max(d, S.up[p] + 1);
-          }
-        }
-        L.init[k] = d;
-      } else {
-        int32_t best = -1;
-        uint32_t bc = GNIL, br = GNIL;
-        for (uint32_t j = r0[q]; j < r1[q]; j++) {
-          const uint32_t w = col[j];
-          if (w < base + GS_RING) {
-            if (cnt[q] < GS_KEEP) keep[q][min(cnt[q], (uint32_t)GS_KEEP - 1u)] = w - base;
-            cnt[q]++;
-          } else {
-            const int32_t dw = S.down[w];
-            const uint32_t rw = S.crank[w];
-            if (dw > best || (dw == best && rw < br)) {
-              best = dw;
-              bc = w;
-              br = rw;
-            }
-          }
-        }
-        L.init[k] = best;
-        L.ibc[k] = bc;
-        L.ibr[k] = br;
-        L.rc[i & M] = S.crank[i];
+      L.lev[k] = lv[q];
+      L.flg[k] = (uint8_t)rl[q];
+      L.init[k] = dd[q];
+      if (!UP) {
+        L.ibc[k] = bc[q];
+        L.ibr[k] = br[q];
+        L.rc[i & M] = cr[q];
       }
     }
     // first GS_KEEP links packed per node; the rest in the window's list
@@ -468,40 +493,63 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(1);
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
-  // From the graph's own CSR rows, one H* node per thread: a row's children
-  // (or parents) in batches of GA_B with their loads in flight together, no
-  // atomics.  (Counting and scattering the whole edge list with cursor
+  // From the graph's own CSR rows, no atomics.  A thread walks the child and
+  // parent rows of GA_N H* nodes at once, one entry of every row per step, so
+  // 2*GA_N independent load chains (column, flag, compact index) are in flight
+  // instead of one.  (Counting and scattering the whole edge list with cursor
   // atomics cost a latency-bound pass over all E edges per direction.)
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
-  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
-    uint32_t k = 0;
-    const uint32_t j1 = ptr[x + 1];
-    for (uint32_t j = ptr[x]; j < j1; j += GA_B) {
-      uint32_t y[GA_B];
-      bool h[GA_B];
+  constexpr int GA_N = 4;
+  auto hrows = [&](uint32_t i0, bool fill) {
+    uint32_t a[2 * GA_N], b[2 * GA_N], k[2 * GA_N], x[GA_N];
 #pragma unroll
-      for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
+    for (int q = 0; q < GA_N; q++) x[q] = i0 + q * GB < n ? hs[i0 + q * GB] : 0u;
 #pragma unroll
-      for (int q = 0; q < GA_B; q++) h[q] = j + q < j1 && INH(y[q]);
-      if (out) {
-        uint32_t hy[GA_B];
+    for (int q = 0; q < GA_N; q++) {
+      const bool in = i0 + q * GB < n;
+      a[2 * q] = in ? gv.fp[x[q]] : 0u;
+      b[2 * q] = in ? gv.fp[x[q] + 1] : 0u;
+      a[2 * q + 1] = in ? gv.rp[x[q]] : 0u;
+      b[2 * q + 1] = in ? gv.rp[x[q] + 1] : 0u;
+    }
 #pragma unroll
-        for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
+    for (int r = 0; r < 2 * GA_N; r++)
+      k[r] = fill && i0 + (r >> 1) * GB < n ? ((r & 1) ? S.pcoff : S.ccoff)[i0 + (r >> 1) * GB] : 0u;
+    bool more = false;
 #pragma unroll
-        for (int q = 0; q < GA_B; q++)
-          if (h[q]) out[k++] = hy[q];
-      } else {
+    for (int r = 0; r < 2 * GA_N; r++) more |= a[r] < b[r];
+    while (more) {
+      uint32_t y[2 * GA_N];
+      bool h[2 * GA_N];
 #pragma unroll
-        for (int q = 0; q < GA_B; q++) k += h[q] ? 1u : 0u;
+      for (int r = 0; r < 2 * GA_N; r++) y[r] = a[r] < b[r] ? ((r & 1) ? gv.rc : gv.fc)[a[r]] : 0u;
+#pragma unroll
+      for (int r = 0; r < 2 * GA_N; r++) h[r] = a[r] < b[r] && INH(y[r]);
+      if (fill) {
+        uint32_t hy[2 * GA_N];
+#pragma unroll
+        for (int r = 0; r < 2 * GA_N; r++) hy[r] = h[r] ? hidx[y[r]] : 0u;
+#pragma unroll
+        for (int r = 0; r < 2 * GA_N; r++)
+          if (h[r]) ((r & 1) ? S.par : S.child)[k[r]] = hy[r];
+      }
+      more = false;
+#pragma unroll
+      for (int r = 0; r < 2 * GA_N; r++) {
+        k[r] += h[r] ? 1u : 0u;
+        a[r] += a[r] < b[r] ? 1u : 0u;
+        more |= a[r] < b[r];
       }
     }
-    return k;
+    if (!fill)
+#pragma unroll
+      for (int q = 0; q < GA_N; q++)
+        if (i0 + q * GB < n) {
+          S.ccoff[i0 + q * GB] = k[2 * q];
+          S.pcoff[i0 + q * GB] = k[2 * q + 1];
+        }
   };
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t x = hs[i];
-    S.ccoff[i] = hrow(gv.fp, gv.fc, x, nullptr);
-    S.pcoff[i] = hrow(gv.rp, gv.rc, x, nullptr);
-  }
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) hrows(i0, false);
   if (tid == 0) {
     S.ccoff[n] = 0;
     S.pcoff[n] = 0;
@@ -509,11 +557,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
   block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t x = hs[i];
-    hrow(gv.fp, gv.fc, x, S.child + S.ccoff[i]);
-    hrow(gv.rp, gv.rc, x, S.par + S.pcoff[i]);
-  }
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) hrows(i0, true);
 #undef INH
   __syncthreads();
   STAMP(2);

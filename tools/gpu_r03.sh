@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 { cat /sys/fs/cgroup/cpu.max; nproc; python -c "import os; print(len(os.sched_getaffinity(0)))"; } > gpurun_out/${tag}_box_cpu.txt 2>&1
 if [ "$mode" = all ] || [ "$mode" = tests ]; then
   timeout -k 10 900 python -u -m pytest ${NEMO_TESTS:-tests} -m gpu -x -v --timeout 900 --timeout-method thread \
-    ${NEMO_PYTEST_ARGS} > gpurun_out/${tag}_gputest.log 2>&1 || exit $?
+    ${NEMO_K:+-k "$NEMO_K"} ${NEMO_PYTEST_ARGS} > gpurun_out/${tag}_gputest.log 2>&1 || exit $?
 fi
 if [ "$mode" = all ] || [ "$mode" = bench ]; then
   timeout -k 10 400 python bench.py ${NEMO_BENCH_ARGS} --json-out gpurun_out/${tag}_bench.json > gpurun_out/${tag}_bench.log 2>&1 || exit $?

@@ -15,6 +15,8 @@ dense = len(sys.argv) > 4 and sys.argv[4] == "dense"  # C5's ~4 edges per node (
 extra = {"body_extra": 6, "nval": 3, "nloc": 4} if dense else {}
 corpus, _ = synth.generate(runs, target_nodes=nodes, eot=eot, threads=16, **extra)
 eng = E.Engine(0)
+if os.environ.get("NEMO_GLOB_BLOCK"):
+    eng.set_option("chains_glob_block", int(os.environ["NEMO_GLOB_BLOCK"]))
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 G = corpus.n_graphs
 st = eng.debug_copy("stamps", 0, 16 * 8 * G).view(np.uint64).reshape(G, 16).astype(np.int64)
