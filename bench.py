@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                     help="off: the timed steps run without per-launch HIP events (two extra steps collect them)")
     ap.add_argument("--stage-blocks", type=int, default=0, help="bulk D2H staging by a k_to_host grid of this size (0: runtime copies)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="N=1 only: the corpus run-sharded over this many libnemohip contexts on the one GPU, each "
+                         "on its own stream, their phases issued in turn so that one lane's latency-bound level "
+                         "sweeps overlap another's bandwidth-bound passes (default: the config's)")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
     return ap.parse_args()
@@ -73,12 +77,15 @@ def parse():
 
 # workload per config (generator settings: tools/synth.py CONFIGS); cpu_runs: the bounded sample the CPU
 # baseline times when a whole pass would take minutes
-CONFIGS = {"c3": {"runs": 10000, "gen": "c3", "cpu_runs": None},
-           "c3_molly": {"runs": 10000, "gen": "c3_molly", "cpu_runs": None},
-           "c4": {"runs_total": 100000, "gen": "c3", "cpu_runs": 5000},
-           # the CPU oracle is superlinear in graph size on C5's shape (>15 min per 1M-node run), so its
-           # bounded sample is 4 runs of the same shape at 50k-node graphs (EOT 100, same density)
-           "c5": {"runs": 128, "gen": "c5", "cpu_runs": 4, "cpu_sample": {"target_nodes": 50_000, "eot": 100}}}
+CONFIGS = {"c3": {"runs": 10000, "gen": "c3", "cpu_runs": None, "lanes": 1},
+           "c3_molly": {"runs": 10000, "gen": "c3_molly", "cpu_runs": None, "lanes": 1},
+           "c4": {"runs_total": 100000, "gen": "c3", "cpu_runs": 5000, "lanes": 1},
+           # C5 (1k runs of 1M-node graphs) does not fit 288 GB at once: the bench keeps a batch of 320 runs
+           # resident (~240 GB) and times passes over it.  The CPU oracle is superlinear in graph size on
+           # C5's shape (~30 min per 1M-node graph), so its bounded sample is 4 runs of the same shape at
+           # 50k-node graphs (EOT 100, same density)
+           "c5": {"runs": 320, "gen": "c5", "cpu_runs": 4, "cpu_sample": {"target_nodes": 50_000, "eot": 100},
+                  "lanes": 1}}
 
 
 def cpu_info():
@@ -161,15 +168,25 @@ def main():
     has_run0 = bool(owned[corpus.run_index(0)]) if 0 in set(its.tolist()) else False
     mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
 
-    eng = Engine(local)
-    eng.set_option("stage_blocks", args.stage_blocks)
-    for kv in args.set:
-        k, v = kv.split("=", 1)
-        eng.set_option(k, int(v))
-    stream = torch.cuda.current_stream()
-    eng.set_stream(stream.cuda_stream)
+    def new_engine():
+        e = Engine(local)
+        e.set_option("stage_blocks", args.stage_blocks)
+        for kv in args.set:
+            k, v = kv.split("=", 1)
+            e.set_option(k, int(v))
+        return e
+
+    lanes_n = 1 if world > 1 else (args.lanes or cfg.get("lanes", 1))
     free0 = torch.cuda.mem_get_info()[0]
-    eng.load(corpus)
+    if lanes_n > 1:
+        lanes = make_lanes(corpus, lanes_n, new_engine, success, failed, mode)
+        engines = [ln["eng"] for ln in lanes]
+        eng = engines[0]
+    else:
+        eng = new_engine()
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        eng.load(corpus)
+        engines = [eng]
     d_red = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda")
     V0 = corpus.graph_size(2 * corpus.run_index(0) + 1)
 
@@ -228,12 +245,15 @@ def main():
         state, chain_off, chain_ht = eng.simplified_view()
         return state, chain_off, chain_ht, masks, miss
 
+    if lanes_n > 1:
+        step = lambda: step_lanes(lanes, corpus, mode)  # noqa: E731
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     hbm_used = free0 - torch.cuda.mem_get_info()[0]  # the resident corpus + every buffer a step grew
-    eng.set_timing(args.kernel_timing == "on")
-    eng.reset_timings()
+    for e in engines:
+        e.set_timing(args.kernel_timing == "on")
+        e.reset_timings()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -245,12 +265,18 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if args.kernel_timing == "off":
-        eng.set_timing(True)
+        for e in engines:
+            e.set_timing(True)
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-    tim = eng.timings()
-    eng.set_timing(False)
+    tim = {}
+    for e in engines:  # per-launch figures of every lane (a lane's launch overlaps the others')
+        for k, v in e.timings().items():
+            a = tim.setdefault(k, {"launches": 0, "ms": 0.0, "bytes": 0.0, "edges": 0.0})
+            for f in a:
+                a[f] += v[f]
+        e.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -285,8 +311,10 @@ def main():
             traffic = None
     e2e = None
     if rank == 0 and world == 1 and args.e2e_runs > 0 and not strong and args.config != "c5":
-        eng.close()
+        for e in engines:
+            e.close()
         eng = Engine(local)
+        engines = [eng]
         e2e = e2e_leg(args, gen, eng, threads, mode)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -318,7 +346,11 @@ def main():
                    "nodes_total_rank0": Vn, "edges_total_rank0": E, "edges_per_node": round(E / max(Vn, 1), 3),
                    "failed_runs_rank0": len(failed), "diff_mode": args.diff_mode,
                    "parallelism": f"run-sharded x{n_gpus}, RCCL all-reduce of the prototype vector"
-                                  + (" + broadcast of failedRuns[0]'s label set" if label_bcast else "")},
+                                  + (" + broadcast of failedRuns[0]'s label set" if label_bcast else "")
+                                  + (f"; on the GPU, {lanes_n} lanes: the rank's runs LPT-sharded over {lanes_n} "
+                                     "contexts, one stream each, phases issued in turn, vectors summed on the "
+                                     "host" if lanes_n > 1 else ""),
+                   "lib_options": args.set},
         "edges_traversed_per_s": round(edges_per_s, 1),
         "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -344,10 +376,85 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as fh:
                 fh.write(line + "\n")
-    eng.close()
+    for e in engines:
+        e.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def make_lanes(corpus, n, new_engine, success, failed, mode):
+    """The N=1 corpus run-sharded over n contexts on the one GPU (nemo_partition_runs' LPT shards, run 0
+    replicated, not owned, in every lane).  Each lane loads its runs; the reference diff mode's label
+    source (failedRuns[0]'s post-goal labels, differential-provenance.go:22-43) is handed to every lane
+    as a host label set (nemo_diffprov_host_labels)."""
+    from nemo_amd.corpus import DIFF_REFERENCE, NODE_RULE
+    from nemo_amd.shard import partition_runs, shard_layout
+    parts = partition_runs(corpus, n)
+    f0_labels = None
+    if failed and mode == DIFF_REFERENCE:
+        g = 2 * corpus.run_index(failed[0]) + 1
+        a, b = int(corpus.node_off[g]), int(corpus.node_off[g + 1])
+        f0_labels = corpus.label[a:b][(corpus.node_word[a:b] & NODE_RULE) == 0].copy()
+    fset = set(failed)
+    lanes = []
+    for k in range(n):
+        runs, own = shard_layout(corpus, k, n, parts)
+        sub = corpus.subset(runs, own)
+        o = sub.owned if sub.owned is not None else np.ones(sub.n_runs, np.uint8)
+        its = [int(x) for x in sub.iteration]
+        e = new_engine()
+        e.load(sub)
+        lf = [it for it, ok in zip(its, o) if ok and it in fset]
+        has0 = 0 in its and bool(o[its.index(0)])
+        lanes.append({"eng": e, "corpus": sub, "failed": lf, "has0": has0, "success": success,
+                      "fidx": np.array([sub.run_index(f) for f in lf], np.int64), "labels": f0_labels})
+    return lanes
+
+
+def step_lanes(lanes, corpus, mode):
+    """One step over every lane: each phase is issued on every lane's stream before the next phase, so
+    the lanes' kernels run side by side; then the host-side retrieval, as the single-context step."""
+    from nemo_amd import engine as E
+    from nemo_amd.corpus import DIFF_PER_RUN
+    for ln in lanes:
+        ln["eng"].rebuild()
+    for ln in lanes:
+        ln["eng"].mark()
+    for ln in lanes:
+        if ln["labels"] is not None:
+            ln["eng"].diffprov_host_labels(ln["failed"], ln["labels"])
+        else:
+            ln["eng"].diffprov(ln["failed"], DIFF_PER_RUN)
+    for ln in lanes:
+        ln["eng"].simplify()
+    for ln in lanes:
+        ln["eng"].protos_partial(ln["success"], 0)
+    for ln in lanes:
+        ln["eng"].stage_simplified()
+    for ln in lanes:
+        if ln["has0"]:
+            ln["eng"].triggers()
+    for ln in lanes:
+        ln["eng"].pull(1)
+    for ln in lanes:
+        ln["eng"].pull(2)
+    vec = sum(ln["eng"].reduce_vector().astype(np.int64) for ln in lanes)  # the vectors summed (prototype.go:79-130)
+    T = corpus.n_tables
+    _, inter, uni = E.reduce_interpret(vec.astype(np.uint32), T, corpus.table_post)
+    inter, uni = np.asarray(inter, np.int64), np.asarray(uni, np.int64)
+    out = []
+    for ln in lanes:
+        e = ln["eng"]
+        tabs = e.run_tables(1)
+        if len(ln["fidx"]):  # missingFrom (prototype.go:141-206) for every failed run
+            _ = (tabs[ln["fidx"]][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
+            _ = (tabs[ln["fidx"]][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
+        if ln["has0"]:
+            e.trigger_rows()
+        masks = e.diff_masks_view() if ln["failed"] else None
+        out.append((e.simplified_view(), masks, e.missing()))
+    return out
 
 
 def e2e_leg(args, gen, eng, threads, mode):

@@ -22,6 +22,7 @@ namespace nemo {
 // graph's level walks are latency chains run by one wave, so a CU makes
 // progress on several graphs at once (a 1024-thread, 146 KB workgroup held a
 // whole CU for one graph).
+#define GA_B 4   // row entries loaded together while building the H* adjacency
 #define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bucketing)
 #define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
@@ -493,63 +494,42 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(1);
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
-  // From the graph's own CSR rows, no atomics.  A thread walks the child and
-  // parent rows of GA_N H* nodes at once, one entry of every row per step, so
-  // 2*GA_N independent load chains (column, flag, compact index) are in flight
-  // instead of one.  (Counting and scattering the whole edge list with cursor
-  // atomics cost a latency-bound pass over all E edges per direction.)
+  // From the graph's own CSR rows, one H* node per thread: a row's children
+  // (or parents) in batches of GA_B with their loads in flight together, no
+  // atomics.  (Counting and scattering the whole edge list with cursor
+  // atomics cost a latency-bound pass over all E edges per direction; walking
+  // four nodes' rows in lockstep, one entry per row and step, was slower: the
+  // step count is the longest of the rows.)
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
-  constexpr int GA_N = 4;
-  auto hrows = [&](uint32_t i0, bool fill) {
-    uint32_t a[2 * GA_N], b[2 * GA_N], k[2 * GA_N], x[GA_N];
+  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
+    uint32_t k = 0;
+    const uint32_t j1 = ptr[x + 1];
+    for (uint32_t j = ptr[x]; j < j1; j += GA_B) {
+      uint32_t y[GA_B];
+      bool h[GA_B];
 #pragma unroll
-    for (int q = 0; q < GA_N; q++) x[q] = i0 + q * GB < n ? hs[i0 + q * GB] : 0u;
+      for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
 #pragma unroll
-    for (int q = 0; q < GA_N; q++) {
-      const bool in = i0 + q * GB < n;
-      a[2 * q] = in ? gv.fp[x[q]] : 0u;
-      b[2 * q] = in ? gv.fp[x[q] + 1] : 0u;
-      a[2 * q + 1] = in ? gv.rp[x[q]] : 0u;
-      b[2 * q + 1] = in ? gv.rp[x[q] + 1] : 0u;
-    }
+      for (int q = 0; q < GA_B; q++) h[q] = j + q < j1 && INH(y[q]);
+      if (out) {
+        uint32_t hy[GA_B];
 #pragma unroll
-    for (int r = 0; r < 2 * GA_N; r++)
-      k[r] = fill && i0 + (r >> 1) * GB < n ? ((r & 1) ? S.pcoff : S.ccoff)[i0 + (r >> 1) * GB] : 0u;
-    bool more = false;
+        for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
 #pragma unroll
-    for (int r = 0; r < 2 * GA_N; r++) more |= a[r] < b[r];
-    while (more) {
-      uint32_t y[2 * GA_N];
-      bool h[2 * GA_N];
+        for (int q = 0; q < GA_B; q++)
+          if (h[q]) out[k++] = hy[q];
+      } else {
 #pragma unroll
-      for (int r = 0; r < 2 * GA_N; r++) y[r] = a[r] < b[r] ? ((r & 1) ? gv.rc : gv.fc)[a[r]] : 0u;
-#pragma unroll
-      for (int r = 0; r < 2 * GA_N; r++) h[r] = a[r] < b[r] && INH(y[r]);
-      if (fill) {
-        uint32_t hy[2 * GA_N];
-#pragma unroll
-        for (int r = 0; r < 2 * GA_N; r++) hy[r] = h[r] ? hidx[y[r]] : 0u;
-#pragma unroll
-        for (int r = 0; r < 2 * GA_N; r++)
-          if (h[r]) ((r & 1) ? S.par : S.child)[k[r]] = hy[r];
-      }
-      more = false;
-#pragma unroll
-      for (int r = 0; r < 2 * GA_N; r++) {
-        k[r] += h[r] ? 1u : 0u;
-        a[r] += a[r] < b[r] ? 1u : 0u;
-        more |= a[r] < b[r];
+        for (int q = 0; q < GA_B; q++) k += h[q] ? 1u : 0u;
       }
     }
-    if (!fill)
-#pragma unroll
-      for (int q = 0; q < GA_N; q++)
-        if (i0 + q * GB < n) {
-          S.ccoff[i0 + q * GB] = k[2 * q];
-          S.pcoff[i0 + q * GB] = k[2 * q + 1];
-        }
+    return k;
   };
-  for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) hrows(i0, false);
+  for (uint32_t i = tid; i < n; i += GB) {
+    const uint32_t x = hs[i];
+    S.ccoff[i] = hrow(gv.fp, gv.fc, x, nullptr);
+    S.pcoff[i] = hrow(gv.rp, gv.rc, x, nullptr);
+  }
   if (tid == 0) {
     S.ccoff[n] = 0;
     S.pcoff[n] = 0;
@@ -557,7 +537,11 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
   block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
-  for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) hrows(i0, true);
+  for (uint32_t i = tid; i < n; i += GB) {
+    const uint32_t x = hs[i];
+    hrow(gv.fp, gv.fc, x, S.child + S.ccoff[i]);
+    hrow(gv.rp, gv.rc, x, S.par + S.pcoff[i]);
+  }
 #undef INH
   __syncthreads();
   STAMP(2);
