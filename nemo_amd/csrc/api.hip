@@ -58,7 +58,6 @@ struct nemo_ctx {
   uint64_t glob_min_v = 65536;       // graphs with V >= this take k_chains_glob (set before load)
   uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   uint32_t glob_block_force = 0;     // chains_glob_block option (0 = by the number of deep graphs)
-  uint32_t chains_wpe = 4;           // chains_waves option: k_chains' first tier (4 or 5 waves per SIMD)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
@@ -506,11 +505,6 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->stage_blocks = value < 0 ? 0u : (uint32_t)value;
     return NEMO_OK;
   }
-  if (!strcmp(name, "chains_waves")) {  // 4 or 5; takes effect at the next load
-    if (value != 4 && value != 5) return fail(c, NEMO_ERR_INVALID, "chains_waves: 4 or 5");
-    c->chains_wpe = (uint32_t)value;
-    return NEMO_OK;
-  }
   if (!strcmp(name, "chains_glob_block")) {  // 0 (by corpus), 256 or 512; takes effect at the next load
     if (value != 0 && value != 256 && value != 512) return fail(c, NEMO_ERR_INVALID, "chains_glob_block: 0, 256 or 512");
     c->glob_block_force = (uint32_t)value;
@@ -805,7 +799,6 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     uint32_t n_deep = 0;
     for (uint32_t g = 0; g < G; g++) n_deep += off[g] != ~0ull;
     d.glob_block = c->glob_block_force ? c->glob_block_force : (n_deep > 512 ? 256u : 512u);
-    d.chains_wpe = c->chains_wpe;
     d.gscratch = nullptr;
     if (words) A(d.gscratch, words);
   }

@@ -171,7 +171,6 @@ struct DevCorpus {
   Tier t_ms, t_diff, t_pull;             // the LDS tiers of k_marksimp, k_diff_lds, k_pull_lds
   uint32_t gblock;                       // workgroup size of the global-tier kernels (256, or 1024 for deep corpora)
   uint32_t glob_block;                   // k_chains_glob's workgroup size (256 or 512)
-  uint32_t chains_wpe;                   // k_chains' first tier: 4 (HCAP 1664) or 5 (HCAP 1024) waves per SIMD
   uint32_t pg_chunks;                    // k_pg_* workgroups per listed graph (by the largest post graph)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null

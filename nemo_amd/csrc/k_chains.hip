@@ -1139,10 +1139,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_sel(DevCorpus c) {
   wave_append(need, g, sel + 1, sel);
 }
 
-// WPE: waves per SIMD the register budget is cut for (4: 119 VGPRs, no spills;
-// 5: 96 VGPRs, a few spilled), with HCAP sized so that the LDS image allows it
-template <int HCAP, int UCAP, int WPE>
-__global__ __launch_bounds__(NEMO_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_chains(DevCorpus c) {
+template <int HCAP, int UCAP>
+__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
   chains_graph<HCAP, UCAP>(c, blockIdx.x);
 }
 
@@ -1161,10 +1159,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 #define CHAINS_GRID 1024u
 void launch_chains(const DevCorpus &c, hipStream_t s) {
   if (!c.G) return;
-  if (c.chains_wpe == 5)  // 25 KB of LDS and 96 VGPRs: five workgroups per CU
-    hipLaunchKernelGGL((k_chains<1024, 120, 5>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
-  else  // 40.9 KB and 119 VGPRs: four
-    hipLaunchKernelGGL((k_chains<1664, 120, 4>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  hipLaunchKernelGGL((k_chains<1664, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
   launch_zero(c.sel + c.G + 1, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_chains_sel, dim3((c.G + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
   hipLaunchKernelGGL((k_chains_list<2048, 512>), dim3(std::min(c.G, CHAINS_GRID)), dim3(NEMO_BLOCK), 0, s, c);

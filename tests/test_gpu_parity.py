@@ -317,19 +317,18 @@ def test_chains_glob_tier(kind, block):
         e.close()
 
 
-@pytest.mark.parametrize("waves", [4, 5])
-@pytest.mark.parametrize("shape", ["wide_hstar", "many_levels", "long_chains", "c3"])
-def test_chains_lds_tiers(shape, waves):
-    # k_chains<1664, 120> (4 workgroups/CU) or k_chains<1024, 120> (chains_waves 5: 5 per CU) hands
-    # graphs whose chain subgraph, level count or longest prefix exceed it to k_chains<2048, 512>;
-    # both against the oracle on graphs that land in each tier
+@pytest.mark.parametrize("shape", ["wide_hstar", "many_levels", "long_chains"])
+def test_chains_lds_tiers(eng, shape):
+    # k_chains<1664, 120> (4 workgroups/CU) hands graphs whose chain subgraph,
+    # level count or longest prefix exceed it to k_chains<2048, 512>; both
+    # against the oracle on graphs that land in each tier
     from nemo_amd.corpus import corpus_from_graphs
     from tools import synth
     if shape == "wide_hstar":  # H* of ~1.7-2k nodes: past the first tier's 1664
         corpus, _ = synth.generate(8, target_nodes=5600, eot=10)
     elif shape == "many_levels":  # > 120 Kahn levels: the first tier's old front
         corpus, _ = synth.generate(8, target_nodes=3000, eot=60)
-    elif shape == "long_chains":  # one @next chain of 80 rules (prefix length 159 > 118): the second tier
+    else:  # one @next chain of 80 rules (prefix length 159 > 118): the second tier
         def chain(cond, n):
             goals = [{"id": f"goal{i}", "label": f"log(a, {i})", "table": cond if i == 0 else "log", "time": "1"}
                      for i in range(n + 1)]
@@ -339,14 +338,7 @@ def test_chains_lds_tiers(shape, waves):
             return {"goals": goals, "rules": rules, "edges": edges}
         corpus = corpus_from_graphs([(0, "success", chain("pre", 80), chain("post", 80)),
                                      (1, "failure", chain("pre", 40), chain("post", 70))])
-    if shape == "c3":
-        corpus, _ = synth.generate(64, **synth.CONFIGS["c3"])
-    e = E.Engine(0)
-    try:
-        e.set_option("chains_waves", waves)
-        _check(e, corpus, mode=DIFF_PER_RUN, pulls=True)
-    finally:
-        e.close()
+    _check(eng, corpus, mode=DIFF_PER_RUN, pulls=True)
 
 
 @pytest.mark.parametrize("block", [256, 1024])
