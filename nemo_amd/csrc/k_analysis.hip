@@ -423,37 +423,78 @@ __global__ __launch_bounds__(PG_BLOCK) void k_pg_c(DevCorpus c) {
 }
 // rules reachable from G2: one wave per graph, one wave barrier per Kahn level
 // (pull form: a node's parents lie on earlier levels, whose bits are final).
-// Deep graphs have ~20k levels of a few dozen nodes, so a level costs its
-// dependent-load chain: each node's parent ids, then their flag / SB bytes,
-// are fetched PG_BATCH at a time, independent of each other.  The graph is a
-// chain of latencies, so it is one wave: many graphs then share a CU (a
+// Deep graphs have ~20k levels of a few dozen nodes, so the sweep is a chain
+// of latencies, and one wave per graph lets many graphs share a CU (a
 // 1024-thread workgroup had 15 idle waves per level and one graph per CU).
+// The wave walks 64-position chunks of the Kahn order with a three-stage
+// pipeline: the Kahn order of chunk k+2 and the static data of chunk k+1
+// (node word, flags, row bounds, own SB byte) are loaded while chunk k reads
+// its parents' SB bytes, so a chunk's critical path is the parent ids (PG_BATCH
+// at a time) and their flag / SB bytes, not the four dependent loads before.
 #define PG_BATCH 4
 __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
   const uint32_t *lst = proto_list(c);
-  const uint32_t nl = lst[0];
-  for (uint32_t b = blockIdx.x; b < nl; b += gridDim.x) {
+  const uint32_t ngr = lst[0];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t b = blockIdx.x; b < ngr; b += gridDim.x) {
     const uint32_t r = lst[1 + b], g = 2 * r + 1;
     const GraphView gv = c.view(g);
-    const uint8_t *f = gv.flags;
+    const uint32_t nlev = gv.nlev;
+    if (nlev == 0) continue;
+    const uint8_t *__restrict__ f = gv.flags;
     uint8_t *sb = c.sb + gv.n0;
+    const uint32_t *__restrict__ topo = gv.topo;
     const uint32_t *ch = c.chain + 5 * gv.n0, nch = c.nch[g];
     const uint32_t *clf = c.cl_first + gv.n0, *cln = c.cl_next + gv.n0;
-    for (uint32_t l = 0; l < gv.nlev; l++) {
-      const uint32_t e = gv.lvl[l + 1];
-      for (uint32_t i = gv.lvl[l] + threadIdx.x; i < e; i += PG_SWEEP) {
-        const uint32_t x = gv.topo[i];
-        const uint32_t w = gv.word[x], fx = f[x];
-        const bool rule = is_rule(w);
-        if (rule ? !((fx & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT || (fx & NEMO_F_HEAD))
-                 : (fx & NEMO_F_DELETED) != 0)
-          continue;
+    // chunk cursors (level, start, end): levels are contiguous, so the next
+    // level starts where this one ends and only its end is loaded
+    auto adv = [&](uint32_t &l, uint32_t &s, uint32_t &e) {
+      if (s + PG_SWEEP < e) {
+        s += PG_SWEEP;
+      } else {
+        l++;
+        s = e;
+        e = l < nlev ? gv.lvl[l + 1] : e;
+      }
+    };
+    struct Stat {
+      uint32_t x, w, fx, j0, j1, sbx;
+    };
+    auto stat = [&](uint32_t x) {
+      Stat t{x, 0, 0, 0, 0, 0};
+      if (x != NEMO_NONE) {
+        t.w = gv.word[x];
+        t.fx = f[x];
+        t.j0 = gv.rp[x];
+        t.j1 = gv.rp[x + 1];
+        t.sbx = sb[x];
+      }
+      return t;
+    };
+    uint32_t l0 = 0, s0 = gv.lvl[0], e0 = gv.lvl[1];
+    uint32_t l1 = l0, s1 = s0, e1 = e0;
+    adv(l1, s1, e1);
+    uint32_t l2 = l1, s2 = s1, e2 = e1;
+    adv(l2, s2, e2);
+    Stat cur = stat(s0 + lane < e0 ? topo[s0 + lane] : NEMO_NONE);
+    uint32_t x1 = s1 + lane < e1 ? topo[s1 + lane] : NEMO_NONE;
+    while (l0 < nlev) {
+      // prefetch: chunk k+2's nodes, chunk k+1's static data
+      const uint32_t x2 = s2 + lane < e2 ? topo[s2 + lane] : NEMO_NONE;
+      const Stat nxt = stat(x1);
+      // chunk k
+      const uint32_t x = cur.x, fx = cur.fx;
+      const bool rule = is_rule(cur.w);
+      const bool live = x != NEMO_NONE && (rule ? ((fx & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT ||
+                                                    (fx & NEMO_F_HEAD))
+                                                 : (fx & NEMO_F_DELETED) == 0);
+      if (live) {
         // a rule is reached from a live G2 / RCH goal parent; a goal from an RCH
         // regular rule parent, or a tail parent one of whose chains has an RCH head
         const uint32_t want = rule ? (SB_G2 | SB_RCH) : SB_RCH;
         bool rch = false;
-        const uint32_t j1 = gv.rp[x + 1];
-        for (uint32_t j = gv.rp[x]; j < j1 && !rch; j += PG_BATCH) {
+        const uint32_t j1 = cur.j1;
+        for (uint32_t j = cur.j0; j < j1 && !rch; j += PG_BATCH) {
           uint32_t p[PG_BATCH], fp_[PG_BATCH], bp[PG_BATCH];
 #pragma unroll
           for (int q = 0; q < PG_BATCH; q++) p[q] = j + q < j1 ? gv.rc[j + q] : NEMO_NONE;
@@ -475,9 +516,14 @@ __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
             }
           }
         }
-        if (rch) sb[x] |= SB_RCH;
+        if (rch) sb[x] = (uint8_t)(cur.sbx | SB_RCH);  // only x sets its own RCH bit
       }
-      __syncthreads();
+      if (l1 != l0) __syncthreads();  // the next chunk starts a level: this level's bits are final
+      cur = nxt;
+      x1 = x2;
+      l0 = l1, s0 = s1, e0 = e1;
+      l1 = l2, s1 = s2, e1 = e2;
+      adv(l2, s2, e2);
     }
   }
 }
