@@ -302,11 +302,10 @@ def main():
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc):  # per timed group, keyed by the workload's node count (tools/pmc_summary.py)
         try:
-            pj = json.load(open(pmc)).get(dname, {})
-            if pj.get("workload_nodes") == int(corpus.node_off[-1]):
-                traffic = pj.get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc)).get(dname, {}).get(str(int(corpus.node_off[-1])), {})
+            traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     e2e = None

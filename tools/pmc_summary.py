@@ -10,6 +10,11 @@ Writes
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
 FETCH_SIZE tallies 128-B read requests at 64 B (MI355X_MICROARCH.md, HBM
 section), WRITE_SIZE is exact for wide stores.  Other widths are uncalibrated.
+
+pmc_summary.json holds one entry per workload (its node count) under each
+timed group of the library (the names bench.py's roofline uses): a group's
+traffic per launch is the sum over the kernels its launch issues (GROUPS),
+each launched once per group launch.  Earlier workloads' entries are kept.
 """
 import csv
 import glob
@@ -41,6 +46,24 @@ def per_kernel(pattern, counter=None):
             continue
         acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
+
+
+# timed group (libnemohip's nemo_timings names) -> rocprof kernel base names issued inside it
+GROUPS = {
+    "k_build": ["k_build"],
+    "k_csr": ["k_load_sel", "k_csr"],
+    "k_csrb": ["k_cb_zero", "k_cb_hist", "k_cb_scan", "k_cb_part", "k_cb_bucket", "k_csrb_fin", "k_csrb_zero",
+               "k_csrb_count", "k_csrb_scan", "k_csrb_scatter", "k_csrb_rows"],
+    "k_topo": ["k_topo", "k_topo_deep"],
+    "k_marksimp": ["k_marksimp"],
+    "k_mark": ["k_mark", "k_mw_mark_z", "k_mw_mark_a", "k_mw_mark_b"],
+    "k_simplify": ["k_simplify_flags", "k_mw_simplify_1", "k_mw_simplify_2", "k_mw_simplify_3", "k_mw_simplify_4"],
+    "k_chains": ["k_chains", "k_chains_sel", "k_chains_list", "k_chains_big", "k_chains_glob"],
+    "k_proto": ["k_proto_lds", "k_proto_sel", "k_pg_init", "k_pg_link", "k_pg_a", "k_pg_b", "k_pg_c", "k_pg_sweep",
+                "k_pg_d", "k_pg_gate"],
+    "k_pull": ["k_pull_lds", "k_pull_sel", "k_pull", "k_mwp_count", "k_mwp_scan", "k_mwp_write", "k_scan64"],
+    "k_diff": ["k_dprep_a", "k_dprep_scan", "k_dprep_b", "k_diff_lds", "k_diff", "k_diff_expand"],
+}
 
 
 def main():
@@ -85,11 +108,26 @@ def main():
         b[1] += fk
         b[2] += wk
         b[3] = max(b[3], n)
-    summary = {k: {"workload_nodes": nodes, "hbm_bytes_per_launch": round(hbm), "fetch_kib": round(fk, 1),
-                   "write_kib": round(wk, 1), "launches": n, "round": tag}
-               for k, (hbm, fk, wk, n) in sorted(base_hbm.items())}
-    summary["_rule"] = "2*FETCH_SIZE + WRITE_SIZE, KiB->bytes (summed over template tiers)"
-    json.dump(summary, open(os.path.join(prof, "pmc_summary.json"), "w"), indent=1)
+    path = os.path.join(prof, "pmc_summary.json")
+    try:
+        summary = json.load(open(path))
+        if "_rule" in summary and not summary.get("_per_workload"):
+            summary = {}  # the round-2 layout (one workload): superseded
+    except (OSError, ValueError):
+        summary = {}
+    for grp, members in GROUPS.items():
+        parts = [base_hbm[m] for m in members if m in base_hbm]
+        if not parts:
+            continue
+        hbm = sum(p[0] for p in parts)
+        summary.setdefault(grp, {})[str(nodes)] = {
+            "hbm_bytes_per_launch": round(hbm), "fetch_kib": round(sum(p[1] for p in parts), 1),
+            "write_kib": round(sum(p[2] for p in parts), 1), "kernels": [m for m in members if m in base_hbm],
+            "round": tag, "config": bj["config"].get("workload", "")[:40]}
+    summary["_rule"] = ("2*FETCH_SIZE + WRITE_SIZE, KiB->bytes, per launch of the timed group (the sum over the "
+                        "kernels it issues), keyed by the workload's node count")
+    summary["_per_workload"] = True
+    json.dump(summary, open(path, "w"), indent=1)
     open(os.path.join(prof, f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
