@@ -212,6 +212,7 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define NIL16 0xFFFFu
 #define CF_ROWS 20  // topo positions per thread per compaction round (fast front)
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
+#define CH_K 3      // up/down sweeps: parents (children) of a node read together
 
 template <int HCAP, int UCAP>
 struct ChainsLDS {
@@ -603,49 +604,73 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
   }
   // up: longest H* path from a next rule ending here; down/nxt/tail: the
   // lexicographically least longest continuation to a next rule
-  // both sweeps in one loop, one barrier per level: waves 0-1 walk the levels
-  // forward (up), waves 2-3 backward (down); they touch disjoint arrays, so
-  // their dependent LDS chains overlap instead of adding up
-  constexpr uint32_t HALF = NEMO_BLOCK / 2;
-  const bool upper = tid < HALF;
-  const uint32_t ht = upper ? tid : tid - HALF;
-  for (uint32_t s = 0; s < ns; s++) {
-    if (upper) {
-      const uint32_t e = L.seg[s + 1];
-      for (uint32_t i = L.seg[s] + ht; i < e; i += HALF) {
-        int32_t d = RULE(i) ? 0 : -1;
-        const uint32_t j1 = L.u.adj.pcoff[i + 1];
-        for (uint32_t j = L.u.adj.pcoff[i]; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
-        L.up[i] = (int16_t)d;
-      }
-    } else {
-      const uint32_t sd = ns - 1 - s;
-      const uint32_t e = L.seg[sd + 1];
-      for (uint32_t i = L.seg[sd] + ht; i < e; i += HALF) {
-        // one pass: the deepest child, ties to the smallest ID rank
-        int32_t best = -1;
-        uint32_t bc = NIL16, br = NEMO_NONE;
-        const uint32_t j1 = L.u.adj.ccoff[i + 1];
-        for (uint32_t j = L.u.adj.ccoff[i]; j < j1; j++) {
-          const uint32_t w = L.u.adj.child[j];
-          const int32_t dw = L.down[w];
-          const uint32_t rw = L.crank[w];
-          if (dw > best || (dw == best && rw < br)) {
-            best = dw;
-            bc = w;
-            br = rw;
+  // both sweeps at once, each by ONE wave and without a barrier: wave 0 walks
+  // the levels forward (up), wave 1 backward (down).  A wave's LDS operations
+  // complete in order, so a level reads the values its own wave wrote for the
+  // levels before; the two waves touch disjoint arrays.  A node's first
+  // CH_K parents (children) are read together, clamped (their values are
+  // discarded past the row's end), so a level costs a few LDS round trips.
+  if (tid < 128) {
+    const bool fwd = tid < 64;
+    const uint32_t lane = tid & 63u;
+    for (uint32_t s = 0; s < ns; s++) {
+      const uint32_t sl = fwd ? s : ns - 1 - s;
+      const uint32_t e = L.seg[sl + 1];
+      for (uint32_t i = L.seg[sl] + lane; i < e; i += 64) {
+        const bool ru = RULE(i);
+        if (fwd) {
+          int32_t d = ru ? 0 : -1;
+          const uint32_t j0 = L.u.adj.pcoff[i], j1 = L.u.adj.pcoff[i + 1];
+          uint32_t p[CH_K];
+          int32_t v[CH_K];
+#pragma unroll
+          for (int q = 0; q < CH_K; q++) p[q] = min((uint32_t)L.u.adj.par[min(j0 + q, ECAP - 1u)], (uint32_t)HCAP - 1u);
+#pragma unroll
+          for (int q = 0; q < CH_K; q++) v[q] = L.up[p[q]];
+#pragma unroll
+          for (int q = 0; q < CH_K; q++) d = j0 + q < j1 ? max(d, v[q] + 1) : d;
+          for (uint32_t j = j0 + CH_K; j < j1; j++) d = max(d, (int32_t)L.up[L.u.adj.par[j]] + 1);
+          L.up[i] = (int16_t)d;
+        } else {
+          // one pass: the deepest child, ties to the smallest ID rank
+          int32_t best = -1;
+          uint32_t bc = NIL16, br = NEMO_NONE;
+          auto take = [&](uint32_t w, int32_t dw, uint32_t rw) {
+            if (dw > best || (dw == best && rw < br)) {
+              best = dw;
+              bc = w;
+              br = rw;
+            }
+          };
+          const uint32_t j0 = L.u.adj.ccoff[i], j1 = L.u.adj.ccoff[i + 1];
+          uint32_t w[CH_K], rw[CH_K];
+          int32_t dw[CH_K];
+#pragma unroll
+          for (int q = 0; q < CH_K; q++) w[q] = min((uint32_t)L.u.adj.child[min(j0 + q, ECAP - 1u)], (uint32_t)HCAP - 1u);
+#pragma unroll
+          for (int q = 0; q < CH_K; q++) {
+            dw[q] = L.down[w[q]];
+            rw[q] = L.crank[w[q]];
           }
+#pragma unroll
+          for (int q = 0; q < CH_K; q++)
+            if (j0 + q < j1) take(w[q], dw[q], rw[q]);
+          for (uint32_t j = j0 + CH_K; j < j1; j++) {
+            const uint32_t x = L.u.adj.child[j];
+            take(x, L.down[x], L.crank[x]);
+          }
+          int32_t d = best >= 0 ? best + 1 : (ru ? 0 : -1);
+          if (ru && d < 0) d = 0;
+          if (d > 0 && best < 0) bc = NIL16;
+          L.down[i] = (int16_t)d;
+          L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
+          if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
         }
-        int32_t d = best >= 0 ? best + 1 : (RULE(i) ? 0 : -1);
-        if (RULE(i) && d < 0) d = 0;
-        if (d > 0 && best < 0) bc = NIL16;
-        L.down[i] = (int16_t)d;
-        L.nxt[i] = (uint16_t)(d > 0 ? bc : NIL16);
-        if (d < 0) s_fail = 1;  // a goal without a chain continuation: impossible on H*
       }
+      wsync();  // the level's writes before the next level's reads (compiler order; the wave's DS ops are in order)
     }
-    __syncthreads();
   }
+  __syncthreads();
   {
     uint32_t m = 0;
     for (uint32_t i = tid; i < n; i += NEMO_BLOCK) m = max(m, (uint32_t)max((int32_t)L.up[i], 0));

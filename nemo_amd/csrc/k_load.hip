@@ -48,7 +48,10 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 // workgroups share a CU.  A graph with an in-degree above 255 is flagged
 // (redo) and rebuilt by k_csr + k_topo, which also take the graphs beyond
 // the caps; both tiers produce the same outputs and validations.
-#define BLD_EPT 32  // edges per thread held in registers (bld_e <= BLD_EPT * NEMO_BLOCK)
+#ifndef BLD_BLOCK
+#define BLD_BLOCK 256  // k_build workgroup size (512: 3.91 ms against 3.66 at C3)
+#endif
+#define BLD_OCC(B) ((B) == 256 ? 4 : 6)  // waves per SIMD the register budget is cut for
 #define BLD_KB 4    // Kahn: children of a node processed per round
 
 #define BLD_RS 8    // row entries sorted in registers (longer rows: insertion sort in LDS)
@@ -76,11 +79,11 @@ __device__ __forceinline__ void sort_net8(uint32_t *x) {
   }
 }
 
-// k_build's row sort: rows v0 and v0 + NEMO_BLOCK ([a, a + n) in col), both
+// k_build's row sort: rows v0 and v0 + B ([a, a + n) in col), both
 // rows' LDS reads issued together and the entries sorted in registers (a row
 // longer than RS: insertion sort in LDS); reverse rows (dir 0) also count the
 // relationships created (pre-post-prov.go:150-210: distinct, goal<->rule).
-template <int RS>
+template <int RS, int B>
 __device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t *s_rule, uint32_t E, uint32_t V,
                                                   int dir, uint32_t v0, const uint32_t (&a)[2],
                                                   const uint32_t (&n)[2]) {
@@ -94,7 +97,7 @@ __device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t 
     }
 #pragma unroll
   for (int q = 0; q < 2; q++) {
-    const uint32_t v = v0 + q * NEMO_BLOCK, b = a[q] + n[q];
+    const uint32_t v = v0 + q * B, b = a[q] + n[q];
     if (n[q] <= (uint32_t)RS) {
       if (n[q] >= 2) {
         if (RS == 4) sort_net4(x[q]);
@@ -155,9 +158,11 @@ __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint3
   return c.bld_bytes != 0u && V <= c.bld_v && E <= c.bld_e;
 }
 
-__global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
+template <int B>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B)))) void k_build(DevCorpus c) {
+  constexpr int EPT = 8192 / B;  // edges per thread held in registers (bld_e <= 8192)
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_lds[NEMO_WAVES];
+  __shared__ uint32_t s_lds[B / 64];
   __shared__ uint32_t s_bad, s_created, s_tail, s_cnt[3];
   __shared__ uint32_t s_sink[64];  // per-lane no-op atomic targets (one bank each: no same-address serialisation)
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
@@ -180,16 +185,16 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
   STAMP(10);
   // every load of the graph's input issued back to back: edge e = tid + q*BLOCK
   // as (src << 16 | dst), and the rule bits of the node words
-  uint32_t sd[BLD_EPT];
+  uint32_t sd[EPT];
   bool bad = false;
 #pragma unroll
-  for (int q = 0; q < BLD_EPT; q++) {
-    const uint32_t e = tid + q * NEMO_BLOCK;
+  for (int q = 0; q < EPT; q++) {
+    const uint32_t e = tid + q * B;
     const uint32_t x = e < E ? es[e] : 0u, y = e < E ? ed[e] : 0u;
     bad |= e < E && (x >= V || y >= V);
     sd[q] = (x << 16) | (y & 0xFFFFu);
   }
-  for (uint32_t w = tid; w < (V + 31) / 32; w += NEMO_BLOCK) s_rule[w] = 0;
+  for (uint32_t w = tid; w < (V + 31) / 32; w += B) s_rule[w] = 0;
   if (tid == 0) {
     s_bad = 0;
     s_created = 0;
@@ -198,16 +203,16 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     c.redo[g] = 0;
   }
   __syncthreads();
-  for (uint32_t base = 0; base < V; base += 8 * NEMO_BLOCK) {
+  for (uint32_t base = 0; base < V; base += 8 * B) {
     bool r[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + tid + q * NEMO_BLOCK;
+      const uint32_t v = base + tid + q * B;
       r[q] = v < V && is_rule(word[v]);
     }
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + tid + q * NEMO_BLOCK;
+      const uint32_t v = base + tid + q * B;
       const uint64_t m = __ballot(r[q]);
       if ((lane_id() & 31) == 0 && v < V) {
         const uint32_t bits = (uint32_t)(m >> (lane_id() & 32));
@@ -226,12 +231,12 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
   for (int dir = 0; dir < 2; dir++) {  // 0: reverse rows (parents), 1: forward rows (children)
     const int ks = dir ? 16 : 0, vs = dir ? 0 : 16;  // key / value shifts in sd
     uint32_t *optr = dir ? c.fp + n0 + g : c.rp + n0 + g, *ocol = dir ? c.fc + e0 : c.rc + e0;
-    for (uint32_t w = tid; w < (V + 2) / 2; w += NEMO_BLOCK) ptr32[w] = 0;
+    for (uint32_t w = tid; w < (V + 2) / 2; w += B) ptr32[w] = 0;
     __syncthreads();
     if (dir == 0) STAMP(0);
 #pragma unroll
-    for (int q = 0; q < BLD_EPT; q++)
-      if (tid + q * NEMO_BLOCK < E) {
+    for (int q = 0; q < EPT; q++)
+      if (tid + q * B < E) {
         const uint32_t k = (sd[q] >> ks) & 0xFFFFu;
         atomicAdd(&ptr32[k >> 1], 1u << (16 * (k & 1)));
       }
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     if (dir == 0) STAMP(1);
     if (dir == 0) {  // in-degrees; a graph beyond the u8 counters goes to the global tier
       bool heavy = false;
-      for (uint32_t w = tid; 4 * w < V; w += NEMO_BLOCK) {
+      for (uint32_t w = tid; 4 * w < V; w += B) {
         uint32_t x = 0;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
@@ -257,14 +262,14 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
       }
     }
     if (dir == 0) STAMP(2);
-    block_scan_inplace(ptr, V + 1, s_lds);
+    block_scan_inplace<B>(ptr, V + 1, s_lds);
     if (dir == 0) STAMP(3);
-    for (uint32_t v = tid; v <= V; v += NEMO_BLOCK) optr[v] = ptr[v];
+    for (uint32_t v = tid; v <= V; v += B) optr[v] = ptr[v];
     __syncthreads();
     if (dir == 0) STAMP(4);
 #pragma unroll
-    for (int q = 0; q < BLD_EPT; q++)
-      if (tid + q * NEMO_BLOCK < E) {
+    for (int q = 0; q < EPT; q++)
+      if (tid + q * B < E) {
         const uint32_t k = (sd[q] >> ks) & 0xFFFFu, sh = 16 * (k & 1);
         col[(atomicAdd(&ptr32[k >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)((sd[q] >> vs) & 0xFFFFu);
       }
@@ -273,31 +278,31 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     // sort every row; two rows per thread at a time with all their LDS reads
     // issued together, the entries sorted in registers (a latency chain of a
     // few LDS round trips instead of one per entry)
-    for (uint32_t v0 = tid; v0 < V; v0 += 2 * NEMO_BLOCK) {
+    for (uint32_t v0 = tid; v0 < V; v0 += 2 * B) {
       uint32_t a[2], n[2];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const uint32_t v = v0 + q * NEMO_BLOCK;
+        const uint32_t v = v0 + q * B;
         a[q] = v < V && v ? ptr[v - 1] : 0u;
         n[q] = v < V ? ptr[v] - a[q] : 0u;
       }
       // rows of at most four entries everywhere in the wave (most reverse rows,
       // goals' forward rows): the 4-key network; else the 8-key one
       if (!__any(n[0] > 4u || n[1] > 4u))
-        created += sort_row_pair<4>(col, s_rule, E, V, dir, v0, a, n);
+        created += sort_row_pair<4, B>(col, s_rule, E, V, dir, v0, a, n);
       else
-        created += sort_row_pair<BLD_RS>(col, s_rule, E, V, dir, v0, a, n);
+        created += sort_row_pair<BLD_RS, B>(col, s_rule, E, V, dir, v0, a, n);
     }
     __syncthreads();
     if (dir == 0) STAMP(6);
-    for (uint32_t j = tid; j < E; j += NEMO_BLOCK) ocol[j] = col[j];
+    for (uint32_t j = tid; j < E; j += B) ocol[j] = col[j];
     __syncthreads();
     STAMP(12 + dir);
   }
   atomicAdd(&s_created, created);
   // Kahn levels over the forward rows still in LDS (ptr[v] = end of row v)
   uint32_t *nlv = c.nlv + n0;
-  for (uint32_t base = 0; base < V; base += NEMO_BLOCK) {
+  for (uint32_t base = 0; base < V; base += B) {
     const uint32_t v = base + tid;
     const bool src = v < V && cnt8[v] == 0u;
     lds_append16(src, v, q16, &s_tail);
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
   while (lo < hi) {
     uint32_t *cur = &s_cnt[nl % 3];
     if (tid == 0) s_cnt[(nl + 1) % 3] = 0;
-    for (uint32_t base = lo; base < hi; base += NEMO_BLOCK) {
+    for (uint32_t base = lo; base < hi; base += B) {
       const uint32_t i = base + tid;
       // branch-free: reads and atomics at clamped / sink addresses, so the
       // BLD_KB slots' round trips overlap instead of waiting one by one
@@ -367,13 +372,13 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
     hi += s_cnt[(nl - 1) % 3];  // after the barrier: plain LDS read
     if (tid == 0) lvl[nl] = lo;
   }
-  for (uint32_t i = tid; i < hi; i += NEMO_BLOCK) topo[i] = q16[i];
+  for (uint32_t i = tid; i < hi; i += B) topo[i] = q16[i];
   if ((g & 1u) && hi == V) {
     // post graphs: the forward edges in source Kahn order for k_proto_lds (e2:
     // src << 16 | dst) and each Kahn position's first edge (posoff).  Every
     // thread copies the rows of a contiguous chunk of Kahn positions, four at a
     // time with their LDS reads issued together (rows past four entries loop).
-    const uint32_t chunk = (V + NEMO_BLOCK - 1) / NEMO_BLOCK, i0 = min(V, tid * chunk), i1 = min(V, i0 + chunk);
+    const uint32_t chunk = (V + B - 1) / B, i0 = min(V, tid * chunk), i1 = min(V, i0 + chunk);
     uint32_t sum = 0;
     for (uint32_t i = i0; i < i1; i += 4) {
       uint32_t u[4];
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(NEMO_BLOCK, 4) void k_build(DevCorpus c) {
       }
     }
     uint32_t tot;
-    uint32_t off = block_exscan(sum, &tot, s_lds);
+    uint32_t off = block_exscan<B>(sum, &tot, s_lds);
     uint32_t *e2 = c.e2 + e0, *po = c.posoff + n0;
     for (uint32_t i = i0; i < i1; i += 4) {
       uint32_t u[4], a[4], n[4], y[4][4];
@@ -856,8 +861,8 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
 
 void launch_build(const DevCorpus &c, hipStream_t s) {
   if (!c.bld_bytes) return;
-  hipFuncSetAttribute((const void *)k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.bld_bytes);
-  hipLaunchKernelGGL(k_build, dim3(c.G), dim3(NEMO_BLOCK), c.bld_bytes, s, c);
+  hipFuncSetAttribute((const void *)k_build<BLD_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.bld_bytes);
+  hipLaunchKernelGGL(k_build<BLD_BLOCK>, dim3(c.G), dim3(BLD_BLOCK), c.bld_bytes, s, c);
 }
 void launch_load(const DevCorpus &c, hipStream_t s) {
   if (!c.G) return;

@@ -18,7 +18,8 @@ import numpy as np
 from .corpus import CChain, CMissing, Corpus
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnemohip.so")
+# NEMO_LIB: a variant build of the same library (A/B kernel experiments: tools/variants.sh)
+LIB_PATH = os.environ.get("NEMO_LIB") or os.path.join(_HERE, "libnemohip.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "nemohip.h")
 _LIB = None
 
