@@ -212,7 +212,9 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define NIL16 0xFFFFu
 #define CF_ROWS 20  // topo positions per thread per compaction round (fast front)
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
+#ifndef CH_K
 #define CH_K 3      // up/down sweeps: parents (children) of a node read together
+#endif
 
 template <int HCAP, int UCAP>
 struct ChainsLDS {

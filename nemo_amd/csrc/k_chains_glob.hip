@@ -37,6 +37,7 @@ namespace nemo {
 struct GlobScratch {
   uint32_t *bm, *bmpre, *crank, *rule;
   uint32_t *ccoff, *pcoff, *child, *par;
+  uint32_t *cend, *pend;        // row ends (rows are laid out by full degree; ha / hb until the pointer jumping)
   int32_t *up, *down;
   uint32_t *nxt, *bp, *po, *fpos, *ub, *uoff, *cnt, *grp;
   uint32_t *ha, *hb, *ta, *tb;  // pointer-jumping buffers (heads, tails)
@@ -85,6 +86,8 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
   s.tb = take(V);
   s.S = take(V);
   s.A = take(V);
+  s.cend = s.ha;
+  s.pend = s.hb;
   s.va = s.ha;
   s.vb = s.hb;
   s.pa = s.ta;
@@ -151,7 +154,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
   constexpr uint32_t M = GS_RING - 1u;
   constexpr uint32_t PT = GS_WN / GB;  // window nodes per thread
   const uint32_t tid = threadIdx.x, lane = lane_id();
-  const uint32_t *off = UP ? S.pcoff : S.ccoff, *col = UP ? S.par : S.child;
+  const uint32_t *off = UP ? S.pcoff : S.ccoff, *oend = UP ? S.pend : S.cend, *col = UP ? S.par : S.child;
   const uint32_t nwin = (n + GS_WN - 1) / GS_WN;
   for (uint32_t wi = 0; wi < nwin; wi++) {
     const uint32_t w0 = UP ? wi * GS_WN : (n > (wi + 1) * GS_WN ? n - (wi + 1) * GS_WN : 0u);
@@ -169,7 +172,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       const uint32_t k = tid + q * GB, i = w0 + k;
       const bool in = k < nw;
       r0[q] = in ? off[i] : 0u;
-      r1[q] = in ? off[i + 1] : 0u;
+      r1[q] = in ? oend[i] : 0u;
       cnt[q] = 0;
     }
     // the PT rows walked together, GS_SB entries of each per step: every load of
@@ -335,7 +338,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
               const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
               for (uint32_t t = GS_KEEP; t < ac; t++) d = max(d, L.rv[(base + L.adj[ao + t - GS_KEEP]) & M] + 1);
               if (fl & GS_SPILL)
-                for (uint32_t j = off[i]; j < off[i + 1]; j++) {
+                for (uint32_t j = off[i]; j < oend[i]; j++) {
                   const uint32_t p = col[j];
                   d = max(d, (p >= base ? L.rv[p & M] : S.up[p]) + 1);
                 }
@@ -368,7 +371,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
                 take(w, L.rv[w & M], L.rc[w & M]);
               }
               if (fl & GS_SPILL)
-                for (uint32_t j = off[i]; j < off[i + 1]; j++) {
+                for (uint32_t j = off[i]; j < oend[i]; j++) {
                   const uint32_t w = col[j];
                   if (w < base + GS_RING) take(w, L.rv[w & M], L.rc[w & M]);
                   else take(w, S.down[w], S.crank[w]);
@@ -496,10 +499,13 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
   // From the graph's own CSR rows, one H* node per thread: a row's children
   // (or parents) in batches of GA_B with their loads in flight together, no
-  // atomics.  (Counting and scattering the whole edge list with cursor
-  // atomics cost a latency-bound pass over all E edges per direction; walking
-  // four nodes' rows in lockstep, one entry per row and step, was slower: the
-  // step count is the longest of the rows.)
+  // atomics.  Each H* row is laid out by the node's full degree (one scan of
+  // the degrees, no counting pass over the neighbours' flags); the H*
+  // entries fill its front and cend / pend mark where they stop.  (Counting
+  // and scattering the whole edge list with cursor atomics cost a
+  // latency-bound pass over all E edges per direction; walking four nodes'
+  // rows in lockstep, one entry per row and step, was slower: the step count
+  // is the longest of the rows.)
 #define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
   auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
     uint32_t k = 0;
@@ -511,24 +517,28 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
 #pragma unroll
       for (int q = 0; q < GA_B; q++) h[q] = j + q < j1 && INH(y[q]);
-      if (out) {
-        uint32_t hy[GA_B];
+      uint32_t hy[GA_B];
 #pragma unroll
-        for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
+      for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
 #pragma unroll
-        for (int q = 0; q < GA_B; q++)
-          if (h[q]) out[k++] = hy[q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < GA_B; q++) k += h[q] ? 1u : 0u;
-      }
+      for (int q = 0; q < GA_B; q++)
+        if (h[q]) out[k++] = hy[q];
     }
     return k;
   };
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t x = hs[i];
-    S.ccoff[i] = hrow(gv.fp, gv.fc, x, nullptr);
-    S.pcoff[i] = hrow(gv.rp, gv.rc, x, nullptr);
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+    uint32_t x[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) x[q] = i0 + q * GB < n ? hs[i0 + q * GB] : 0u;
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB;
+      const uint32_t fa = gv.fp[x[q]], fb = gv.fp[x[q] + 1], ra = gv.rp[x[q]], rb = gv.rp[x[q] + 1];
+      if (i < n) {
+        S.ccoff[i] = fb - fa;
+        S.pcoff[i] = rb - ra;
+      }
+    }
   }
   if (tid == 0) {
     S.ccoff[n] = 0;
@@ -538,9 +548,9 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
   block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
   for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t x = hs[i];
-    hrow(gv.fp, gv.fc, x, S.child + S.ccoff[i]);
-    hrow(gv.rp, gv.rc, x, S.par + S.pcoff[i]);
+    const uint32_t x = hs[i], c0 = S.ccoff[i], p0 = S.pcoff[i];
+    S.cend[i] = c0 + hrow(gv.fp, gv.fc, x, S.child + c0);
+    S.pend[i] = p0 + hrow(gv.rp, gv.rc, x, S.par + p0);
   }
 #undef INH
   __syncthreads();
@@ -610,7 +620,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       const bool in = i < n;
       k[q] = in ? S.up[i] : 0;
       r0[q] = in ? S.pcoff[i] : 0u;
-      r1[q] = in ? S.pcoff[i + 1] : 0u;
+      r1[q] = in ? S.pend[i] : 0u;
     }
 #pragma unroll
     for (int q = 0; q < GU; q++) p0[q] = k[q] > 0 && r1[q] > r0[q] ? S.par[r0[q]] : GNIL;
@@ -673,7 +683,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       const uint32_t cr = act ? S.crank[i] : 0u;
       if (act && bpi == MULTI) {
         uint32_t bpo = GNIL;
-        for (uint32_t q = S.pcoff[i]; q < S.pcoff[i + 1]; q++) {
+        for (uint32_t q = S.pcoff[i]; q < S.pend[i]; q++) {
           const uint32_t p = S.par[q];
           if ((uint32_t)S.up[p] == k - 1 && S.po[p] < bpo) {
             bpi = p;
@@ -706,7 +716,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       uint32_t bpi = S.bp[i];
       if (bpi == MULTI) {
         uint32_t bpo = GNIL;
-        for (uint32_t q = S.pcoff[i]; q < S.pcoff[i + 1]; q++) {
+        for (uint32_t q = S.pcoff[i]; q < S.pend[i]; q++) {
           const uint32_t p = S.par[q];
           if ((uint32_t)S.up[p] == k - 1 && S.po[p] < bpo) {
             bpi = p;

@@ -52,9 +52,10 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 #define BLD_BLOCK 256  // k_build workgroup size (512: 3.91 ms against 3.66 at C3)
 #endif
 #define BLD_OCC(B) ((B) == 256 ? 4 : 6)  // waves per SIMD the register budget is cut for
+#ifndef BLD_KB
 #define BLD_KB 4    // Kahn: children of a node processed per round
+#endif
 
-#define BLD_RS 8    // row entries sorted in registers (longer rows: insertion sort in LDS)
 
 // 5-comparator sorting network for 4 keys
 __device__ __forceinline__ void sort_net4(uint32_t *x) {
@@ -73,6 +74,23 @@ __device__ __forceinline__ void sort_net8(uint32_t *x) {
                             {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
 #pragma unroll
   for (int k = 0; k < 19; k++) {
+    const uint32_t a = x[P[k][0]], b = x[P[k][1]];
+    x[P[k][0]] = min(a, b);
+    x[P[k][1]] = max(a, b);
+  }
+}
+
+// 63-comparator odd-even merge network for 16 keys
+__device__ __forceinline__ void sort_net16(uint32_t *x) {
+  constexpr int P[63][2] = {
+      {0, 1},   {2, 3},   {0, 2},   {1, 3},   {1, 2},   {4, 5},   {6, 7},   {4, 6},   {5, 7},   {5, 6},   {0, 4},
+      {2, 6},   {2, 4},   {1, 5},   {3, 7},   {3, 5},   {1, 2},   {3, 4},   {5, 6},   {8, 9},   {10, 11}, {8, 10},
+      {9, 11},  {9, 10},  {12, 13}, {14, 15}, {12, 14}, {13, 15}, {13, 14}, {8, 12},  {10, 14}, {10, 12}, {9, 13},
+      {11, 15}, {11, 13}, {9, 10},  {11, 12}, {13, 14}, {0, 8},   {4, 12},  {4, 8},   {2, 10},  {6, 14},  {6, 10},
+      {2, 4},   {6, 8},   {10, 12}, {1, 9},   {5, 13},  {5, 9},   {3, 11},  {7, 15},  {7, 11},  {3, 5},   {7, 9},
+      {11, 13}, {1, 2},   {3, 4},   {5, 6},   {7, 8},   {9, 10},  {11, 12}, {13, 14}};
+#pragma unroll
+  for (int k = 0; k < 63; k++) {
     const uint32_t a = x[P[k][0]], b = x[P[k][1]];
     x[P[k][0]] = min(a, b);
     x[P[k][1]] = max(a, b);
@@ -101,7 +119,8 @@ __device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t 
     if (n[q] <= (uint32_t)RS) {
       if (n[q] >= 2) {
         if (RS == 4) sort_net4(x[q]);
-        else sort_net8(x[q]);
+        else if (RS == 8) sort_net8(x[q]);
+        else sort_net16(x[q]);
 #pragma unroll
         for (int i = 0; i < RS; i++)
           if ((uint32_t)i < n[q]) col[a[q] + i] = (uint16_t)x[q][i];
@@ -141,17 +160,6 @@ __device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t 
 __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
   return lds_align(4u * ((v + 31u) / 32u)) + lds_align(2u * (v + 2u)) + lds_align(2u * e) + lds_align(v) +
          lds_align(2u * v);
-}
-
-// wave_append into an LDS u16 queue
-__device__ __forceinline__ void lds_append16(bool pred, uint32_t val, uint16_t *q, uint32_t *tail) {
-  const uint64_t m = __ballot(pred);
-  if (m == 0) return;
-  const int leader = __ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if ((int)lane_id() == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
-  base = __builtin_amdgcn_readlane(base, leader);  // leader is wave-uniform: no LDS round trip
-  if (pred) q[base + mbcnt(m)] = (uint16_t)val;
 }
 
 __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint32_t E) {
@@ -290,8 +298,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
       // goals' forward rows): the 4-key network; else the 8-key one
       if (!__any(n[0] > 4u || n[1] > 4u))
         created += sort_row_pair<4, B>(col, s_rule, E, V, dir, v0, a, n);
-      else
-        created += sort_row_pair<BLD_RS, B>(col, s_rule, E, V, dir, v0, a, n);
+      else if (!__any(n[0] > 8u || n[1] > 8u))
+        created += sort_row_pair<8, B>(col, s_rule, E, V, dir, v0, a, n);
+      else  // a row past eight entries in the wave: the 16-key network (an LDS insertion sort held the wave)
+        created += sort_row_pair<16, B>(col, s_rule, E, V, dir, v0, a, n);
     }
     __syncthreads();
     if (dir == 0) STAMP(6);
@@ -302,11 +312,36 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
   atomicAdd(&s_created, created);
   // Kahn levels over the forward rows still in LDS (ptr[v] = end of row v)
   uint32_t *nlv = c.nlv + n0;
-  for (uint32_t base = 0; base < V; base += B) {
-    const uint32_t v = base + tid;
-    const bool src = v < V && cnt8[v] == 0u;
-    lds_append16(src, v, q16, &s_tail);
-    if (src) nlv[v] = 0;
+  // the sources in node order: each thread counts those of a contiguous run
+  // of counter words (all its reads in flight together), one block scan
+  // places them (no per-wave append chain)
+  {
+    constexpr int SW = 4;  // counter words (4 nodes each) per thread per round
+    const uint32_t nw4 = (V + 3) / 4;
+    uint32_t o = 0;
+    for (uint32_t base = 0; base < nw4; base += SW * B) {
+      const uint32_t w0 = base + tid * SW;
+      uint32_t x[SW], n = 0;
+#pragma unroll
+      for (int k = 0; k < SW; k++) x[k] = cnt32[min(w0 + k, nw4 - 1u)];
+#pragma unroll
+      for (int k = 0; k < SW; k++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) n += w0 + k < nw4 && 4 * (w0 + k) + b < V && ((x[k] >> (8 * b)) & 0xFFu) == 0u;
+      uint32_t tot;
+      uint32_t i = o + block_exscan<B>(n, &tot, s_lds);
+#pragma unroll
+      for (int k = 0; k < SW; k++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t v = 4 * (w0 + k) + b;
+          if (w0 + k < nw4 && v < V && ((x[k] >> (8 * b)) & 0xFFu) == 0u) q16[i++] = (uint16_t)v;
+        }
+      o += tot;
+    }
+    if (tid == 0) s_tail = o;
+    for (uint32_t v = tid; v < V; v += B)  // coalesced
+      if (cnt8[v] == 0u) nlv[v] = 0;
   }
   __syncthreads();
   STAMP(14);

@@ -2,7 +2,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-T=r03m
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gputest.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --no-cpu-baseline --e2e-runs 0 --json-out gpurun_out/${T}_bench.json > gpurun_out/${T}_bench.log 2>&1 || exit $?
-NEMO_LIB=var/b256/libnemohip.so timeout -k 10 300 python bench.py --no-cpu-baseline --e2e-runs 0 --json-out gpurun_out/${T}_b256_bench.json > gpurun_out/${T}_b256_bench.log 2>&1 || exit $?
+T=r03s
+for v in main odd main2 odd2; do
+  case $v in main*) L=;; *) L=var/${v%2}/libnemohip.so;; esac
+  NEMO_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --e2e-runs 0 --json-out gpurun_out/${T}_${v}_bench.json > gpurun_out/${T}_${v}_bench.log 2>&1 || exit $?
+done
