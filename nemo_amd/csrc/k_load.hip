@@ -777,8 +777,13 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
 #define TD_B 256
 #define TD_Q 2048u
 #define TD_EPT 4  // frontier edges per thread per round
+// The LDS frontier holds each node's row (first edge, degree), not the node:
+// a child's row bounds are loaded together with its in-degree atomic (for
+// every child, ready or not), so a level starts from LDS instead of waiting on
+// an HBM round trip for its rows.  Frontier entries past TD_Q are read back
+// from topo[] and their rows loaded.
 __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
-  __shared__ uint32_t s_q[2][TD_Q];
+  __shared__ uint2 s_q[2][TD_Q];
   // appends of level L go to s_n[(L + 1) % 3]: read after the level's barrier,
   // reset during level L + 2, so one barrier per level orders everything
   __shared__ uint32_t s_n[3];
@@ -809,7 +814,10 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
       const uint32_t i = base + mbcnt(m);
       topo[i] = v;
       nlv[v] = 0;
-      if (i < TD_Q) s_q[0][i] = v;
+      if (i < TD_Q) {
+        const uint32_t a = fp[v];
+        s_q[0][i] = make_uint2(a, fp[v + 1] - a);
+      }
     }
   }
   __syncthreads();
@@ -817,7 +825,7 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   while (lo < hi) {
     const uint32_t n = hi - lo, kn = k3 == 2 ? 0u : k3 + 1u;  // this level's append counter
     if (tid == 0) s_n[kn == 2 ? 0u : kn + 1u] = 0;            // = (nl + 3) % 3: free since level nl - 1
-    uint32_t *qn = s_q[cur ^ 1];
+    uint2 *qn = s_q[cur ^ 1];
     // edge-parallel: a chunk of TD_B frontier nodes publishes its rows (start,
     // exclusive degree offset); every thread then takes edges of the chunk, so
     // each lane has ~one child load and one counter atomic in flight instead of
@@ -826,9 +834,15 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
       const uint32_t i = b + tid, nc = min((uint32_t)TD_B, n - b);
       uint32_t j0 = 0, d = 0;
       if (i < n) {
-        const uint32_t u = i < TD_Q ? s_q[cur][i] : topo[lo + i];
-        j0 = fp[u];
-        d = fp[u + 1] - j0;
+        if (i < TD_Q) {
+          const uint2 r = s_q[cur][i];
+          j0 = r.x;
+          d = r.y;
+        } else {
+          const uint32_t u = topo[lo + i];
+          j0 = fp[u];
+          d = fp[u + 1] - j0;
+        }
       }
       uint32_t tot;
       const uint32_t eo = block_exscan<TD_B>(d, &tot, s_red);
@@ -836,7 +850,7 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
       s_j0[tid] = j0;
       __syncthreads();
       for (uint32_t e0 = 0; e0 < tot; e0 += TD_B * TD_EPT) {
-        uint32_t ch[TD_EPT];
+        uint32_t ch[TD_EPT], ra[TD_EPT], rb[TD_EPT];
         bool rdy[TD_EPT];
 #pragma unroll
         for (int k = 0; k < TD_EPT; k++) {
@@ -855,7 +869,11 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
         uint32_t r = 0;
 #pragma unroll
         for (int k = 0; k < TD_EPT; k++) {
-          const uint32_t old = ch[k] != NEMO_NONE ? atomicSub(&cnt[ch[k]], 1u) : 0u;
+          const bool ok = ch[k] != NEMO_NONE;
+          const uint32_t cw = ok ? ch[k] : 0u;
+          const uint32_t old = ok ? atomicSub(&cnt[cw], 1u) : 0u;
+          ra[k] = fp[cw];  // the child's row, in flight with its atomic
+          rb[k] = fp[cw + 1];
           rdy[k] = old == 1u;
           r += rdy[k] ? 1u : 0u;
         }
@@ -870,7 +888,7 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
             if (!rdy[k]) continue;
             topo[hi + at] = ch[k];
             nlv[ch[k]] = nl + 1;
-            if (at < TD_Q) qn[at] = ch[k];
+            if (at < TD_Q) qn[at] = make_uint2(ra[k], rb[k] - ra[k]);
             at++;
           }
         }
@@ -977,8 +995,30 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
 // by LDS cursors and each row sorted there, then written out coalesced.  A
 // bucket of more than CB_LDS_E edges (a hub-heavy one) sorts in HBM instead.
 #define CB_LDS_E 14336u
-#define CB_WSORT_MIN 20u
-__global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
+#define CB_CB 4  // a bucket's edges per thread per batch (loads in flight together)
+#define CB_WSORT_MIN 17u
+
+// a row [a, a + n) of u32 entries (n <= RS) sorted in registers, its reads
+// in flight together; returns a bit per duplicate entry (x[i-1] == x[i])
+template <int RS>
+__device__ __forceinline__ uint32_t cb_sort_row(uint32_t *rows, uint32_t a, uint32_t n, uint32_t (&x)[16]) {
+  uint32_t dup = 0;
+#pragma unroll
+  for (int i = 0; i < RS; i++) x[i] = (uint32_t)i < n ? rows[a + i] : 0xFFFFFFFFu;
+  if (n < 2) return 0;
+  if (RS == 4) sort_net4(x);
+  else if (RS == 8) sort_net8(x);
+  else sort_net16(x);
+#pragma unroll
+  for (int i = 0; i < RS; i++)
+    if ((uint32_t)i < n) rows[a + i] = x[i];
+#pragma unroll
+  for (int i = 1; i < RS; i++) dup |= ((uint32_t)i < n && x[i - 1] == x[i] ? 1u : 0u) << i;
+  return dup;
+}
+
+// (<= 64 VGPRs: two 1024-thread workgroups per CU, as the LDS allows)
+__global__ __launch_bounds__(CB_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_cb_bucket(DevCorpus c, int dir) {
   __shared__ uint32_t cnt[CB_NB + 1];
   __shared__ uint32_t s_long[CB_NB], s_nlong;
   __shared__ uint32_t rows[CB_LDS_E];
@@ -988,41 +1028,115 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   const uint32_t nbk = (V + CB_NB - 1) / CB_NB, nck = (E + CB_CHUNK - 1) / CB_CHUNK;
-  const uint32_t bk = blockIdx.x;
+  const uint32_t bk = blockIdx.x, tid = threadIdx.x;
   if (bk >= nbk || !csrb_take(c, g, V, E) || c.err[g]) return;
   const uint32_t *off = c.cb_hist + c.cb_hoff[b];
   const uint32_t lo = off[(uint64_t)bk * nck], hi = bk + 1 < nbk ? off[(uint64_t)(bk + 1) * nck] : E;
   const uint32_t v0 = bk * CB_NB, nv = min(V, v0 + CB_NB) - v0, ne = hi - lo;
   const uint32_t *ek = c.cb_key + e0 + lo, *ev = c.cb_val + e0 + lo;
   uint32_t *ptr = (dir ? c.rp : c.fp) + n0 + g, *col = (dir ? c.rc : c.fc) + e0 + lo;
+  const uint32_t *word = c.word + n0;
   const bool lds = ne <= CB_LDS_E;
   uint32_t *dst = lds ? rows : col;  // where the rows are assembled and sorted
-  for (uint32_t i = threadIdx.x; i <= nv; i += CB_BLOCK) cnt[i] = 0;
-  if (threadIdx.x == 0) s_cr = 0;
+  // degrees; forward rows also check each edge's goal/rule kinds
+  // (pre-post-prov.go:150-210 creates a relationship only between a goal and
+  // a rule): the node words of both ends gathered with the batch's loads in
+  // flight together, instead of a dependent load per row entry after the sort
+  uint32_t created = 0;
+  for (uint32_t i = tid; i <= nv; i += CB_BLOCK) cnt[i] = 0;
+  if (tid == 0) s_cr = 0;
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) atomicAdd(&cnt[ek[j] - v0], 1u);
-  __syncthreads();
-  block_scan_inplace<CB_BLOCK>(cnt, nv + 1, s_lds);
-  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) ptr[v0 + i] = lo + cnt[i];
-  if (bk + 1 == nbk && threadIdx.x == 0) ptr[V] = E;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) dst[atomicAdd(&cnt[ek[j] - v0], 1u)] = ev[j];
-  __threadfence_block();
-  __syncthreads();  // cnt[i] = end of row i (local)
-  // rows sorted (a merged duplicate DUETO edge is adjacent): short rows by
-  // their thread, rows of CB_WSORT_MIN..64 entries by a whole wave (bitonic
-  // network over shuffles) -- one thread heap-sorting a 60-entry row in LDS
-  // held the workgroup for most of its time
-  if (threadIdx.x == 0) s_nlong = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
-    const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i], n = z - a;
-    const bool wide = n >= CB_WSORT_MIN && n <= 64u;
-    wave_append(wide, i, s_long, &s_nlong);
-    if (!wide) sort_row(dst + a, n);
+  for (uint32_t j0 = tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
+    uint32_t k[CB_CB], v[CB_CB];
+#pragma unroll
+    for (int q = 0; q < CB_CB; q++) {
+      const uint32_t j = j0 + q * CB_BLOCK;
+      k[q] = j < ne ? ek[j] : v0;
+      v[q] = j < ne && dir == 0 ? ev[j] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < CB_CB; q++)
+      if (j0 + q * CB_BLOCK < ne) atomicAdd(&cnt[k[q] - v0], 1u);
+    if (dir == 0) {
+      uint32_t wk[CB_CB], wv[CB_CB];
+#pragma unroll
+      for (int q = 0; q < CB_CB; q++) {
+        wk[q] = word[k[q]];
+        wv[q] = word[v[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < CB_CB; q++) created += j0 + q * CB_BLOCK < ne && is_rule(wk[q]) != is_rule(wv[q]) ? 1u : 0u;
+    }
   }
   __syncthreads();
-  for (uint32_t q = threadIdx.x >> 6; q < s_nlong; q += CB_BLOCK / 64) {
+  block_scan_inplace<CB_BLOCK>(cnt, nv + 1, s_lds);
+  for (uint32_t i = tid; i < nv; i += CB_BLOCK) ptr[v0 + i] = lo + cnt[i];
+  if (bk + 1 == nbk && tid == 0) ptr[V] = E;
+  __syncthreads();
+  for (uint32_t j0 = tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
+    uint32_t k[CB_CB], v[CB_CB];
+#pragma unroll
+    for (int q = 0; q < CB_CB; q++) {
+      const uint32_t j = j0 + q * CB_BLOCK;
+      k[q] = j < ne ? ek[j] : v0;
+      v[q] = j < ne ? ev[j] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < CB_CB; q++)
+      if (j0 + q * CB_BLOCK < ne) dst[atomicAdd(&cnt[k[q] - v0], 1u)] = v[q];
+  }
+  __threadfence_block();
+  __syncthreads();  // cnt[i] = end of row i (local)
+  // rows sorted (a merged duplicate DUETO edge is adjacent).  In LDS: rows of
+  // up to 16 entries in registers (4-, 8- or 16-key networks, two rows per
+  // thread), rows of CB_WSORT_MIN..64 entries by a whole wave (bitonic network
+  // over shuffles), longer ones by their thread; in HBM: by their thread (one
+  // thread heap-sorting a 60-entry row in LDS held the workgroup for most of
+  // its time).  A duplicate's relationship is created once: forward rows take
+  // it back out of the edge-parallel count above.
+  if (tid == 0) s_nlong = 0;
+  __syncthreads();
+  if (lds) {
+    static_assert(CB_NB == 2 * CB_BLOCK, "two rows per thread");
+    uint32_t ra[2], rn[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t i = tid + q * CB_BLOCK;
+      ra[q] = i < nv && i ? cnt[i - 1] : 0u;
+      rn[q] = i < nv ? cnt[i] - ra[q] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t i = tid + q * CB_BLOCK;
+      const bool wide = rn[q] >= CB_WSORT_MIN && rn[q] <= 64u;
+      wave_append(wide, i, s_long, &s_nlong);
+      if (rn[q] > 64u) sort_row(dst + ra[q], rn[q]);
+    }
+    // one row at a time (register budget); the network by the longest such row in the wave
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t sn = rn[q] <= 16u ? rn[q] : 0u;
+      uint32_t x[16], dup;
+      if (!__any(sn > 4u)) dup = cb_sort_row<4>(dst, ra[q], sn, x);
+      else if (!__any(sn > 8u)) dup = cb_sort_row<8>(dst, ra[q], sn, x);
+      else dup = cb_sort_row<16>(dst, ra[q], sn, x);
+      if (dir == 0 && dup) {  // rare
+        const bool rv = is_rule(word[v0 + tid + q * CB_BLOCK]);
+#pragma unroll
+        for (int i = 1; i < 16; i++)
+          if ((dup >> i) & 1u) created -= rv != is_rule(word[x[i]]) ? 1u : 0u;
+      }
+    }
+  } else {
+    for (uint32_t i = tid; i < nv; i += CB_BLOCK) {
+      const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i], n = z - a;
+      const bool wide = n >= CB_WSORT_MIN && n <= 64u;
+      wave_append(wide, i, s_long, &s_nlong);
+      if (!wide) sort_row(dst + a, n);
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = tid >> 6; q < s_nlong; q += CB_BLOCK / 64) {
     const uint32_t i = s_long[q], a = i ? cnt[i - 1] : 0u, n = cnt[i] - a, l = lane_id();
     uint32_t x = l < n ? dst[a + l] : 0xFFFFFFFFu;
 #pragma unroll
@@ -1037,25 +1151,26 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_bucket(DevCorpus c, int dir) {
   }
   __threadfence_block();
   __syncthreads();
-  // forward rows count relationships created (pre-post-prov.go:150-210)
-  const uint32_t *word = c.word + n0;
-  uint32_t created = 0;
-  for (uint32_t i = threadIdx.x; i < nv; i += CB_BLOCK) {
-    const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i];
-    if (dir) continue;
-    const bool rv = is_rule(word[v0 + i]);
-    for (uint32_t j = a; j < z; j++) {
-      const uint32_t t = dst[j];
-      if (!(j > a && dst[j - 1] == t) && rv != is_rule(word[t])) created++;
+  // forward rows: duplicates in the rows the register networks did not sort
+  // (wide and long rows, and every row of a bucket sorted in HBM) are taken
+  // back out of the edge-parallel count
+  if (dir == 0) {
+    for (uint32_t i = tid; i < nv; i += CB_BLOCK) {
+      const uint32_t a = i ? cnt[i - 1] : 0u, z = cnt[i];
+      if (lds && z - a <= 16u) continue;
+      for (uint32_t j = a + 1; j < z; j++) {
+        const uint32_t t = dst[j];
+        if (dst[j - 1] == t && is_rule(word[v0 + i]) != is_rule(word[t])) created--;
+      }
     }
   }
   __syncthreads();
   if (lds)
-    for (uint32_t j = threadIdx.x; j < ne; j += CB_BLOCK) col[j] = rows[j];
+    for (uint32_t j = tid; j < ne; j += CB_BLOCK) col[j] = rows[j];
   for (int d = 32; d >= 1; d >>= 1) created += __shfl_xor(created, d);
   if (lane_id() == 0 && created) atomicAdd(&s_cr, created);
   __syncthreads();
-  if (threadIdx.x == 0 && s_cr) atomicAdd(&c.created[g], s_cr);
+  if (tid == 0 && s_cr) atomicAdd(&c.created[g], s_cr);
 }
 __global__ __launch_bounds__(CSRB_BLOCK) void k_cb_zero(DevCorpus c) {
   const uint32_t b = blockIdx.x * CSRB_BLOCK + threadIdx.x;

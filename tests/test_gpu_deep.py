@@ -96,3 +96,52 @@ def test_cycle_in_big_graph_refused(eng):
     with pytest.raises(E.NemoError) as ei:
         eng.load(corpus)
     assert ei.value.code == 4
+
+
+def _inject(corpus, g, extra):
+    """Append graph-local edges `extra` [(src, dst)] to graph g (behind the host layer's back)."""
+    import numpy as np
+    eo = corpus.edge_off.astype(np.int64)
+    a, b = int(eo[g]), int(eo[g + 1])
+    xs = np.array([e[0] for e in extra], np.uint32)
+    ys = np.array([e[1] for e in extra], np.uint32)
+    corpus.edge_src = np.concatenate([corpus.edge_src[:b], xs, corpus.edge_src[b:]])
+    corpus.edge_dst = np.concatenate([corpus.edge_dst[:b], ys, corpus.edge_dst[b:]])
+    eo[g + 1:] += len(extra)
+    corpus.edge_off = eo.astype(np.uint64)
+
+
+def _created(corpus, g):
+    """pre-post-prov.go:150-210's relationships-created count: distinct edges joining a goal and a rule."""
+    import numpy as np
+    from nemo_amd.corpus import NODE_RULE
+    eo, no = corpus.edge_off.astype(np.int64), corpus.node_off.astype(np.int64)
+    rule = (corpus.node_word[no[g]:no[g + 1]] & NODE_RULE) != 0
+    pairs = set(zip(corpus.edge_src[eo[g]:eo[g + 1]].tolist(), corpus.edge_dst[eo[g]:eo[g + 1]].tolist()))
+    return sum(1 for x, y in pairs if rule[x] != rule[y]), int(eo[g + 1] - eo[g])
+
+
+@pytest.mark.parametrize("case", ["short_rows", "wide_row", "long_row", "hbm_bucket"])
+def test_load_error_counts_in_big_graph(eng, case):
+    """The bucketed CSR build's relationships-created count (edge-parallel goal/rule check, duplicates
+    taken back out per row) against a direct count, in each of its row-sort paths: rows of <= 16
+    entries (register networks), 17..64 (wave sort), > 64 (thread sort), and a bucket past the LDS
+    capacity (rows assembled and sorted in HBM)."""
+    hub = {"short_rows": 0, "wide_row": 30, "long_row": 300, "hbm_bucket": 15000}[case]
+    graphs = [(0, "success", wide_prov("pre", 3000, 1), wide_prov("post", 3000, 2, hub=hub))]
+    corpus = corpus_from_graphs(graphs)
+    assert corpus.graph_size(1) >= 8192
+    eo = corpus.edge_off.astype(int)
+    src, dst = corpus.edge_src[eo[1]:eo[2]], corpus.edge_dst[eo[1]:eo[2]]
+    # duplicates of a few edges (short rows, and the last edge of a0's row: the hub's), plus a goal -> goal edge
+    extra = [(int(src[i]), int(dst[i])) for i in (0, 5, 17, 17)]
+    a0 = [i for i in range(len(src)) if int(src[i]) == int(src[1])]  # goal a0's forward row (the hub)
+    extra += [(int(src[a0[-1]]), int(dst[a0[-1]]))] * 2
+    extra.append((int(src[0]), int(src[1])))
+    _inject(corpus, 1, extra)
+    want, E_ = _created(corpus, 1)
+    assert want != E_
+    with pytest.raises(E.NemoError) as ei:
+        eng.load(corpus)
+    assert f"inserted number of edges ({want}) does not equal number of antecedent provenance edges ({E_})" \
+        in str(ei.value)
