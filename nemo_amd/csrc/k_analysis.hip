@@ -431,7 +431,14 @@ __global__ __launch_bounds__(PG_BLOCK) void k_pg_c(DevCorpus c) {
 // (node word, flags, row bounds, own SB byte) are loaded while chunk k reads
 // its parents' SB bytes, so a chunk's critical path is the parent ids (PG_BATCH
 // at a time) and their flag / SB bytes, not the four dependent loads before.
-#define PG_BATCH 4
+#define PG_BATCH 8  // parents of a node staged ahead (more: read in the chunk's own pass)
+// One wave per graph walks the Kahn order in 64-position chunks.  A chunk's
+// reads that do not depend on the sweep are staged ahead in a five-stage
+// pipeline: chunk k+4's node ids, chunk k+3's static node data (word, flags,
+// parent row, own SB byte), chunk k+2's first parents, chunk k+1's parents'
+// flags; chunk k itself then waits on one round trip, its parents' SB bytes
+// (written by earlier chunks of this wave: the level fence orders them).
+// Every stage's loads of an iteration are issued together, chunk k's first.
 __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
   const uint32_t *lst = proto_list(c);
   const uint32_t ngr = lst[0];
@@ -448,20 +455,28 @@ __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
     const uint32_t *clf = c.cl_first + gv.n0, *cln = c.cl_next + gv.n0;
     // chunk cursors (level, start, end): levels are contiguous, so the next
     // level starts where this one ends and only its end is loaded
-    auto adv = [&](uint32_t &l, uint32_t &s, uint32_t &e) {
-      if (s + PG_SWEEP < e) {
-        s += PG_SWEEP;
+    struct Cur {
+      uint32_t l, s, e;
+    };
+    auto adv = [&](Cur q) {
+      if (q.s + PG_SWEEP < q.e) {
+        q.s += PG_SWEEP;
       } else {
-        l++;
-        s = e;
-        e = l < nlev ? gv.lvl[l + 1] : e;
+        q.l++;
+        q.s = q.e;
+        q.e = q.l < nlev ? gv.lvl[q.l + 1] : q.e;
       }
+      return q;
     };
-    struct Stat {
+    struct It {
       uint32_t x, w, fx, j0, j1, sbx;
+      uint32_t p[PG_BATCH], fp[PG_BATCH];
     };
-    auto stat = [&](uint32_t x) {
-      Stat t{x, 0, 0, 0, 0, 0};
+    auto ld_x = [&](const Cur &q) { return q.s + lane < q.e ? topo[q.s + lane] : NEMO_NONE; };
+    auto ld_static = [&](uint32_t x) {
+      It t;
+      t.x = x;
+      t.w = t.fx = t.j0 = t.j1 = t.sbx = 0;
       if (x != NEMO_NONE) {
         t.w = gv.word[x];
         t.fx = f[x];
@@ -471,20 +486,34 @@ __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
       }
       return t;
     };
-    uint32_t l0 = 0, s0 = gv.lvl[0], e0 = gv.lvl[1];
-    uint32_t l1 = l0, s1 = s0, e1 = e0;
-    adv(l1, s1, e1);
-    uint32_t l2 = l1, s2 = s1, e2 = e1;
-    adv(l2, s2, e2);
-    Stat cur = stat(s0 + lane < e0 ? topo[s0 + lane] : NEMO_NONE);
-    uint32_t x1 = s1 + lane < e1 ? topo[s1 + lane] : NEMO_NONE;
-    while (l0 < nlev) {
-      // prefetch: chunk k+2's nodes, chunk k+1's static data
-      const uint32_t x2 = s2 + lane < e2 ? topo[s2 + lane] : NEMO_NONE;
-      const Stat nxt = stat(x1);
+    auto ld_par = [&](It &t) {
+#pragma unroll
+      for (int q = 0; q < PG_BATCH; q++) t.p[q] = t.j0 + q < t.j1 ? gv.rc[t.j0 + q] : NEMO_NONE;
+    };
+    auto ld_pflag = [&](It &t) {
+#pragma unroll
+      for (int q = 0; q < PG_BATCH; q++) t.fp[q] = t.p[q] != NEMO_NONE ? f[t.p[q]] : 0u;
+    };
+    Cur c0{0, gv.lvl[0], gv.lvl[1]};
+    Cur c1 = adv(c0), c2 = adv(c1), c3 = adv(c2), c4 = adv(c3);
+    // prologue: chunk k through stage 3, k+1 through 2, k+2 through 1, k+3's ids
+    It A = ld_static(ld_x(c0)), B = ld_static(ld_x(c1)), C = ld_static(ld_x(c2));
+    uint32_t xD = ld_x(c3);
+    ld_par(A);
+    ld_par(B);
+    ld_pflag(A);
+    while (c0.l < nlev) {
+      // chunk k's parents' SB bytes first, then every prefetch stage
+      uint32_t bp[PG_BATCH];
+#pragma unroll
+      for (int q = 0; q < PG_BATCH; q++) bp[q] = A.p[q] != NEMO_NONE ? sb[A.p[q]] : 0u;
+      const uint32_t xE = ld_x(c4);
+      It D = ld_static(xD);
+      ld_par(C);
+      ld_pflag(B);
       // chunk k
-      const uint32_t x = cur.x, fx = cur.fx;
-      const bool rule = is_rule(cur.w);
+      const uint32_t x = A.x, fx = A.fx;
+      const bool rule = is_rule(A.w);
       const bool live = x != NEMO_NONE && (rule ? ((fx & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT ||
                                                     (fx & NEMO_F_HEAD))
                                                  : (fx & NEMO_F_DELETED) == 0);
@@ -493,37 +522,35 @@ __global__ __launch_bounds__(PG_SWEEP) void k_pg_sweep(DevCorpus c) {
         // regular rule parent, or a tail parent one of whose chains has an RCH head
         const uint32_t want = rule ? (SB_G2 | SB_RCH) : SB_RCH;
         bool rch = false;
-        const uint32_t j1 = cur.j1;
-        for (uint32_t j = cur.j0; j < j1 && !rch; j += PG_BATCH) {
-          uint32_t p[PG_BATCH], fp_[PG_BATCH], bp[PG_BATCH];
-#pragma unroll
-          for (int q = 0; q < PG_BATCH; q++) p[q] = j + q < j1 ? gv.rc[j + q] : NEMO_NONE;
-#pragma unroll
-          for (int q = 0; q < PG_BATCH; q++) {
-            fp_[q] = p[q] != NEMO_NONE ? f[p[q]] : 0u;
-            bp[q] = p[q] != NEMO_NONE ? sb[p[q]] : 0u;
+        auto parent = [&](uint32_t pq, uint32_t fpq, uint32_t bpq) {
+          if (rule) {
+            rch |= !(fpq & NEMO_F_DELETED) && (bpq & want);
+          } else if ((fpq & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT) {
+            rch |= (bpq & SB_RCH) != 0;
+          } else if (fpq & NEMO_F_TAIL) {
+            uint32_t hops = 0;
+            for (uint32_t k = clf[pq]; k < nch && hops++ < nch && !rch; k = cln[k]) rch = (sb[ch[5 * k]] & SB_RCH) != 0;
           }
+        };
 #pragma unroll
-          for (int q = 0; q < PG_BATCH; q++) {
-            if (p[q] == NEMO_NONE) continue;
-            if (rule) {
-              rch |= !(fp_[q] & NEMO_F_DELETED) && (bp[q] & want);
-            } else if ((fp_[q] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT) {
-              rch |= (bp[q] & SB_RCH) != 0;
-            } else if (fp_[q] & NEMO_F_TAIL) {
-              uint32_t hops = 0;
-              for (uint32_t k = clf[p[q]]; k < nch && hops++ < nch && !rch; k = cln[k]) rch = (sb[ch[5 * k]] & SB_RCH) != 0;
-            }
-          }
+        for (int q = 0; q < PG_BATCH; q++)
+          if (A.p[q] != NEMO_NONE && !rch) parent(A.p[q], A.fp[q], bp[q]);
+        for (uint32_t j = A.j0 + PG_BATCH; j < A.j1 && !rch; j++) {  // rows past the staged parents
+          const uint32_t pq = gv.rc[j];
+          parent(pq, f[pq], sb[pq]);
         }
-        if (rch) sb[x] = (uint8_t)(cur.sbx | SB_RCH);  // only x sets its own RCH bit
+        if (rch) sb[x] = (uint8_t)(A.sbx | SB_RCH);  // only x sets its own RCH bit
       }
-      if (l1 != l0) __syncthreads();  // the next chunk starts a level: this level's bits are final
-      cur = nxt;
-      x1 = x2;
-      l0 = l1, s0 = s1, e0 = e1;
-      l1 = l2, s1 = s2, e1 = e2;
-      adv(l2, s2, e2);
+      if (c1.l != c0.l) __syncthreads();  // the next chunk starts a level: this level's bits are final
+      A = B;
+      B = C;
+      C = D;
+      xD = xE;
+      c0 = c1;
+      c1 = c2;
+      c2 = c3;
+      c3 = c4;
+      c4 = adv(c4);
     }
   }
 }
