@@ -5,9 +5,10 @@
 // with every per-node array in a global scratch region, so it scales to
 // chain subgraphs of hundreds of thousands of nodes and thousands of levels
 // (1M-node graphs, EOT ~ 2000).  One 256- or 512-thread
-// workgroup per graph; long walks (chain heads and tails, ancestor sums) use
-// pointer jumping, the final order a stable counting sort of the
-// preorder-ordered chains by length.  The graphs are the
+// workgroup per graph; the chain tails come out of the down sweep, the chain
+// heads and ancestor sums out of one top-down pass over the up-levels, the
+// final order a stable counting sort of the preorder-ordered chains by
+// length.  The graphs are the
 // ones the host gave a scratch region (DevCorpus::gs_off, V >= glob_min_v);
 // k_chains and k_chains_big skip them.
 #include <algorithm>
@@ -105,6 +106,8 @@ struct GSweepLds {
   uint32_t rc[GS_RING];  // down: crank by ring slot
   int32_t init[GS_WN];   // up: value over the parents outside the ring; down: best such child's down
   uint32_t ibc[GS_WN], ibr[GS_WN];  // down: that child and its crank; ibc then nxt
+  uint32_t rt[GS_RING];  // down: tail (end of the nxt chain) by ring slot
+  uint32_t ibt[GS_WN];   // down: the staged far best child's tail
   uint32_t lev[GS_WN];   // Kahn level
   uint64_t lk[GS_WN][2]; // first GS_KEEP in-ring links (u16 offsets from the ring base)
   uint16_t aoff[GS_WN], acnt[GS_WN];  // GS_MORE: link t in [GS_KEEP, acnt) at adj[aoff + t - GS_KEEP]
@@ -179,7 +182,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
     // a step (columns, then the far values) in flight at once
     uint32_t rl[PT], lv[PT], cr[PT];
     int32_t dd[PT];
-    uint32_t bc[PT], br[PT];
+    uint32_t bc[PT], br[PT], bt[PT];
 #pragma unroll
     for (int q = 0; q < PT; q++) {
       const uint32_t k = tid + q * GB, i = w0 + k;
@@ -188,7 +191,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       lv[q] = in ? nlv[hs[i]] : 0u;
       cr[q] = in && !UP ? S.crank[i] : 0u;
       dd[q] = UP ? (rl[q] ? 0 : -1) : -1;
-      bc[q] = br[q] = GNIL;
+      bc[q] = br[q] = bt[q] = GNIL;
     }
     bool more = false;
 #pragma unroll
@@ -201,7 +204,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 #pragma unroll
         for (int h = 0; h < GS_SB; h++) p[q][h] = r0[q] + t + h < r1[q] ? col[r0[q] + t + h] : GNIL;
       int32_t fv[PT][GS_SB];
-      uint32_t fr[PT][GS_SB];
+      uint32_t fr[PT][GS_SB], ft[PT][GS_SB];
 #pragma unroll
       for (int q = 0; q < PT; q++)
 #pragma unroll
@@ -209,6 +212,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
           far[q][h] = p[q][h] != GNIL && (UP ? p[q][h] < base : p[q][h] >= base + GS_RING);
           fv[q][h] = far[q][h] ? (UP ? S.up[p[q][h]] : S.down[p[q][h]]) : 0;
           fr[q][h] = far[q][h] && !UP ? S.crank[p[q][h]] : 0u;
+          ft[q][h] = far[q][h] && !UP ? S.ta[p[q][h]] : 0u;
         }
       more = false;
 #pragma unroll
@@ -225,6 +229,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
             dd[q] = fv[q][h];
             bc[q] = p[q][h];
             br[q] = fr[q][h];
+            bt[q] = ft[q][h];
           }
         }
         more |= r0[q] + t + GS_SB < r1[q];
@@ -240,6 +245,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       if (!UP) {
         L.ibc[k] = bc[q];
         L.ibr[k] = br[q];
+        L.ibt[k] = bt[q];
         L.rc[i & M] = cr[q];
       }
     }
@@ -292,7 +298,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
     if (tid < 64) {
       uint32_t k = 0;
       auto fetch = [&](uint32_t k0, uint32_t &lv, uint64_t (&lk)[2], int32_t &ini, uint32_t &bc, uint32_t &br,
-                       uint32_t &fl) {
+                       uint32_t &bt, uint32_t &fl) {
         const uint32_t q = k0 + lane, kk = UP ? q : nw - 1u - q;
         const bool in = q < nw;
         const uint32_t kc = in ? kk : 0u;
@@ -304,22 +310,23 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
         if (!UP) {
           bc = L.ibc[kc];
           br = L.ibr[kc];
+          bt = L.ibt[kc];
         }
       };
-      uint32_t lv, bc = 0, br = 0, fl;
+      uint32_t lv, bc = 0, br = 0, bt = 0, fl;
       uint64_t lk[2];
       int32_t ini;
-      fetch(0, lv, lk, ini, bc, br, fl);
+      fetch(0, lv, lk, ini, bc, br, bt, fl);
       while (k < nw) {
         const uint32_t q = k + lane, kk = UP ? q : nw - 1u - q;
         const uint32_t l = __builtin_amdgcn_readfirstlane(lv);
         const bool mine = q < nw && lv == l;
         const uint64_t m = __ballot(mine);  // contiguous from lane 0: nodes are sorted by level
         const uint32_t kn = k + (uint32_t)__popcll(m);
-        uint32_t lv2, bc2 = 0, br2 = 0, fl2;
+        uint32_t lv2, bc2 = 0, br2 = 0, bt2 = 0, fl2;
         uint64_t lk2[2];
         int32_t ini2;
-        fetch(kn, lv2, lk2, ini2, bc2, br2, fl2);
+        fetch(kn, lv2, lk2, ini2, bc2, br2, bt2, fl2);
         if (mine) {
           const uint32_t i = w0 + kk;
           uint32_t u[GS_KEEP];
@@ -346,39 +353,42 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
             L.rv[i & M] = d;
           } else {
             int32_t best = ini;
-            auto take = [&](uint32_t w, int32_t dw, uint32_t rw) {
+            auto take = [&](uint32_t w, int32_t dw, uint32_t rw, uint32_t tw) {
               if (dw > best || (dw == best && rw < br)) {
                 best = dw;
                 bc = w;
                 br = rw;
+                bt = tw;
               }
             };
             int32_t dv[GS_KEEP];
-            uint32_t rr[GS_KEEP];
+            uint32_t rr[GS_KEEP], tt[GS_KEEP];
 #pragma unroll
             for (int h = 0; h < GS_KEEP; h++) {
               dv[h] = L.rv[(base + u[h]) & M];
               rr[h] = L.rc[(base + u[h]) & M];
+              tt[h] = L.rt[(base + u[h]) & M];
             }
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int h = 0; h < GS_KEEP; h++)
-              if (u[h] != GS_NOLINK) take(base + u[h], dv[h], rr[h]);
+              if (u[h] != GS_NOLINK) take(base + u[h], dv[h], rr[h], tt[h]);
             if (fl & GS_MORE) {
               const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
               for (uint32_t t = GS_KEEP; t < ac; t++) {
                 const uint32_t w = base + L.adj[ao + t - GS_KEEP];
-                take(w, L.rv[w & M], L.rc[w & M]);
+                take(w, L.rv[w & M], L.rc[w & M], L.rt[w & M]);
               }
               if (fl & GS_SPILL)
                 for (uint32_t j = off[i]; j < oend[i]; j++) {
                   const uint32_t w = col[j];
-                  if (w < base + GS_RING) take(w, L.rv[w & M], L.rc[w & M]);
-                  else take(w, S.down[w], S.crank[w]);
+                  if (w < base + GS_RING) take(w, L.rv[w & M], L.rc[w & M], L.rt[w & M]);
+                  else take(w, S.down[w], S.crank[w], S.ta[w]);
                 }
             }
             int32_t d = best >= 0 ? best + 1 : ((fl & 1u) ? 0 : -1);
             L.rv[i & M] = d;
+            L.rt[i & M] = d > 0 ? bt : i;   // tail: the end of the nxt chain
             L.ibc[kk] = d > 0 ? bc : GNIL;  // nxt (the staged far best is consumed)
             if (d < 0) *s_fail = 1;  // a goal without a chain continuation: impossible on H*
           }
@@ -394,6 +404,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
         ini = ini2;
         bc = bc2;
         br = br2;
+        bt = bt2;
         fl = fl2;
         wsync();
       }
@@ -408,6 +419,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       } else {
         S.down[i] = L.rv[i & M];
         S.nxt[i] = L.ibc[k];
+        S.ta[i] = L.rt[i & M];
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -455,6 +467,13 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // a stream compaction of the Kahn order (level-sorted already) by the H*
   // flag: block scans over CP positions per thread, no counter atomics
   for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
+  // every node's compact index, GNIL outside H* (a coalesced pass): the
+  // adjacency then tests a neighbour's membership and maps it with one gather
+  for (uint32_t v0 = tid; v0 < V; v0 += GB * GU) {
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+      if (v0 + q * GB < V) hidx[v0 + q * GB] = GNIL;
+  }
   __syncthreads();
   uint32_t n = 0;
   for (uint32_t base = 0; base < V; base += GB * CP) {
@@ -506,23 +525,19 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // latency-bound pass over all E edges per direction; walking four nodes'
   // rows in lockstep, one entry per row and step, was slower: the step count
   // is the longest of the rows.)
-#define INH(v) ((f[v] & NEMO_F_DELETED) != 0)
   auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
     uint32_t k = 0;
     const uint32_t j1 = ptr[x + 1];
     for (uint32_t j = ptr[x]; j < j1; j += GA_B) {
       uint32_t y[GA_B];
-      bool h[GA_B];
 #pragma unroll
       for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
-#pragma unroll
-      for (int q = 0; q < GA_B; q++) h[q] = j + q < j1 && INH(y[q]);
       uint32_t hy[GA_B];
 #pragma unroll
-      for (int q = 0; q < GA_B; q++) hy[q] = h[q] ? hidx[y[q]] : 0u;
+      for (int q = 0; q < GA_B; q++) hy[q] = j + q < j1 ? hidx[y[q]] : GNIL;
 #pragma unroll
       for (int q = 0; q < GA_B; q++)
-        if (h[q]) out[k++] = hy[q];
+        if (hy[q] != GNIL) out[k++] = hy[q];
     }
     return k;
   };
@@ -552,7 +567,6 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     S.cend[i] = c0 + hrow(gv.fp, gv.fc, x, S.child + c0);
     S.pend[i] = p0 + hrow(gv.rp, gv.rc, x, S.par + p0);
   }
-#undef INH
   __syncthreads();
   STAMP(2);
   // ---- up (forward) and down/nxt (backward): windowed single-wave sweeps -----------
@@ -745,65 +759,14 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     __syncthreads();
   }
   STAMP(5);
-  // ---- heads (roots of the bp forest) and tails (ends of nxt) by pointer jumping -----
-  uint32_t *h0 = S.ha, *h1 = S.hb, *t0 = S.ta, *t1 = S.tb;
-  for (uint32_t i = tid; i < n; i += GB) {
-    h0[i] = S.up[i] > 0 ? S.bp[i] : i;
-    t0[i] = S.nxt[i] != GNIL ? S.nxt[i] : i;
-  }
-  __syncthreads();
-  // (HBM passes below take GU elements per thread per round, every load of
-  // the round issued before its stores: one dependent chain per round, not
-  // one per element)
-  for (uint32_t span = 1; span <= maxlen; span <<= 1) {
-    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
-      uint32_t a[GU], b[GU];
-#pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB;
-        a[q] = i < n ? h0[i] : 0u;
-        b[q] = i < n ? t0[i] : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < GU; q++) {
-        a[q] = h0[a[q]];
-        b[q] = t0[b[q]];
-      }
-#pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB;
-        if (i < n) {
-          h1[i] = a[q];
-          t1[i] = b[q];
-        }
-      }
-    }
-    __syncthreads();
-    uint32_t *x = h0;
-    h0 = h1;
-    h1 = x;
-    x = t0;
-    t0 = t1;
-    t1 = x;
-  }
-  // one representative per accepted path (the witness whose best parent does not continue into it)
-  for (uint32_t i = tid; i < n; i += GB) {
-    const bool rep = S.up[i] == 0 || S.nxt[S.bp[i]] != i;
-    if (!rep) continue;
-    const uint32_t k = atomicAdd(&s_nch, 1u);
-    uint32_t *r = tmp + 5 * k;
-    r[0] = h0[i];
-    r[1] = t0[i];
-    r[2] = (uint32_t)(S.up[i] + S.down[i]);
-    r[3] = S.crank[h0[i]];
-    r[4] = i;
-  }
-  __threadfence_block();
-  __syncthreads();
-  const uint32_t nch = s_nch;
-  STAMP(6);
   // ---- preorder of the representatives: pre(v) = up(v) + sum of off over v and its bp
-  // ancestors, off = sizes of the earlier siblings (sizes laid out in (level, po) order)
+  // ancestors, off = sizes of the earlier siblings (sizes laid out in (level, po) order).
+  // Subtree sizes bottom-up, then ONE top-down pass over the up-levels adds each
+  // node's best parent's sum to its own and copies the parent's head (the root
+  // of its bp path); the tails (ends of the nxt chains) came out of the down
+  // sweep.  (Pointer jumping made ~12 rounds of random gathers over the whole
+  // H* for each of heads, tails and the preorder sums.)
+  uint32_t *va = S.va, *hd = S.hb, *tl = S.ta;
   for (uint32_t i = tid; i < n; i += GB) S.S[i] = 1;
   __syncthreads();
   for (uint32_t k = maxup; k >= 1; k--) {
@@ -816,44 +779,53 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   for (uint32_t i = tid; i < n; i += GB) S.A[S.uoff[S.up[i]] + S.po[i]] = S.S[i];
   __syncthreads();
   block_scan_inplace<GB, 16>(S.A, n, s_lds);
-  uint32_t *va = S.va, *vb = S.vb, *pa = S.pa, *pb = S.pb;
   for (uint32_t i = tid; i < n; i += GB) {
     const uint32_t k = S.up[i], base = S.uoff[k];
     va[i] = S.A[base + S.po[i]] - S.A[base + S.fpos[i]];
-    pa[i] = k ? S.bp[i] : GNIL;
+    if (k == 0) hd[i] = i;
   }
   __syncthreads();
-  for (uint32_t r = 1; r <= maxup; r <<= 1) {
-    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
-      uint32_t p[GU], v[GU], vp[GU], pp[GU];
+  for (uint32_t k = 1; k <= maxup; k++) {
+    for (uint32_t j0 = S.uoff[k] + tid; j0 < S.uoff[k + 1]; j0 += GB * GU) {
+      uint32_t i[GU], p[GU], v[GU], vp[GU], hp[GU];
+      const uint32_t b = S.uoff[k + 1];
+#pragma unroll
+      for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < b ? S.ub[j0 + q * GB] : GNIL;
 #pragma unroll
       for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB;
-        p[q] = i < n ? pa[i] : GNIL;
-        v[q] = i < n ? va[i] : 0u;
+        p[q] = i[q] != GNIL ? S.bp[i[q]] : 0u;
+        v[q] = i[q] != GNIL ? va[i[q]] : 0u;
       }
 #pragma unroll
       for (int q = 0; q < GU; q++) {
-        const uint32_t pq = p[q] != GNIL ? p[q] : 0u;
-        vp[q] = va[pq];
-        pp[q] = pa[pq];
+        vp[q] = i[q] != GNIL ? va[p[q]] : 0u;
+        hp[q] = i[q] != GNIL ? hd[p[q]] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t i = i0 + q * GB;
-        if (i >= n) continue;
-        vb[i] = p[q] != GNIL ? v[q] + vp[q] : v[q];
-        pb[i] = p[q] != GNIL ? pp[q] : GNIL;
-      }
+      for (int q = 0; q < GU; q++)
+        if (i[q] != GNIL) {
+          va[i[q]] = v[q] + vp[q];
+          hd[i[q]] = hp[q];
+        }
     }
     __syncthreads();
-    uint32_t *x = va;
-    va = vb;
-    vb = x;
-    x = pa;
-    pa = pb;
-    pb = x;
   }
+  STAMP(6);
+  // one representative per accepted path (the witness whose best parent does not continue into it)
+  for (uint32_t i = tid; i < n; i += GB) {
+    const bool rep = S.up[i] == 0 || S.nxt[S.bp[i]] != i;
+    if (!rep) continue;
+    const uint32_t k = atomicAdd(&s_nch, 1u);
+    uint32_t *r = tmp + 5 * k;
+    r[0] = hd[i];
+    r[1] = tl[i];
+    r[2] = (uint32_t)(S.up[i] + S.down[i]);
+    r[3] = S.crank[hd[i]];
+    r[4] = i;
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t nch = s_nch;
   STAMP(7);
   // ---- acceptance order (len desc, preorder asc) -------------------------------------
   // pre = va + up is the representative's preorder index (unique, < n): the chains

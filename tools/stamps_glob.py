@@ -20,8 +20,8 @@ if os.environ.get("NEMO_GLOB_BLOCK"):
 eng.load(corpus); eng.mark(); eng.simplify(); eng.synchronize()
 G = corpus.n_graphs
 st = eng.debug_copy("stamps", 0, 16 * 8 * G).view(np.uint64).reshape(G, 16).astype(np.int64)
-names = ["H* compact + ranks", "adjacency", "up/down", "bucket + bp", "prefix ranks", "heads/tails + reps",
-         "preorder", "bitonic sort", "output + tail lists"]
+names = ["H* compact + ranks", "adjacency", "up/down", "bucket + bp", "prefix ranks", "preorder + heads",
+         "reps", "order sort", "output + tail lists"]
 ok = st[:, 9] > 0
 d = np.diff(st[ok][:, :10], axis=1)
 print("graphs", int(ok.sum()), "total ticks per graph: median", np.median(d.sum(1)))
