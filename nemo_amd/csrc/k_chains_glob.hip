@@ -469,10 +469,25 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
   // every node's compact index, GNIL outside H* (a coalesced pass): the
   // adjacency then tests a neighbour's membership and maps it with one gather
-  for (uint32_t v0 = tid; v0 < V; v0 += GB * GU) {
+  // With identity ID ranks (no rank array) the rank bitmap is the H* flag in
+  // node order, stored a word per half-wave (no scattered atomics)
+  const bool idrank = gv.rank == nullptr;
+  for (uint32_t v0 = 0; v0 < V; v0 += GB * GU) {
+    bool h[GU];
 #pragma unroll
-    for (int q = 0; q < GU; q++)
-      if (v0 + q * GB < V) hidx[v0 + q * GB] = GNIL;
+    for (int q = 0; q < GU; q++) {
+      const uint32_t v = v0 + q * GB + tid;
+      h[q] = v < V && (f[v] & NEMO_F_DELETED);
+      if (v < V) hidx[v] = GNIL;
+    }
+    if (idrank) {
+#pragma unroll
+      for (int q = 0; q < GU; q++) {
+        const uint32_t v = v0 + q * GB + tid;
+        const uint64_t m = __ballot(h[q]);
+        if ((lane_id() & 31) == 0 && v < V) S.bm[v >> 5] = (uint32_t)(m >> (lane_id() & 32));
+      }
+    }
   }
   __syncthreads();
   uint32_t n = 0;
@@ -497,7 +512,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       S.rule[i] = is_rule(gv.word[x[q]]) ? 1u : 0u;
       const uint32_t r = gv.rank_of(x[q]);
       S.crank[i] = r;
-      atomicOr(&S.bm[r >> 5], 1u << (r & 31));
+      if (!idrank) atomicOr(&S.bm[r >> 5], 1u << (r & 31));
       i++;
     }
     n += tot;
@@ -812,10 +827,15 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(6);
   // one representative per accepted path (the witness whose best parent does not continue into it)
-  for (uint32_t i = tid; i < n; i += GB) {
-    const bool rep = S.up[i] == 0 || S.nxt[S.bp[i]] != i;
+  for (uint32_t i0 = 0; i0 < n; i0 += GB) {
+    const uint32_t i = i0 + tid;
+    const bool rep = i < n && (S.up[i] == 0 || S.nxt[S.bp[i]] != i);
+    const uint64_t m = __ballot(rep);  // one LDS atomic per wave
+    uint32_t b = 0;
+    if (m && lane_id() == 0) b = atomicAdd(&s_nch, (uint32_t)__popcll(m));
+    b = __builtin_amdgcn_readlane(b, 0);
     if (!rep) continue;
-    const uint32_t k = atomicAdd(&s_nch, 1u);
+    const uint32_t k = b + mbcnt(m);
     uint32_t *r = tmp + 5 * k;
     r[0] = hd[i];
     r[1] = tl[i];
