@@ -850,7 +850,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     for (size_t b = 0; b < big.size(); b++) {
       const uint32_t g = big[b];
       const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
-      const uint64_t nbk = (v + 2047) / 2048, nck = (e + 8191) / 8192;  // k_load.hip CB_NB, CB_CHUNK
+      const uint64_t nbk = (v + CB_NB - 1) / CB_NB, nck = (e + CB_CHUNK - 1) / CB_CHUNK;
       fits &= nbk <= CB_MAXB;
       hoff[b + 1] = hoff[b] + std::max<uint64_t>(nbk * nck, 1);
       d.cb_maxbk = std::max<uint32_t>(d.cb_maxbk, (uint32_t)nbk);

@@ -16,6 +16,12 @@
 #define NEMO_BLOCK 256
 #define NEMO_CSR_BIG 8192u  // graphs of at least this many nodes: multi-workgroup CSR build (k_csrb_*)
 #define CB_MAXB 8192u       // the bucketed CSR build's buckets per graph (of 2048 nodes): V <= 16M
+#ifndef CB_NB
+#define CB_NB 2048u         // nodes per bucket of the bucketed CSR build
+#endif
+#ifndef CB_CHUNK
+#define CB_CHUNK 16384u     // edges per histogram / partition chunk of the bucketed CSR build
+#endif
 #define NEMO_WAVES (NEMO_BLOCK / 64)
 #define NEMO_NONE 0xFFFFFFFFu
 

@@ -146,7 +146,9 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #define GS_MORE 0x2u   // more than GS_KEEP in-ring links: the rest in the window's list
 #define GS_SPILL 0x4u  // ... or, past the list's capacity, in HBM
 #define GS_KEEP 8      // in-ring links packed per node (u16 each, GS_NOLINK = none)
+#ifndef GS_SB
 #define GS_SB 4        // row entries per row and step while staging a window
+#endif
 #define GS_NOLINK 0xFFFFu
 template <bool UP, int GB>
 __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, const uint32_t *hs, const uint32_t *nlv,

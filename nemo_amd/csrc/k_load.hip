@@ -776,7 +776,9 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
 //     wave; 256 threads, so the barriers of a level are four waves'.
 #define TD_B 256
 #define TD_Q 2048u
+#ifndef TD_EPT
 #define TD_EPT 4  // frontier edges per thread per round
+#endif
 // The LDS frontier holds each node's row (first edge, degree), not the node:
 // a child's row bounds are loaded together with its in-degree atomic (for
 // every child, ready or not), so a level starts from LDS instead of waiting on
@@ -938,9 +940,9 @@ void launch_load(const DevCorpus &c, hipStream_t s) {
 // their row pointers and scatters the values into their rows with LDS
 // cursors, then sorts the rows (and, forward, counts relationships created).
 // Every global write is then a streaming store into a contiguous range.
-#define CB_NB 2048u
-#define CB_CHUNK 8192u
+#ifndef CB_BLOCK
 #define CB_BLOCK 1024
+#endif
 __global__ __launch_bounds__(CB_BLOCK) void k_cb_hist(DevCorpus c, int dir) {
   __shared__ uint32_t h[CB_MAXB];
   const uint32_t b = blockIdx.y, g = c.big[b];
@@ -994,7 +996,9 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
 // One bucket's rows built in LDS: degrees, row starts, the values scattered
 // by LDS cursors and each row sorted there, then written out coalesced.  A
 // bucket of more than CB_LDS_E edges (a hub-heavy one) sorts in HBM instead.
+#ifndef CB_LDS_E
 #define CB_LDS_E 14336u
+#endif
 #define CB_CB 4  // a bucket's edges per thread per batch (loads in flight together)
 #define CB_WSORT_MIN 17u
 
