@@ -23,7 +23,9 @@ namespace nemo {
 // graph's level walks are latency chains run by one wave, so a CU makes
 // progress on several graphs at once (a 1024-thread, 146 KB workgroup held a
 // whole CU for one graph).
-#define GA_B 4   // row entries loaded together while building the H* adjacency
+#define GA_B 4   // row entries loaded together while building the H* adjacency (a long row's tail)
+#define GA_N 4   // H* nodes per thread per round of the adjacency
+#define GA_F 6   // ... and the first entries of each of their rows
 #define GU 8     // elements per thread per round of the HBM passes (pointer jumping, bucketing)
 #define CP 16    // Kahn positions per thread per round of the H* compaction
 #define GNIL 0xFFFFFFFFu
@@ -542,10 +544,10 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // latency-bound pass over all E edges per direction; walking four nodes'
   // rows in lockstep, one entry per row and step, was slower: the step count
   // is the longest of the rows.)
-  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t *out) -> uint32_t {
+  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t j00, uint32_t *out) -> uint32_t {
     uint32_t k = 0;
     const uint32_t j1 = ptr[x + 1];
-    for (uint32_t j = ptr[x]; j < j1; j += GA_B) {
+    for (uint32_t j = j00; j < j1; j += GA_B) {
       uint32_t y[GA_B];
 #pragma unroll
       for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
@@ -579,11 +581,46 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
   block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t x = hs[i], c0 = S.ccoff[i], p0 = S.pcoff[i];
-    S.cend[i] = c0 + hrow(gv.fp, gv.fc, x, S.child + c0);
-    S.pend[i] = p0 + hrow(gv.rp, gv.rc, x, S.par + p0);
-  }
+  // the rows written GA_N nodes per thread at a time: their bounds, first
+  // GA_F entries and those entries' compact indices each a round of loads in
+  // flight together (one node at a time was a chain of three dependent
+  // round trips per node and direction); longer rows finish by themselves
+  auto hrows = [&](const uint32_t *ptr, const uint32_t *col, const uint32_t *off, uint32_t *endp, uint32_t *out) {
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) {
+      uint32_t x[GA_N], a[GA_N], b[GA_N], o[GA_N], k[GA_N];
+#pragma unroll
+      for (int q = 0; q < GA_N; q++) {
+        const uint32_t i = i0 + q * GB;
+        x[q] = i < n ? hs[i] : 0u;
+        o[q] = i < n ? off[i] : 0u;
+        k[q] = 0;
+      }
+#pragma unroll
+      for (int q = 0; q < GA_N; q++) {
+        a[q] = ptr[x[q]];
+        b[q] = i0 + q * GB < n ? ptr[x[q] + 1] : a[q];
+      }
+      uint32_t y[GA_N][GA_F], hy[GA_N][GA_F];
+#pragma unroll
+      for (int q = 0; q < GA_N; q++)
+#pragma unroll
+        for (int h = 0; h < GA_F; h++) y[q][h] = a[q] + h < b[q] ? col[a[q] + h] : 0u;
+#pragma unroll
+      for (int q = 0; q < GA_N; q++)
+#pragma unroll
+        for (int h = 0; h < GA_F; h++) hy[q][h] = a[q] + h < b[q] ? hidx[y[q][h]] : GNIL;
+#pragma unroll
+      for (int q = 0; q < GA_N; q++) {
+#pragma unroll
+        for (int h = 0; h < GA_F; h++)
+          if (hy[q][h] != GNIL) out[o[q] + k[q]++] = hy[q][h];
+        if (b[q] > a[q] + GA_F) k[q] += hrow(ptr, col, x[q], a[q] + GA_F, out + o[q] + k[q]);
+        if (i0 + q * GB < n) endp[i0 + q * GB] = o[q] + k[q];
+      }
+    }
+  };
+  hrows(gv.fp, gv.fc, S.ccoff, S.cend, S.child);
+  hrows(gv.rp, gv.rc, S.pcoff, S.pend, S.par);
   __syncthreads();
   STAMP(2);
   // ---- up (forward) and down/nxt (backward): windowed single-wave sweeps -----------
@@ -829,21 +866,40 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(6);
   // one representative per accepted path (the witness whose best parent does not continue into it)
-  for (uint32_t i0 = 0; i0 < n; i0 += GB) {
-    const uint32_t i = i0 + tid;
-    const bool rep = i < n && (S.up[i] == 0 || S.nxt[S.bp[i]] != i);
-    const uint64_t m = __ballot(rep);  // one LDS atomic per wave
-    uint32_t b = 0;
-    if (m && lane_id() == 0) b = atomicAdd(&s_nch, (uint32_t)__popcll(m));
-    b = __builtin_amdgcn_readlane(b, 0);
-    if (!rep) continue;
-    const uint32_t k = b + mbcnt(m);
-    uint32_t *r = tmp + 5 * k;
-    r[0] = hd[i];
-    r[1] = tl[i];
-    r[2] = (uint32_t)(S.up[i] + S.down[i]);
-    r[3] = S.crank[hd[i]];
-    r[4] = i;
+  // (GU nodes per thread per round, each round's gathers in flight together)
+  for (uint32_t i0 = 0; i0 < n; i0 += GB * GU) {
+    uint32_t up[GU], bp[GU], nb[GU], h[GU], t[GU], dn[GU], ch[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB + tid;
+      const bool in = i < n;
+      up[q] = in ? (uint32_t)S.up[i] : 0u;
+      bp[q] = in ? S.bp[i] : 0u;
+      h[q] = in ? hd[i] : 0u;
+      t[q] = in ? tl[i] : 0u;
+      dn[q] = in ? (uint32_t)S.down[i] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      nb[q] = up[q] ? S.nxt[bp[q]] : 0u;
+      ch[q] = S.crank[h[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB + tid;
+      const bool rep = i < n && (up[q] == 0 || nb[q] != i);
+      const uint64_t m = __ballot(rep);  // one LDS atomic per wave
+      uint32_t b = 0;
+      if (m && lane_id() == 0) b = atomicAdd(&s_nch, (uint32_t)__popcll(m));
+      b = __builtin_amdgcn_readlane(b, 0);
+      if (!rep) continue;
+      uint32_t *r = tmp + 5 * (b + mbcnt(m));
+      r[0] = h[q];
+      r[1] = t[q];
+      r[2] = up[q] + dn[q];
+      r[3] = ch[q];
+      r[4] = i;
+    }
   }
   __threadfence_block();
   __syncthreads();
