@@ -210,7 +210,10 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 //   HCAP: H* nodes (and H* edges per direction) staged in LDS
 //   UCAP: Kahn levels of the graph / distinct prefix lengths (longest chain path + 2)
 #define NIL16 0xFFFFu
-#define CF_ROWS 20  // topo positions per thread per compaction round (fast front)
+#define CF_ROWS 20  // nodes per thread per compaction round (fast front)
+#ifndef CF_Q
+#define CF_Q 4      // ... taken CF_Q consecutive nodes per load
+#endif
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
 #ifndef CH_K
 #define CH_K 3      // up/down sweeps: parents (children) of a node read together
@@ -288,17 +291,42 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
     // ID rank).  Node-order reads are coalesced: flags, level, word, rank.
     const uint32_t *nlv = c.nlv + gv.n0;
     uint32_t lev[CF_ROWS], rk[CF_ROWS], hm = 0, rl = 0;
+    // node of slot q: CF_Q consecutive nodes per thread and load, so the
+    // flags come four to a u32 and the levels, words (and ranks) four to a
+    // 16-byte load
+    auto xq = [&](uint32_t sbase, int q) { return sbase + CF_Q * ((q / CF_Q) * NEMO_BLOCK + tid) + (q % CF_Q); };
     auto rows = [&](uint32_t sbase) {
       uint8_t fl[CF_ROWS];
       uint32_t wd[CF_ROWS];
 #pragma unroll
-      for (int q = 0; q < CF_ROWS; q++) {
-        const uint32_t x = sbase + q * NEMO_BLOCK + tid;
-        const bool in = x < gv.V;
-        fl[q] = in ? f[x] : (uint8_t)0;
-        lev[q] = in ? nlv[x] : 0u;
-        wd[q] = in ? gv.word[x] : 0u;
-        rk[q] = in ? gv.rank_of(x) : 0u;
+      for (int g4 = 0; g4 < CF_ROWS / CF_Q; g4++) {
+        const uint32_t x0 = xq(sbase, g4 * CF_Q);
+        if (CF_Q == 4 && x0 + 3 < gv.V) {  // a whole quad inside the graph
+          uint32_t f4;
+          __builtin_memcpy(&f4, f + x0, 4);
+          uint4 l4, w4;
+          __builtin_memcpy(&l4, nlv + x0, 16);
+          __builtin_memcpy(&w4, gv.word + x0, 16);
+          const uint32_t l[4] = {l4.x, l4.y, l4.z, l4.w}, w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int b = 0; b < CF_Q; b++) {
+            fl[g4 * CF_Q + b] = (uint8_t)(f4 >> (8 * b));
+            lev[g4 * CF_Q + b] = l[b];
+            wd[g4 * CF_Q + b] = w[b];
+            rk[g4 * CF_Q + b] = gv.rank_of(x0 + b);
+          }
+        } else {
+#pragma unroll
+          for (int b = 0; b < CF_Q; b++) {
+            const int q = g4 * CF_Q + b;
+            const uint32_t x = x0 + b;
+            const bool in = x < gv.V;
+            fl[q] = in ? f[x] : (uint8_t)0;
+            lev[q] = in ? nlv[x] : 0u;
+            wd[q] = in ? gv.word[x] : 0u;
+            rk[q] = in ? gv.rank_of(x) : 0u;
+          }
+        }
       }
       hm = rl = 0;
 #pragma unroll
@@ -332,7 +360,7 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
 #pragma unroll
       for (int q = 0; q < CF_ROWS; q++) {
         if (!((hm >> q) & 1u)) continue;
-        const uint32_t x = sbase + q * NEMO_BLOCK + tid;
+        const uint32_t x = xq(sbase, q);
         const uint32_t i = atomicAdd(&hist[lev[q]], 1u);
         hs[i] = x;
         hmap[x] = (uint16_t)i;
