@@ -397,11 +397,26 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
     for (int pass = 0; pass < 2; pass++) {
       for (uint32_t ebase = 0; ebase < gv.E; ebase += CF_EPT * NEMO_BLOCK) {
         if (!(one_e && pass == 1)) {
-          uint32_t sd[CF_EPT];
+          uint32_t sd[CF_EPT];  // (four consecutive edges per thread and 16-byte load)
 #pragma unroll
-          for (int q = 0; q < CF_EPT; q++) {
-            const uint32_t e = ebase + q * NEMO_BLOCK + tid;
-            sd[q] = e < gv.E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
+          for (int g4 = 0; g4 < CF_EPT / 4; g4++) {
+            const uint32_t e0 = ebase + 4 * (g4 * NEMO_BLOCK + tid);
+            uint32_t xs[4], ys[4];
+            if (e0 + 3 < gv.E) {
+              uint4 a4, b4;
+              __builtin_memcpy(&a4, es + e0, 16);
+              __builtin_memcpy(&b4, ed + e0, 16);
+              xs[0] = a4.x, xs[1] = a4.y, xs[2] = a4.z, xs[3] = a4.w;
+              ys[0] = b4.x, ys[1] = b4.y, ys[2] = b4.z, ys[3] = b4.w;
+            } else {
+#pragma unroll
+              for (int b = 0; b < 4; b++) {
+                xs[b] = e0 + b < gv.E ? es[e0 + b] : 0u;
+                ys[b] = e0 + b < gv.E ? ed[e0 + b] : 0u;
+              }
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++) sd[4 * g4 + b] = e0 + b < gv.E ? (xs[b] << 16) | ys[b] : 0xFFFFFFFFu;
           }
 #pragma unroll
           for (int q = 0; q < CF_EPT; q++) {

@@ -193,14 +193,33 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
   STAMP(10);
   // every load of the graph's input issued back to back: edge e = tid + q*BLOCK
   // as (src << 16 | dst), and the rule bits of the node words
+  // (four consecutive edges per thread and 16-byte load; ~0u marks an empty
+  // slot: a valid pair has src < 16384)
   uint32_t sd[EPT];
   bool bad = false;
 #pragma unroll
-  for (int q = 0; q < EPT; q++) {
-    const uint32_t e = tid + q * B;
-    const uint32_t x = e < E ? es[e] : 0u, y = e < E ? ed[e] : 0u;
-    bad |= e < E && (x >= V || y >= V);
-    sd[q] = (x << 16) | (y & 0xFFFFu);
+  for (int g4 = 0; g4 < EPT / 4; g4++) {
+    const uint32_t e0 = 4 * (g4 * B + tid);
+    uint32_t xs[4], ys[4];
+    if (e0 + 3 < E) {
+      uint4 a4, b4;
+      __builtin_memcpy(&a4, es + e0, 16);
+      __builtin_memcpy(&b4, ed + e0, 16);
+      xs[0] = a4.x, xs[1] = a4.y, xs[2] = a4.z, xs[3] = a4.w;
+      ys[0] = b4.x, ys[1] = b4.y, ys[2] = b4.z, ys[3] = b4.w;
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        xs[b] = e0 + b < E ? es[e0 + b] : 0u;
+        ys[b] = e0 + b < E ? ed[e0 + b] : 0u;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const bool in = e0 + b < E;
+      bad |= in && (xs[b] >= V || ys[b] >= V);
+      sd[4 * g4 + b] = in ? (xs[b] << 16) | (ys[b] & 0xFFFFu) : ~0u;
+    }
   }
   for (uint32_t w = tid; w < (V + 31) / 32; w += B) s_rule[w] = 0;
   if (tid == 0) {
@@ -211,21 +230,34 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     c.redo[g] = 0;
   }
   __syncthreads();
+  // (four consecutive node words per thread and 16-byte load: eight lanes'
+  // nibbles make one bitmap word)
   for (uint32_t base = 0; base < V; base += 8 * B) {
-    bool r[8];
+    uint32_t nib[2];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + tid + q * B;
-      r[q] = v < V && is_rule(word[v]);
+    for (int g4 = 0; g4 < 2; g4++) {
+      const uint32_t v0 = base + 4 * (g4 * B + tid);
+      uint32_t w[4];
+      if (v0 + 3 < V) {
+        uint4 w4;
+        __builtin_memcpy(&w4, word + v0, 16);
+        w[0] = w4.x, w[1] = w4.y, w[2] = w4.z, w[3] = w4.w;
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) w[b] = v0 + b < V ? word[v0 + b] : 0u;
+      }
+      nib[g4] = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) nib[g4] |= (v0 + b < V && is_rule(w[b]) ? 1u : 0u) << b;
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + tid + q * B;
-      const uint64_t m = __ballot(r[q]);
-      if ((lane_id() & 31) == 0 && v < V) {
-        const uint32_t bits = (uint32_t)(m >> (lane_id() & 32));
-        if (bits) atomicOr(&s_rule[v >> 5], bits);
-      }
+    for (int g4 = 0; g4 < 2; g4++) {
+      const uint32_t v0 = base + 4 * (g4 * B + tid);
+      uint32_t x = nib[g4] << (4 * (tid & 7));
+      x |= (uint32_t)__shfl_xor((int)x, 1);
+      x |= (uint32_t)__shfl_xor((int)x, 2);
+      x |= (uint32_t)__shfl_xor((int)x, 4);
+      if ((tid & 7) == 0 && v0 < V && x) atomicOr(&s_rule[v0 >> 5], x);
     }
   }
   if (bad) s_bad = 1;
@@ -244,7 +276,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     if (dir == 0) STAMP(0);
 #pragma unroll
     for (int q = 0; q < EPT; q++)
-      if (tid + q * B < E) {
+      if (sd[q] != ~0u) {
         const uint32_t k = (sd[q] >> ks) & 0xFFFFu;
         atomicAdd(&ptr32[k >> 1], 1u << (16 * (k & 1)));
       }
@@ -277,7 +309,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     if (dir == 0) STAMP(4);
 #pragma unroll
     for (int q = 0; q < EPT; q++)
-      if (tid + q * B < E) {
+      if (sd[q] != ~0u) {
         const uint32_t k = (sd[q] >> ks) & 0xFFFFu, sh = 16 * (k & 1);
         col[(atomicAdd(&ptr32[k >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)((sd[q] >> vs) & 0xFFFFu);
       }
