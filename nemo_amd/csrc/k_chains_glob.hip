@@ -479,22 +479,27 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // With identity ID ranks (no rank array) the rank bitmap is the H* flag in
   // node order, stored a word per half-wave (no scattered atomics)
   const bool idrank = gv.rank == nullptr;
-  for (uint32_t v0 = 0; v0 < V; v0 += GB * GU) {
-    bool h[GU];
+  // (each thread 32 consecutive nodes: their flags in two 16-byte loads, the
+  // map in eight 16-byte stores, the bitmap word built in a register)
+  for (uint32_t v0 = 32 * tid; v0 < V; v0 += 32 * GB) {
+    uint32_t bits = 0;
+    if (v0 + 31 < V) {
+      uint4 fa, fb;
+      __builtin_memcpy(&fa, f + v0, 16);
+      __builtin_memcpy(&fb, f + v0 + 16, 16);
+      const uint32_t fw[8] = {fa.x, fa.y, fa.z, fa.w, fb.x, fb.y, fb.z, fb.w};
 #pragma unroll
-    for (int q = 0; q < GU; q++) {
-      const uint32_t v = v0 + q * GB + tid;
-      h[q] = v < V && (f[v] & NEMO_F_DELETED);
-      if (v < V) hidx[v] = GNIL;
-    }
-    if (idrank) {
+      for (int k = 0; k < 32; k++) bits |= ((fw[k >> 2] >> (8 * (k & 3))) & NEMO_F_DELETED ? 1u : 0u) << k;
+      const uint4 nil = make_uint4(GNIL, GNIL, GNIL, GNIL);
 #pragma unroll
-      for (int q = 0; q < GU; q++) {
-        const uint32_t v = v0 + q * GB + tid;
-        const uint64_t m = __ballot(h[q]);
-        if ((lane_id() & 31) == 0 && v < V) S.bm[v >> 5] = (uint32_t)(m >> (lane_id() & 32));
+      for (int k = 0; k < 8; k++) __builtin_memcpy(hidx + v0 + 4 * k, &nil, 16);
+    } else {
+      for (uint32_t v = v0; v < V; v++) {
+        bits |= (f[v] & NEMO_F_DELETED ? 1u : 0u) << (v - v0);
+        hidx[v] = GNIL;
       }
     }
+    if (idrank) S.bm[v0 >> 5] = bits;
   }
   __syncthreads();
   uint32_t n = 0;

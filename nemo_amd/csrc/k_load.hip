@@ -162,6 +162,22 @@ __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e) {
          lds_align(2u * v);
 }
 
+// u16 LDS array -> u32 HBM array, four entries per thread and store (8-byte
+// LDS read, 16-byte global store); src must be 8-byte aligned
+template <int B>
+__device__ __forceinline__ void lds16_to_hbm32(uint32_t *dst, const uint16_t *src, uint32_t n) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t j = 4 * tid; j < n; j += 4 * B) {
+    if (j + 3 < n) {
+      const uint2 h = *(const uint2 *)(src + j);
+      const uint4 w = make_uint4(h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16);
+      __builtin_memcpy(dst + j, &w, 16);
+    } else {
+      for (uint32_t k = j; k < n; k++) dst[k] = src[k];
+    }
+  }
+}
+
 __device__ __forceinline__ bool build_fits(const DevCorpus &c, uint32_t V, uint32_t E) {
   return c.bld_bytes != 0u && V <= c.bld_v && E <= c.bld_e;
 }
@@ -304,7 +320,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     if (dir == 0) STAMP(2);
     block_scan_inplace<B>(ptr, V + 1, s_lds);
     if (dir == 0) STAMP(3);
-    for (uint32_t v = tid; v <= V; v += B) optr[v] = ptr[v];
+    lds16_to_hbm32<B>(optr, ptr, V + 1);
     __syncthreads();
     if (dir == 0) STAMP(4);
 #pragma unroll
@@ -337,7 +353,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     }
     __syncthreads();
     if (dir == 0) STAMP(6);
-    for (uint32_t j = tid; j < E; j += B) ocol[j] = col[j];
+    lds16_to_hbm32<B>(ocol, col, E);
     __syncthreads();
     STAMP(12 + dir);
   }
@@ -439,7 +455,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     hi += s_cnt[(nl - 1) % 3];  // after the barrier: plain LDS read
     if (tid == 0) lvl[nl] = lo;
   }
-  for (uint32_t i = tid; i < hi; i += B) topo[i] = q16[i];
+  lds16_to_hbm32<B>(topo, q16, hi);
   if ((g & 1u) && hi == V) {
     // post graphs: the forward edges in source Kahn order for k_proto_lds (e2:
     // src << 16 | dst) and each Kahn position's first edge (posoff).  Every
@@ -987,10 +1003,27 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_hist(DevCorpus c, int dir) {
   const uint32_t *key = (dir ? c.edst : c.esrc) + e0, *oth = (dir ? c.esrc : c.edst) + e0;
   const uint32_t a = blockIdx.x * CB_CHUNK, z = min(E, a + CB_CHUNK);
   bool bad = false;
-  for (uint32_t e = a + threadIdx.x; e < z; e += CB_BLOCK) {
-    const uint32_t k = key[e];
-    bad |= k >= V || oth[e] >= V;
-    if (k < V) atomicAdd(&h[k / CB_NB], 1u);
+  for (uint32_t e0 = a + 4 * threadIdx.x; e0 < z; e0 += 4 * CB_BLOCK) {  // four edges per thread and load
+    uint32_t k[4], o[4];
+    if (e0 + 3 < z) {
+      uint4 k4, o4;
+      __builtin_memcpy(&k4, key + e0, 16);
+      __builtin_memcpy(&o4, oth + e0, 16);
+      k[0] = k4.x, k[1] = k4.y, k[2] = k4.z, k[3] = k4.w;
+      o[0] = o4.x, o[1] = o4.y, o[2] = o4.z, o[3] = o4.w;
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        k[b] = e0 + b < z ? key[e0 + b] : 0u;
+        o[b] = e0 + b < z ? oth[e0 + b] : 0u;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      if (e0 + b >= z) continue;
+      bad |= k[b] >= V || o[b] >= V;
+      if (k[b] < V) atomicAdd(&h[k[b] / CB_NB], 1u);
+    }
   }
   if (__any(bad) && lane_id() == 0) atomicMax(&c.err[g], (uint32_t)NEMO_ERR_INVALID);
   __syncthreads();
@@ -1018,11 +1051,28 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cb_part(DevCorpus c, int dir) {
   const uint32_t *key = (dir ? c.edst : c.esrc) + e0, *oth = (dir ? c.esrc : c.edst) + e0;
   uint32_t *ok = c.cb_key + e0, *ov = c.cb_val + e0;
   const uint32_t a = blockIdx.x * CB_CHUNK, z = min(E, a + CB_CHUNK);
-  for (uint32_t e = a + threadIdx.x; e < z; e += CB_BLOCK) {
-    const uint32_t k = key[e], v = oth[e];
-    const uint32_t pos = atomicAdd(&cur[k / CB_NB], 1u);
-    ok[pos] = k;
-    ov[pos] = v;
+  for (uint32_t e0 = a + 4 * threadIdx.x; e0 < z; e0 += 4 * CB_BLOCK) {  // four edges per thread and load
+    uint32_t k[4], o[4];
+    if (e0 + 3 < z) {
+      uint4 k4, o4;
+      __builtin_memcpy(&k4, key + e0, 16);
+      __builtin_memcpy(&o4, oth + e0, 16);
+      k[0] = k4.x, k[1] = k4.y, k[2] = k4.z, k[3] = k4.w;
+      o[0] = o4.x, o[1] = o4.y, o[2] = o4.z, o[3] = o4.w;
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        k[b] = e0 + b < z ? key[e0 + b] : 0u;
+        o[b] = e0 + b < z ? oth[e0 + b] : 0u;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      if (e0 + b >= z) continue;
+      const uint32_t pos = atomicAdd(&cur[k[b] / CB_NB], 1u);
+      ok[pos] = k[b];
+      ov[pos] = o[b];
+    }
   }
 }
 // One bucket's rows built in LDS: degrees, row starts, the values scattered
@@ -1082,17 +1132,29 @@ __global__ __launch_bounds__(CB_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (uint32_t i = tid; i <= nv; i += CB_BLOCK) cnt[i] = 0;
   if (tid == 0) s_cr = 0;
   __syncthreads();
-  for (uint32_t j0 = tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
-    uint32_t k[CB_CB], v[CB_CB];
+  // (CB_CB consecutive edges per thread and 16-byte load)
+  auto ld_kv = [&](uint32_t j0, uint32_t (&k)[CB_CB], uint32_t (&v)[CB_CB], bool want_v) {
+    static_assert(CB_CB == 4, "one 16-byte load per array");
+    if (j0 + 3 < ne) {
+      uint4 k4, v4 = make_uint4(0, 0, 0, 0);
+      __builtin_memcpy(&k4, ek + j0, 16);
+      if (want_v) __builtin_memcpy(&v4, ev + j0, 16);
+      k[0] = k4.x, k[1] = k4.y, k[2] = k4.z, k[3] = k4.w;
+      v[0] = v4.x, v[1] = v4.y, v[2] = v4.z, v[3] = v4.w;
+    } else {
 #pragma unroll
-    for (int q = 0; q < CB_CB; q++) {
-      const uint32_t j = j0 + q * CB_BLOCK;
-      k[q] = j < ne ? ek[j] : v0;
-      v[q] = j < ne && dir == 0 ? ev[j] : 0u;
+      for (int q = 0; q < CB_CB; q++) {
+        k[q] = j0 + q < ne ? ek[j0 + q] : v0;
+        v[q] = j0 + q < ne && want_v ? ev[j0 + q] : 0u;
+      }
     }
+  };
+  for (uint32_t j0 = CB_CB * tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
+    uint32_t k[CB_CB], v[CB_CB];
+    ld_kv(j0, k, v, dir == 0);
 #pragma unroll
     for (int q = 0; q < CB_CB; q++)
-      if (j0 + q * CB_BLOCK < ne) atomicAdd(&cnt[k[q] - v0], 1u);
+      if (j0 + q < ne) atomicAdd(&cnt[k[q] - v0], 1u);
     if (dir == 0) {
       uint32_t wk[CB_CB], wv[CB_CB];
 #pragma unroll
@@ -1101,7 +1163,7 @@ __global__ __launch_bounds__(CB_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         wv[q] = word[v[q]];
       }
 #pragma unroll
-      for (int q = 0; q < CB_CB; q++) created += j0 + q * CB_BLOCK < ne && is_rule(wk[q]) != is_rule(wv[q]) ? 1u : 0u;
+      for (int q = 0; q < CB_CB; q++) created += j0 + q < ne && is_rule(wk[q]) != is_rule(wv[q]) ? 1u : 0u;
     }
   }
   __syncthreads();
@@ -1109,17 +1171,12 @@ __global__ __launch_bounds__(CB_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (uint32_t i = tid; i < nv; i += CB_BLOCK) ptr[v0 + i] = lo + cnt[i];
   if (bk + 1 == nbk && tid == 0) ptr[V] = E;
   __syncthreads();
-  for (uint32_t j0 = tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
+  for (uint32_t j0 = CB_CB * tid; j0 < ne; j0 += CB_CB * CB_BLOCK) {
     uint32_t k[CB_CB], v[CB_CB];
-#pragma unroll
-    for (int q = 0; q < CB_CB; q++) {
-      const uint32_t j = j0 + q * CB_BLOCK;
-      k[q] = j < ne ? ek[j] : v0;
-      v[q] = j < ne ? ev[j] : 0u;
-    }
+    ld_kv(j0, k, v, true);
 #pragma unroll
     for (int q = 0; q < CB_CB; q++)
-      if (j0 + q * CB_BLOCK < ne) dst[atomicAdd(&cnt[k[q] - v0], 1u)] = v[q];
+      if (j0 + q < ne) dst[atomicAdd(&cnt[k[q] - v0], 1u)] = v[q];
   }
   __threadfence_block();
   __syncthreads();  // cnt[i] = end of row i (local)
