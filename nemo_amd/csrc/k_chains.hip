@@ -215,6 +215,9 @@ __device__ bool wave_component(const GraphView &gv, CompLDS &L, const uint32_t *
 #define CF_Q 4      // ... taken CF_Q consecutive nodes per load
 #endif
 #define CF_EPT 32   // input edges per thread per adjacency round (fast front)
+#ifndef PR_GROUP_MIN
+#define PR_GROUP_MIN 96  // prefix ranks: levels above this many nodes rank by groups, smaller ones by counting all keys
+#endif
 #ifndef CH_K
 #define CH_K 3      // up/down sweeps: parents (children) of a node read together
 #endif
@@ -791,7 +794,7 @@ __device__ __forceinline__ void chains_graph(const DevCorpus c, const uint32_t g
       __syncthreads();
       continue;
     }
-    const bool grouped = m > 96;
+    const bool grouped = m > PR_GROUP_MIN;
     const uint32_t mp = a - L.uoff[k - 1];  // size of level k-1: po(bp) < mp
     uint32_t *cnt = L.u.rk.bk, *grp = L.u.rk.bk + mp + 1;
     if (grouped) {

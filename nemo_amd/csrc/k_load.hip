@@ -455,6 +455,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     hi += s_cnt[(nl - 1) % 3];  // after the barrier: plain LDS read
     if (tid == 0) lvl[nl] = lo;
   }
+  STAMP(7);
   lds16_to_hbm32<B>(topo, q16, hi);
   if ((g & 1u) && hi == V) {
     // post graphs: the forward edges in source Kahn order for k_proto_lds (e2:

@@ -30,3 +30,8 @@ b = np.concatenate([st[:, 11:12], st[:, 0:7], st[:, 12:13]], axis=1)[ok]
 db = np.diff(b, axis=1)
 for i, nm in enumerate(sub):
     print(f"  rev {nm:16s} median {np.median(db[:, i]):9.0f}")
+# the Kahn phase split: the level loop itself, then the Kahn-order copy and (post graphs) e2 emission
+kl = (st[:, 7] - st[:, 14])[ok]
+ke = (st[:, 15] - st[:, 7])[ok]
+print(f"  Kahn loop         median {np.median(kl):9.0f}")
+print(f"  topo copy + e2    median {np.median(ke):9.0f}")
