@@ -120,6 +120,18 @@ struct GSweepLds {
   uint8_t flg[GS_WN];    // bit 0 rule, GS_MORE, GS_SPILL
 };
 
+// four consecutive entries [i, i + 4) of an HBM array (one 16-byte load when
+// all four exist, `fill` past n)
+template <typename T>
+__device__ __forceinline__ void ld4(const T *p, uint32_t i, uint32_t n, T *o, T fill) {
+  if (i + 3 < n) {
+    __builtin_memcpy(o, p + i, 16);
+  } else {
+#pragma unroll
+    for (int b = 0; b < 4; b++) o[b] = i + b < n ? p[i + b] : fill;
+  }
+}
+
 template <int GB>
 __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #pragma unroll
@@ -534,12 +546,30 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     if (tid == 0) c.nch[g] = 0;
     return;
   }
-  for (uint32_t w = tid; w < nw; w += GB) S.bmpre[w] = __popc(S.bm[w]);
+  // (GU entries per thread and round below: each round's loads, then its
+  // gathers, in flight together)
+  for (uint32_t w0 = tid; w0 < nw; w0 += GB * GU) {
+    uint32_t x[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) x[q] = w0 + q * GB < nw ? S.bm[w0 + q * GB] : 0u;
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+      if (w0 + q * GB < nw) S.bmpre[w0 + q * GB] = __popc(x[q]);
+  }
   __syncthreads();
   block_scan_inplace<GB, 16>(S.bmpre, nw, s_lds);
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t r = S.crank[i];
-    S.crank[i] = S.bmpre[r >> 5] + __popc(S.bm[r >> 5] & ((1u << (r & 31)) - 1u));
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+    uint32_t r[GU], bp_[GU], bw[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) r[q] = i0 + q * GB < n ? S.crank[i0 + q * GB] : 0u;
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      bp_[q] = S.bmpre[r[q] >> 5];
+      bw[q] = S.bm[r[q] >> 5];
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+      if (i0 + q * GB < n) S.crank[i0 + q * GB] = bp_[q] + __popc(bw[q] & ((1u << (r[q] & 31)) - 1u));
   }
   STAMP(1);
   // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
@@ -656,9 +686,19 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   glob_sweep<false, GB>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
   STAMP(3);
   uint32_t mu = 0, ml = 0;
-  for (uint32_t i = tid; i < n; i += GB) {
-    mu = max(mu, (uint32_t)max(S.up[i], 0));
-    ml = max(ml, (uint32_t)max(S.up[i] + S.down[i], 0));
+  for (uint32_t b0 = 0; b0 < n; b0 += 16 * GB) {  // four quads of consecutive nodes per thread and round
+    int32_t u[16], d[16];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; g4++) {
+      const uint32_t i = b0 + 4 * (g4 * GB + tid);
+      ld4(S.up, i, n, u + 4 * g4, 0);
+      ld4(S.down, i, n, d + 4 * g4, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      mu = max(mu, (uint32_t)max(u[q], 0));
+      ml = max(ml, (uint32_t)max(u[q] + d[q], 0));
+    }
   }
   const uint32_t maxup = gmax_u32<GB>(mu, s_lds);
   const uint32_t maxlen = gmax_u32<GB>(ml, s_lds);
@@ -853,13 +893,46 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     }
     __syncthreads();
   }
-  for (uint32_t i = tid; i < n; i += GB) S.A[S.uoff[S.up[i]] + S.po[i]] = S.S[i];
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+    uint32_t k[GU], po[GU], sz[GU], base[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const bool in = i0 + q * GB < n;
+      k[q] = in ? (uint32_t)S.up[i0 + q * GB] : 0u;
+      po[q] = in ? S.po[i0 + q * GB] : 0u;
+      sz[q] = in ? S.S[i0 + q * GB] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) base[q] = S.uoff[k[q]];
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+      if (i0 + q * GB < n) S.A[base[q] + po[q]] = sz[q];
+  }
   __syncthreads();
   block_scan_inplace<GB, 16>(S.A, n, s_lds);
-  for (uint32_t i = tid; i < n; i += GB) {
-    const uint32_t k = S.up[i], base = S.uoff[k];
-    va[i] = S.A[base + S.po[i]] - S.A[base + S.fpos[i]];
-    if (k == 0) hd[i] = i;
+  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+    uint32_t k[GU], po[GU], fp[GU], base[GU], a1[GU], a0[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const bool in = i0 + q * GB < n;
+      k[q] = in ? (uint32_t)S.up[i0 + q * GB] : 0u;
+      po[q] = in ? S.po[i0 + q * GB] : 0u;
+      fp[q] = in ? S.fpos[i0 + q * GB] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) base[q] = S.uoff[k[q]];
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      a1[q] = S.A[base[q] + po[q]];
+      a0[q] = S.A[base[q] + fp[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      const uint32_t i = i0 + q * GB;
+      if (i >= n) continue;
+      va[i] = a1[q] - a0[q];
+      if (k[q] == 0) hd[i] = i;
+    }
   }
   __syncthreads();
   for (uint32_t k = 1; k <= maxup; k++) {
@@ -935,9 +1008,18 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   // by length.  (A bitonic network over the padded key array made ~190 passes.)
   for (uint32_t i = tid; i < n; i += GB) S.grp[i] = GNIL;
   __syncthreads();
-  for (uint32_t q = tid; q < nch; q += GB) {
-    const uint32_t rep = tmp[5 * q + 4];
-    S.grp[va[rep] + (uint32_t)S.up[rep]] = q;  // chain of each preorder index
+  for (uint32_t q0 = tid; q0 < nch; q0 += GB * GU) {  // chain of each preorder index
+    uint32_t rp[GU], v[GU], u[GU];
+#pragma unroll
+    for (int q = 0; q < GU; q++) rp[q] = q0 + q * GB < nch ? tmp[5 * (q0 + q * GB) + 4] : 0u;
+#pragma unroll
+    for (int q = 0; q < GU; q++) {
+      v[q] = va[rp[q]];
+      u[q] = (uint32_t)S.up[rp[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+      if (q0 + q * GB < nch) S.grp[v[q] + u[q]] = q0 + q * GB;
   }
   __syncthreads();
   unsigned long long *ka = S.key, *kb = S.key + nch;  // nch <= n <= V: both fit the 2V keys
@@ -981,14 +1063,31 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   STAMP(8);
   uint32_t *out = c.chain + 5 * gv.n0;
-  for (uint32_t pos = tid; pos < nch; pos += GB) {
-    const uint32_t q = S.grp[(uint32_t)(ka[pos] & 0xFFFFFFFFu)];
-    uint32_t *w = out + 5 * pos;
-    w[0] = hs[tmp[5 * q]];
-    w[1] = hs[tmp[5 * q + 1]];
-    w[2] = tmp[5 * q + 2];
-    w[3] = gv.rank_of(w[0]);
-    w[4] = 0;
+  for (uint32_t p0 = tid; p0 < nch; p0 += GB * GU) {
+    uint32_t q[GU], h[GU], t[GU], l[GU], hh[GU], tt[GU];
+#pragma unroll
+    for (int k = 0; k < GU; k++) q[k] = p0 + k * GB < nch ? S.grp[(uint32_t)(ka[p0 + k * GB] & 0xFFFFFFFFu)] : 0u;
+#pragma unroll
+    for (int k = 0; k < GU; k++) {
+      h[k] = tmp[5 * q[k]];
+      t[k] = tmp[5 * q[k] + 1];
+      l[k] = tmp[5 * q[k] + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < GU; k++) {
+      hh[k] = hs[h[k]];
+      tt[k] = hs[t[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < GU; k++) {
+      if (p0 + k * GB >= nch) continue;
+      uint32_t *w = out + 5 * (p0 + k * GB);
+      w[0] = hh[k];
+      w[1] = tt[k];
+      w[2] = l[k];
+      w[3] = gv.rank_of(hh[k]);
+      w[4] = 0;
+    }
   }
   STAMP(9);
   if (tid == 0) {
