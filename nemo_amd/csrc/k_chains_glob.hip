@@ -167,6 +167,9 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #define GS_SB 4        // row entries per row and step while staging a window
 #endif
 #define GS_NOLINK 0xFFFFu
+#ifndef GS_PF
+#define GS_PF 1        // next window's per-node staging data loaded during this window's sweep
+#endif
 template <bool UP, int GB>
 __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, const uint32_t *hs, const uint32_t *nlv,
                                            uint32_t *s_fail, GSweepLds &L, uint32_t *s_red, unsigned long long *st) {
@@ -178,9 +181,32 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t *off = UP ? S.pcoff : S.ccoff, *oend = UP ? S.pend : S.cend, *col = UP ? S.par : S.child;
   const uint32_t nwin = (n + GS_WN - 1) / GS_WN;
+  auto win = [&](uint32_t wi, uint32_t &w0, uint32_t &w1) {
+    w0 = UP ? wi * GS_WN : (n > (wi + 1) * GS_WN ? n - (wi + 1) * GS_WN : 0u);
+    w1 = UP ? min(n, w0 + GS_WN) : n - wi * GS_WN;
+  };
+  // a window's per-node data (row bounds, rule flag, node, crank) does not
+  // depend on the sweep, so the next window's is loaded before this window's
+  // sweep starts (GS_PF): wave 0 sweeps while those loads are in flight
+  uint32_t pr0[PT], pr1[PT], prl[PT], phs[PT], pcr[PT];
+  auto prefetch = [&](uint32_t wi) {
+    uint32_t a, b;
+    win(wi, a, b);
+#pragma unroll
+    for (int q = 0; q < PT; q++) {
+      const uint32_t k = tid + q * GB, i = a + k;
+      const bool in = wi < nwin && k < b - a;
+      pr0[q] = in ? off[i] : 0u;
+      pr1[q] = in ? oend[i] : 0u;
+      prl[q] = in ? S.rule[i] : 0u;
+      phs[q] = in ? hs[i] : 0u;
+      pcr[q] = in && !UP ? S.crank[i] : 0u;
+    }
+  };
+  if (GS_PF) prefetch(0);
   for (uint32_t wi = 0; wi < nwin; wi++) {
-    const uint32_t w0 = UP ? wi * GS_WN : (n > (wi + 1) * GS_WN ? n - (wi + 1) * GS_WN : 0u);
-    const uint32_t w1 = UP ? min(n, w0 + GS_WN) : n - wi * GS_WN;
+    uint32_t w0, w1;
+    win(wi, w0, w1);
     const uint32_t nw = w1 - w0;
     // ring = [base, base + GS_RING) around the window; link offsets relative to base
     const uint32_t base = UP ? (w1 > GS_RING ? w1 - GS_RING : 0u) : w0;
@@ -193,8 +219,8 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
     for (int q = 0; q < PT; q++) {
       const uint32_t k = tid + q * GB, i = w0 + k;
       const bool in = k < nw;
-      r0[q] = in ? off[i] : 0u;
-      r1[q] = in ? oend[i] : 0u;
+      r0[q] = GS_PF ? pr0[q] : (in ? off[i] : 0u);
+      r1[q] = GS_PF ? pr1[q] : (in ? oend[i] : 0u);
       cnt[q] = 0;
     }
     // the PT rows walked together, GS_SB entries of each per step: every load of
@@ -206,9 +232,9 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
     for (int q = 0; q < PT; q++) {
       const uint32_t k = tid + q * GB, i = w0 + k;
       const bool in = k < nw;
-      rl[q] = in ? S.rule[i] : 0u;
-      lv[q] = in ? nlv[hs[i]] : 0u;
-      cr[q] = in && !UP ? S.crank[i] : 0u;
+      rl[q] = GS_PF ? prl[q] : (in ? S.rule[i] : 0u);
+      lv[q] = in ? nlv[GS_PF ? phs[q] : hs[i]] : 0u;
+      cr[q] = GS_PF ? pcr[q] : (in && !UP ? S.crank[i] : 0u);
       dd[q] = UP ? (rl[q] ? 0 : -1) : -1;
       bc[q] = br[q] = bt[q] = GNIL;
     }
@@ -309,6 +335,7 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
     acc_s += t_b - t_a;
     t_a = t_b;
 #endif
+    if (GS_PF) prefetch(wi + 1);
     // ---- sweep (wave 0): the window's nodes level by level ----
     // Everything but the ring values is static, so the next batch's node data
     // (level, first links, staged far value) is read while the current batch
