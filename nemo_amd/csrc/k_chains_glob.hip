@@ -167,6 +167,7 @@ __device__ __forceinline__ uint32_t gmax_u32(uint32_t v, uint32_t *lds) {
 #define GS_SB 4        // row entries per row and step while staging a window
 #endif
 #define GS_NOLINK 0xFFFFu
+#define GS_RW 8        // row entries per load round when a node's extra in-ring links are listed
 #ifndef GS_PF
 #define GS_PF 1        // next window's per-node staging data loaded during this window's sweep
 #endif
@@ -317,13 +318,19 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
       L.flg[k] |= fits ? GS_MORE : (GS_MORE | GS_SPILL);
       L.aoff[k] = (uint16_t)(fits ? o : 0u);  // adj index of link t = aoff + t - GS_KEEP
       L.acnt[k] = (uint16_t)(fits ? cnt[q] : GS_KEEP);
-      if (fits) {
+      if (fits) {  // the row again, GS_RW entries per load round (one at a time was a chain of round trips)
         uint32_t x = 0;
-        for (uint32_t j = r0[q]; j < r1[q]; j++) {
-          const uint32_t p = col[j];
-          if (UP ? p >= base : p < base + GS_RING) {
-            if (x >= GS_KEEP) L.adj[o + x - GS_KEEP] = (uint16_t)(p - base);
-            x++;
+        for (uint32_t j = r0[q]; j < r1[q]; j += GS_RW) {
+          uint32_t pv[GS_RW];
+#pragma unroll
+          for (int h = 0; h < GS_RW; h++) pv[h] = j + h < r1[q] ? col[j + h] : GNIL;
+#pragma unroll
+          for (int h = 0; h < GS_RW; h++) {
+            const uint32_t p = pv[h];
+            if (p != GNIL && (UP ? p >= base : p < base + GS_RING)) {
+              if (x >= GS_KEEP) L.adj[o + x - GS_KEEP] = (uint16_t)(p - base);
+              x++;
+            }
           }
         }
       }
@@ -389,7 +396,16 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
             for (int h = 0; h < GS_KEEP; h++) d = max(d, u[h] != GS_NOLINK ? v[h] + 1 : d);
             if (fl & GS_MORE) {  // links past the first four: the window's list, or HBM
               const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
-              for (uint32_t t = GS_KEEP; t < ac; t++) d = max(d, L.rv[(base + L.adj[ao + t - GS_KEEP]) & M] + 1);
+              for (uint32_t t = GS_KEEP; t < ac; t += 4) {  // four links' reads in flight per round
+                uint32_t a4[4];
+                int32_t v4[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) a4[h] = L.adj[ao + min(t + h, ac - 1u) - GS_KEEP];
+#pragma unroll
+                for (int h = 0; h < 4; h++) v4[h] = L.rv[(base + a4[h]) & M];
+#pragma unroll
+                for (int h = 0; h < 4; h++) d = max(d, v4[h] + 1);  // clamped duplicates are harmless in a max
+              }
               if (fl & GS_SPILL)
                 for (uint32_t j = off[i]; j < oend[i]; j++) {
                   const uint32_t p = col[j];
@@ -421,9 +437,19 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
               if (u[h] != GS_NOLINK) take(base + u[h], dv[h], rr[h], tt[h]);
             if (fl & GS_MORE) {
               const uint32_t ao = L.aoff[kk], ac = L.acnt[kk];
-              for (uint32_t t = GS_KEEP; t < ac; t++) {
-                const uint32_t w = base + L.adj[ao + t - GS_KEEP];
-                take(w, L.rv[w & M], L.rc[w & M], L.rt[w & M]);
+              for (uint32_t t = GS_KEEP; t < ac; t += 4) {  // four links' reads in flight per round
+                uint32_t w4[4], r4[4], t4[4];
+                int32_t d4[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) w4[h] = base + L.adj[ao + min(t + h, ac - 1u) - GS_KEEP];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                  d4[h] = L.rv[w4[h] & M];
+                  r4[h] = L.rc[w4[h] & M];
+                  t4[h] = L.rt[w4[h] & M];
+                }
+#pragma unroll
+                for (int h = 0; h < 4; h++) take(w4[h], d4[h], r4[h], t4[h]);  // a clamped repeat cannot win twice
               }
               if (fl & GS_SPILL)
                 for (uint32_t j = off[i]; j < oend[i]; j++) {
