@@ -72,6 +72,9 @@ def parse():
                          "sweeps overlap another's bandwidth-bound passes (default: the config's)")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
+    ap.add_argument("--diff-reps", type=int, default=5,
+                    help="per_run differential-provenance leg after the timed steps (roofline_diff): this many "
+                         "nemo_diffprov(failed, NEMO_DIFF_PER_RUN) calls over the resident corpus (0: off)")
     return ap.parse_args()
 
 
@@ -300,14 +303,10 @@ def main():
     per_launch_bytes = d["bytes"] / d["launches"]
     avg_ms = d["ms"] / d["launches"]
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):  # per timed group, keyed by the workload's node count (tools/pmc_summary.py)
-        try:
-            pj = json.load(open(pmc)).get(dname, {}).get(str(int(corpus.node_off[-1])), {})
-            traffic = pj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(dname, corpus)
+    rdiff = None
+    if args.diff_reps > 0 and lanes_n == 1:
+        rdiff = diff_leg(args, eng, corpus, failed, world, torch, dist)
     e2e = None
     if rank == 0 and world == 1 and args.e2e_runs > 0 and not strong and args.config != "c5":
         for e in engines:
@@ -369,6 +368,8 @@ def main():
         out["e2e"] = e2e
     if "k_diff" in tim:  # all entries of a diffprov call run concurrently: the launch time is each entry's latency
         out["k_diff_entry_latency_ms"] = round(tim["k_diff"]["ms"] / tim["k_diff"]["launches"], 4)
+    if rdiff is not None:
+        out["roofline_diff"] = rdiff
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -380,6 +381,69 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(group, corpus):
+    """HBM bytes per launch of a timed group from profiles/pmc_summary.json (tools/pmc_summary.py: 2 x
+    FETCH_SIZE + WRITE_SIZE of the group's kernels), keyed by the workload's node count; None if absent."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(pmc):
+        return None
+    try:
+        return json.load(open(pmc)).get(group, {}).get(str(int(corpus.node_off[-1])), {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def diff_leg(args, eng, corpus, failed, world, torch, dist):
+    """roofline_diff: CreateNaiveDiffProv (differential-provenance.go:22-146) in the per-run label mode, every
+    distinct failed run computed, over the corpus already resident in HBM.  Each rep is one
+    nemo_diffprov(failed, NEMO_DIFF_PER_RUN) call plus its host hand-over (D masks, missing events).  The
+    library's k_diff group is timed with HIP events on the stream its kernels run on; its bytes are the HBM
+    lower bound DESIGN.md section 3 gives (run 0's post graph once, every label source, every D mask)."""
+    from nemo_amd.corpus import DIFF_PER_RUN
+    t_all = torch.tensor([0.0, 0.0, 0.0, float(len(failed))], dtype=torch.float64, device="cuda")
+    if failed:
+        eng.set_timing(True)
+        eng.reset_timings()
+        walls = []
+        for _ in range(args.diff_reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            eng.diffprov(failed, DIFF_PER_RUN)
+            eng.diff_masks_view()
+            eng.missing()
+            walls.append(time.perf_counter() - t)
+        k = eng.timings().get("k_diff")
+        eng.set_timing(False)
+        t_all[0] = k["ms"] / k["launches"]
+        t_all[1] = k["bytes"] / k["launches"]
+        t_all[2] = k["edges"] / k["launches"]
+        wall_ms = float(np.median(walls)) * 1e3
+    else:
+        wall_ms = 0.0
+    if world > 1:  # every rank's leg runs at once: the slowest rank's launch, the ranks' bytes and entries summed
+        mx = t_all[0:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_all)
+        t_all[0] = mx[0]
+    ms, nbytes, edges, entries = (float(x) for x in t_all.tolist())
+    if ms <= 0:
+        return None
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    r0 = corpus.run_index(0)
+    g0 = 2 * r0 + 1
+    return {"bound": "hbm", "kernel": "k_diff", "mode": "per_run", "entries": int(entries),
+            "distinct_label_sources": int(entries), "v0": int(corpus.graph_size(g0)),
+            "e0": int(corpus.edge_off[g0 + 1] - corpus.edge_off[g0]),
+            "bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 4), "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic("k_diff_per_run", corpus),
+            "edges_traversed_per_s": round(edges / (ms * 1e-3), 1),
+            "wall_ms_per_call": round(wall_ms, 3), "reps": args.diff_reps,
+            "bytes_formula": "8 E0 + 16 V0 (run 0's post graph) + 8 V per label source + V0 per D mask "
+                             "(DESIGN.md section 3, k_diff row)",
+            "edges_formula": "3 E0 per distinct label source (Fwd*, Bwd*, longest path)"}
 
 
 def make_lanes(corpus, n, new_engine, success, failed, mode):

@@ -144,6 +144,11 @@ func (n *Neo4J) LoadRawProvenance() error {
 				words = append(words, C.uint32_t(n.intern(&n.tables, n.tableID, goal.Table)))
 				labels = append(labels, C.uint32_t(n.intern(&n.labels, n.labelID, goal.Label)))
 			}
+			// Goal.id IS UNIQUE (pre-post-prov.go:66-81): a duplicate is not a second node
+			nGoals := len(index)
+			if nGoals != len(prov.Goals) {
+				return fmt.Errorf("Run %d: inserted number of goals (%d) does not equal number of antecedent provenance goals (%d)", run.Iteration, nGoals, len(prov.Goals))
+			}
 			for _, rule := range prov.Rules {
 				index[rule.ID] = uint32(len(ids))
 				ids = append(ids, rule.ID)
@@ -151,8 +156,8 @@ func (n *Neo4J) LoadRawProvenance() error {
 				words = append(words, C.uint32_t(w))
 				labels = append(labels, C.uint32_t(n.intern(&n.labels, n.labelID, rule.Label)))
 			}
-			if len(index) != len(ids) { // Goal.id / Rule.id IS UNIQUE (pre-post-prov.go:66-81,126-141)
-				return fmt.Errorf("Run %d: inserted number of nodes does not equal number of %s provenance nodes", run.Iteration, cond)
+			if len(index)-nGoals != len(prov.Rules) { // Rule.id IS UNIQUE (:126-141)
+				return fmt.Errorf("Run %d: inserted number of rules (%d) does not equal number of antecedent provenance rules (%d)", run.Iteration, len(index)-nGoals, len(prov.Rules))
 			}
 			// rank of each ID inside the graph: the canonical @next tie-break (DESIGN.md §1)
 			order := make([]int, len(ids))
@@ -305,29 +310,35 @@ func (n *Neo4J) node(g int, i uint32, flags []uint8, run *uint) graph.Node {
 		"id": id, "label": rule.Label, "table": rule.Table, "type": rule.Type}}
 }
 
-func (n *Neo4J) flags(g int) []uint8 {
+func (n *Neo4J) flags(g int) ([]uint8, error) {
 	f := make([]uint8, n.graphs[g].n()+1)
-	C.nemo_fetch_node_flags(n.ctx, C.uint32_t(g), C.uint32_t(g+1), (*C.uint8_t)(&f[0]), C.uint64_t(len(f)))
-	return f
+	if err := n.err(C.nemo_fetch_node_flags(n.ctx, C.uint32_t(g), C.uint32_t(g+1), (*C.uint8_t)(&f[0]), C.uint64_t(len(f)))); err != nil {
+		return nil, err
+	}
+	return f, nil
 }
 
 // paths turns pulled slot `slot` of graph g into the []graph.Path rows
 // createDOT / createDiffDot consume, in (source, target) order.
-func (n *Neo4J) paths(slot uint32, g int, run *uint) []graph.Path {
+func (n *Neo4J) paths(slot uint32, g int, run *uint) ([]graph.Path, error) {
 	var cnt C.uint64_t
-	C.nemo_fetch_pulled(n.ctx, C.uint32_t(slot), nil, nil, 0, &cnt)
+	if err := n.err(C.nemo_fetch_pulled(n.ctx, C.uint32_t(slot), nil, nil, 0, &cnt)); err != nil {
+		return nil, err
+	}
 	s, d := make([]uint32, cnt+1), make([]uint32, cnt+1)
-	C.nemo_fetch_pulled(n.ctx, C.uint32_t(slot), (*C.uint32_t)(&s[0]), (*C.uint32_t)(&d[0]), cnt, &cnt)
+	if err := n.err(C.nemo_fetch_pulled(n.ctx, C.uint32_t(slot), (*C.uint32_t)(&s[0]), (*C.uint32_t)(&d[0]), cnt, &cnt)); err != nil {
+		return nil, err
+	}
 	return n.edgeRows(s[:cnt], d[:cnt], g, run)
 }
 
 // rawPaths: the rows of raw graph g (run i, pre-post-prov.go:298-301) are its
 // loaded edges, which the binding holds, so no device pull is needed.
-func (n *Neo4J) rawPaths(g int) []graph.Path {
+func (n *Neo4J) rawPaths(g int) ([]graph.Path, error) {
 	return n.edgeRows(n.graphs[g].src, n.graphs[g].dst, g, nil)
 }
 
-func (n *Neo4J) edgeRows(s, d []uint32, g int, run *uint) []graph.Path {
+func (n *Neo4J) edgeRows(s, d []uint32, g int, run *uint) ([]graph.Path, error) {
 	cnt := len(s)
 	idx := make([]int, cnt)
 	for i := range idx {
@@ -339,13 +350,16 @@ func (n *Neo4J) edgeRows(s, d []uint32, g int, run *uint) []graph.Path {
 		}
 		return d[idx[a]] < d[idx[b]]
 	})
-	fl := n.flags(g)
+	fl, err := n.flags(g)
+	if err != nil {
+		return nil, err
+	}
 	out := make([]graph.Path, 0, cnt)
 	for _, j := range idx {
 		out = append(out, graph.Path{Nodes: []graph.Node{n.node(g, s[j], fl, run), n.node(g, d[j], fl, run)},
 			Relationships: []graph.UnboundRelationship{{Type: "DUETO"}}})
 	}
-	return out
+	return out, nil
 }
 
 // PullPrePostProv (pre-post-prov.go:288-459): raw graphs (run i) and
@@ -355,11 +369,18 @@ func (n *Neo4J) PullPrePostProv() ([]*gographviz.Graph, []*gographviz.Graph, []*
 	pre, post := make([]*gographviz.Graph, R), make([]*gographviz.Graph, R)
 	preC, postC := make([]*gographviz.Graph, R), make([]*gographviz.Graph, R)
 	var err error
+	var rows []graph.Path
 	for r := 0; r < R; r++ {
-		if pre[r], err = createDOT(n.rawPaths(2*r), "pre"); err != nil {
+		if rows, err = n.rawPaths(2 * r); err != nil {
 			return nil, nil, nil, nil, err
 		}
-		if post[r], err = createDOT(n.rawPaths(2*r+1), "post"); err != nil {
+		if pre[r], err = createDOT(rows, "pre"); err != nil {
+			return nil, nil, nil, nil, err
+		}
+		if rows, err = n.rawPaths(2*r + 1); err != nil {
+			return nil, nil, nil, nil, err
+		}
+		if post[r], err = createDOT(rows, "post"); err != nil {
 			return nil, nil, nil, nil, err
 		}
 	}
@@ -368,10 +389,16 @@ func (n *Neo4J) PullPrePostProv() ([]*gographviz.Graph, []*gographviz.Graph, []*
 	}
 	for r := 0; r < R; r++ {
 		clean := 1000 + n.Runs[r].Iteration
-		if preC[r], err = createDOT(n.paths(uint32(2*r), 2*r, &clean), "pre"); err != nil {
+		if rows, err = n.paths(uint32(2*r), 2*r, &clean); err != nil {
 			return nil, nil, nil, nil, err
 		}
-		if postC[r], err = createDOT(n.paths(uint32(2*r+1), 2*r+1, &clean), "post"); err != nil {
+		if preC[r], err = createDOT(rows, "pre"); err != nil {
+			return nil, nil, nil, nil, err
+		}
+		if rows, err = n.paths(uint32(2*r+1), 2*r+1, &clean); err != nil {
+			return nil, nil, nil, nil, err
+		}
+		if postC[r], err = createDOT(rows, "post"); err != nil {
 			return nil, nil, nil, nil, err
 		}
 	}
@@ -491,14 +518,19 @@ func (n *Neo4J) CreateNaiveDiffProv(symmetric bool, failedRuns []uint, successPo
 		return unsafe.Slice((*uint8)(unsafe.Pointer(masks)), int(ne)*V0)[e*V0 : (e+1)*V0]
 	}
 	var cnt C.uint64_t
-	C.nemo_fetch_missing(n.ctx, nil, 0, &cnt)
+	if err := n.err(C.nemo_fetch_missing(n.ctx, nil, 0, &cnt)); err != nil {
+		return nil, nil, nil, err
+	}
 	rows := make([]C.nemo_missing, cnt+1)
 	if err := n.err(C.nemo_fetch_missing(n.ctx, &rows[0], cnt, &cnt)); err != nil {
 		return nil, nil, nil, err
 	}
 	// D-children of every missing rule from run 0's post edges (the interned arrays)
 	children := n.childrenOf(g0)
-	fl := n.flags(g0)
+	fl, err := n.flags(g0)
+	if err != nil {
+		return nil, nil, nil, err
+	}
 	missing := make([][]*fi.Missing, len(failedRuns))
 	for _, row := range rows[:cnt] {
 		e, rule := int(row.entry), uint32(row.rule)
@@ -519,13 +551,18 @@ func (n *Neo4J) CreateNaiveDiffProv(symmetric bool, failedRuns []uint, successPo
 	diffEdges := make([][]graph.Path, len(failedRuns))
 	for e, it := range failedRuns {
 		run := 2000 + it
-		diffEdges[e] = n.paths(uint32(e), g0, &run)
+		if diffEdges[e], err = n.paths(uint32(e), g0, &run); err != nil {
+			return nil, nil, nil, err
+		}
 	}
 	diffDots, failedDots := make([]*gographviz.Graph, len(failedRuns)), make([]*gographviz.Graph, len(failedRuns))
 	for e, it := range failedRuns {
 		gf := 2*n.runIdx[it] + 1
-		var err error
-		diffDots[e], failedDots[e], err = createDiffDot(2000+it, diffEdges[e], it, n.rawPaths(gf), 0,
+		failedRows, err := n.rawPaths(gf)
+		if err != nil {
+			return nil, nil, nil, err
+		}
+		diffDots[e], failedDots[e], err = createDiffDot(2000+it, diffEdges[e], it, failedRows, 0,
 			successPostProv, missing[e])
 		if err != nil {
 			return nil, nil, nil, err
@@ -571,7 +608,9 @@ func (n *Neo4J) triggers() (*triggerRows, error) {
 		return nil, err
 	}
 	var np, nq, na C.uint64_t
-	C.nemo_fetch_triggers(n.ctx, nil, 0, &np, nil, 0, &nq, nil, 0, &na)
+	if err := n.err(C.nemo_fetch_triggers(n.ctx, nil, 0, &np, nil, 0, &nq, nil, 0, &na)); err != nil {
+		return nil, err
+	}
 	pre, post, asy := make([]C.uint32_t, 3*np+1), make([]C.uint32_t, 2*nq+1), make([]C.uint32_t, na+1)
 	if err := n.err(C.nemo_fetch_triggers(n.ctx, &pre[0], np, &np, &post[0], nq, &nq, &asy[0], na, &na)); err != nil {
 		return nil, err
@@ -606,7 +645,14 @@ func (n *Neo4J) GenerateCorrections() ([]string, error) {
 	}
 	r0 := n.runIdx[0]
 	gp, gq := 2*r0, 2*r0+1
-	flp, flq := n.flags(gp), n.flags(gq)
+	flp, err := n.flags(gp)
+	if err != nil {
+		return nil, err
+	}
+	flq, err := n.flags(gq)
+	if err != nil {
+		return nil, err
+	}
 	preTriggers := map[*fi.Rule][]*GoalRulePair{}
 	for _, row := range t.pre {
 		goal := goalOf(n.node(gp, row[1], flp, nil))
@@ -642,7 +688,10 @@ func (n *Neo4J) GenerateExtensions() (bool, []string, error) {
 		return false, nil, err
 	}
 	gp := 2 * n.runIdx[0]
-	fl := n.flags(gp)
+	fl, err := n.flags(gp)
+	if err != nil {
+		return false, nil, err
+	}
 	state := map[string]string{}
 	for _, r := range t.async { // one suggestion per distinct table (:83-90)
 		table := n.node(gp, r, fl, nil).Properties["table"].(string)

@@ -335,20 +335,24 @@ int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index, const cha
 void nemo_ingest_free(nemo_ingest *h);
 /* Streaming form: the same directory parsed chunk by chunk
  * so that chunk i is loaded and analysed on the device while chunk i+1 is
- * being parsed.  Interning is shared across chunks (ids in graph order, as the
- * one-shot ingest assigns them); table "pre"/"post" ids are fixed by the first
- * chunk.  nemo_ingest_next parses the next `chunk` runs into a corpus and,
- * with `with_run0`, prepends the run of iteration 0 as a replicated, not-owned
- * run to every chunk after the one holding it (the good run of the diffs,
- * differential-provenance.go:26).  Run 0 is parsed first, into the first
- * chunk, wherever runs.json lists it, so every chunk that holds a failed run
- * also holds the good run.  Returns NEMO_ERR_NOTFOUND when no run is left;
- * validation failures as nemo_ingest_molly.  Lifetime: the ingest keeps two
- * buffers, so the arrays of chunk i stay valid until the call that returns
- * chunk i+2; chunk i can be uploaded while chunk i+1 is parsed.             */
+ * being parsed.  Interning is shared across chunks; ids are assigned in parse
+ * order (below), so they can differ from nemo_ingest_molly's when run 0 or
+ * failedRuns[0] is not first in runs.json; table "pre"/"post" ids are fixed
+ * by the first chunk.  nemo_ingest_next parses the next `chunk` runs into a
+ * corpus and, with `with_run0`, prepends the run of iteration 0 as a
+ * replicated, not-owned run to every chunk after the one holding it (the good
+ * run of the diffs, differential-provenance.go:26).  Parse order: the run of
+ * iteration 0, then the run at index `first_failed` (failedRuns[0], whose
+ * post-goal labels every reference-mode diff uses, :22-43; -1: none), then
+ * the rest in runs.json order.  So with chunk >= 2 the first chunk holds
+ * both, and every chunk that holds a failed run also holds the good run.
+ * Returns NEMO_ERR_NOTFOUND when no run is left; validation failures as
+ * nemo_ingest_molly.  Lifetime: the ingest keeps two buffers, so the arrays
+ * of chunk i stay valid until the call that returns chunk i+2; chunk i can be
+ * uploaded while chunk i+1 is parsed.                                      */
 typedef struct nemo_ingest_stream nemo_ingest_stream;
-int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
-                     nemo_ingest_stream **out);
+int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int64_t first_failed,
+                     int threads, nemo_ingest_stream **out);
 int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_run0, nemo_corpus *corpus, char *err,
                      size_t err_cap);
 uint64_t nemo_ingest_stream_count(const nemo_ingest_stream *s, int kind);

@@ -1894,6 +1894,8 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "redo") base = c->dc.redo;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
+  int rc = join_aux(c);  // the diff kernels on `aux` write dbits, dmask and the Kahn relayout
+  if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(out, (const char *)base + offset, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return NEMO_OK;

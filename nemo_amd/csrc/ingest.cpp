@@ -611,13 +611,13 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
 
 // ---- streaming ingest: chunk i is analysed on the device
 // while chunk i+1 is being parsed.  Interning is shared across chunks (ids are
-// assigned in graph order, as the one-shot ingest assigns them), so the
-// chunks' label and table ids agree with each other; the run of iteration 0
+// assigned in parse order), so the chunks' label and table ids agree with
+// each other; the run of iteration 0
 // is replicated, not owned, into every chunk after the one holding it.
 struct nemo_ingest_stream {
   std::string dir;
   std::vector<uint32_t> iteration;
-  std::vector<uint32_t> order;  // parse order: run 0 first, then runs.json order
+  std::vector<uint32_t> order;  // parse order: run 0, failedRuns[0], then runs.json order
   int threads = 1;
   uint32_t next = 0;  // next position in `order`
   std::unordered_map<std::string, uint32_t> tmap, lmap;
@@ -637,15 +637,17 @@ struct nemo_ingest_stream {
   uint32_t calls = 0;
 };
 
-extern "C" int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs, int threads,
-                                nemo_ingest_stream **out) {
-  if (!out_dir || !out || (n_runs && !iterations)) return NEMO_ERR_INVALID;
+extern "C" int nemo_ingest_open(const char *out_dir, const uint32_t *iterations, uint32_t n_runs,
+                                int64_t first_failed, int threads, nemo_ingest_stream **out) {
+  if (!out_dir || !out || (n_runs && !iterations) || first_failed >= (int64_t)n_runs) return NEMO_ERR_INVALID;
   auto *s = new nemo_ingest_stream();
   s->dir = out_dir;
   s->iteration.assign(iterations, iterations + n_runs);
   s->threads = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  // run 0 is the good run of every diff (differential-provenance.go:26): it is
-  // parsed first, so every chunk that holds a failed run also holds run 0
+  // run 0 is the good run of every diff (differential-provenance.go:26) and
+  // failedRuns[0] the label source of every reference-mode diff (:22-43): both
+  // are parsed first, so the first chunk holds them and every chunk that holds
+  // a failed run also holds the good run
   int64_t r0 = -1;
   for (uint32_t r = 0; r < n_runs && r0 < 0; r++)
     if (iterations[r] == 0) r0 = r;
@@ -653,8 +655,9 @@ extern "C" int nemo_ingest_open(const char *out_dir, const uint32_t *iterations,
     s->order.push_back((uint32_t)r0);
     s->run0 = 0;
   }
+  if (first_failed >= 0 && first_failed != r0) s->order.push_back((uint32_t)first_failed);
   for (uint32_t r = 0; r < n_runs; r++)
-    if ((int64_t)r != r0) s->order.push_back(r);
+    if ((int64_t)r != r0 && (int64_t)r != first_failed) s->order.push_back(r);
   *out = s;
   return NEMO_OK;
 }

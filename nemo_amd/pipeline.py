@@ -34,7 +34,7 @@ def _lib():
     L = E.lib()
     if not getattr(L, "_stream_sigs", False):
         vp, P = ctypes.c_void_p, ctypes.POINTER
-        L.nemo_ingest_open.argtypes = [ctypes.c_char_p, vp, ctypes.c_uint32, ctypes.c_int, P(vp)]
+        L.nemo_ingest_open.argtypes = [ctypes.c_char_p, vp, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int, P(vp)]
         L.nemo_ingest_open.restype = ctypes.c_int
         L.nemo_ingest_next.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, P(CCorpus), ctypes.c_char_p, ctypes.c_size_t]
         L.nemo_ingest_next.restype = ctypes.c_int
@@ -57,10 +57,12 @@ class IngestStream:
             self.runs = json.load(fh)
         self.iteration = np.asarray([int(r["iteration"]) for r in self.runs], dtype=np.uint32)
         self.status = {int(r["iteration"]): r.get("status", "") for r in self.runs}
+        # failedRuns[0] (GetFailedRunsIters order, molly.go:53) is parsed right after run 0
+        first_failed = next((i for i, r in enumerate(self.runs) if r.get("status", "") != "success"), -1)
         self.L = _lib()
         self.h = ctypes.c_void_p()
         rc = self.L.nemo_ingest_open(out_dir.encode(), self.iteration.ctypes.data if len(self.iteration) else None,
-                                     len(self.iteration), threads, ctypes.byref(self.h))
+                                     len(self.iteration), first_failed, threads, ctypes.byref(self.h))
         if rc != 0:
             raise LoadError(f"nemo_ingest_open failed ({rc})")
 
@@ -144,12 +146,14 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
     if 0 in success:
         success = [0] + [x for x in success if x != 0]
     failed = [it for it in its if not ok[it]]
-    if failed and 0 not in ok:
-        raise LoadError("failed runs but no run of iteration 0: the diffs need the good run "
-                        "(differential-provenance.go:26)")
+    if failed and diff_mode == DIFF_REFERENCE and chunk < 2:
+        raise ValueError("the reference diff mode needs chunk >= 2: run 0 and failedRuns[0] share the first chunk")
+    # no run of iteration 0: CreateNaiveDiffProv's MATCH on run 0 finds nothing (differential-provenance.go:
+    # 22-28) and every diff is empty, which the library reports as zero entries
+    has_good = 0 in ok
     f0 = failed[0] if failed else None
     f0_labels = None
-    run_of = {it: r for r, it in enumerate(its)}  # the stream parses run 0 first, then runs.json order
+    run_of = {it: r for r, it in enumerate(its)}  # results are kept in runs.json order
     res = PipelineResult(n_runs=len(its))
     acc = np.zeros(0, np.int64)  # summed [cnt[T], first[T], achvd, first_nonempty, prehold, nruns]
     T_seen = 0
@@ -193,7 +197,7 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
         chunk_its = [int(x) for x, o in zip(c.iteration, own) if o]
         cf = [f for f in failed if f in set(chunk_its)]
         if cf and diff_mode == DIFF_REFERENCE:
-            if f0_labels is None:  # failedRuns[0] is the first failed run in parse order: it is in this chunk
+            if f0_labels is None:  # the stream parses run 0 and failedRuns[0] first: both are in the first chunk
                 g = 2 * c.run_index(f0) + 1
                 n0, n1 = int(c.node_off[g]), int(c.node_off[g + 1])
                 f0_labels = c.label[n0:n1][(c.node_word[n0:n1] & NODE_RULE) == 0].copy()
@@ -207,7 +211,7 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
         # host hand-over, as bench.py retrieves it
         state, chain_off, chain_ht = engine.simplified_view()
         tabs = (engine.run_tables(0), engine.run_tables(1))
-        masks = engine.diff_masks_view() if cf else None
+        masks = engine.diff_masks_view() if cf and has_good else None
         miss = engine.missing()
         trig = engine.trigger_rows() if has0 else None
         if keep:
@@ -225,7 +229,7 @@ def run(out_dir: str, engine: "E.Engine", chunk: int = 500, threads: int = 0, di
                     rows[:, 0] = 2 * r + k
                     res.chains.append(rows)
                 res.run_tables[r] = (tabs[0][lr].copy(), tabs[1][lr].copy())
-            for e, f in enumerate(cf):
+            for e, f in enumerate(cf if has_good else []):
                 res.diff_mask[f] = np.asarray(masks[e]).copy()
                 res.missing[f] = np.sort(miss[miss[:, 0] == e][:, 1])
             if trig is not None:

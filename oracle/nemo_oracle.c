@@ -798,23 +798,36 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
     g->flags = out->flags + n0;
   }
   int nth = o->threads > 0 ? o->threads : 1;
+  /* diff_only: the graphs CreateNaiveDiffProv reads, run 0's post graph and each entry's label source */
+  uint8_t *need = calloc((size_t)G + 1, 1);
+  if (o->diff_only) {
+    int r0 = find_run(c, 0);
+    if (r0 >= 0) need[2 * r0 + 1] = 1;
+    for (size_t e = 0; e < o->n_failed && !o->diff_labels; e++) {
+      int fr = find_run(c, o->diff_mode == NEMO_DIFF_PER_RUN ? o->failed_iters[e] : o->failed_iters[0]);
+      if (fr >= 0) need[2 * fr + 1] = 1;
+    }
+  }
   /* LoadRawProvenance (pre-post-prov.go:247-285) then SimplifyProv (preprocessing.go:351-387) */
 #pragma omp parallel for schedule(dynamic, 4) num_threads(nth)
   for (uint32_t gi = 0; gi < G; gi++) {
     graph_t *g = &gs[gi];
+    if (o->diff_only && !need[gi]) continue;
     load_graph(g, c->iteration[gi / 2]);
     if (!g->err) topo_sort(g, c->iteration[gi / 2]);
-    if (!g->err) {
+    if (!g->err && !o->diff_only) {
       mark_holds(g, T);
       clean_copy(g);
       collapse(g);
     }
   }
+  free(need);
   for (uint32_t gi = 0; gi < G; gi++)
     if (gs[gi].err) {
       oerr(out, gs[gi].err, "%s", gs[gi].msg);
       goto done;
     }
+  if (o->diff_only) goto diff;
   /* graph' per graph: proto list (post), table set (post), pulled edges */
   out->proto_bits = calloc((size_t)c->n_runs * W + 1, sizeof(uint32_t));
   out->graph_tables = calloc((size_t)c->n_runs * W + 1, sizeof(uint32_t));
@@ -912,6 +925,7 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
     }
   }
   /* differential provenance (differential-provenance.go:18-243) */
+diff:
   out->run0 = find_run(c, 0);
   if (out->run0 >= 0 && o->n_failed > 0) {
     const graph_t *g0 = &gs[2 * out->run0 + 1];
@@ -933,7 +947,7 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
     out->v0 = gs[2 * out->run0 + 1].V;
   }
   /* triggers on run 0 (corrections.go:30-34,121-125) and async rules (extensions.go:63-67) */
-  if (out->run0 >= 0) {
+  if (out->run0 >= 0 && !o->diff_only) {
     const graph_t *gp = &gs[2 * out->run0], *gq = &gs[2 * out->run0 + 1];
     uint64_t cap = 16;
     out->pre_rows = malloc(cap * 3 * sizeof(uint32_t));

@@ -37,6 +37,9 @@ typedef struct oracle_opts {
   const uint32_t *diff_labels;    /* non-NULL: failGoals label set of every diff entry
                                      (sharded reference mode: failedRuns[0]'s labels) */
   size_t n_diff_labels;
+  int diff_only;                  /* 1: only CreateNaiveDiffProv (differential-provenance.go:18-146):
+                                     load run 0's post graph and the label sources, no simplification,
+                                     prototypes, pulls or triggers (implies skip_pulls)              */
 } oracle_opts;
 
 typedef struct oracle_out {

@@ -69,6 +69,7 @@ class COpts(ctypes.Structure):
         ("skip_pulls", ctypes.c_int),
         ("diff_labels", ctypes.c_void_p),
         ("n_diff_labels", ctypes.c_size_t),
+        ("diff_only", ctypes.c_int),
     ]
 
 
@@ -131,8 +132,12 @@ class OracleResult:
 
 
 def analyze(corpus: Corpus, success: Sequence[int], failed: Sequence[int], diff_mode: int = 0,
-            threads: int = 1, skip_pulls: bool = False, diff_labels: Optional[Sequence[int]] = None) -> OracleResult:
-    """diff_labels: failGoals label set of every diff entry (the sharded reference mode's broadcast set)."""
+            threads: int = 1, skip_pulls: bool = False, diff_labels: Optional[Sequence[int]] = None,
+            diff_only: bool = False) -> OracleResult:
+    """diff_labels: failGoals label set of every diff entry (the sharded reference mode's broadcast set).
+    diff_only: only CreateNaiveDiffProv (run 0's post graph and the label sources are loaded; flags,
+    chains, prototypes, pulls and triggers come back empty)."""
+    skip_pulls = skip_pulls or diff_only
     L = lib()
     cs = corpus.c_struct()
     s = np.asarray(success, dtype=np.uint32)
@@ -140,7 +145,8 @@ def analyze(corpus: Corpus, success: Sequence[int], failed: Sequence[int], diff_
     dl = None if diff_labels is None else np.ascontiguousarray(diff_labels, dtype=np.uint32)
     dbuf = None if dl is None else (dl if len(dl) else np.zeros(1, np.uint32))  # non-NULL even when empty
     o = COpts(threads, s.ctypes.data if len(s) else None, len(s), f.ctypes.data if len(f) else None, len(f),
-              diff_mode, int(skip_pulls), None if dbuf is None else dbuf.ctypes.data, 0 if dl is None else len(dl))
+              diff_mode, int(skip_pulls), None if dbuf is None else dbuf.ctypes.data, 0 if dl is None else len(dl),
+              int(diff_only))
     out = COut()
     rc = L.oracle_analyze(ctypes.byref(cs), ctypes.byref(o), ctypes.byref(out))
     try:
@@ -152,8 +158,8 @@ def analyze(corpus: Corpus, success: Sequence[int], failed: Sequence[int], diff_
         res = OracleResult(
             flags=_arr(out.flags, out.V, np.uint8),
             chains=ch.reshape(-1, 5),
-            proto_bits=_arr(out.proto_bits, R * W, np.uint32).reshape(R, W),
-            graph_tables=_arr(out.graph_tables, R * W, np.uint32).reshape(R, W),
+            proto_bits=_arr(out.proto_bits, R * W, np.uint32).reshape(-1, W),
+            graph_tables=_arr(out.graph_tables, R * W, np.uint32).reshape(-1, W),
             reduce=_arr(out.reduce, 2 * out.n_tables + 4, np.uint32),
             achieved=out.achieved,
             inter=list(_arr(out.inter, out.n_inter, np.uint32)),

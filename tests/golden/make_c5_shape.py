@@ -15,7 +15,14 @@ src<<32|dst keys); per run: the proto table bits (success runs) and the simplifi
 per failed run in the per-run diff mode: sha256 + popcount of the D mask over run 0's post graph and
 the missing rules.  The reference mode's entries all equal failedRuns[0]'s per-run entry.
 
-Usage: python tests/golden/make_c5_shape.py  (writes tests/golden/c5_shape/digest.json)
+Two additions pin the digest further (round 4):
+  --diff-all   the per-run diff of EVERY failed run of the 128-run corpus (the oracle's diff-only mode:
+               run 0's post graph and each failed run's post-goal labels), under "diff_per_run_all";
+  --rescan     the oracle's literal greedy rescan (NEMO_ORACLE_RESCAN=1, preprocessing.go:108-138 as the
+               queries read) on the digest's four runs, its flags and chains compared with the digest's
+               (which come from greedy_incremental), recorded as "rescan_equal".
+
+Usage: python tests/golden/make_c5_shape.py [--diff-all | --rescan]  (writes tests/golden/c5_shape/digest.json)
 """
 import hashlib
 import json
@@ -28,7 +35,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
-BENCH_RUNS = 128  # bench.py CONFIGS["c5"]["runs"]
+BENCH_RUNS = 128  # the first 128 runs of bench.py --config c5 (each run's graphs depend only on its own seed)
 OUT = os.path.join(ROOT, "tests", "golden", "c5_shape", "digest.json")
 
 
@@ -109,5 +116,75 @@ def main():
     print("wrote", OUT, f"total {time.time() - t0:.0f}s")
 
 
+def diff_all():
+    """Per-run D masks and missing rules of every failed run of the corpus (oracle diff-only mode)."""
+    from oracle import oracle as O
+    t0 = time.time()
+    full = bench_corpus(threads=min(16, os.cpu_count() or 1))
+    ok = [st == "success" for st in full.status]
+    its = [int(x) for x in full.iteration]
+    r0 = its.index(0)
+    frs = [r for r in range(full.n_runs) if not ok[r]]
+    sub = full.subset([r0] + frs)
+    del full
+    f_its = [its[r] for r in frs]
+    t = time.time()
+    orc = O.analyze(sub, [0], f_its, diff_mode=1, threads=min(8, os.cpu_count() or 1), diff_only=True)
+    dig = json.load(open(OUT))
+    ent = {}
+    for e, it in enumerate(f_its):
+        m = orc.diff_mask[e]
+        ent[str(it)] = {"mask_sha256": sha(m), "mask_popcount": int(np.count_nonzero(m)),
+                        "missing": sorted(int(x) for x in orc.missing[orc.missing[:, 0] == e][:, 1])}
+    dig["diff_per_run_all"] = {"failed_iters": f_its, "entries": ent, "oracle_seconds": round(time.time() - t, 1),
+                               "how": "oracle diff-only mode (run 0's post graph + each failed run's post-goal "
+                                      "labels), per-run label mode"}
+    for r in dig["runs"]:  # the four-run digest's own entries must agree
+        if "diff_per_run" in r:
+            assert r["diff_per_run"] == ent[str(r["iteration"])], r["iteration"]
+    with open(OUT, "w") as fh:
+        json.dump(dig, fh, indent=1)
+    print(f"{len(f_its)} failed runs, wrote {OUT}, total {time.time() - t0:.0f}s")
+
+
+def rescan():
+    """The literal greedy rescan on the digest's runs: flags and chains must equal the digest's."""
+    from oracle import oracle as O
+    t0 = time.time()
+    full = bench_corpus(threads=min(16, os.cpu_count() or 1))
+    runs, f_its = pick_runs(full)
+    sub = full.subset(runs)
+    del full
+    dig = json.load(open(OUT))
+    os.environ["NEMO_ORACLE_RESCAN"] = "1"
+    t = time.time()
+    s = [0] + [x for x in sub.success_iters() if x != 0]
+    orc = O.analyze(sub, s, f_its, diff_mode=1, threads=min(8, os.cpu_count() or 1), skip_pulls=True)
+    del os.environ["NEMO_ORACLE_RESCAN"]
+    secs = time.time() - t
+    same = True
+    for i, r in enumerate(dig["runs"]):
+        assert int(sub.iteration[i]) == r["iteration"]
+        for k in (0, 1):
+            g = 2 * i + k
+            a, b = int(sub.node_off[g]), int(sub.node_off[g + 1])
+            ch = orc.chains[orc.chains[:, 0] == g][:, 1:5]
+            want = r["graphs"][k]
+            ok = sha(orc.flags[a:b]) == want["flags_sha256"] and chain_digest(ch) == want["chains"]
+            print(f"run {r['iteration']} graph {k}: {'equal' if ok else 'DIFFERENT'}", flush=True)
+            same &= ok
+    dig["rescan_equal"] = {"equal": bool(same), "graphs": 2 * len(dig["runs"]), "oracle_seconds": round(secs, 1),
+                           "how": "NEMO_ORACLE_RESCAN=1 (greedy_rescan, the literal recompute after every "
+                                  "accepted chain) on the digest's runs: flags and chains vs the digest"}
+    with open(OUT, "w") as fh:
+        json.dump(dig, fh, indent=1)
+    print(f"rescan equal={same}, wrote {OUT}, total {time.time() - t0:.0f}s")
+
+
 if __name__ == "__main__":
-    main()
+    if "--diff-all" in sys.argv:
+        diff_all()
+    elif "--rescan" in sys.argv:
+        rescan()
+    else:
+        main()

@@ -1,14 +1,16 @@
-"""GPU parity on the bench's own C5 workload (bench.py --config c5: 128 runs of ~1M-node / ~4.2M-edge
-graphs at EOT 2000), against the oracle digest tests/golden/c5_shape/digest.json that
+"""GPU parity on the bench's own C5 workload: the first 128 runs of bench.py --config c5's corpus (~1M-node
+/ ~4.2M-edge graphs at EOT 2000; the bench keeps 320 runs resident, and each run's graphs depend only on
+its own seed), against the oracle digest tests/golden/c5_shape/digest.json that
 tests/golden/make_c5_shape.py computed once in the build container (the oracle's greedy chain cover
 takes ~15 min per 1M-node graph, too long for a GPU test).
 
 The whole 128-run corpus goes through libnemohip at its default tiers (deep CSR / Kahn, k_chains_glob,
-the k_pg_* protos, the global k_diff tier, the multi-workgroup pulls), exactly as the bench runs it; the
+the k_pg_* protos, the global diff tier, the multi-workgroup pulls), exactly as the bench runs it; the
 digest's four runs (run 0, a success run, the first two failed runs) are then compared field by field:
-node flags, accepted chains, simplified-graph edges, proto bits, table sets, and the D masks and missing
-rules of both diff modes (the reference mode's entries all equal failedRuns[0]'s per-run entry,
-differential-provenance.go:22-43).  Reference: preprocessing.go:13-348, prototype.go:9-206,
+node flags, accepted chains, simplified-graph edges, proto bits, table sets; the per-run D masks and
+missing rules of all 16 failed runs (the digest's diff_per_run_all, from the oracle's diff-only mode);
+and the reference mode, whose entries all equal failedRuns[0]'s per-run entry
+(differential-provenance.go:22-43).  Reference: preprocessing.go:13-348, prototype.go:9-206,
 differential-provenance.go:18-146, pre-post-prov.go:288-459.
 """
 import json
@@ -70,6 +72,15 @@ def test_c5_bench_corpus_matches_oracle_digest():
                 masks, miss = modes[DIFF_PER_RUN]
                 assert sha(masks[e]) == d["mask_sha256"] and int(np.count_nonzero(masks[e])) == d["mask_popcount"]
                 assert sorted(int(x) for x in miss[miss[:, 0] == e][:, 1]) == d["missing"]
+        # per-run mode: every failed run of the corpus (diff_per_run_all)
+        alld = dig["diff_per_run_all"]
+        assert alld["failed_iters"] == f
+        masks, miss = modes[DIFF_PER_RUN]
+        for e, it in enumerate(f):
+            d = alld["entries"][str(it)]
+            assert sha(masks[e]) == d["mask_sha256"], f"per-run D mask of failed run {it}"
+            assert int(np.count_nonzero(masks[e])) == d["mask_popcount"]
+            assert sorted(int(x) for x in miss[miss[:, 0] == e][:, 1]) == d["missing"], f"missing of {it}"
         # reference mode: every entry is failedRuns[0]'s per-run entry
         d0 = next(e["diff_per_run"] for e in dig["runs"] if e["iteration"] == f_its[0])
         masks, miss = modes[DIFF_REFERENCE]

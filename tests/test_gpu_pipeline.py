@@ -94,3 +94,32 @@ def test_pipeline_run0_not_first(eng, tmp_path):
     for e, it in enumerate(f):
         assert np.array_equal(res.diff_mask[it], orc.diff_mask[e]), f"D mask of failed run {it}"
         assert np.array_equal(res.missing[it], np.sort(orc.missing[orc.missing[:, 0] == e][:, 1])), it
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("chunk", [2, 32])
+def test_pipeline_run0_failed_not_first(eng, tmp_path, chunk):
+    """Run 0 itself failed and runs.json lists another failed run before it: failedRuns[0] (the reference
+    diff's label source, differential-provenance.go:22-43) is not run 0, and the stream parses it right
+    after run 0, so the first chunk holds both."""
+    import json
+    import os
+    from tests.test_ingest import rotate_dir
+    corpus, info = synth.generate(90, target_nodes=700, body_extra=3, p_fault=0.3)
+    d = str(tmp_path / "molly")
+    synth.write_molly(corpus, info, d)
+    rotate_dir(d, 40)
+    runs = json.load(open(os.path.join(d, "runs.json")))
+    for r in runs:
+        if int(r["iteration"]) == 0:
+            r["status"] = "failure"
+    json.dump(runs, open(os.path.join(d, "runs.json"), "w"))
+    one = load_molly_native(d, threads=8)
+    s, f = one.success_iters(), one.failed_iters()
+    assert 0 in f and f[0] != 0 and one.run_index(f[0]) < one.run_index(0)
+    orc = O.analyze(one, s, f, diff_mode=DIFF_REFERENCE, threads=8, skip_pulls=True)
+    res = P.run(d, eng, chunk=chunk, threads=8, diff_mode=DIFF_REFERENCE, keep=True)
+    assert _names(res.inter, res.tables) == _names(orc.inter, one.tables)
+    for e, it in enumerate(f):
+        assert np.array_equal(res.diff_mask[it], orc.diff_mask[e]), f"D mask of failed run {it}"
+        assert np.array_equal(res.missing[it], np.sort(orc.missing[orc.missing[:, 0] == e][:, 1])), it

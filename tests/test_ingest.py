@@ -116,45 +116,66 @@ def test_c_writer_matches_python_writer(tmp_path):
         assert open(os.path.join(p, n), "rb").read() == open(os.path.join(d, n), "rb").read(), n
 
 
+def _named(c, tables, labels, g):
+    """Graph g of corpus c with interned ids replaced by their strings: (words with the table name,
+    label names, id ranks, edges).  Stream and one-shot interning assign ids in different orders."""
+    from nemo_amd.corpus import TABLE_MASK
+    n0, n1 = int(c.node_off[g]), int(c.node_off[g + 1])
+    e0, e1 = int(c.edge_off[g]), int(c.edge_off[g + 1])
+    w = np.asarray(c.node_word)[n0:n1]
+    return ([(int(x) & ~TABLE_MASK, tables[int(x) & TABLE_MASK]) for x in w],
+            [labels[int(x)] for x in np.asarray(c.label)[n0:n1]], np.asarray(c.id_rank)[n0:n1].tolist(),
+            np.asarray(c.edge_src)[e0:e1].tolist(), np.asarray(c.edge_dst)[e0:e1].tolist())
+
+
+def _stream_runs(st, chunk, one):
+    """Every owned run of the stream as (iteration, pre graph, post graph) by name, plus the chunks'
+    checks: every chunk after the one holding run 0 starts with run 0, replicated and not owned."""
+    out, seen0 = [], False
+    while True:
+        c = st.next(chunk)  # valid until the call after next: read it now
+        if c is None:
+            break
+        tables, labels = st.strings(STR_TABLE), st.strings(STR_LABEL)  # ids interned so far
+        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
+        if seen0:
+            assert int(c.iteration[0]) == 0 and own[0] == 0
+        for lr in range(c.n_runs):
+            if own[lr]:
+                out.append((int(c.iteration[lr]), _named(c, tables, labels, 2 * lr),
+                            _named(c, tables, labels, 2 * lr + 1)))
+        seen0 = seen0 or 0 in set(int(x) for x in c.iteration)
+        assert tables[c.table_pre] == "pre" and tables[c.table_post] == "post"
+    return out, st.strings(STR_TABLE), st.strings(STR_LABEL)
+
+
+def _expected_order(one):
+    """Parse order: run 0, failedRuns[0] (first non-success run in runs.json order), the rest."""
+    its = [int(x) for x in one.iteration]
+    f0 = next((it for it, s in zip(its, one.status) if s != "success"), None)
+    head = [0] if 0 in its else []
+    if f0 is not None and f0 != 0:
+        head.append(f0)
+    return head + [it for it in its if it not in head]
+
+
 @pytest.mark.parametrize("chunk", [1, 7, 16, 40, 100])
 def test_stream_chunks_match_one_shot(tmp_path, chunk):
-    """nemo_ingest_next's chunks, owned runs concatenated, equal nemo_ingest_molly's corpus; every chunk
-    after the one holding run 0 starts with run 0 replicated (not owned)."""
+    """nemo_ingest_next's chunks, owned runs concatenated, hold nemo_ingest_molly's runs in parse order
+    (run 0, failedRuns[0], the rest), each equal by name to the one-shot ingest's; every chunk after the
+    one holding run 0 starts with run 0 replicated (not owned)."""
     from nemo_amd.pipeline import IngestStream
     _, _, d = _synth_dir(tmp_path)
     one = load_molly_native(d, threads=4)
+    assert any(s != "success" for s in one.status)
     st = IngestStream(d, threads=3)
-    parts = {k: [] for k in ("node_word", "label", "id_rank", "edge_src", "edge_dst")}
-    sizes_v, sizes_e, its = [], [], []
-    seen0 = False
-    while True:
-        c = st.next(chunk)
-        if c is None:
-            break
-        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
-        if seen0 and chunk < one.n_runs:
-            assert int(c.iteration[0]) == 0 and own[0] == 0
-        for lr in range(c.n_runs):
-            if not own[lr]:
-                continue
-            its.append(int(c.iteration[lr]))
-            for g in (2 * lr, 2 * lr + 1):
-                n0, n1 = int(c.node_off[g]), int(c.node_off[g + 1])
-                e0, e1 = int(c.edge_off[g]), int(c.edge_off[g + 1])
-                for k in ("node_word", "label", "id_rank"):
-                    parts[k].append(np.asarray(getattr(c, k))[n0:n1].copy())
-                for k in ("edge_src", "edge_dst"):
-                    parts[k].append(np.asarray(getattr(c, k))[e0:e1].copy())
-                sizes_v.append(n1 - n0)
-                sizes_e.append(e1 - e0)
-        seen0 = seen0 or 0 in set(int(x) for x in c.iteration)
-        assert (c.table_pre, c.table_post) == (one.table_pre, one.table_post)
-    assert its == [int(x) for x in one.iteration]
-    assert np.array_equal(np.diff(one.node_off.astype(np.int64)), sizes_v)
-    assert np.array_equal(np.diff(one.edge_off.astype(np.int64)), sizes_e)
-    for k, v in parts.items():
-        assert np.array_equal(np.concatenate(v), np.asarray(getattr(one, k))), k
-    assert st.strings(STR_LABEL) == one.labels and st.strings(STR_TABLE) == one.tables
+    runs, tables, labels = _stream_runs(st, chunk, one)
+    assert [it for it, _, _ in runs] == _expected_order(one)
+    for it, pre, post in runs:
+        r = one.run_index(it)
+        assert pre == _named(one, one.tables, one.labels, 2 * r), it
+        assert post == _named(one, one.tables, one.labels, 2 * r + 1), it
+    assert sorted(tables) == sorted(one.tables) and sorted(labels) == sorted(one.labels)
     st.close()
 
 
@@ -184,39 +205,29 @@ def rotate_dir(d, k):
     json.dump(runs[k:] + runs[:k], open(os.path.join(d, "runs.json"), "w"))
 
 
-@pytest.mark.parametrize("chunk", [4, 11])
+@pytest.mark.parametrize("chunk", [2, 4, 11])
 def test_stream_parses_run0_first(tmp_path, chunk):
-    """runs.json with run 0 in the middle: the stream parses run 0 into the first chunk (owned) and
-    replicates it into every later chunk, so each chunk with a failed run holds the good run; every run's
-    arrays equal the one-shot ingest's for the same iteration."""
+    """runs.json with run 0 in the middle and a failed run listed before it: the stream parses run 0 and
+    then failedRuns[0] into the first chunk (run 0 owned there) and replicates run 0 into every later
+    chunk, so each chunk with a failed run holds the good run and the reference diff's label source is
+    known from the first chunk on; every run equals the one-shot ingest's for the same iteration."""
     from nemo_amd.pipeline import IngestStream
     _, _, d = _synth_dir(tmp_path, n_runs=30, nodes=200)
     rotate_dir(d, 17)
     one = load_molly_native(d, threads=4)
     assert int(one.iteration[0]) == 17 and int(one.iteration[13]) == 0
+    order = _expected_order(one)
+    f0 = order[1]
+    assert one.run_index(f0) < one.run_index(0), "the fixture must list failedRuns[0] before run 0"
     st = IngestStream(d, threads=2)
-    first, its = True, []
-    while True:
-        c = st.next(chunk)
-        if c is None:
-            break
-        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
-        assert int(c.iteration[0]) == 0 and bool(own[0]) == first
-        first = False
-        for lr in range(c.n_runs):
-            if not own[lr]:
-                continue
-            it = int(c.iteration[lr])
-            its.append(it)
-            r = one.run_index(it)
-            for k in (0, 1):
-                g, go = 2 * lr + k, 2 * r + k
-                a, b = int(c.node_off[g]), int(c.node_off[g + 1])
-                oa, ob = int(one.node_off[go]), int(one.node_off[go + 1])
-                assert np.array_equal(np.asarray(c.node_word)[a:b], np.asarray(one.node_word)[oa:ob])
-                assert np.array_equal(np.asarray(c.id_rank)[a:b], np.asarray(one.id_rank)[oa:ob])
-                ea, eb = int(c.edge_off[g]), int(c.edge_off[g + 1])
-                oea, oeb = int(one.edge_off[go]), int(one.edge_off[go + 1])
-                assert np.array_equal(np.asarray(c.edge_src)[ea:eb], np.asarray(one.edge_src)[oea:oeb])
-    assert its == [0] + [int(x) for x in one.iteration if int(x) != 0]
+    c = st.next(chunk)
+    assert [int(x) for x in c.iteration[:2]] == [0, f0]
+    st.close()
+    st = IngestStream(d, threads=2)
+    runs, _, _ = _stream_runs(st, chunk, one)
+    assert [it for it, _, _ in runs] == order
+    for it, pre, post in runs:
+        r = one.run_index(it)
+        assert pre == _named(one, one.tables, one.labels, 2 * r), it
+        assert post == _named(one, one.tables, one.labels, 2 * r + 1), it
     st.close()

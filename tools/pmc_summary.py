@@ -120,6 +120,8 @@ def main():
         if not parts:
             continue
         hbm = sum(p[0] for p in parts)
+        if grp == "k_diff" and bj["config"].get("diff_mode") == "per_run":
+            grp = "k_diff_per_run"  # bench.py's roofline_diff (a run with --diff-mode per_run: every launch per-run)
         summary.setdefault(grp, {})[str(nodes)] = {
             "hbm_bytes_per_launch": round(hbm), "fetch_kib": round(sum(p[1] for p in parts), 1),
             "write_kib": round(sum(p[2] for p in parts), 1), "kernels": [m for m in members if m in base_hbm],
