@@ -71,7 +71,7 @@ struct nemo_ctx {
   uint32_t *d_red = nullptr;
 
   // diff
-  uint32_t n_entries = 0, diff_cap = 0;
+  uint32_t n_entries = 0, diff_cap = 0, legacy_cap = 0;
   uint32_t *d_r0lab = nullptr, *d_r0idx = nullptr, n_r0lab = 0;
   uint32_t *d_r0hkey = nullptr, *d_r0hval = nullptr, r0hmask = 0;
   uint32_t *d_dsrc = nullptr, *d_miss = nullptr, *d_nmiss = nullptr;
@@ -91,6 +91,17 @@ struct nemo_ctx {
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr;
   bool aux_pending = false;
+  // the multi-entry diff (k_dx.hip): g0's Kahn-order relayout, built with the
+  // CSR in every load / rebuild, and the per-call buffers (grow-only)
+  nemo::DxPrep dxp{};
+  bool dx_ok = false;                // relayout allocated: run 0 present, every row fits a window
+  int diff_legacy = 0;               // option diff_legacy: one workgroup per entry (k_diff.hip)
+  uint32_t diff_window = 0;          // option diff_window (test knob): 0 by size, 1 windowed, 2 tiny windows
+  uint32_t g0_maxdeg = 0;
+  uint32_t dx_nu_cap = 0, dx_nch_cap = 0;
+  uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr;
+  uint64_t *d_dxw = nullptr, *d_dxlp = nullptr;  // [5][nch][V0] Good, F, B, D, L|LP; [nch] LP summary
+  bool dx_last = false;              // the last diffprov ran the multi-entry kernels
 
   // pulls: per-slot (offset, count) and the region cursor come back to pinned
   // memory asynchronously; the first fetch waits for them
@@ -382,10 +393,15 @@ static void release_corpus(nemo_ctx *c) {
   c->d_dtopo = nullptr;
   c->d_dmap = nullptr;
   c->d_dumask = nullptr;
+  c->dxp = nemo::DxPrep{};
+  c->dx_ok = false;
+  c->dx_nu_cap = c->dx_nch_cap = 0;
+  c->d_dxpb = c->d_dxsval = nullptr;
+  c->d_dxw = c->d_dxlp = nullptr;
   c->n_uniq = 0;
   c->dmap.clear();
   c->aux_pending = false;
-  c->n_entries = c->diff_cap = 0;
+  c->n_entries = c->diff_cap = c->legacy_cap = 0;
   c->miss_cap = 0;
   c->d_pcnt = c->d_psrc = c->d_pdst = nullptr;
   c->d_poff = nullptr;
@@ -491,6 +507,15 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     }
     c->lds_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     if (c->loaded) set_lds_tier(c);
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "diff_legacy")) {  // 1: CreateNaiveDiffProv by the one-workgroup-per-entry kernels
+    c->diff_legacy = value > 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "diff_window")) {  // test knob of the multi-entry diff's walks: 0, 1 or 2
+    if (value < 0 || value > 2) return fail(c, NEMO_ERR_INVALID, "diff_window: 0, 1 or 2");
+    c->diff_window = (uint32_t)value;
     return NEMO_OK;
   }
   if (!strcmp(name, "stage_sdma")) {
@@ -689,6 +714,13 @@ static int device_load(nemo_ctx *c) {
                   [&] { nemo::launch_csr_big(c->dc, c->big_chunks, c->stream); })))
     return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
+  // run 0's post graph in Kahn order for the multi-entry diff: read the Kahn
+  // order, both CSRs and the node words; write positions, rows both ways, level bounds
+  if (c->dx_ok) {
+    const double V0 = c->dxp.V0, E0 = c->dxp.E0;
+    if ((rc = timed(c, "k_dxprep", 16 * E0 + 44 * V0, 0, [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->stream); })))
+      return rc;
+  }
   return NEMO_OK;
 }
 
@@ -955,6 +987,29 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       HIPCHK(c, hipMemcpyAsync(c->d_r0idx, ix.data(), ix.size() * 4, hipMemcpyHostToDevice, s));
     }
     HIPCHK(c, hipStreamSynchronize(s));  // host vectors go out of scope
+    // the multi-entry diff's relayout of g0: every row must fit one walk window
+    const uint64_t n0 = c->node_off[g0], nv = c->node_off[g0 + 1] - n0;
+    const uint64_t e0 = c->edge_off[g0], ne = c->edge_off[g0 + 1] - e0;
+    std::vector<uint32_t> din(nv, 0), dout(nv, 0);
+    uint32_t maxdeg = 0;
+    for (uint64_t e = e0; e < e0 + ne; e++) {
+      if (in->edge_src[e] < nv) maxdeg = std::max(maxdeg, ++dout[in->edge_src[e]]);
+      if (in->edge_dst[e] < nv) maxdeg = std::max(maxdeg, ++din[in->edge_dst[e]]);
+    }
+    c->dx_ok = nv > 0 && nv < 0xFFFFFFFFull && maxdeg <= nemo::dx_max_row();
+    c->g0_maxdeg = maxdeg;
+    if (c->dx_ok) {
+      nemo::DxPrep &p = c->dxp;
+      p.g0 = g0;
+      p.V0 = (uint32_t)nv;
+      p.E0 = (uint32_t)ne;
+      p.r0idx = c->d_r0idx;
+      p.n_r0lab = c->n_r0lab;
+      if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
+          (rc = dalloc(c, &p.lend, nv)) || (rc = dalloc(c, &p.rp, nv + 1)) || (rc = dalloc(c, &p.fp, nv + 1)) ||
+          (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))
+        return rc;
+    }
   }
   // trigger outputs of run 0: pre rows (a, g, r) <= sum over goals of in*out
   // degree, post rows (g, r) <= edges, async rules <= nodes (corrections.go:30-34,121-125)
@@ -1244,24 +1299,40 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   const uint32_t g0 = 2 * c->run0 + 1;
   const uint64_t V0 = c->node_off[g0 + 1] - c->node_off[g0];
   const uint64_t E0 = c->edge_off[g0 + 1] - c->edge_off[g0];
+  const bool dx = c->dx_ok && !c->diff_legacy && (c->diff_window != 2 || c->g0_maxdeg <= nemo::dx_max_row_tiny());
   int rc;
   if (n_failed > c->diff_cap) {
-    dfree(c, c->d_dsrc);
-    dfree(c, c->d_dbits);
-    dfree(c, c->d_dmask);
-    dfree(c, c->d_dumask);
-    dfree(c, c->d_ddepth);
-    dfree(c, c->d_miss);
-    c->d_dumask = nullptr;
+    for (void *q : {(void *)c->d_dsrc, (void *)c->d_dmask, (void *)c->d_miss, (void *)c->d_dbits, (void *)c->d_dumask,
+                    (void *)c->d_ddepth, (void *)c->d_dtopo})
+      dfree(c, q);
+    c->d_dbits = c->d_dumask = nullptr;
+    c->d_ddepth = nullptr;
+    c->d_dtopo = nullptr;
+    c->legacy_cap = 0;
     if ((rc = dalloc(c, &c->d_dsrc, 2 * n_failed))) return rc;
-    if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dumask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
-    dfree(c, c->d_dtopo);
-    if ((rc = dalloc(c, &c->d_dtopo, 4 * V0 + 2 * E0 + 2 + c->n_r0lab))) return rc;
     if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
     c->diff_cap = (uint32_t)n_failed;
+  }
+  if (!dx && n_failed > c->legacy_cap) {  // the one-workgroup-per-entry kernels' scratch
+    if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dumask, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dtopo, 4 * V0 + 2 * E0 + 2 + c->n_r0lab))) return rc;
+    c->legacy_cap = (uint32_t)n_failed;
+  }
+  const uint32_t nch = (nu + 63) / 64, w32 = (uint32_t)((V0 + 31) / 32);
+  if (dx && (nu > c->dx_nu_cap || nch > c->dx_nch_cap)) {
+    for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxw, (void *)c->d_dxlp}) dfree(c, q);
+    c->d_dxpb = c->d_dxsval = nullptr;
+    c->d_dxw = c->d_dxlp = nullptr;
+    c->dx_nu_cap = c->dx_nch_cap = 0;
+    if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
+    if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dxw, 5 * (size_t)nch * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dxlp, (size_t)nch))) return rc;
+    c->dx_nu_cap = nu;
+    c->dx_nch_cap = nch;
   }
   if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;
   c->d_dmap = c->d_dsrc + n_failed;
@@ -1276,40 +1347,76 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   nemo::launch_to_host(c->d_dsrc, src, 2 * n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
   nemo::launch_zero(c->d_nmiss, 4, s);
-  nemo::DiffArgs a;
-  a.g0 = g0;
-  a.src = c->d_dsrc;
-  a.ref_labels = d_labels;
-  a.r0lab = c->d_r0lab;
-  a.r0idx = c->d_r0idx;
-  a.n_r0lab = c->n_r0lab;
-  a.r0hkey = c->d_r0hkey;
-  a.r0hval = c->d_r0hval;
-  a.r0hmask = c->r0hmask;
-  a.bits = c->d_dbits;
-  a.depth = c->d_ddepth;
-  a.tpos = c->d_dtopo;
-  a.tinfo = a.tpos + V0;
-  a.trp = a.tinfo + V0;
-  a.tfp = a.trp + V0 + 1;
-  a.trc = a.tfp + V0 + 1;
-  a.tfc = a.trc + E0;
-  a.r0pos = a.tfc + E0;
-  a.mask = expand ? c->d_dumask : c->d_dmask;
-  a.missing = c->d_miss;
-  a.n_missing = c->d_nmiss;
   // HBM lower bound: run 0's post graph once (rows both ways, node word, Kahn
   // order: 8E0 + 16V0 -- every entry re-reads it from L2), each distinct label
   // source and each entry's D mask (V0); the three reachability sweeps per
   // computed entry are counted as traversed edges, not as HBM bytes
   const double bytes = 8.0 * E0 + 16.0 * V0 + src_bytes + (double)n_failed * V0;
-  rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0,
-                [&] {
-                  // the Kahn-order relayout only when g0 may fall outside the LDS tier
-                  const bool lds = c->dc.t_diff.bytes && V0 <= c->dc.t_diff.v && E0 <= c->dc.t_diff.e;
-                  nemo::launch_diff(c->dc, a, nu, lds ? 0u : (uint32_t)V0, s);
-                  if (expand) nemo::launch_diff_expand(c->d_dmask, c->d_dumask, c->d_dmap, V0, (uint32_t)n_failed, s);
-                });
+  c->dx_last = dx;
+  if (dx) {
+    nemo::DxArgs a{};
+    a.p = c->dxp;
+    a.nu = nu;
+    a.nch = nch;
+    a.src = c->d_dsrc;
+    a.ref_labels = d_labels;
+    a.r0lab = c->d_r0lab;
+    a.r0hkey = c->d_r0hkey;
+    a.r0hval = c->d_r0hval;
+    a.r0hmask = c->r0hmask;
+    a.pb = c->d_dxpb;
+    a.w32 = w32;
+    uint64_t maxsrc = d_labels ? labels_cap : 0;
+    for (uint32_t u = 0; u < nu && !d_labels; u++)
+      maxsrc = std::max<uint64_t>(maxsrc, c->node_off[src[u] + 1] - c->node_off[src[u]]);
+    a.lab_per = 4096;
+    a.lab_split = (uint32_t)std::max<uint64_t>(1, (maxsrc + a.lab_per - 1) / a.lab_per);
+    const size_t plane = (size_t)nch * V0;
+    a.gw = c->d_dxw;
+    a.fw = a.gw + plane;
+    a.bw = a.fw + plane;
+    a.dw = a.bw + plane;
+    a.lw = a.dw + plane;
+    a.lpany = c->d_dxlp;
+    a.sval = c->d_dxsval;
+    a.mask = c->d_dmask;
+    a.map = c->d_dmap;
+    a.n_entries = (uint32_t)n_failed;
+    a.missing = c->d_miss;
+    a.n_missing = c->d_nmiss;
+    a.window = c->diff_window;
+    rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0, [&] { nemo::launch_dx(c->dc, a, s); });
+  } else {
+    nemo::DiffArgs a;
+    a.g0 = g0;
+    a.src = c->d_dsrc;
+    a.ref_labels = d_labels;
+    a.r0lab = c->d_r0lab;
+    a.r0idx = c->d_r0idx;
+    a.n_r0lab = c->n_r0lab;
+    a.r0hkey = c->d_r0hkey;
+    a.r0hval = c->d_r0hval;
+    a.r0hmask = c->r0hmask;
+    a.bits = c->d_dbits;
+    a.depth = c->d_ddepth;
+    a.tpos = c->d_dtopo;
+    a.tinfo = a.tpos + V0;
+    a.trp = a.tinfo + V0;
+    a.tfp = a.trp + V0 + 1;
+    a.trc = a.tfp + V0 + 1;
+    a.tfc = a.trc + E0;
+    a.r0pos = a.tfc + E0;
+    a.mask = expand ? c->d_dumask : c->d_dmask;
+    a.missing = c->d_miss;
+    a.n_missing = c->d_nmiss;
+    rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0,
+                  [&] {
+                    // the Kahn-order relayout only when g0 may fall outside the LDS tier
+                    const bool lds = c->dc.t_diff.bytes && V0 <= c->dc.t_diff.v && E0 <= c->dc.t_diff.e;
+                    nemo::launch_diff(c->dc, a, nu, lds ? 0u : (uint32_t)V0, s);
+                    if (expand) nemo::launch_diff_expand(c->d_dmask, c->d_dumask, c->d_dmap, V0, (uint32_t)n_failed, s);
+                  });
+  }
   if (rc) return rc;
   // D masks and the missing-event count -> pinned host
   if ((rc = ensure_event(c, &c->ev_diff))) return rc;

@@ -28,6 +28,51 @@ struct DiffArgs {
   uint32_t *n_missing;      // counter
 };
 
+// Run 0's post graph g0 relaid in Kahn order (k_dx.hip k_dxp_*, built with the
+// CSR in every load / rebuild): positions 0..V0-1 are the Kahn order; parents
+// in Kahn order and children in reversed Kahn order ("walk order"), as walk
+// indices, so that a window of consecutive positions reads one contiguous row range.
+struct DxPrep {
+  uint32_t g0, V0, E0;
+  uint32_t *tpos;            // [V0] node -> position
+  uint32_t *info;            // [V0] level << 3 | DXI_RULE
+  uint32_t *lbeg, *lend;     // [V0] first position of the position's Kahn level / of the next level
+  uint32_t *rp, *rc;         // [V0 + 1], [E0 + 4] parents of position i, as positions
+  uint32_t *fp, *fc;         // [V0 + 1], [E0 + 4] children of position V0-1-i, as reversed positions
+  const uint32_t *r0idx;     // [n_r0lab] node of each sorted run-0 goal label
+  uint32_t *r0pos;           // [n_r0lab] its position
+  uint32_t n_r0lab;
+};
+#define DXI_RULE 1u   // the position is a rule
+
+// One multi-entry CreateNaiveDiffProv call (k_dx.hip): nu distinct label
+// sources in chunks of 64, one bit per source in every u64 word.
+struct DxArgs {
+  DxPrep p;
+  uint32_t nu, nch;          // distinct label sources, 64-source chunks
+  const uint32_t *src;       // [nu] label-source graph (post graph of the source run)
+  const uint32_t *ref_labels;  // label mode: [n, label...] of the single source (src unused)
+  const uint32_t *r0lab, *r0hkey, *r0hval;
+  uint32_t r0hmask;
+  uint32_t *pb;              // [nu][w32] present bitmaps over positions
+  uint32_t w32;              // ceil(V0 / 32)
+  uint32_t lab_per;          // source nodes per k_dx_label workgroup
+  uint32_t lab_split;        // workgroups per source (1: LDS bitmap stored whole)
+  uint64_t *gw;              // [nch][V0] Good bits by position
+  uint64_t *fw;              // [nch][V0] Fwd*(Good) by position
+  uint64_t *bw;              // [nch][V0] Bwd*(Good) by REVERSED position (V0 - 1 - pos)
+  uint64_t *dw;              // [nch][V0] D = F & B by position
+  uint64_t *lw;              // [nch][V0] D-leaf goals | LP rules (rules with a D-leaf child) by position
+  uint64_t *lpany;           // [nch] sources with at least one LP rule
+  uint32_t *sval;            // [nu][V0] depth + 1 of D nodes (0 elsewhere) by position
+  uint8_t *mask;             // [n_entries][V0] D masks by node (output)
+  const uint32_t *map;       // [n_entries] entry -> source
+  uint32_t n_entries;
+  uint32_t *missing;         // [2 * cap] (source, rule node)
+  uint32_t *n_missing;
+  uint32_t window;           // test knob: 0 by size, 1 windowed walks, 2 tiny windows (ring misses)
+};
+
 struct PullArgs {
   uint32_t which;           // 0 raw, 1 simplified, 2 diff
   uint32_t g0;              // graph of which == 2
@@ -68,6 +113,10 @@ void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint
 // entry e's D mask = unique result map[e]'s ([n_entries][V0] from [n_uniq][V0])
 void launch_diff_expand(uint8_t *mask, const uint8_t *umask, const uint32_t *map, uint64_t V0, uint32_t n_entries,
                         hipStream_t s);
+void launch_dx_prep(const DevCorpus &c, const DxPrep &p, hipStream_t s);
+void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s);
+uint32_t dx_max_row();       // the longest row of g0 the multi-entry diff takes
+uint32_t dx_max_row_tiny();  // the same under the tiny-window test knob
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
 void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
                         hipStream_t s);

@@ -1,0 +1,554 @@
+// k_dx.hip — CreateNaiveDiffProv (differential-provenance.go:18-146) for many
+// label sources at once.
+//
+// Every diff entry works on run 0's post graph g0 and differs only in its
+// label source (failGoals = collect(failed.label), :22-24):
+//   Good_u = goals of g0 whose label is not a post-goal label of source u
+//   D_u    = Fwd*(Good_u) ∩ Bwd*(Good_u)                (:22-32, APOC export)
+//   missing_u = D_u rules with a D_u-leaf goal child at maximal depth (:82-98)
+// Reachability is the same sweep for every source, so one bit per source in a
+// u64 word carries 64 sources through one Kahn-order walk (a "chunk").  Depth
+// (the longest path from a D root) is per source; it runs four sources per
+// workgroup, one walking wave each, over the same staged graph windows.
+//
+// Kernels per call (launch_dx):
+//   k_dx_label   present bitmaps: g0 positions whose label a source holds
+//   k_dx_good    Good words per chunk (64 bitmaps transposed by ballots)
+//   k_dx_walk<0> Fwd* and Bwd* (grid chunks x 2: forward / reversed walk)
+//   k_dx_leaf    D = F & B, D-leaf goals
+//   k_dx_lp      LP rules (D rules with a D-leaf child), chunks' LP summary
+//   k_dx_walk<2> depth per source, the maximal LP depth, missing rows
+//   k_dx_mask    D masks by node for every entry (entries -> sources)
+// g0's Kahn-order relayout (k_dxp_*) is built with the CSR in every load /
+// rebuild (launch_dx_prep), since it depends on the graph alone.
+//
+// The walk (k_dx_walk): positions in walk order (Kahn order, or reversed for
+// Bwd*) are taken in windows.  All waves stage a window: its rows' links as a
+// CSR of ring indices, the init value of every position (Good, or 0) written
+// into its ring slot, the end of its Kahn level.  A link to a position older
+// than the ring reads that position's final value from HBM and is folded into
+// its owner's init at staging.  Then one wave per source walks the window's
+// levels: each level is one step of independent lanes (no barrier, a wave's
+// LDS operations complete in order), value = init op (ring values of links).
+#include "device.h"
+#include "internal.h"
+
+namespace nemo {
+
+// ---- g0 relayout (launch_dx_prep) ---------------------------------------------------
+// pass 1, one thread per position i: node -> position, row lengths (parents in
+// Kahn order, children in reversed Kahn order), level bounds, rule bit
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_a(DevCorpus c, DxPrep p) {
+  const GraphView gv = c.view(p.g0);
+  const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i == 0) {
+    p.rp[gv.V] = 0;
+    p.fp[gv.V] = 0;
+  }
+  if (i >= gv.V) return;
+  const uint32_t v = gv.topo[i];
+  p.tpos[v] = i;
+  p.rp[i] = gv.rp[v + 1] - gv.rp[v];
+  p.fp[gv.V - 1u - i] = gv.fp[v + 1] - gv.fp[v];
+  const uint32_t l = c.nlv[gv.n0 + v];
+  p.lbeg[i] = gv.lvl[l];
+  p.lend[i] = gv.lvl[l + 1];
+  p.info[i] = (l << 3) | (is_rule(gv.word[v]) ? DXI_RULE : 0u);
+}
+// pass 2, one workgroup: row starts
+__global__ __launch_bounds__(1024) void k_dxp_scan(DxPrep p) {
+  __shared__ uint32_t s_red[16];
+  block_scan_inplace<1024, 16>(p.rp, p.V0 + 1, s_red);
+  block_scan_inplace<1024, 16>(p.fp, p.V0 + 1, s_red);
+}
+// pass 3, one thread per position: rows as walk indices (parents as positions,
+// children as reversed positions), label entries as positions
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_b(DevCorpus c, DxPrep p) {
+  const GraphView gv = c.view(p.g0);
+  const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i < p.n_r0lab) p.r0pos[i] = p.tpos[p.r0idx[i]];
+  if (i >= gv.V) return;
+  const uint32_t v = gv.topo[i], V = gv.V;
+  uint32_t o = p.rp[i];
+  for (uint32_t j = gv.rp[v]; j < gv.rp[v + 1]; j++) p.rc[o++] = p.tpos[gv.rc[j]];
+  o = p.fp[V - 1u - i];
+  for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) p.fc[o++] = V - 1u - p.tpos[gv.fc[j]];
+}
+
+void launch_dx_prep(const DevCorpus &c, const DxPrep &p, hipStream_t s) {
+  const uint32_t nb = (std::max(p.V0, p.n_r0lab) + NEMO_BLOCK - 1) / NEMO_BLOCK;
+  if (!nb) return;
+  hipLaunchKernelGGL(k_dxp_a, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, p);
+  hipLaunchKernelGGL(k_dxp_scan, dim3(1), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_dxp_b, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, p);
+}
+
+// ---- present bitmaps ------------------------------------------------------------------
+// Workgroup (x, u): source u's nodes [x * lab_per, ...).  Every goal label is
+// looked up in g0's label table (open-addressed: key = label + 1) and each g0
+// goal carrying it gets its position's bit.  Bitmaps of up to DXL_LDS words
+// are gathered in LDS and stored whole (one workgroup per source) or ORed in
+// by word; larger ones take global atomics.
+#define DXL_LDS 4096u
+#define DXL_BATCH 8
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) {
+  __shared__ uint32_t bm[DXL_LDS];
+  const uint32_t u = blockIdx.y, tid = threadIdx.x;
+  const bool lds = a.w32 <= DXL_LDS;
+  const uint32_t *lab, *word;
+  uint32_t n;
+  if (a.ref_labels) {
+    lab = a.ref_labels + 1;
+    word = nullptr;
+    n = a.ref_labels[0];
+  } else {
+    const GraphView s = c.view(a.src[u]);
+    lab = s.label;
+    word = s.word;
+    n = s.V;
+  }
+  uint32_t *pb = a.pb + (size_t)u * a.w32;
+  if (lds) {
+    for (uint32_t w = tid; w < a.w32; w += NEMO_BLOCK) bm[w] = 0;
+    __syncthreads();
+  }
+  const uint32_t lo = blockIdx.x * a.lab_per, hi = min(n, lo + a.lab_per);
+  for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
+    uint32_t lb[DXL_BATCH], h[DXL_BATCH], pos[DXL_BATCH], live = 0;
+#pragma unroll
+    for (int q = 0; q < DXL_BATCH; q++) {
+      const uint32_t x = base + q * NEMO_BLOCK + tid;
+      const bool in = x < hi && (!word || !is_rule(word[x]));
+      lb[q] = in ? lab[x] : 0u;
+      h[q] = hash_label(lb[q]) & a.r0hmask;
+      pos[q] = NEMO_NONE;
+      live |= (in ? 1u : 0u) << q;
+    }
+    while (live) {
+      uint32_t k[DXL_BATCH];
+#pragma unroll
+      for (int q = 0; q < DXL_BATCH; q++) k[q] = ((live >> q) & 1u) ? a.r0hkey[h[q]] : 0u;
+#pragma unroll
+      for (int q = 0; q < DXL_BATCH; q++) {
+        if (!((live >> q) & 1u)) continue;
+        if (k[q] == lb[q] + 1u) {
+          pos[q] = h[q];
+          live &= ~(1u << q);
+        } else if (k[q] == 0u) {
+          live &= ~(1u << q);
+        } else {
+          h[q] = (h[q] + 1u) & a.r0hmask;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < DXL_BATCH; q++)
+      if (pos[q] != NEMO_NONE) pos[q] = a.r0hval[pos[q]];
+#pragma unroll
+    for (int q = 0; q < DXL_BATCH; q++) {
+      if (pos[q] == NEMO_NONE) continue;
+      for (uint32_t i = pos[q]; i < a.p.n_r0lab && a.r0lab[i] == lb[q]; i++) {
+        const uint32_t p = a.p.r0pos[i];
+        if (lds) atomicOr(&bm[p >> 5], 1u << (p & 31u));
+        else atomicOr(&pb[p >> 5], 1u << (p & 31u));
+      }
+    }
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (uint32_t w = tid; w < a.w32; w += NEMO_BLOCK) {
+    if (a.lab_split == 1) pb[w] = bm[w];
+    else if (bm[w]) atomicOr(&pb[w], bm[w]);
+  }
+}
+
+// ---- Good words: chunk c's 64 bitmaps transposed, one wave per 64 positions ----------
+// lane e holds source 64c+e's bitmap words for the 64 positions; 64 ballots
+// hand position p0+l's 64 source bits to lane l.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
+  const uint32_t c = blockIdx.y, lane = lane_id(), V = a.p.V0;
+  const uint32_t p0 = (blockIdx.x * (NEMO_BLOCK / 64) + (threadIdx.x >> 6)) * 64u;
+  if (p0 >= V) return;  // wave-uniform
+  const uint32_t u = c * 64u + lane;
+  const bool valid = u < a.nu;
+  const uint32_t *row = a.pb + (size_t)(valid ? u : 0u) * a.w32;
+  const uint32_t wi = p0 >> 5;
+  const uint32_t w0 = valid ? row[wi] : 0u;
+  const uint32_t w1 = (valid && wi + 1 < a.w32) ? row[wi + 1] : 0u;
+  uint64_t pres = 0;
+#pragma unroll
+  for (uint32_t b = 0; b < 32; b++) {
+    const uint64_t m = __ballot((w0 >> b) & 1u);
+    pres = lane == b ? m : pres;
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 32; b++) {
+    const uint64_t m = __ballot((w1 >> b) & 1u);
+    pres = lane == 32u + b ? m : pres;
+  }
+  const uint64_t vm = __ballot(valid);
+  const uint32_t pos = p0 + lane;
+  if (pos < V) a.gw[(size_t)c * V + pos] = (a.p.info[pos] & DXI_RULE) ? 0ull : (~pres & vm);
+}
+
+// ---- the windowed walk ------------------------------------------------------------------
+// MODE 0: reachability, T = u64 (64 sources per bit column), one walker;
+//         blockIdx.y = 0: Fwd* over parents in Kahn order, 1: Bwd* over
+//         children in reversed Kahn order.  value = Good | OR(links).
+// MODE 2: depth, T = u32, NE walkers (sources 4·blockIdx.x + e), Kahn order
+//         over parents: value = D ? 1 + max(links) : 0 (depth + 1 of D nodes;
+//         a non-D parent contributes 0, so the max runs over D parents).
+// WHOLE: the graph is one window (ring = positions, no wrap, no misses).
+#define DX_NT 256
+#define DX_SEG 256u
+template <typename T, int NE>
+struct DxLds {
+  T *ring0;          // NE rings of [R + 1] (stride rs); [R] is the identity (sink)
+  uint32_t rs;
+  uint32_t *off;     // [W + 1] absolute row starts of the window's positions
+  uint16_t *ent;     // [EC] ring index of each link (R: folded into the owner's init)
+  uint16_t *send;    // [W] end of the position's level in the window (relative)
+  uint8_t *gate;     // [NE][W] depth: 1 = D node, 2 = LP rule
+};
+template <typename T, int NE>
+__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC) {
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 1u)) + lds_align(4u * (W + 1u)) + lds_align(2u * EC) +
+         lds_align(2u * W) + NE * lds_align(W);
+}
+template <typename T, int NE>
+__device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC) {
+  uint8_t *p = (uint8_t *)base;
+  DxLds<T, NE> L;
+  L.ring0 = (T *)p;
+  L.rs = lds_align((uint32_t)sizeof(T) * (R + 1u)) / (uint32_t)sizeof(T);
+  p += NE * lds_align((uint32_t)sizeof(T) * (R + 1u));
+  L.off = (uint32_t *)p;
+  p += lds_align(4u * (W + 1u));
+  L.ent = (uint16_t *)p;
+  p += lds_align(2u * EC);
+  L.send = (uint16_t *)p;
+  p += lds_align(2u * W);
+  L.gate = p;
+  return L;
+}
+struct DxWalkCfg {
+  uint32_t W, R, EC;  // window positions, ring slots, links per window
+  uint32_t whole;     // 1: the whole graph is one window
+};
+
+template <typename T>
+__device__ __forceinline__ T dx_op(T a, T b, bool orop) {
+  if constexpr (sizeof(T) == 8) return a | b;
+  else return orop ? (a | b) : max(a, b);
+}
+
+template <int MODE, int NE, bool WHOLE>
+__global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg cfg) {
+  using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
+  extern __shared__ __align__(16) uint8_t dyn[];
+  __shared__ uint32_t s_n;
+  __shared__ T s_lmax[NE];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC;
+  const bool rev = MODE == 0 && blockIdx.y == 1;
+  const uint32_t chunk = MODE == 0 ? blockIdx.x : 0u;
+  DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC);
+  // walk-order rows (parents in Kahn order / children in reversed order); per
+  // walker e: its source (depth), ring and value array, computed from e (a
+  // dynamically indexed register array would live in scratch memory)
+  const uint32_t *rowp = rev ? a.p.fp : a.p.rp, *col = rev ? a.p.fc : a.p.rc;
+  auto srcu = [&](uint32_t e) -> uint32_t {  // NEMO_NONE: no source, or no LP rule (nothing to walk)
+    if (MODE == 0) return 0u;
+    const uint32_t u = blockIdx.x * NE + e;
+    return u < a.nu && ((a.lpany[u >> 6] >> (u & 63u)) & 1ull) ? u : NEMO_NONE;
+  };
+  auto ringp = [&](uint32_t e) -> T * { return L.ring0 + (size_t)e * L.rs; };
+  auto gvalp = [&](uint32_t e) -> T * {
+    if (MODE == 0) return (T *)((rev ? a.bw : a.fw) + (size_t)chunk * V);
+    return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
+  };
+  bool any = MODE == 0;
+  for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
+  if (!any) return;  // workgroup-uniform
+  if (tid < (uint32_t)NE) {
+    ringp(tid)[R] = (T)0;
+    s_lmax[tid] = 0;
+  }
+  for (uint32_t w0 = 0; w0 < V;) {
+    const uint32_t nmax = min(W, V - w0);
+    // ---- staging 1: the window's row starts; it ends where its links would pass EC ----
+    for (uint32_t k = tid; k <= nmax; k += DX_NT) L.off[k] = rowp[w0 + k];
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    {
+      uint32_t best = 0;
+      for (uint32_t k = tid + 1; k <= nmax; k += DX_NT)
+        if (L.off[k] - L.off[0] <= EC) best = max(best, k);
+      for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor(best, d));
+      if (lane == 0) atomicMax(&s_n, best);
+    }
+    __syncthreads();
+    const uint32_t n = s_n, w1 = w0 + n, base = L.off[0], ne = L.off[n] - base;
+    // ---- staging 2: init values into the positions' ring slots (no link of the
+    // window reads those: they hold positions older than the ring), gates, level ends ----
+    for (uint32_t k = tid; k < n; k += DX_NT) {
+      const uint32_t i = w0 + k, pos = rev ? V - 1u - i : i;
+      const uint32_t sl = WHOLE ? i : (i & (R - 1u));
+      const uint32_t le = rev ? V - a.p.lbeg[pos] : a.p.lend[pos];
+      L.send[k] = (uint16_t)(min(le, w1) - w0);
+      if (MODE == 0) {
+        ringp(0)[sl] = (T)a.gw[(size_t)chunk * V + pos];
+      } else {
+        const bool rule = (a.p.info[pos] & DXI_RULE) != 0;
+#pragma unroll
+        for (uint32_t e = 0; e < (uint32_t)NE; e++) {
+          uint8_t g = 0;
+          const uint32_t u = srcu(e);
+          if (u != NEMO_NONE) {
+            const uint32_t b = u & 63u;
+            const uint64_t dv = a.dw[(size_t)(u >> 6) * V + pos];
+            const uint64_t lv = rule ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
+            g = (uint8_t)(((dv >> b) & 1ull) | (((lv >> b) & 1ull) << 1));
+          }
+          ringp(e)[sl] = (T)0;
+          L.gate[e * W + k] = g;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- staging 3: the window's links, one contiguous range of col, in 16-B
+    // aligned chunks.  A link older than the ring reads its final value from
+    // HBM (written and fenced by an earlier window's walk) and is folded into
+    // its owner's init; the others become ring indices ----
+    {
+      const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
+      for (uint32_t cb = c0; cb < c1; cb += 4 * DX_NT) {
+        uint4 v4[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t ck = cb + q * DX_NT + tid;
+          v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(col)[ck] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t ck = cb + q * DX_NT + tid;
+          const uint32_t qs[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const uint32_t j = 4 * ck + b;
+            if (ck >= c1 || j < base || j >= base + ne) continue;
+            const uint32_t x = qs[b];  // walk index of the linked position
+            if (WHOLE || x + R >= w1) {
+              L.ent[j - base] = (uint16_t)(WHOLE ? x : (x & (R - 1u)));
+              continue;
+            }
+            L.ent[j - base] = (uint16_t)R;
+            uint32_t lo = 0, hi = n;  // the owner: off[lo] <= j < off[hi]
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (L.off[mid] <= j) lo = mid;
+              else hi = mid;
+            }
+            const uint32_t sl = (w0 + lo) & (R - 1u);
+#pragma unroll
+            for (uint32_t e = 0; e < (uint32_t)NE; e++) {
+              if (MODE == 2 && srcu(e) == NEMO_NONE) continue;
+              const T val = __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[sl], (unsigned long long)val);
+              else atomicMax((uint32_t *)&ringp(e)[sl], (uint32_t)val);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- the walk: wave e < NE walks source e through the window's levels; a
+    // level (<= DX_SEG positions) is one step of independent lanes ----
+    if (wv < (uint32_t)NE) {
+      const uint32_t e = wv;
+      T *ring = ringp(e), *gv = gvalp(e);
+      const bool live = srcu(e) != NEMO_NONE;
+      T lmax = 0;
+      for (uint32_t s = 0; s < n && live;) {
+        const uint32_t send = min((uint32_t)__builtin_amdgcn_readfirstlane(L.send[s]), s + DX_SEG);
+        const uint32_t cnt = send - s;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if ((uint32_t)(64 * q) >= cnt) break;  // uniform
+          const uint32_t k = s + 64u * q + lane;
+          const bool in = k < send;
+          const uint32_t kk = in ? k : s;
+          const uint32_t sl = WHOLE ? w0 + kk : ((w0 + kk) & (R - 1u));
+          const uint32_t o0 = L.off[kk] - base, m = in ? L.off[kk + 1] - L.off[kk] : 0u;
+          T v = ring[sl];
+          uint32_t mm = m;
+          for (int d = 32; d >= 1; d >>= 1) mm = max(mm, (uint32_t)__shfl_xor(mm, d));
+          for (uint32_t t = 0; t < mm; t += 4) {
+            uint32_t ix[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+              const uint32_t j = o0 + t + b;
+              const uint32_t xj = L.ent[j < EC ? j : 0u];
+              ix[b] = t + b < m ? xj : R;
+            }
+            T x[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) x[b] = ring[ix[b]];
+#pragma unroll
+            for (int b = 0; b < 4; b++) v = dx_op<T>(v, x[b], MODE == 0);
+          }
+          if (MODE == 2) {
+            const uint8_t g = L.gate[e * W + kk];
+            v = (g & 1u) ? v + 1u : (T)0;
+            if (in && (g & 2u)) lmax = v > lmax ? v : lmax;
+          }
+          if (in) {
+            ring[sl] = v;
+            gv[w0 + k] = v;
+          }
+        }
+        s = send;
+        wsync();
+      }
+      if (MODE == 2) {
+        for (int d = 32; d >= 1; d >>= 1) {
+          const T y = __shfl_xor(lmax, d);
+          lmax = y > lmax ? y : lmax;
+        }
+        if (lane == 0 && lmax > s_lmax[e]) s_lmax[e] = lmax;
+      }
+      __threadfence();  // the window's values are final in HBM before later windows (and the rows pass) read them
+    }
+    __syncthreads();
+    w0 = w1;
+  }
+  if (MODE != 2) return;
+  // missing rows: LP rules at the maximal depth, depth + 1 == maxLen (:82-98)
+  const GraphView g0 = c.view(a.p.g0);
+  for (uint32_t e = 0; e < (uint32_t)NE; e++) {
+    const uint32_t u = srcu(e);
+    const T mx = s_lmax[e];
+    if (u == NEMO_NONE || mx == 0) continue;
+    const uint32_t b = u & 63u;
+    const T *ring = ringp(e), *gv = gvalp(e);
+    for (uint32_t pos = tid; pos < V; pos += DX_NT) {
+      bool hit;
+      if (WHOLE) {
+        hit = (L.gate[e * W + pos] & 2u) && ring[pos] == mx;
+      } else {
+        hit = (a.p.info[pos] & DXI_RULE) && ((a.lw[(size_t)(u >> 6) * V + pos] >> b) & 1ull) &&
+              __hip_atomic_load(gv + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mx;
+      }
+      if (!hit) continue;
+      const uint32_t k = atomicAdd(a.n_missing, 1u);
+      a.missing[2 * k] = u;
+      a.missing[2 * k + 1] = g0.topo[pos];
+    }
+  }
+}
+
+// ---- D and D-leaf goals: one thread per (position, chunk) ----------------------------
+// D = F & B; a D goal is a leaf when no child is in D (:82-98, leaf = D goal
+// with D-out-degree 0).  Children of position p: the reversed-order row of
+// V-1-p, as reversed positions.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_leaf(DxArgs a) {
+  const uint32_t c = blockIdx.y, V = a.p.V0;
+  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (pos >= V) return;
+  const uint64_t *F = a.fw + (size_t)c * V, *B = a.bw + (size_t)c * V;
+  const uint32_t r = V - 1u - pos;
+  const uint64_t d = F[pos] & B[r];
+  a.dw[(size_t)c * V + pos] = d;
+  if (a.p.info[pos] & DXI_RULE) return;  // k_dx_lp writes the rules' word
+  uint64_t dc = 0;
+  if (d)
+    for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) {
+      const uint32_t x = a.p.fc[j];  // reversed position of a child
+      dc |= F[V - 1u - x] & B[x];
+    }
+  a.lw[(size_t)c * V + pos] = d & ~dc;
+}
+// LP rules: D rules with a D-leaf goal child; the chunk's summary of sources with any
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_lp(DxArgs a) {
+  const uint32_t c = blockIdx.y, V = a.p.V0;
+  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  uint64_t lp = 0;
+  if (pos < V && (a.p.info[pos] & DXI_RULE)) {
+    const uint64_t d = a.dw[(size_t)c * V + pos];
+    const uint64_t *Lw = a.lw + (size_t)c * V;
+    const uint32_t r = V - 1u - pos;
+    if (d)
+      for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) lp |= Lw[V - 1u - a.p.fc[j]];
+    lp &= d;
+    a.lw[(size_t)c * V + pos] = lp;
+  }
+  for (int d = 32; d >= 1; d >>= 1) lp |= __shfl_xor(lp, d);
+  if (lane_id() == 0 && lp) atomicOr((unsigned long long *)&a.lpany[c], (unsigned long long)lp);
+}
+
+// ---- D masks by node for every entry ------------------------------------------------
+// thread: one node, DXM_E consecutive entries (entries of one source share its bit word)
+#define DXM_E 8u
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
+  const uint32_t V = a.p.V0, v = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (v >= V) return;
+  const uint32_t pos = a.p.tpos[v];
+  const uint32_t e0 = blockIdx.y * DXM_E, e1 = min(a.n_entries, e0 + DXM_E);
+  uint32_t lc = NEMO_NONE;
+  uint64_t w = 0;
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t u = a.map[e], c = u >> 6;
+    if (c != lc) {
+      w = a.dw[(size_t)c * V + pos];
+      lc = c;
+    }
+    a.mask[(size_t)e * V + v] = (uint8_t)((w >> (u & 63u)) & 1ull);
+  }
+}
+
+// ---- launch -----------------------------------------------------------------------------
+template <int MODE, int NE, bool WHOLE>
+static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxWalkCfg &cfg, dim3 grid, hipStream_t s) {
+  using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
+  const uint32_t bytes = dx_lds_bytes<T, NE>(cfg.W, cfg.R, cfg.EC);
+  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)bytes);
+  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE>), grid, dim3(DX_NT), bytes, s, c, a, cfg);
+}
+
+#define DX_LDS_MAX (160u * 1024u - 1024u)
+// windowed configurations: W positions, R ring slots (power of two, > W), EC links
+static const DxWalkCfg kReach = {2048, 8192, 16384, 0};
+static const DxWalkCfg kDepth = {1024, 4096, 8192, 0};
+static const DxWalkCfg kTiny = {64, 128, 1024, 0};  // test knob (window = 2): most links leave the ring
+
+// every row of g0 must fit one window's links (launch_dx's windowed configurations)
+uint32_t dx_max_row() { return std::min(kReach.EC, kDepth.EC); }
+uint32_t dx_max_row_tiny() { return kTiny.EC; }
+
+void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
+  const uint32_t V = a.p.V0, E = a.p.E0;
+  if (!V || !a.nu) return;
+  const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
+  if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
+  launch_zero(a.lpany, (uint64_t)a.nch * 8u, s);
+  hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
+  hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  // reachability: the whole graph in one window when its image fits
+  const DxWalkCfg whole = {V, V, std::max(E, 1u), 1};
+  const bool small = a.window == 0 && V < 0xFFFFu && E <= 0xFFFFu;
+  if (small && dx_lds_bytes<uint64_t, 1>(V, V, whole.EC) <= DX_LDS_MAX)
+    walk_launch<0, 1, true>(c, a, whole, dim3(a.nch, 2), s);
+  else
+    walk_launch<0, 1, false>(c, a, a.window == 2 ? kTiny : kReach, dim3(a.nch, 2), s);
+  hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  if (small && dx_lds_bytes<uint32_t, 4>(V, V, whole.EC) <= DX_LDS_MAX)
+    walk_launch<2, 4, true>(c, a, whole, dim3((a.nu + 3) / 4), s);
+  else
+    walk_launch<2, 4, false>(c, a, a.window == 2 ? kTiny : kDepth, dim3((a.nu + 3) / 4), s);
+  if (a.n_entries)
+    hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
+}
+
+}  // namespace nemo

@@ -1,0 +1,108 @@
+"""GPU parity of the multi-entry CreateNaiveDiffProv (nemo_amd/csrc/k_dx.hip): D masks and missing rules of
+every diff entry against the oracle (oracle/nemo_oracle.c, diff-only mode) and against the one-workgroup-per-
+entry kernels (option diff_legacy), bit-exact.
+
+Reference: differential-provenance.go:18-146 (Good = run-0 post goals whose label is not a post-goal label of
+the label source; D = Fwd*(Good) ∩ Bwd*(Good); missing = D rules with a D-leaf child at maximal depth).
+
+The walks are exercised in their three forms: the whole of run 0's post graph in one LDS window (small
+graphs), Kahn-order windows with a ring of recent values (diff_window=1), and tiny windows whose ring most
+links leave (diff_window=2), so that the values of earlier windows are read back from HBM at staging.
+Sources come in 64-wide chunks: corpora with more than 64 failed runs take several.
+"""
+import numpy as np
+import pytest
+
+from nemo_amd import engine as E
+from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE
+from oracle import oracle as O
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def _rows(m):
+    m = np.asarray(m, np.int64).reshape(-1, 2)
+    return m[np.lexsort((m[:, 1], m[:, 0]))]
+
+
+def _device(eng, corpus, f, mode, window=0, legacy=0):
+    eng.set_option("diff_window", window)
+    eng.set_option("diff_legacy", legacy)
+    try:
+        eng.diffprov(f, mode)
+        return eng.diff_masks(len(f)), _rows(eng.missing())
+    finally:
+        eng.set_option("diff_window", 0)
+        eng.set_option("diff_legacy", 0)
+
+
+def _check_corpus(eng, corpus, windows=(0, 1, 2)):
+    f = corpus.failed_iters()
+    assert f and 0 in set(int(x) for x in corpus.iteration)
+    eng.load(corpus)
+    eng.mark()
+    for mode in (DIFF_PER_RUN, DIFF_REFERENCE):
+        orc = O.analyze(corpus, [0], f, diff_mode=mode, threads=8, diff_only=True)
+        want_m, want_r = orc.diff_mask, _rows(orc.missing)
+        for w in windows:
+            m, r = _device(eng, corpus, f, mode, window=w)
+            assert np.array_equal(m, want_m), f"D masks differ (mode {mode}, window {w}): " \
+                f"{int((m != want_m).any(1).sum())} of {len(f)} entries"
+            assert np.array_equal(r, want_r), f"missing rows differ (mode {mode}, window {w})"
+        lm, lr = _device(eng, corpus, f, mode, legacy=1)
+        assert np.array_equal(lm, want_m) and np.array_equal(lr, want_r), "legacy kernels differ"
+
+
+def test_c3_shape_many_sources(eng):
+    # ~5k-node graphs (the bench's C3 shape), > 64 failed runs: two 64-source chunks
+    corpus, _ = synth.generate(170, p_fault=0.55, prepend_run0=True, **synth.CONFIGS["c3"])
+    assert len(corpus.failed_iters()) > 64
+    _check_corpus(eng, corpus)
+
+
+def test_deep_shape(eng):
+    # the C5 generator's shape at 40k-node graphs: ~4 edges per node, long-span parents, windowed walks
+    corpus, _ = synth.generate(10, target_nodes=40000, eot=40, body_extra=6, nval=3, nloc=4, p_fault=0.5,
+                               prepend_run0=True)
+    assert corpus.edge_off[-1] > 3.5 * corpus.node_off[-1]
+    _check_corpus(eng, corpus)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_corpora(eng, seed):
+    # small random provenance graphs (tests/small.py): empty D sets, isolated Good goals, no LP rules
+    from tests.small import random_corpus
+    for k in range(6):
+        corpus, _ = random_corpus(100 * seed + k, n_runs=6, max_nodes=40)
+        if not corpus.failed_iters() or 0 not in set(int(x) for x in corpus.iteration):
+            continue
+        _check_corpus(eng, corpus)
+
+
+def test_label_set_mode(eng):
+    # nemo_diffprov_host_labels: one label set for every entry (the sharded reference mode)
+    corpus, _ = synth.generate(40, p_fault=0.5, prepend_run0=True, **synth.CONFIGS["c3"])
+    f = corpus.failed_iters()
+    eng.load(corpus)
+    eng.mark()
+    g = 2 * corpus.run_index(f[0]) + 1
+    a, b = int(corpus.node_off[g]), int(corpus.node_off[g + 1])
+    from nemo_amd.corpus import NODE_RULE
+    labels = corpus.label[a:b][(corpus.node_word[a:b] & NODE_RULE) == 0]
+    orc = O.analyze(corpus, [0], f, diff_mode=DIFF_REFERENCE, threads=8, diff_only=True)
+    for w in (0, 2):
+        eng.set_option("diff_window", w)
+        try:
+            eng.diffprov_host_labels(f, labels)
+            assert np.array_equal(eng.diff_masks(len(f)), orc.diff_mask)
+            assert np.array_equal(_rows(eng.missing()), _rows(orc.missing))
+        finally:
+            eng.set_option("diff_window", 0)
