@@ -72,6 +72,11 @@ def parse():
                          "sweeps overlap another's bandwidth-bound passes (default: the config's)")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
+    ap.add_argument("--runs-total", type=int, default=None,
+                    help="C5 at its configured size (BASELINE configs[4]: 1k runs): the runs in batches of "
+                         "--batch-runs, each uploaded (H2D + CSR) on one of two contexts while the previous batch is "
+                         "analysed on the other; value = runs/s of whole passes including the uploads")
+    ap.add_argument("--batch-runs", type=int, default=160)
     ap.add_argument("--diff-reps", type=int, default=5,
                     help="per_run differential-provenance leg after the timed steps (roofline_diff): this many "
                          "nemo_diffprov(failed, NEMO_DIFF_PER_RUN) calls over the resident corpus (0: off)")
@@ -147,6 +152,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     threads = cpu_info()["threads"]  # host generation / e2e ingest: every core the quota allows
+    if args.runs_total:
+        return runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist)
     t0 = time.time()
     if strong:  # C4: one fixed corpus, LPT-sharded by Σ(V+E) (nemo_partition_runs), run 0 replicated
         R_total = args.runs_per_gpu * world if args.runs_per_gpu else cfg["runs_total"]
@@ -370,6 +377,150 @@ def main():
         out["k_diff_entry_latency_ms"] = round(tim["k_diff"]["ms"] / tim["k_diff"]["launches"], 4)
     if rdiff is not None:
         out["roofline_diff"] = rdiff
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    for e in engines:
+        e.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
+    """C5 at its configured size (BASELINE.json configs[4]: 1k runs of 1M-node graphs), which does not fit
+    one MI355X's 288 GB at once.  The rank's runs are generated up front (host memory) in batches of
+    --batch-runs, each a corpus of its own with run 0 replicated, not owned, after the first.  A pass loads
+    batch i+1 (nemo_load_corpus: H2D + CSR + Kahn levels) on one of two contexts, from a second host thread,
+    while batch i is analysed on the other: mark, diff (reference mode: failedRuns[0]'s label set, taken
+    from the batch holding it), simplify, protos partial, hand-over, pulls, every D2H.  The batches' proto
+    vectors are summed on the host (prototype.go:79-130).  value = runs of a pass / its wall time, uploads
+    included; generation is not timed (it stands in for reading Molly output)."""
+    import threading
+
+    from nemo_amd import engine as E
+    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE, NODE_RULE
+    from tools import synth
+    mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
+    R = args.runs_total // world
+    base = rank * R
+    B = max(1, min(args.batch_runs, R))
+    t0 = time.time()
+    batches = []
+    for a in range(0, R, B):
+        c, _ = synth.generate(min(B, R - a), run_base=base + a, prepend_run0=True, threads=threads, **gen)
+        batches.append(c)
+    gen_s = time.time() - t0
+    succ_all, fail_all = [], []
+    for c in batches:
+        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
+        for it, st, o in zip(c.iteration, c.status, own):
+            if o:
+                (succ_all if st == "success" else fail_all).append(int(it))
+    success = [0] + [x for x in succ_all if x != 0]
+    f0_labels = None
+    if fail_all and mode == DIFF_REFERENCE:
+        f0 = min(fail_all) if world == 1 else None
+        for c in batches:
+            if f0 is not None and f0 in set(int(x) for x in c.iteration):
+                g = 2 * c.run_index(f0) + 1
+                a_, b_ = int(c.node_off[g]), int(c.node_off[g + 1])
+                f0_labels = c.label[a_:b_][(c.node_word[a_:b_] & NODE_RULE) == 0].copy()
+                break
+
+    def new_engine():
+        e = E.Engine(local)
+        for kv in args.set:
+            k, v = kv.split("=", 1)
+            e.set_option(k, int(v))
+        return e
+
+    engines = [new_engine(), new_engine()]
+    T = batches[0].n_tables
+
+    def analyse(eng, c):
+        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
+        its = [int(x) for x, o in zip(c.iteration, own) if o]
+        fset = set(fail_all)
+        bf = [it for it in its if it in fset]
+        eng.mark()
+        if bf:
+            if f0_labels is not None:
+                eng.diffprov_host_labels(bf, f0_labels)
+            else:
+                eng.diffprov(bf, DIFF_PER_RUN)
+        eng.simplify()
+        eng.protos_partial(success, 0)
+        eng.stage_simplified()
+        has0 = 0 in its
+        if has0:
+            eng.triggers()
+        eng.pull(1)
+        if bf:
+            eng.pull(2)
+        vec = eng.reduce_vector().astype(np.int64)
+        eng.run_tables(1)
+        if has0:
+            eng.trigger_rows()
+        if bf:
+            eng.diff_masks_view()
+        eng.missing()
+        eng.simplified_view()
+        return vec
+
+    def one_pass():
+        vec = np.zeros(2 * T + 4, np.int64)
+        engines[0].load(batches[0])
+        for i in range(len(batches)):
+            th = None
+            if i + 1 < len(batches):
+                nxt = engines[(i + 1) % 2]
+                th = threading.Thread(target=nxt.load, args=(batches[i + 1],))
+                th.start()
+            vec += analyse(engines[i % 2], batches[i])
+            if th is not None:
+                th.join()
+        torch.cuda.synchronize()
+        return E.reduce_interpret(vec.astype(np.uint32), T, batches[0].table_post)
+
+    for _ in range(args.warmup):
+        one_pass()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        one_pass()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    runs = sum(int((c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)).sum()) for c in batches)
+    total = runs * world
+    Vn = sum(int(c.node_off[-1]) for c in batches)
+    E_ = sum(int(c.edge_off[-1]) for c in batches)
+    out = {"metric": METRIC, "value": round(total * args.steps / elapsed, 2), "unit": "runs/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": "C5 at its configured size: runs_total runs x (pre, post) graphs of ~nodes_per_graph "
+                                  "nodes / ~4 edges per node at EOT eot (BASELINE configs[4]); a step is one pass "
+                                  "over every run, batches of batch_runs uploaded on one context while the previous "
+                                  "batch is analysed on another, uploads included",
+                      "runs_total": total, "runs_per_gpu": runs, "batch_runs": B, "batches_per_gpu": len(batches),
+                      "nodes_per_graph": gen["target_nodes"], "eot": gen["eot"], "nodes_total_rank0": Vn,
+                      "edges_total_rank0": E_, "edges_per_node": round(E_ / max(Vn, 1), 3),
+                      "failed_runs_rank0": len(fail_all), "diff_mode": args.diff_mode,
+                      "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped)",
+                      "lib_options": args.set},
+           "roofline": None, "cpu_baseline": None, "gen_seconds_rank0": round(gen_s, 2),
+           "note": "no per-kernel roofline on this line: the resident-batch line (--config c5) carries it"}
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
