@@ -195,25 +195,36 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 // MODE 0: reachability, T = u64 (64 sources per bit column), one walker;
 //         blockIdx.y = 0: Fwd* over parents in Kahn order, 1: Bwd* over
 //         children in reversed Kahn order.  value = Good | OR(links).
-// MODE 2: depth, T = u32, NE walkers (sources 4·blockIdx.x + e), Kahn order
-//         over parents: value = D ? 1 + max(links) : 0 (depth + 1 of D nodes;
-//         a non-D parent contributes 0, so the max runs over D parents).
+// MODE 2: depth, T = u32, NE walkers (sources NE·blockIdx.x + e), Kahn order
+//         over parents: s = D ? 1 + max(s of links) : 0 (depth + 1 of D nodes;
+//         a non-D parent has s = 0, so the max runs over D parents).  While a
+//         window is walked a ring slot holds DX_NOTD (not in D: absorbs every
+//         max) or DX_IND | r, r = the max so far; s = r + 1.
 // WHOLE: the graph is one window (ring = positions, no wrap, no misses).
+//
+// A window: staging (all waves) -> the walk (waves e < NE) -> finalize (all
+// waves: values to HBM, LP maxima).  Staging writes the window's links as u32
+// records (ring slot of the linked position | ring slot of the owner << 16) in
+// walk order, and the link range of every level segment.  The walk of a level
+// is then one pass over its links, lanes over links: read the record, read the
+// linked value, apply it to the owner's slot with an LDS atomic; a level only
+// reads slots of earlier levels, and a wave's LDS operations complete in
+// order, so no barrier separates the levels.
 #define DX_NT 256
-#define DX_SEG 256u
+#define DX_NOTD 0xFFFFFFFFu
+#define DX_IND 0x80000000u
 template <typename T, int NE>
 struct DxLds {
   T *ring0;          // NE rings of [R + 1] (stride rs); [R] is the identity (sink)
   uint32_t rs;
   uint32_t *off;     // [W + 1] absolute row starts of the window's positions
-  uint16_t *ent;     // [EC] ring index of each link (R: folded into the owner's init)
-  uint16_t *send;    // [W] end of the position's level in the window (relative)
-  uint8_t *gate;     // [NE][W] depth: 1 = D node, 2 = LP rule
+  uint32_t *lk;      // [EC] links: ring slot of the linked position (R: none) | owner's slot << 16
+  uint16_t *seg;     // [W + 1] first link of each level segment (relative); seg[nseg] = links
 };
 template <typename T, int NE>
 __host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC) {
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 1u)) + lds_align(4u * (W + 1u)) + lds_align(2u * EC) +
-         lds_align(2u * W) + NE * lds_align(W);
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 1u)) + lds_align(4u * (W + 1u)) + lds_align(4u * EC) +
+         lds_align(2u * (W + 1u));
 }
 template <typename T, int NE>
 __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC) {
@@ -224,11 +235,9 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_
   p += NE * lds_align((uint32_t)sizeof(T) * (R + 1u));
   L.off = (uint32_t *)p;
   p += lds_align(4u * (W + 1u));
-  L.ent = (uint16_t *)p;
-  p += lds_align(2u * EC);
-  L.send = (uint16_t *)p;
-  p += lds_align(2u * W);
-  L.gate = p;
+  L.lk = (uint32_t *)p;
+  p += lds_align(4u * EC);
+  L.seg = (uint16_t *)p;
   return L;
 }
 struct DxWalkCfg {
@@ -236,18 +245,13 @@ struct DxWalkCfg {
   uint32_t whole;     // 1: the whole graph is one window
 };
 
-template <typename T>
-__device__ __forceinline__ T dx_op(T a, T b, bool orop) {
-  if constexpr (sizeof(T) == 8) return a | b;
-  else return orop ? (a | b) : max(a, b);
-}
-
 template <int MODE, int NE, bool WHOLE>
 __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg cfg) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
+  constexpr int PS = 8;  // positions per thread per staging group (contiguous: segment order = thread order)
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_n;
-  __shared__ T s_lmax[NE];
+  __shared__ uint32_t s_n, s_red[DX_NT / 64];
+  __shared__ uint32_t s_lmax[NE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC;
   const bool rev = MODE == 0 && blockIdx.y == 1;
@@ -267,17 +271,33 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
     if (MODE == 0) return (T *)((rev ? a.bw : a.fw) + (size_t)chunk * V);
     return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
   };
+  auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
   bool any = MODE == 0;
   for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
   if (!any) return;  // workgroup-uniform
   if (tid < (uint32_t)NE) {
-    ringp(tid)[R] = (T)0;
+    ringp(tid)[R] = MODE == 0 ? (T)0 : (T)DX_NOTD;  // the sink reads as "no value": OR 0, depth s = 0
     s_lmax[tid] = 0;
   }
+  uint32_t lmax[NE];
+#pragma unroll
+  for (int e = 0; e < NE; e++) lmax[e] = 0;
   for (uint32_t w0 = 0; w0 < V;) {
     const uint32_t nmax = min(W, V - w0);
-    // ---- staging 1: the window's row starts; it ends where its links would pass EC ----
-    for (uint32_t k = tid; k <= nmax; k += DX_NT) L.off[k] = rowp[w0 + k];
+    // ---- staging 1: row starts; the window ends where its links would pass EC ----
+    for (uint32_t k0 = 0; k0 <= nmax; k0 += 8 * DX_NT) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t k = k0 + q * DX_NT + tid;
+        v[q] = k <= nmax ? rowp[w0 + k] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t k = k0 + q * DX_NT + tid;
+        if (k <= nmax) L.off[k] = v[q];
+      }
+    }
     if (tid == 0) s_n = 0;
     __syncthreads();
     {
@@ -289,37 +309,55 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
     }
     __syncthreads();
     const uint32_t n = s_n, w1 = w0 + n, base = L.off[0], ne = L.off[n] - base;
-    // ---- staging 2: init values into the positions' ring slots (no link of the
-    // window reads those: they hold positions older than the ring), gates, level ends ----
-    for (uint32_t k = tid; k < n; k += DX_NT) {
-      const uint32_t i = w0 + k, pos = rev ? V - 1u - i : i;
-      const uint32_t sl = WHOLE ? i : (i & (R - 1u));
-      const uint32_t le = rev ? V - a.p.lbeg[pos] : a.p.lend[pos];
-      L.send[k] = (uint16_t)(min(le, w1) - w0);
-      if (MODE == 0) {
-        ringp(0)[sl] = (T)a.gw[(size_t)chunk * V + pos];
-      } else {
-        const bool rule = (a.p.info[pos] & DXI_RULE) != 0;
+    // ---- staging 2: per position (PS consecutive per thread): init value into
+    // its ring slot (no link of the window reads those slots: they hold
+    // positions older than the ring), the owner half of its links' records, the
+    // level segments (a position that starts its level starts a segment) ----
+    uint32_t nseg = 0;
+    for (uint32_t g0 = 0; g0 < n; g0 += PS * DX_NT) {
+      const uint32_t k0 = g0 + tid * PS;
+      uint32_t lb[PS], st = 0;
+      T ini[PS][NE];
 #pragma unroll
-        for (uint32_t e = 0; e < (uint32_t)NE; e++) {
-          uint8_t g = 0;
-          const uint32_t u = srcu(e);
-          if (u != NEMO_NONE) {
-            const uint32_t b = u & 63u;
-            const uint64_t dv = a.dw[(size_t)(u >> 6) * V + pos];
-            const uint64_t lv = rule ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
-            g = (uint8_t)(((dv >> b) & 1ull) | (((lv >> b) & 1ull) << 1));
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q;
+        const bool in = k < n;
+        const uint32_t i = w0 + (in ? k : 0u), pos = rev ? V - 1u - i : i;
+        lb[q] = rev ? V - a.p.lend[pos] : a.p.lbeg[pos];  // the walk index where the position's level starts
+        if (MODE == 0) {
+          ini[q][0] = in ? (T)a.gw[(size_t)chunk * V + pos] : (T)0;
+        } else {
+#pragma unroll
+          for (int e = 0; e < NE; e++) {
+            const uint32_t u = srcu(e);
+            const uint64_t dv = u != NEMO_NONE && in ? a.dw[(size_t)(u >> 6) * V + pos] : 0ull;
+            ini[q][e] = ((dv >> (u & 63u)) & 1ull) ? DX_IND : DX_NOTD;
           }
-          ringp(e)[sl] = (T)0;
-          L.gate[e * W + k] = g;
         }
       }
+#pragma unroll
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q;
+        if (k >= n) continue;
+        const uint32_t sl = slot(w0 + k);
+#pragma unroll
+        for (int e = 0; e < NE; e++) ringp(e)[sl] = ini[q][e];
+        for (uint32_t j = L.off[k]; j < L.off[k + 1]; j++) ((uint16_t *)&L.lk[j - base])[1] = (uint16_t)sl;
+        st |= (k == 0 || lb[q] == w0 + k ? 1u : 0u) << q;
+      }
+      uint32_t tot;
+      uint32_t o = nseg + block_exscan<DX_NT>((uint32_t)__popc(st), &tot, s_red);
+#pragma unroll
+      for (int q = 0; q < PS; q++)
+        if ((st >> q) & 1u) L.seg[o++] = (uint16_t)(L.off[k0 + q] - base);
+      nseg += tot;
     }
+    if (tid == 0) L.seg[nseg] = (uint16_t)ne;
     __syncthreads();
-    // ---- staging 3: the window's links, one contiguous range of col, in 16-B
-    // aligned chunks.  A link older than the ring reads its final value from
-    // HBM (written and fenced by an earlier window's walk) and is folded into
-    // its owner's init; the others become ring indices ----
+    // ---- staging 3: the links, one contiguous range of col, in 16-B aligned
+    // chunks.  A link older than the ring reads its final value from HBM
+    // (written and fenced by an earlier window's finalize) and is applied to
+    // its owner's init; the others get the linked position's ring slot ----
     {
       const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
       for (uint32_t cb = c0; cb < c1; cb += 4 * DX_NT) {
@@ -338,108 +376,104 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
             const uint32_t j = 4 * ck + b;
             if (ck >= c1 || j < base || j >= base + ne) continue;
             const uint32_t x = qs[b];  // walk index of the linked position
+            uint16_t *rec = (uint16_t *)&L.lk[j - base];
             if (WHOLE || x + R >= w1) {
-              L.ent[j - base] = (uint16_t)(WHOLE ? x : (x & (R - 1u)));
+              rec[0] = (uint16_t)slot(x);
               continue;
             }
-            L.ent[j - base] = (uint16_t)R;
-            uint32_t lo = 0, hi = n;  // the owner: off[lo] <= j < off[hi]
-            while (hi - lo > 1) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (L.off[mid] <= j) lo = mid;
-              else hi = mid;
-            }
-            const uint32_t sl = (w0 + lo) & (R - 1u);
+            rec[0] = (uint16_t)R;
+            const uint32_t osl = rec[1];
 #pragma unroll
             for (uint32_t e = 0; e < (uint32_t)NE; e++) {
               if (MODE == 2 && srcu(e) == NEMO_NONE) continue;
               const T val = __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[sl], (unsigned long long)val);
-              else atomicMax((uint32_t *)&ringp(e)[sl], (uint32_t)val);
+              if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[osl], (unsigned long long)val);
+              else atomicMax((uint32_t *)&ringp(e)[osl], DX_IND | (uint32_t)val);
             }
           }
         }
       }
     }
     __syncthreads();
-    // ---- the walk: wave e < NE walks source e through the window's levels; a
-    // level (<= DX_SEG positions) is one step of independent lanes ----
-    if (wv < (uint32_t)NE) {
-      const uint32_t e = wv;
-      T *ring = ringp(e), *gv = gvalp(e);
-      const bool live = srcu(e) != NEMO_NONE;
-      T lmax = 0;
-      for (uint32_t s = 0; s < n && live;) {
-        const uint32_t send = min((uint32_t)__builtin_amdgcn_readfirstlane(L.send[s]), s + DX_SEG);
-        const uint32_t cnt = send - s;
+    // ---- the walk: wave e < NE walks source e through the window's level
+    // segments, lanes over a segment's links ----
+    if (wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE)) {
+      T *ring = ringp(wv);
+      uint32_t lo = L.seg[0];
+      for (uint32_t t = 0; t < nseg; t++) {
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(L.seg[t + 1]);
+        for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
+          uint32_t rc[4];
+          T x[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          if ((uint32_t)(64 * q) >= cnt) break;  // uniform
-          const uint32_t k = s + 64u * q + lane;
-          const bool in = k < send;
-          const uint32_t kk = in ? k : s;
-          const uint32_t sl = WHOLE ? w0 + kk : ((w0 + kk) & (R - 1u));
-          const uint32_t o0 = L.off[kk] - base, m = in ? L.off[kk + 1] - L.off[kk] : 0u;
-          T v = ring[sl];
-          uint32_t mm = m;
-          for (int d = 32; d >= 1; d >>= 1) mm = max(mm, (uint32_t)__shfl_xor(mm, d));
-          for (uint32_t t = 0; t < mm; t += 4) {
-            uint32_t ix[4];
+          for (int q = 0; q < 4; q++) {
+            const uint32_t j = j0 + 64u * q + lane;
+            rc[q] = j < hi ? L.lk[j] : ((uint32_t)R | ((uint32_t)R << 16));
+          }
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-              const uint32_t j = o0 + t + b;
-              const uint32_t xj = L.ent[j < EC ? j : 0u];
-              ix[b] = t + b < m ? xj : R;
+          for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            if (j0 + 64u * q + lane >= hi) continue;
+            if (MODE == 0) {
+              atomicOr((unsigned long long *)&ring[rc[q] >> 16], (unsigned long long)x[q]);
+            } else {
+              const uint32_t sv = (uint32_t)x[q] == DX_NOTD ? 0u : ((uint32_t)x[q] & ~DX_IND) + 1u;
+              atomicMax((uint32_t *)&ring[rc[q] >> 16], DX_IND | sv);
             }
-            T x[4];
-#pragma unroll
-            for (int b = 0; b < 4; b++) x[b] = ring[ix[b]];
-#pragma unroll
-            for (int b = 0; b < 4; b++) v = dx_op<T>(v, x[b], MODE == 0);
           }
-          if (MODE == 2) {
-            const uint8_t g = L.gate[e * W + kk];
-            v = (g & 1u) ? v + 1u : (T)0;
-            if (in && (g & 2u)) lmax = v > lmax ? v : lmax;
-          }
-          if (in) {
-            ring[sl] = v;
-            gv[w0 + k] = v;
-          }
+          if (j0 + 256 >= hi) break;
         }
-        s = send;
+        lo = hi;
         wsync();
       }
-      if (MODE == 2) {
-        for (int d = 32; d >= 1; d >>= 1) {
-          const T y = __shfl_xor(lmax, d);
-          lmax = y > lmax ? y : lmax;
-        }
-        if (lane == 0 && lmax > s_lmax[e]) s_lmax[e] = lmax;
-      }
-      __threadfence();  // the window's values are final in HBM before later windows (and the rows pass) read them
     }
+    __syncthreads();
+    // ---- finalize: the window's values to HBM (depth: s, and the LP maxima) ----
+    for (uint32_t k0 = 0; k0 < n; k0 += 4 * DX_NT) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t k = k0 + q * DX_NT + tid;
+        if (k >= n) continue;
+        const uint32_t i = w0 + k, sl = slot(i);
+        if (MODE == 0) {
+          gvalp(0)[i] = ringp(0)[sl];
+        } else {
+          const bool rule = (a.p.info[i] & DXI_RULE) != 0;
+#pragma unroll
+          for (int e = 0; e < NE; e++) {
+            const uint32_t u = srcu(e);
+            if (u == NEMO_NONE) continue;
+            const uint32_t r = (uint32_t)ringp(e)[sl];
+            const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
+            gvalp(e)[i] = (T)sv;
+            if (rule && ((a.lw[(size_t)(u >> 6) * V + i] >> (u & 63u)) & 1ull)) lmax[e] = max(lmax[e], sv);
+          }
+        }
+      }
+    }
+    __threadfence();  // the values are final in HBM before later windows (and the rows pass) read them
     __syncthreads();
     w0 = w1;
   }
   if (MODE != 2) return;
   // missing rows: LP rules at the maximal depth, depth + 1 == maxLen (:82-98)
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    uint32_t m = lmax[e];
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d));
+    if (lane == 0 && m) atomicMax(&s_lmax[e], m);
+  }
+  __syncthreads();
   const GraphView g0 = c.view(a.p.g0);
   for (uint32_t e = 0; e < (uint32_t)NE; e++) {
-    const uint32_t u = srcu(e);
-    const T mx = s_lmax[e];
+    const uint32_t u = srcu(e), mx = s_lmax[e];
     if (u == NEMO_NONE || mx == 0) continue;
     const uint32_t b = u & 63u;
-    const T *ring = ringp(e), *gv = gvalp(e);
+    const T *gv = gvalp(e);
     for (uint32_t pos = tid; pos < V; pos += DX_NT) {
-      bool hit;
-      if (WHOLE) {
-        hit = (L.gate[e * W + pos] & 2u) && ring[pos] == mx;
-      } else {
-        hit = (a.p.info[pos] & DXI_RULE) && ((a.lw[(size_t)(u >> 6) * V + pos] >> b) & 1ull) &&
-              __hip_atomic_load(gv + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mx;
-      }
-      if (!hit) continue;
+      if (!(a.p.info[pos] & DXI_RULE) || !((a.lw[(size_t)(u >> 6) * V + pos] >> b) & 1ull)) continue;
+      if (__hip_atomic_load(gv + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != mx) continue;
       const uint32_t k = atomicAdd(a.n_missing, 1u);
       a.missing[2 * k] = u;
       a.missing[2 * k + 1] = g0.topo[pos];
@@ -518,8 +552,8 @@ static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxWalkCfg &cf
 
 #define DX_LDS_MAX (160u * 1024u - 1024u)
 // windowed configurations: W positions, R ring slots (power of two, > W), EC links
-static const DxWalkCfg kReach = {2048, 8192, 16384, 0};
-static const DxWalkCfg kDepth = {1024, 4096, 8192, 0};
+static const DxWalkCfg kReach = {2048, 8192, 12288, 0};
+static const DxWalkCfg kDepth = {1024, 4096, 6144, 0};
 static const DxWalkCfg kTiny = {64, 128, 1024, 0};  // test knob (window = 2): most links leave the ring
 
 // every row of g0 must fit one window's links (launch_dx's windowed configurations)
