@@ -74,6 +74,7 @@ struct nemo_ctx {
   uint32_t n_entries = 0, diff_cap = 0, legacy_cap = 0;
   uint32_t *d_r0lab = nullptr, *d_r0idx = nullptr, n_r0lab = 0;
   uint32_t *d_r0hkey = nullptr, *d_r0hval = nullptr, r0hmask = 0;
+  uint32_t *d_r0dense = nullptr, nlab = 0;  // the dense label table of the multi-entry diff (DxArgs::r0dense)
   uint32_t *d_dsrc = nullptr, *d_miss = nullptr, *d_nmiss = nullptr;
   uint8_t *d_dbits = nullptr, *d_dmask = nullptr;
   int32_t *d_ddepth = nullptr;
@@ -388,6 +389,8 @@ static void release_corpus(nemo_ctx *c) {
   c->d_r0lab = c->d_r0idx = c->d_dsrc = c->d_miss = c->d_nmiss = nullptr;
   c->d_r0hkey = c->d_r0hval = nullptr;
   c->r0hmask = 0;
+  c->d_r0dense = nullptr;
+  c->nlab = 0;
   c->d_dbits = c->d_dmask = nullptr;
   c->d_ddepth = nullptr;
   c->d_dtopo = nullptr;
@@ -982,6 +985,24 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     if ((rc = dalloc(c, &c->d_r0hval, hcap))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_r0hkey, hkey.data(), hcap * 4, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_r0hval, hval.data(), hcap * 4, hipMemcpyHostToDevice, s));
+    // the same as a dense table over every label id of the corpus, when that is at most 256M entries:
+    // one load per source goal instead of a probe sequence
+    uint32_t maxlab = 0;
+    for (uint64_t v = 0; v < c->V; v++) maxlab = std::max(maxlab, in->label[v]);
+    const uint64_t nlab = c->V ? (uint64_t)maxlab + 1 : 0;
+    std::vector<uint32_t> dense;
+    if (nlab && nlab <= (1ull << 28)) {
+      dense.assign(nlab, NEMO_NONE);
+      for (size_t i = 0; i < l.size();) {
+        size_t j = i;
+        while (j < l.size() && l[j] == l[i]) j++;
+        dense[l[i]] = (uint32_t)(i << 4) | (uint32_t)std::min<size_t>(j - i, 15);
+        i = j;
+      }
+      if ((rc = dalloc(c, &c->d_r0dense, nlab))) return rc;
+      HIPCHK(c, hipMemcpyAsync(c->d_r0dense, dense.data(), nlab * 4, hipMemcpyHostToDevice, s));
+      c->nlab = (uint32_t)nlab;
+    }
     if (!l.empty()) {
       HIPCHK(c, hipMemcpyAsync(c->d_r0lab, l.data(), l.size() * 4, hipMemcpyHostToDevice, s));
       HIPCHK(c, hipMemcpyAsync(c->d_r0idx, ix.data(), ix.size() * 4, hipMemcpyHostToDevice, s));
@@ -1364,6 +1385,8 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.r0hkey = c->d_r0hkey;
     a.r0hval = c->d_r0hval;
     a.r0hmask = c->r0hmask;
+    a.r0dense = c->d_r0dense;
+    a.nlab = c->nlab;
     a.pb = c->d_dxpb;
     a.w32 = w32;
     uint64_t maxsrc = d_labels ? labels_cap : 0;

@@ -9,6 +9,8 @@
 // in graph order, so the result is identical to the sequential interning of
 // nemo_amd/corpus.py (tests/test_ingest.py checks it array for array).
 // Host code only; no device work.
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -56,31 +58,41 @@ inline uint64_t hash_sv(std::string_view s) {
   return h ^ (h >> 29);
 }
 
-struct FlatMap {  // string_view -> u32, keys live in the graph's arena
+struct FlatMap {  // string_view -> u32, keys live in the graph's arena; slots tagged with the hash
+  struct Slot {
+    uint32_t tag, val;  // val ~0u = empty
+  };
+  std::vector<Slot> slot;
   std::vector<std::string_view> key;
-  std::vector<uint32_t> val;
   size_t mask = 0;
   void init(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
+    slot.assign(cap, Slot{0, ~0u});
     key.assign(cap, std::string_view());
-    val.assign(cap, ~0u);
     mask = cap - 1;
   }
   // value of k, inserting v if absent; second = inserted
   std::pair<uint32_t, bool> emplace(std::string_view k, uint32_t v) {
-    for (size_t h = hash_sv(k) & mask;; h = (h + 1) & mask) {
-      if (val[h] == ~0u) {
-        key[h] = k, val[h] = v;
+    const uint64_t h = hash_sv(k);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      Slot &sl = slot[i];
+      if (sl.val == ~0u) {
+        sl = Slot{tag, v};
+        key[i] = k;
         return {v, true};
       }
-      if (key[h] == k) return {val[h], false};
+      if (sl.tag == tag && key[i] == k) return {sl.val, false};
     }
   }
   uint32_t find(std::string_view k) const {
-    for (size_t h = hash_sv(k) & mask;; h = (h + 1) & mask) {
-      if (val[h] == ~0u) return ~0u;
-      if (key[h] == k) return val[h];
+    const uint64_t h = hash_sv(k);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot &sl = slot[i];
+      if (sl.val == ~0u) return ~0u;
+      if (sl.tag == tag && key[i] == k) return sl.val;
     }
   }
 };
@@ -156,14 +168,41 @@ struct Json {
     p += 4;
     return v;
   }
+  // the first '"' or '\\' at or after q (e if none), 16 bytes at a time
+  const char *scan(const char *q) const {
+    const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\');
+    while (e - q >= 16) {
+      const __m128i x = _mm_loadu_si128((const __m128i *)q);
+      const int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, quote), _mm_cmpeq_epi8(x, bslash)));
+      if (m) return q + __builtin_ctz((unsigned)m);
+      q += 16;
+    }
+    while (q < e && *q != '"' && *q != '\\') q++;
+    return q;
+  }
+  // a string as a view: in place when it has no escapes (base = the buffer the
+  // reader walks, which is the arena), else decoded and appended to `o`
+  bool sview(std::vector<char> &o, const char *base, Str &out) {
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    const char *q = scan(p + 1);
+    if (q < e && *q == '"') {
+      out = Str{(uint32_t)(p + 1 - base), (uint32_t)(q - p - 1)};
+      p = q + 1;
+      return true;
+    }
+    const size_t o0 = o.size();
+    if (!str(o)) return false;
+    out = Str{(uint32_t)o0, (uint32_t)(o.size() - o0)};
+    return true;
+  }
   // string into `o` (appended); returns false on error
   bool str(std::vector<char> &o) {
     ws();
     if (p >= e || *p != '"') return ok = false;
     p++;
     while (p < e) {
-      const char *q = p;
-      while (q < e && *q != '"' && *q != '\\') q++;
+      const char *q = scan(p);
       o.insert(o.end(), p, q);
       p = q;
       if (p >= e) break;
@@ -291,36 +330,51 @@ bool clock_time(std::string_view s, bool wild, std::string &out) {
   return false;
 }
 
-bool read_file(const std::string &path, std::vector<char> &buf) {
-  FILE *f = fopen(path.c_str(), "rb");
-  if (!f) return false;
-  fseek(f, 0, SEEK_END);
-  long n = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  buf.resize(n > 0 ? (size_t)n : 0);
-  size_t got = n > 0 ? fread(buf.data(), 1, (size_t)n, f) : 0;
-  fclose(f);
-  return got == buf.size();
-}
-
 uint8_t type_class(std::string_view t) {
   return t == "next" ? NEMO_TYPE_NEXT : t == "async" ? NEMO_TYPE_ASYNC : NEMO_TYPE_OTHER;
 }
 
+// key k (a view into the arena) equals the lower-case keyword s, case-insensitively
+// (encoding/json matches keys case-insensitively): the exact spelling first
+inline bool keyis(std::string_view k, const char *s, size_t n) {
+  if (k.size() != n) return false;
+  if (!memcmp(k.data(), s, n)) return true;
+  for (size_t i = 0; i < n; i++)
+    if (tolower((unsigned char)k[i]) != s[i]) return false;
+  return true;
+}
+
 void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g) {
-  std::vector<char> buf;
-  if (!read_file(path, buf)) {
-    g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
-            " provenance of file '" + path + "'";
-    return;
+  // the file is read into the arena itself: strings without escapes are views
+  // of it, decoded ones and clock times are appended (reserved: no reallocation)
+  {
+    FILE *f = fopen(path.c_str(), "rb");
+    bool ok = f != nullptr;
+    if (ok) {
+      fseek(f, 0, SEEK_END);
+      const long n = ftell(f);
+      fseek(f, 0, SEEK_SET);
+      const size_t sz = n > 0 ? (size_t)n : 0;
+      g.arena.reserve(3 * sz + 64);
+      g.arena.resize(sz);
+      ok = (sz ? fread(g.arena.data(), 1, sz, f) : 0) == sz;
+      fclose(f);
+    }
+    if (!ok) {
+      g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
+              " provenance of file '" + path + "'";
+      return;
+    }
   }
-  g.arena.reserve(2 * buf.size() + 64);  // decoded strings <= file; clock times <= their labels: no reallocation
-  Json j{buf.data(), buf.data() + buf.size()};
+  const size_t fsz = g.arena.size();
+  const char *base = g.arena.data();
+  Json j{base, base + fsz};
   struct Rec {
     Str f[4];
   };
   std::vector<Rec> goals, rules;
   std::vector<std::pair<Str, Str>> edges;
+  goals.reserve(fsz / 160), rules.reserve(fsz / 160), edges.reserve(fsz / 64);
   j.ws();
   if (j.lit("null")) {
   } else if (j.p < j.e && *j.p == '{') {
@@ -329,16 +383,16 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     if (j.p < j.e && *j.p == '}') j.p++;
     else
       while (j.ok) {
-        std::vector<char> &key = j.key;
-        key.clear();
-        if (!j.str(key)) break;
+        Str ks;
+        if (!j.sview(g.arena, base, ks)) break;
+        const std::string_view key = g.sv(ks);
         j.ws();
         if (j.p >= j.e || *j.p != ':') {
           j.ok = false;
           break;
         }
         j.p++;
-        int which = ieq(key, "goals") ? 0 : ieq(key, "rules") ? 1 : ieq(key, "edges") ? 2 : -1;
+        const int which = keyis(key, "goals", 5) ? 0 : keyis(key, "rules", 5) ? 1 : keyis(key, "edges", 5) ? 2 : -1;
         j.ws();
         if (which < 0 || j.lit("null")) {
           if (which < 0) j.skip();
@@ -360,32 +414,33 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
               if (j.p < j.e && *j.p == '}') j.p++;
               else
                 while (j.ok) {
-                  std::vector<char> &k = j.key;
-                  k.clear();
-                  if (!j.str(k)) break;
+                  Str kst;
+                  if (!j.sview(g.arena, base, kst)) break;
+                  const std::string_view k = g.sv(kst);
                   j.ws();
                   if (j.p >= j.e || *j.p != ':') {
                     j.ok = false;
                     break;
                   }
                   j.p++;
-                  static const char *gk[4] = {"id", "label", "table", "time"};
-                  static const char *rk[4] = {"id", "label", "table", "type"};
                   int f = -1;
-                  if (which == 2) f = ieq(k, "from") ? 0 : ieq(k, "to") ? 1 : -1;
-                  else
-                    for (int q = 0; q < 4; q++)
-                      if (ieq(k, which == 0 ? gk[q] : rk[q])) f = q;
+                  if (which == 2) {
+                    f = keyis(k, "from", 4) ? 0 : keyis(k, "to", 2) ? 1 : -1;
+                  } else {
+                    if (keyis(k, "id", 2)) f = 0;
+                    else if (keyis(k, "label", 5)) f = 1;
+                    else if (keyis(k, "table", 5)) f = 2;
+                    else if (keyis(k, which == 0 ? "time" : "type", 4)) f = 3;
+                  }
                   j.ws();
                   if (f < 0) {
                     j.skip();
                   } else if (j.lit("null")) {
                   } else {
-                    Str s{(uint32_t)g.arena.size(), 0};
-                    if (!j.str(g.arena)) break;  // decoded straight into the arena (reserved: no reallocation)
-                    s.len = (uint32_t)(g.arena.size() - s.off);
-                    if (which == 2) (f == 0 ? ed.first : ed.second) = s;
-                    else r.f[f] = s;
+                    Str sv;
+                    if (!j.sview(g.arena, base, sv)) break;
+                    if (which == 2) (f == 0 ? ed.first : ed.second) = sv;
+                    else r.f[f] = sv;
                   }
                   j.ws();
                   if (j.p < j.e && *j.p == ',') {
@@ -486,11 +541,22 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.tclass.push_back(type_class(g.sv(r.f[3])));
   }
   // rank of each node's ID inside the graph (the prefix is common, so unprefixed order == prefixed order)
-  std::vector<uint32_t> order(V);
-  for (uint32_t i = 0; i < V; i++) order[i] = i;
-  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return g.sv(g.id[a]) < g.sv(g.id[b]); });
+  // sorted by the first 8 bytes as a big-endian key (a shorter ID pads with
+  // zero bytes, so the key order agrees with the string order), ties by the whole string
+  std::vector<std::pair<uint64_t, uint32_t>> order(V);
+  for (uint32_t i = 0; i < V; i++) {
+    const std::string_view x = g.sv(g.id[i]);
+    uint64_t k = 0;
+    for (size_t b = 0; b < 8; b++) k = (k << 8) | (b < x.size() ? (uint8_t)x[b] : 0u);
+    order[i] = {k, i};
+  }
+  std::sort(order.begin(), order.end(), [&](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+    if (a.first != b.first) return a.first < b.first;
+    const std::string_view x = g.sv(g.id[a.second]), y = g.sv(g.id[b.second]);
+    return x != y ? x < y : a.second < b.second;
+  });
   g.rank.assign(V, 0);
-  for (uint32_t pos = 0; pos < V; pos++) g.rank[order[pos]] = pos;
+  for (uint32_t pos = 0; pos < V; pos++) g.rank[order[pos].second] = pos;
   FlatSet64 seen;
   seen.init(edges.size());
   size_t created = 0;

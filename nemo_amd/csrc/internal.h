@@ -54,6 +54,10 @@ struct DxArgs {
   const uint32_t *ref_labels;  // label mode: [n, label...] of the single source (src unused)
   const uint32_t *r0lab, *r0hkey, *r0hval;
   uint32_t r0hmask;
+  // label -> (first sorted run-0 goal label entry << 4 | min(count, 15)), NEMO_NONE = not a run-0
+  // post-goal label; labels >= nlab are not either (null: the hash table above)
+  const uint32_t *r0dense;
+  uint32_t nlab;
   uint32_t *pb;              // [nu][w32] present bitmaps over positions
   uint32_t w32;              // ceil(V0 / 32)
   uint32_t lab_per;          // source nodes per k_dx_label workgroup

@@ -113,7 +113,32 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     __syncthreads();
   }
   const uint32_t lo = blockIdx.x * a.lab_per, hi = min(n, lo + a.lab_per);
-  for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
+  auto mark = [&](uint32_t p) {
+    if (lds) atomicOr(&bm[p >> 5], 1u << (p & 31u));
+    else atomicOr(&pb[p >> 5], 1u << (p & 31u));
+  };
+  if (a.r0dense) {  // one dense-table load per source goal, then its run-0 positions
+    for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
+      uint32_t lb[DXL_BATCH], dv[DXL_BATCH];
+#pragma unroll
+      for (int q = 0; q < DXL_BATCH; q++) {
+        const uint32_t x = base + q * NEMO_BLOCK + tid;
+        const bool in = x < hi && (!word || !is_rule(word[x]));
+        lb[q] = in ? lab[x] : NEMO_NONE;
+      }
+#pragma unroll
+      for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab ? a.r0dense[lb[q]] : NEMO_NONE;
+#pragma unroll
+      for (int q = 0; q < DXL_BATCH; q++) {
+        if (dv[q] == NEMO_NONE) continue;
+        const uint32_t i0 = dv[q] >> 4, cnt = dv[q] & 15u;
+        for (uint32_t t = 0; t < cnt; t++) mark(a.p.r0pos[i0 + t]);
+        if (cnt == 15u)  // 15 or more entries: the rest of the run
+          for (uint32_t i = i0 + 15u; i < a.p.n_r0lab && a.r0lab[i] == lb[q]; i++) mark(a.p.r0pos[i]);
+      }
+    }
+  }
+  for (uint32_t base = lo; base < hi && !a.r0dense; base += DXL_BATCH * NEMO_BLOCK) {
     uint32_t lb[DXL_BATCH], h[DXL_BATCH], pos[DXL_BATCH], live = 0;
 #pragma unroll
     for (int q = 0; q < DXL_BATCH; q++) {
@@ -147,11 +172,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
 #pragma unroll
     for (int q = 0; q < DXL_BATCH; q++) {
       if (pos[q] == NEMO_NONE) continue;
-      for (uint32_t i = pos[q]; i < a.p.n_r0lab && a.r0lab[i] == lb[q]; i++) {
-        const uint32_t p = a.p.r0pos[i];
-        if (lds) atomicOr(&bm[p >> 5], 1u << (p & 31u));
-        else atomicOr(&pb[p >> 5], 1u << (p & 31u));
-      }
+      for (uint32_t i = pos[q]; i < a.p.n_r0lab && a.r0lab[i] == lb[q]; i++) mark(a.p.r0pos[i]);
     }
   }
   if (!lds) return;
@@ -245,12 +266,13 @@ struct DxWalkCfg {
   uint32_t whole;     // 1: the whole graph is one window
 };
 
-template <int MODE, int NE, bool WHOLE>
-__global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg cfg) {
+template <int MODE, int NE, bool WHOLE, int NT, int PS>
+__global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg cfg) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  constexpr int PS = 8;  // positions per thread per staging group (contiguous: segment order = thread order)
+  // PS positions per thread per staging group (contiguous, so that the level
+  // segments come out in thread order); windowed: W == PS * NT, one group
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_n, s_red[DX_NT / 64];
+  __shared__ uint32_t s_n, s_red[NT / 64];
   __shared__ uint32_t s_lmax[NE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC;
@@ -285,36 +307,39 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
   for (uint32_t w0 = 0; w0 < V;) {
     const uint32_t nmax = min(W, V - w0);
     // ---- staging 1: row starts; the window ends where its links would pass EC ----
-    for (uint32_t k0 = 0; k0 <= nmax; k0 += 8 * DX_NT) {
-      uint32_t v[8];
+    for (uint32_t k0 = 0; k0 <= nmax; k0 += PS * NT) {
+      uint32_t v[PS];
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const uint32_t k = k0 + q * DX_NT + tid;
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q * NT + tid;
         v[q] = k <= nmax ? rowp[w0 + k] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const uint32_t k = k0 + q * DX_NT + tid;
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q * NT + tid;
         if (k <= nmax) L.off[k] = v[q];
       }
     }
-    if (tid == 0) s_n = 0;
+    if (tid == 0) {
+      s_n = 0;
+      if (nmax % (PS * NT) == 0) L.off[nmax] = rowp[w0 + nmax];  // the loop above stops short of it
+    }
     __syncthreads();
     {
       uint32_t best = 0;
-      for (uint32_t k = tid + 1; k <= nmax; k += DX_NT)
+      for (uint32_t k = tid + 1; k <= nmax; k += NT)
         if (L.off[k] - L.off[0] <= EC) best = max(best, k);
       for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor(best, d));
       if (lane == 0) atomicMax(&s_n, best);
     }
     __syncthreads();
     const uint32_t n = s_n, w1 = w0 + n, base = L.off[0], ne = L.off[n] - base;
-    // ---- staging 2: per position (PS consecutive per thread): init value into
-    // its ring slot (no link of the window reads those slots: they hold
-    // positions older than the ring), the owner half of its links' records, the
-    // level segments (a position that starts its level starts a segment) ----
+    // ---- staging 2: per position: init value into its ring slot (no link of
+    // the window reads those slots: they hold positions older than the ring),
+    // the owner half of its links' records, the level segments (a position
+    // that starts its level starts a segment) ----
     uint32_t nseg = 0;
-    for (uint32_t g0 = 0; g0 < n; g0 += PS * DX_NT) {
+    for (uint32_t g0 = 0; g0 < n; g0 += PS * NT) {
       const uint32_t k0 = g0 + tid * PS;
       uint32_t lb[PS], st = 0;
       T ini[PS][NE];
@@ -346,7 +371,7 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
         st |= (k == 0 || lb[q] == w0 + k ? 1u : 0u) << q;
       }
       uint32_t tot;
-      uint32_t o = nseg + block_exscan<DX_NT>((uint32_t)__popc(st), &tot, s_red);
+      uint32_t o = nseg + block_exscan<NT>((uint32_t)__popc(st), &tot, s_red);
 #pragma unroll
       for (int q = 0; q < PS; q++)
         if ((st >> q) & 1u) L.seg[o++] = (uint16_t)(L.off[k0 + q] - base);
@@ -360,16 +385,16 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
     // its owner's init; the others get the linked position's ring slot ----
     {
       const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
-      for (uint32_t cb = c0; cb < c1; cb += 4 * DX_NT) {
+      for (uint32_t cb = c0; cb < c1; cb += 4 * NT) {
         uint4 v4[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          const uint32_t ck = cb + q * DX_NT + tid;
+          const uint32_t ck = cb + q * NT + tid;
           v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(col)[ck] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          const uint32_t ck = cb + q * DX_NT + tid;
+          const uint32_t ck = cb + q * NT + tid;
           const uint32_t qs[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
 #pragma unroll
           for (int b = 0; b < 4; b++) {
@@ -422,7 +447,6 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
               atomicMax((uint32_t *)&ring[rc[q] >> 16], DX_IND | sv);
             }
           }
-          if (j0 + 256 >= hi) break;
         }
         lo = hi;
         wsync();
@@ -430,16 +454,29 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
     }
     __syncthreads();
     // ---- finalize: the window's values to HBM (depth: s, and the LP maxima) ----
-    for (uint32_t k0 = 0; k0 < n; k0 += 4 * DX_NT) {
+    for (uint32_t k0 = 0; k0 < n; k0 += PS * NT) {
+      uint32_t info[PS];
+      uint64_t lw[PS][NE];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t k = k0 + q * DX_NT + tid;
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q * NT + tid, i = w0 + (k < n ? k : 0u);
+        if (MODE == 2) {
+          info[q] = a.p.info[i];
+#pragma unroll
+          for (int e = 0; e < NE; e++) {
+            const uint32_t u = srcu(e);
+            lw[q][e] = u != NEMO_NONE && k < n ? a.lw[(size_t)(u >> 6) * V + i] : 0ull;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < PS; q++) {
+        const uint32_t k = k0 + q * NT + tid;
         if (k >= n) continue;
         const uint32_t i = w0 + k, sl = slot(i);
         if (MODE == 0) {
           gvalp(0)[i] = ringp(0)[sl];
         } else {
-          const bool rule = (a.p.info[i] & DXI_RULE) != 0;
 #pragma unroll
           for (int e = 0; e < NE; e++) {
             const uint32_t u = srcu(e);
@@ -447,7 +484,7 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
             const uint32_t r = (uint32_t)ringp(e)[sl];
             const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
             gvalp(e)[i] = (T)sv;
-            if (rule && ((a.lw[(size_t)(u >> 6) * V + i] >> (u & 63u)) & 1ull)) lmax[e] = max(lmax[e], sv);
+            if ((info[q] & DXI_RULE) && ((lw[q][e] >> (u & 63u)) & 1ull)) lmax[e] = max(lmax[e], sv);
           }
         }
       }
@@ -466,17 +503,31 @@ __global__ __launch_bounds__(DX_NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalk
   }
   __syncthreads();
   const GraphView g0 = c.view(a.p.g0);
+  constexpr int MB = 8;  // positions per thread per round, loads in flight together
   for (uint32_t e = 0; e < (uint32_t)NE; e++) {
     const uint32_t u = srcu(e), mx = s_lmax[e];
     if (u == NEMO_NONE || mx == 0) continue;
     const uint32_t b = u & 63u;
+    const uint64_t *lwu = a.lw + (size_t)(u >> 6) * V;
     const T *gv = gvalp(e);
-    for (uint32_t pos = tid; pos < V; pos += DX_NT) {
-      if (!(a.p.info[pos] & DXI_RULE) || !((a.lw[(size_t)(u >> 6) * V + pos] >> b) & 1ull)) continue;
-      if (__hip_atomic_load(gv + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != mx) continue;
-      const uint32_t k = atomicAdd(a.n_missing, 1u);
-      a.missing[2 * k] = u;
-      a.missing[2 * k + 1] = g0.topo[pos];
+    for (uint32_t p0 = 0; p0 < V; p0 += MB * NT) {
+      uint32_t inf[MB], sv[MB];
+      uint64_t lv[MB];
+#pragma unroll
+      for (int q = 0; q < MB; q++) {
+        const uint32_t pos = p0 + q * NT + tid, pc = pos < V ? pos : 0u;
+        inf[q] = pos < V ? a.p.info[pc] : 0u;
+        lv[q] = lwu[pc];
+        sv[q] = __hip_atomic_load(gv + pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int q = 0; q < MB; q++) {
+        const uint32_t pos = p0 + q * NT + tid;
+        if (pos >= V || !(inf[q] & DXI_RULE) || !((lv[q] >> b) & 1ull) || sv[q] != mx) continue;
+        const uint32_t k = atomicAdd(a.n_missing, 1u);
+        a.missing[2 * k] = u;
+        a.missing[2 * k + 1] = g0.topo[pos];
+      }
     }
   }
 }
@@ -541,24 +592,29 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
 }
 
 // ---- launch -----------------------------------------------------------------------------
-template <int MODE, int NE, bool WHOLE>
+template <int MODE, int NE, bool WHOLE, int NT, int PS>
 static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxWalkCfg &cfg, dim3 grid, hipStream_t s) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
   const uint32_t bytes = dx_lds_bytes<T, NE>(cfg.W, cfg.R, cfg.EC);
-  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT, PS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)bytes);
-  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE>), grid, dim3(DX_NT), bytes, s, c, a, cfg);
+  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT, PS>), grid, dim3(NT), bytes, s, c, a, cfg);
 }
 
 #define DX_LDS_MAX (160u * 1024u - 1024u)
 // windowed configurations: W positions, R ring slots (power of two, > W), EC links
-static const DxWalkCfg kReach = {2048, 8192, 12288, 0};
-static const DxWalkCfg kDepth = {1024, 4096, 6144, 0};
-static const DxWalkCfg kTiny = {64, 128, 1024, 0};  // test knob (window = 2): most links leave the ring
+// reachability: 1024 threads, 2 positions each per window; depth: 512 threads, 4 walkers
+#define DXR_NT 1024
+#define DXD_NT 512
+static const DxWalkCfg kReach = {2 * DXR_NT, 8192, 12288, 0};
+static const DxWalkCfg kDepth = {2 * DXD_NT, 4096, 6144, 0};
+// test knob (window = 2): windows of the same size, rings barely larger, so most links leave them
+static const DxWalkCfg kTinyR = {2 * DXR_NT, 4096, 12288, 0};
+static const DxWalkCfg kTinyD = {2 * DXD_NT, 2048, 6144, 0};
 
 // every row of g0 must fit one window's links (launch_dx's windowed configurations)
 uint32_t dx_max_row() { return std::min(kReach.EC, kDepth.EC); }
-uint32_t dx_max_row_tiny() { return kTiny.EC; }
+uint32_t dx_max_row_tiny() { return std::min(kTinyR.EC, kTinyD.EC); }
 
 void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   const uint32_t V = a.p.V0, E = a.p.E0;
@@ -572,15 +628,15 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   const DxWalkCfg whole = {V, V, std::max(E, 1u), 1};
   const bool small = a.window == 0 && V < 0xFFFFu && E <= 0xFFFFu;
   if (small && dx_lds_bytes<uint64_t, 1>(V, V, whole.EC) <= DX_LDS_MAX)
-    walk_launch<0, 1, true>(c, a, whole, dim3(a.nch, 2), s);
+    walk_launch<0, 1, true, DXR_NT, 8>(c, a, whole, dim3(a.nch, 2), s);
   else
-    walk_launch<0, 1, false>(c, a, a.window == 2 ? kTiny : kReach, dim3(a.nch, 2), s);
+    walk_launch<0, 1, false, DXR_NT, 2>(c, a, a.window == 2 ? kTinyR : kReach, dim3(a.nch, 2), s);
   hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   if (small && dx_lds_bytes<uint32_t, 4>(V, V, whole.EC) <= DX_LDS_MAX)
-    walk_launch<2, 4, true>(c, a, whole, dim3((a.nu + 3) / 4), s);
+    walk_launch<2, 4, true, DXD_NT, 8>(c, a, whole, dim3((a.nu + 3) / 4), s);
   else
-    walk_launch<2, 4, false>(c, a, a.window == 2 ? kTiny : kDepth, dim3((a.nu + 3) / 4), s);
+    walk_launch<2, 4, false, DXD_NT, 2>(c, a, a.window == 2 ? kTinyD : kDepth, dim3((a.nu + 3) / 4), s);
   if (a.n_entries)
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }

@@ -809,7 +809,7 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
     }
   }
   /* LoadRawProvenance (pre-post-prov.go:247-285) then SimplifyProv (preprocessing.go:351-387) */
-#pragma omp parallel for schedule(dynamic, 4) num_threads(nth)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nth)
   for (uint32_t gi = 0; gi < G; gi++) {
     graph_t *g = &gs[gi];
     if (o->diff_only && !need[gi]) continue;
@@ -831,7 +831,7 @@ int oracle_analyze(const nemo_corpus *c, const oracle_opts *o, oracle_out *out) 
   /* graph' per graph: proto list (post), table set (post), pulled edges */
   out->proto_bits = calloc((size_t)c->n_runs * W + 1, sizeof(uint32_t));
   out->graph_tables = calloc((size_t)c->n_runs * W + 1, sizeof(uint32_t));
-#pragma omp parallel for schedule(dynamic, 4) num_threads(nth)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nth)
   for (uint32_t gi = 0; gi < G; gi++) {
     graph_t *g = &gs[gi];
     gprime_t p;
