@@ -987,8 +987,9 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     HIPCHK(c, hipMemcpyAsync(c->d_r0hval, hval.data(), hcap * 4, hipMemcpyHostToDevice, s));
     // the same as a dense table over every label id of the corpus, when that is at most 256M entries:
     // one load per source goal instead of a probe sequence
-    uint32_t maxlab = 0;
-    for (uint64_t v = 0; v < c->V; v++) maxlab = std::max(maxlab, in->label[v]);
+    uint32_t maxlab = 0;  // over goal labels: only those are looked up (rule labels may be anywhere)
+    for (uint64_t v = 0; v < c->V; v++)
+      if (!(in->node_word[v] & NEMO_NODE_RULE)) maxlab = std::max(maxlab, in->label[v]);
     const uint64_t nlab = c->V ? (uint64_t)maxlab + 1 : 0;
     std::vector<uint32_t> dense;
     if (nlab && nlab <= (1ull << 28)) {

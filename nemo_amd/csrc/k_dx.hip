@@ -489,7 +489,11 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
         }
       }
     }
-    __threadfence();  // the values are final in HBM before later windows (and the rows pass) read them
+    // the values have reached this XCD's L2 before a later window's staging (or
+    // the rows pass) reads them back with L2-served loads, in this workgroup
+    // (a workgroup-scope release fence waits for nothing here, an agent-scope
+    // one writes the whole L2 back: the stores' completion is all that is needed)
+    if (!WHOLE || MODE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     w0 = w1;
   }
