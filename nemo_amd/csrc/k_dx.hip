@@ -304,6 +304,23 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
   uint32_t lmax[NE];
 #pragma unroll
   for (int e = 0; e < NE; e++) lmax[e] = 0;
+#ifdef NEMO_STAMPS
+  // diagnostic build: per-workgroup ticks of each phase (wave 0's view), reach at
+  // 16 wg + 0..7, depth at 16 wg + 8..15: S1, S2, S3, walk, finalize, rows, windows, total
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tk0, tk1, tstart;
+#define DXT(k)          \
+  do {                  \
+    TICK(tk1);          \
+    acc[k] += tk1 - tk0; \
+    tk0 = tk1;          \
+  } while (0)
+  TICK(tk0);
+  tstart = tk0;
+#else
+#define DXT(k) \
+  do {         \
+  } while (0)
+#endif
   for (uint32_t w0 = 0; w0 < V;) {
     const uint32_t nmax = min(W, V - w0);
     // ---- staging 1: row starts; the window ends where its links would pass EC ----
@@ -334,6 +351,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     }
     __syncthreads();
     const uint32_t n = s_n, w1 = w0 + n, base = L.off[0], ne = L.off[n] - base;
+    DXT(0);
     // ---- staging 2: per position: init value into its ring slot (no link of
     // the window reads those slots: they hold positions older than the ring),
     // the owner half of its links' records, the level segments (a position
@@ -379,6 +397,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     }
     if (tid == 0) L.seg[nseg] = (uint16_t)ne;
     __syncthreads();
+    DXT(1);
     // ---- staging 3: the links, one contiguous range of col, in 16-B aligned
     // chunks.  A link older than the ring reads its final value from HBM
     // (written and fenced by an earlier window's finalize) and is applied to
@@ -420,6 +439,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
       }
     }
     __syncthreads();
+    DXT(2);
     // ---- the walk: wave e < NE walks source e through the window's level
     // segments, lanes over a segment's links ----
     if (wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE)) {
@@ -452,6 +472,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
         wsync();
       }
     }
+    DXT(3);
     __syncthreads();
     // ---- finalize: the window's values to HBM (depth: s, and the LP maxima) ----
     for (uint32_t k0 = 0; k0 < n; k0 += PS * NT) {
@@ -495,8 +516,18 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     // one writes the whole L2 back: the stores' completion is all that is needed)
     if (!WHOLE || MODE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    DXT(4);
+#ifdef NEMO_STAMPS
+    acc[6]++;
+#endif
     w0 = w1;
   }
+#ifdef NEMO_STAMPS
+  const uint32_t stw = 16u * (MODE == 0 ? blockIdx.x * 2u + blockIdx.y : blockIdx.x) + (MODE == 0 ? 0u : 8u);
+  if (tid == 0 && c.stamps)
+    for (int k = 0; k < 5; k++) c.stamps[stw + k] = acc[k];
+  if (tid == 0 && c.stamps) c.stamps[stw + 6] = acc[6];
+#endif
   if (MODE != 2) return;
   // missing rows: LP rules at the maximal depth, depth + 1 == maxLen (:82-98)
 #pragma unroll
@@ -534,6 +565,14 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
       }
     }
   }
+#ifdef NEMO_STAMPS
+  DXT(5);
+  if (tid == 0 && c.stamps) {
+    c.stamps[stw + 5] = acc[5];
+    c.stamps[stw + 7] = tk0 - tstart;
+  }
+#endif
+#undef DXT
 }
 
 // ---- D and D-leaf goals: one thread per (position, chunk) ----------------------------
