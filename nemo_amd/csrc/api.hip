@@ -100,7 +100,7 @@ struct nemo_ctx {
   uint32_t diff_window = 0;          // option diff_window (test knob): 0 by size, 1 windowed, 2 tiny windows
   uint32_t g0_maxdeg = 0;
   uint32_t dx_nu_cap = 0, dx_nch_cap = 0;
-  uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr;
+  uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr, *d_dxlpl = nullptr;
   uint64_t *d_dxw = nullptr, *d_dxlp = nullptr;  // [5][nch][V0] Good, F, B, D, L|LP; [nch] LP summary
   bool dx_last = false;              // the last diffprov ran the multi-entry kernels
 
@@ -399,7 +399,7 @@ static void release_corpus(nemo_ctx *c) {
   c->dxp = nemo::DxPrep{};
   c->dx_ok = false;
   c->dx_nu_cap = c->dx_nch_cap = 0;
-  c->d_dxpb = c->d_dxsval = nullptr;
+  c->d_dxpb = c->d_dxsval = c->d_dxlpl = nullptr;
   c->d_dxw = c->d_dxlp = nullptr;
   c->n_uniq = 0;
   c->dmap.clear();
@@ -1345,12 +1345,14 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   }
   const uint32_t nch = (nu + 63) / 64, w32 = (uint32_t)((V0 + 31) / 32);
   if (dx && (nu > c->dx_nu_cap || nch > c->dx_nch_cap)) {
-    for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxw, (void *)c->d_dxlp}) dfree(c, q);
-    c->d_dxpb = c->d_dxsval = nullptr;
+    for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxlpl, (void *)c->d_dxw, (void *)c->d_dxlp})
+      dfree(c, q);
+    c->d_dxpb = c->d_dxsval = c->d_dxlpl = nullptr;
     c->d_dxw = c->d_dxlp = nullptr;
     c->dx_nu_cap = c->dx_nch_cap = 0;
     if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
     if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxw, 5 * (size_t)nch * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxlp, (size_t)nch))) return rc;
     c->dx_nu_cap = nu;
@@ -1403,6 +1405,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.lw = a.dw + plane;
     a.lpany = c->d_dxlp;
     a.sval = c->d_dxsval;
+    a.lplist = c->d_dxlpl;
     a.mask = c->d_dmask;
     a.map = c->d_dmap;
     a.n_entries = (uint32_t)n_failed;

@@ -69,6 +69,7 @@ struct DxArgs {
   uint64_t *lw;              // [nch][V0] D-leaf goals | LP rules (rules with a D-leaf child) by position
   uint64_t *lpany;           // [nch] sources with at least one LP rule
   uint32_t *sval;            // [nu][V0] depth + 1 of D nodes (0 elsewhere) by position
+  uint32_t *lplist;          // [nu][V0] the LP rules' positions of each source (windowed depth walks)
   uint8_t *mask;             // [n_entries][V0] D masks by node (output)
   const uint32_t *map;       // [n_entries] entry -> source
   uint32_t n_entries;

@@ -231,34 +231,40 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 // linked value, apply it to the owner's slot with an LDS atomic; a level only
 // reads slots of earlier levels, and a wave's LDS operations complete in
 // order, so no barrier separates the levels.
-#define DX_NT 256
 #define DX_NOTD 0xFFFFFFFFu
 #define DX_IND 0x80000000u
+#define DX_MC 2048u  // ring misses listed per window (beyond: applied one by one)
 template <typename T, int NE>
 struct DxLds {
-  T *ring0;          // NE rings of [R + 1] (stride rs); [R] is the identity (sink)
+  T *ring0;          // NE rings of [R + 2] (stride rs): [R] the identity (sink), [R + 1] a dump slot
   uint32_t rs;
   uint32_t *off;     // [W + 1] absolute row starts of the window's positions
   uint32_t *lk;      // [EC] links: ring slot of the linked position (R: none) | owner's slot << 16
   uint16_t *seg;     // [W + 1] first link of each level segment (relative); seg[nseg] = links
+  uint32_t *lpb;     // [NE][W / 32 + 1] depth: LP rules of the window, one bit per position
+  uint2 *miss;       // [DX_MC] (linked walk index, owner's slot) of the links older than the ring
 };
 template <typename T, int NE>
-__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC) {
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 1u)) + lds_align(4u * (W + 1u)) + lds_align(4u * EC) +
-         lds_align(2u * (W + 1u));
+__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC, bool whole) {
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 2u)) + lds_align(4u * (W + 1u)) + lds_align(4u * EC) +
+         lds_align(2u * (W + 1u)) + NE * lds_align(4u * (W / 32u + 1u)) + (whole ? 0u : 8u * DX_MC);
 }
 template <typename T, int NE>
 __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC) {
   uint8_t *p = (uint8_t *)base;
   DxLds<T, NE> L;
   L.ring0 = (T *)p;
-  L.rs = lds_align((uint32_t)sizeof(T) * (R + 1u)) / (uint32_t)sizeof(T);
-  p += NE * lds_align((uint32_t)sizeof(T) * (R + 1u));
+  L.rs = lds_align((uint32_t)sizeof(T) * (R + 2u)) / (uint32_t)sizeof(T);
+  p += NE * lds_align((uint32_t)sizeof(T) * (R + 2u));
   L.off = (uint32_t *)p;
   p += lds_align(4u * (W + 1u));
   L.lk = (uint32_t *)p;
   p += lds_align(4u * EC);
   L.seg = (uint16_t *)p;
+  p += lds_align(2u * (W + 1u));
+  L.lpb = (uint32_t *)p;
+  p += NE * lds_align(4u * (W / 32u + 1u));
+  L.miss = (uint2 *)p;
   return L;
 }
 struct DxWalkCfg {
@@ -272,10 +278,10 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
   // PS positions per thread per staging group (contiguous, so that the level
   // segments come out in thread order); windowed: W == PS * NT, one group
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_n, s_red[NT / 64];
-  __shared__ uint32_t s_lmax[NE];
+  __shared__ uint32_t s_n, s_nmiss, s_red[NT / 64];
+  __shared__ uint32_t s_lmax[NE], s_lpn[NE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC;
+  const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC, LW = W / 32u + 1u;
   const bool rev = MODE == 0 && blockIdx.y == 1;
   const uint32_t chunk = MODE == 0 ? blockIdx.x : 0u;
   DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC);
@@ -294,12 +300,18 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
   };
   auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
+  // the missing value of a link older than the ring, applied to its owner's slot
+  auto apply_miss = [&](uint32_t e, uint32_t osl, T val) {
+    if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[osl], (unsigned long long)val);
+    else atomicMax((uint32_t *)&ringp(e)[osl], DX_IND | (uint32_t)val);
+  };
   bool any = MODE == 0;
   for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
   if (!any) return;  // workgroup-uniform
   if (tid < (uint32_t)NE) {
     ringp(tid)[R] = MODE == 0 ? (T)0 : (T)DX_NOTD;  // the sink reads as "no value": OR 0, depth s = 0
     s_lmax[tid] = 0;
+    s_lpn[tid] = 0;
   }
   uint32_t lmax[NE];
 #pragma unroll
@@ -339,8 +351,9 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     }
     if (tid == 0) {
       s_n = 0;
-      if (nmax % (PS * NT) == 0) L.off[nmax] = rowp[w0 + nmax];  // the loop above stops short of it
+      s_nmiss = 0;
     }
+    for (uint32_t w = tid; w < NE * LW && MODE == 2; w += NT) L.lpb[w] = 0;
     __syncthreads();
     {
       uint32_t best = 0;
@@ -355,11 +368,11 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     // ---- staging 2: per position: init value into its ring slot (no link of
     // the window reads those slots: they hold positions older than the ring),
     // the owner half of its links' records, the level segments (a position
-    // that starts its level starts a segment) ----
+    // that starts its level starts a segment), depth: the LP bits ----
     uint32_t nseg = 0;
     for (uint32_t g0 = 0; g0 < n; g0 += PS * NT) {
       const uint32_t k0 = g0 + tid * PS;
-      uint32_t lb[PS], st = 0;
+      uint32_t lb[PS], st = 0, lp[PS];
       T ini[PS][NE];
 #pragma unroll
       for (int q = 0; q < PS; q++) {
@@ -367,14 +380,18 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
         const bool in = k < n;
         const uint32_t i = w0 + (in ? k : 0u), pos = rev ? V - 1u - i : i;
         lb[q] = rev ? V - a.p.lend[pos] : a.p.lbeg[pos];  // the walk index where the position's level starts
+        lp[q] = 0;
         if (MODE == 0) {
           ini[q][0] = in ? (T)a.gw[(size_t)chunk * V + pos] : (T)0;
         } else {
+          const bool rule = in && (a.p.info[pos] & DXI_RULE);
 #pragma unroll
           for (int e = 0; e < NE; e++) {
-            const uint32_t u = srcu(e);
+            const uint32_t u = srcu(e), b = u & 63u;
             const uint64_t dv = u != NEMO_NONE && in ? a.dw[(size_t)(u >> 6) * V + pos] : 0ull;
-            ini[q][e] = ((dv >> (u & 63u)) & 1ull) ? DX_IND : DX_NOTD;
+            const uint64_t lv = u != NEMO_NONE && in ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
+            ini[q][e] = ((dv >> b) & 1ull) ? DX_IND : DX_NOTD;
+            lp[q] |= (rule && ((lv >> b) & 1ull) ? 1u : 0u) << e;
           }
         }
       }
@@ -385,6 +402,9 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
         const uint32_t sl = slot(w0 + k);
 #pragma unroll
         for (int e = 0; e < NE; e++) ringp(e)[sl] = ini[q][e];
+#pragma unroll
+        for (int e = 0; e < NE; e++)
+          if (MODE == 2 && ((lp[q] >> e) & 1u)) atomicOr(&L.lpb[e * LW + (k >> 5)], 1u << (k & 31u));
         for (uint32_t j = L.off[k]; j < L.off[k + 1]; j++) ((uint16_t *)&L.lk[j - base])[1] = (uint16_t)sl;
         st |= (k == 0 || lb[q] == w0 + k ? 1u : 0u) << q;
       }
@@ -399,9 +419,9 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     __syncthreads();
     DXT(1);
     // ---- staging 3: the links, one contiguous range of col, in 16-B aligned
-    // chunks.  A link older than the ring reads its final value from HBM
-    // (written and fenced by an earlier window's finalize) and is applied to
-    // its owner's init; the others get the linked position's ring slot ----
+    // chunks: the linked position's ring slot, or, for a link older than the
+    // ring, an entry of the miss list (its final value is in HBM, written by
+    // an earlier window's finalize) ----
     {
       const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
       for (uint32_t cb = c0; cb < c1; cb += 4 * NT) {
@@ -418,48 +438,78 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
 #pragma unroll
           for (int b = 0; b < 4; b++) {
             const uint32_t j = 4 * ck + b;
-            if (ck >= c1 || j < base || j >= base + ne) continue;
+            const bool in = ck < c1 && j >= base && j < base + ne;
             const uint32_t x = qs[b];  // walk index of the linked position
-            uint16_t *rec = (uint16_t *)&L.lk[j - base];
-            if (WHOLE || x + R >= w1) {
-              rec[0] = (uint16_t)slot(x);
-              continue;
-            }
-            rec[0] = (uint16_t)R;
-            const uint32_t osl = rec[1];
+            const bool far = in && !WHOLE && x + R < w1;
+            if (in) ((uint16_t *)&L.lk[j - base])[0] = (uint16_t)(far ? R : slot(x));
+            if (WHOLE) continue;
+            const uint64_t fm = __ballot(far);
+            if (!fm) continue;  // wave-uniform
+            uint32_t mb = 0;
+            if (lane == (uint32_t)(__ffsll((long long)fm) - 1)) mb = atomicAdd(&s_nmiss, (uint32_t)__popcll(fm));
+            mb = __shfl(mb, __ffsll((long long)fm) - 1) + mbcnt(fm);
+            if (!far) continue;
+            const uint32_t osl = ((uint16_t *)&L.lk[j - base])[1];
+            if (mb < DX_MC) {
+              L.miss[mb] = make_uint2(x, osl);
+            } else {  // the list is full: apply it here
 #pragma unroll
-            for (uint32_t e = 0; e < (uint32_t)NE; e++) {
-              if (MODE == 2 && srcu(e) == NEMO_NONE) continue;
-              const T val = __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[osl], (unsigned long long)val);
-              else atomicMax((uint32_t *)&ringp(e)[osl], DX_IND | (uint32_t)val);
+              for (uint32_t e = 0; e < (uint32_t)NE; e++)
+                if (MODE == 0 || srcu(e) != NEMO_NONE)
+                  apply_miss(e, osl, __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             }
           }
         }
       }
     }
     __syncthreads();
+    if (!WHOLE) {  // the listed misses: their values loaded together, then applied
+      const uint32_t nm = min(s_nmiss, DX_MC);
+      for (uint32_t m0 = 0; m0 < nm; m0 += 4 * NT) {
+        uint2 ms[4];
+        T val[4][NE];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t m = m0 + q * NT + tid;
+          ms[q] = m < nm ? L.miss[m] : make_uint2(0, R + 1);
+#pragma unroll
+          for (int e = 0; e < NE; e++)
+            val[q][e] = m < nm && (MODE == 0 || srcu(e) != NEMO_NONE)
+                            ? __hip_atomic_load(gvalp(e) + ms[q].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : (T)0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int e = 0; e < NE; e++)
+            if (m0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)) apply_miss(e, ms[q].y, val[q][e]);
+      }
+      __syncthreads();
+    }
     DXT(2);
     // ---- the walk: wave e < NE walks source e through the window's level
-    // segments, lanes over a segment's links ----
+    // segments, lanes over a segment's links.  No barrier or fence between
+    // levels: a level reads only slots of earlier levels, and a wave's LDS
+    // operations complete in issue order.  Idle lanes read the sink and write
+    // the dump slot, so the level has no branches ----
     if (wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE)) {
       T *ring = ringp(wv);
-      uint32_t lo = L.seg[0];
+      const uint32_t idle = R | ((R + 1u) << 16);
+      uint32_t lo = L.seg[0], hi = L.seg[nseg > 0 ? 1 : 0];
       for (uint32_t t = 0; t < nseg; t++) {
-        const uint32_t hi = __builtin_amdgcn_readfirstlane(L.seg[t + 1]);
+        const uint32_t hn = L.seg[min(t + 2, nseg)];  // the next level's end, read ahead
         for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
           uint32_t rc[4];
           T x[4];
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const uint32_t j = j0 + 64u * q + lane;
-            rc[q] = j < hi ? L.lk[j] : ((uint32_t)R | ((uint32_t)R << 16));
+            rc[q] = j < hi ? L.lk[j] : idle;
           }
 #pragma unroll
           for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            if (j0 + 64u * q + lane >= hi) continue;
             if (MODE == 0) {
               atomicOr((unsigned long long *)&ring[rc[q] >> 16], (unsigned long long)x[q]);
             } else {
@@ -469,27 +519,14 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
           }
         }
         lo = hi;
-        wsync();
+        hi = __builtin_amdgcn_readfirstlane(hn);
+        asm volatile("" ::: "memory");
       }
     }
     DXT(3);
     __syncthreads();
-    // ---- finalize: the window's values to HBM (depth: s, and the LP maxima) ----
+    // ---- finalize: the window's values to HBM; depth: s, the LP maxima, the LP list ----
     for (uint32_t k0 = 0; k0 < n; k0 += PS * NT) {
-      uint32_t info[PS];
-      uint64_t lw[PS][NE];
-#pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q * NT + tid, i = w0 + (k < n ? k : 0u);
-        if (MODE == 2) {
-          info[q] = a.p.info[i];
-#pragma unroll
-          for (int e = 0; e < NE; e++) {
-            const uint32_t u = srcu(e);
-            lw[q][e] = u != NEMO_NONE && k < n ? a.lw[(size_t)(u >> 6) * V + i] : 0ull;
-          }
-        }
-      }
 #pragma unroll
       for (int q = 0; q < PS; q++) {
         const uint32_t k = k0 + q * NT + tid;
@@ -505,16 +542,19 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
             const uint32_t r = (uint32_t)ringp(e)[sl];
             const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
             gvalp(e)[i] = (T)sv;
-            if ((info[q] & DXI_RULE) && ((lw[q][e] >> (u & 63u)) & 1ull)) lmax[e] = max(lmax[e], sv);
+            if ((L.lpb[e * LW + (k >> 5)] >> (k & 31u)) & 1u) {
+              lmax[e] = max(lmax[e], sv);
+              if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
+            }
           }
         }
       }
     }
     // the values have reached this XCD's L2 before a later window's staging (or
-    // the rows pass) reads them back with L2-served loads, in this workgroup
-    // (a workgroup-scope release fence waits for nothing here, an agent-scope
-    // one writes the whole L2 back: the stores' completion is all that is needed)
-    if (!WHOLE || MODE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the rows pass) reads them back with L2-served loads, in this workgroup (a
+    // workgroup-scope release fence waits for nothing here, an agent-scope one
+    // writes the whole L2 back: the stores' completion is all that is needed)
+    if (!WHOLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     DXT(4);
 #ifdef NEMO_STAMPS
@@ -536,32 +576,43 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d));
     if (lane == 0 && m) atomicMax(&s_lmax[e], m);
   }
+  if (!WHOLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LP lists
   __syncthreads();
   const GraphView g0 = c.view(a.p.g0);
-  constexpr int MB = 8;  // positions per thread per round, loads in flight together
+  constexpr int MB = 8;  // entries per thread per round, loads in flight together
   for (uint32_t e = 0; e < (uint32_t)NE; e++) {
     const uint32_t u = srcu(e), mx = s_lmax[e];
     if (u == NEMO_NONE || mx == 0) continue;
-    const uint32_t b = u & 63u;
-    const uint64_t *lwu = a.lw + (size_t)(u >> 6) * V;
-    const T *gv = gvalp(e);
-    for (uint32_t p0 = 0; p0 < V; p0 += MB * NT) {
-      uint32_t inf[MB], sv[MB];
-      uint64_t lv[MB];
-#pragma unroll
-      for (int q = 0; q < MB; q++) {
-        const uint32_t pos = p0 + q * NT + tid, pc = pos < V ? pos : 0u;
-        inf[q] = pos < V ? a.p.info[pc] : 0u;
-        lv[q] = lwu[pc];
-        sv[q] = __hip_atomic_load(gv + pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int q = 0; q < MB; q++) {
-        const uint32_t pos = p0 + q * NT + tid;
-        if (pos >= V || !(inf[q] & DXI_RULE) || !((lv[q] >> b) & 1ull) || sv[q] != mx) continue;
+    if (WHOLE) {  // the whole graph is in LDS: values in the ring, LP bits in lpb
+      const T *ring = ringp(e);
+      for (uint32_t pos = tid; pos < V; pos += NT) {
+        if (!((L.lpb[e * LW + (pos >> 5)] >> (pos & 31u)) & 1u)) continue;
+        const uint32_t r = (uint32_t)ring[pos];
+        if ((r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u) != mx) continue;
         const uint32_t k = atomicAdd(a.n_missing, 1u);
         a.missing[2 * k] = u;
         a.missing[2 * k + 1] = g0.topo[pos];
+      }
+      continue;
+    }
+    const uint32_t nl = s_lpn[e], *list = a.lplist + (size_t)u * V;
+    const T *gv = gvalp(e);
+    for (uint32_t m0 = 0; m0 < nl; m0 += MB * NT) {
+      uint32_t pos[MB], sv[MB];
+#pragma unroll
+      for (int q = 0; q < MB; q++) {
+        const uint32_t m = m0 + q * NT + tid;
+        pos[q] = m < nl ? __hip_atomic_load(list + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < MB; q++)
+        sv[q] = m0 + q * NT + tid < nl ? __hip_atomic_load(gv + pos[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+      for (int q = 0; q < MB; q++) {
+        if (m0 + q * NT + tid >= nl || sv[q] != mx) continue;
+        const uint32_t k = atomicAdd(a.n_missing, 1u);
+        a.missing[2 * k] = u;
+        a.missing[2 * k + 1] = g0.topo[pos[q]];
       }
     }
   }
@@ -638,7 +689,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
 template <int MODE, int NE, bool WHOLE, int NT, int PS>
 static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxWalkCfg &cfg, dim3 grid, hipStream_t s) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  const uint32_t bytes = dx_lds_bytes<T, NE>(cfg.W, cfg.R, cfg.EC);
+  const uint32_t bytes = dx_lds_bytes<T, NE>(cfg.W, cfg.R, cfg.EC, cfg.whole != 0);
   hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT, PS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)bytes);
   hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT, PS>), grid, dim3(NT), bytes, s, c, a, cfg);
@@ -670,13 +721,13 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   // reachability: the whole graph in one window when its image fits
   const DxWalkCfg whole = {V, V, std::max(E, 1u), 1};
   const bool small = a.window == 0 && V < 0xFFFFu && E <= 0xFFFFu;
-  if (small && dx_lds_bytes<uint64_t, 1>(V, V, whole.EC) <= DX_LDS_MAX)
+  if (small && dx_lds_bytes<uint64_t, 1>(V, V, whole.EC, true) <= DX_LDS_MAX)
     walk_launch<0, 1, true, DXR_NT, 8>(c, a, whole, dim3(a.nch, 2), s);
   else
     walk_launch<0, 1, false, DXR_NT, 2>(c, a, a.window == 2 ? kTinyR : kReach, dim3(a.nch, 2), s);
   hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  if (small && dx_lds_bytes<uint32_t, 4>(V, V, whole.EC) <= DX_LDS_MAX)
+  if (small && dx_lds_bytes<uint32_t, 4>(V, V, whole.EC, true) <= DX_LDS_MAX)
     walk_launch<2, 4, true, DXD_NT, 8>(c, a, whole, dim3((a.nu + 3) / 4), s);
   else
     walk_launch<2, 4, false, DXD_NT, 2>(c, a, a.window == 2 ? kTinyD : kDepth, dim3((a.nu + 3) / 4), s);
