@@ -35,3 +35,14 @@ def test_incremental_equals_rescan(name):
     assert len(a.chains) > 0
     assert np.array_equal(a.chains, b.chains)
     assert np.array_equal(a.flags, b.flags)
+
+
+def test_c5_digest_pinned_by_rescan():
+    """The C5-shape digest (tests/golden/c5_shape/digest.json, whose chains come from greedy_incremental) was
+    recomputed once with greedy_rescan on its eight 1M-node graphs (make_c5_shape.py --rescan): identical
+    flags and chains.  Its per-run diff entries cover every failed run of the 128-run corpus."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_shape", "digest.json")))
+    assert d["rescan_equal"]["equal"] is True and d["rescan_equal"]["graphs"] == 2 * len(d["runs"])
+    alld = d["diff_per_run_all"]
+    assert len(alld["failed_iters"]) == len(alld["entries"]) == 16
