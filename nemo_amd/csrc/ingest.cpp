@@ -12,7 +12,9 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <deque>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -43,33 +45,56 @@ struct Graph {
 };
 
 // ---- open-addressing tables (the per-graph maps are hot: one lookup per node and edge) ----
+// Keys of more than 8 bytes are hashed from whole 8-byte loads inside the key.
+inline uint64_t load8(const char *p) {
+  uint64_t w;
+  memcpy(&w, p, 8);
+  return w;
+}
 inline uint64_t hash_sv(std::string_view s) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ s.size();
-  size_t i = 0;
-  for (; i + 8 <= s.size(); i += 8) {
-    uint64_t w;
-    memcpy(&w, s.data() + i, 8);
+  const size_t n = s.size();
+  const char *p = s.data();
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+  if (n <= 8) {  // exact bytes (a short key may end a buffer)
+    uint64_t w = 0;
+    memcpy(&w, p, n);
     h = (h ^ w) * 0xff51afd7ed558ccdull;
-    h ^= h >> 32;
+  } else if (n <= 16) {
+    h = (h ^ load8(p)) * 0xff51afd7ed558ccdull;
+    h = (h ^ (h >> 32) ^ load8(p + n - 8)) * 0xc4ceb9fe1a85ec53ull;
+  } else {
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      h = (h ^ load8(p + i)) * 0xff51afd7ed558ccdull;
+      h ^= h >> 32;
+    }
+    h = (h ^ load8(p + n - 8)) * 0xc4ceb9fe1a85ec53ull;
   }
-  uint64_t w = 0;
-  memcpy(&w, s.data() + i, s.size() - i);
-  h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
-  return h ^ (h >> 29);
+  h ^= h >> 33;  // fmix64: every key bit reaches the low (slot) bits
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
 }
 
-struct FlatMap {  // string_view -> u32, keys live in the graph's arena; slots tagged with the hash
+// string_view -> u32 with hash-tagged slots, reused from graph to graph by one
+// thread: a slot is live only in the epoch that wrote it, so no clearing
+struct FlatMap {
   struct Slot {
-    uint32_t tag, val;  // val ~0u = empty
+    uint32_t tag, val, epoch, pad;
   };
   std::vector<Slot> slot;
   std::vector<std::string_view> key;
   size_t mask = 0;
+  uint32_t epoch = 0;
   void init(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
-    slot.assign(cap, Slot{0, ~0u});
-    key.assign(cap, std::string_view());
+    if (cap > slot.size() || ++epoch == 0) {
+      slot.assign(std::max(cap, slot.size()), Slot{0, 0, 0, 0});
+      key.assign(slot.size(), std::string_view());
+      epoch = 1;
+    }
     mask = cap - 1;
   }
   // value of k, inserting v if absent; second = inserted
@@ -78,8 +103,8 @@ struct FlatMap {  // string_view -> u32, keys live in the graph's arena; slots t
     const uint32_t tag = (uint32_t)(h >> 32);
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       Slot &sl = slot[i];
-      if (sl.val == ~0u) {
-        sl = Slot{tag, v};
+      if (sl.epoch != epoch) {
+        sl = Slot{tag, v, epoch, 0};
         key[i] = k;
         return {v, true};
       }
@@ -91,29 +116,87 @@ struct FlatMap {  // string_view -> u32, keys live in the graph's arena; slots t
     const uint32_t tag = (uint32_t)(h >> 32);
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       const Slot &sl = slot[i];
-      if (sl.val == ~0u) return ~0u;
+      if (sl.epoch != epoch) return ~0u;
       if (sl.tag == tag && key[i] == k) return sl.val;
     }
   }
 };
 
-struct FlatSet64 {
-  std::vector<uint64_t> slot;  // key + 1, 0 = empty
+struct FlatSet64 {  // u64 keys, reused like FlatMap
+  struct Slot {
+    uint64_t key;
+    uint32_t epoch, pad;
+  };
+  std::vector<Slot> slot;
   size_t mask = 0;
+  uint32_t epoch = 0;
   void init(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
-    slot.assign(cap, 0);
+    if (cap > slot.size() || ++epoch == 0) {
+      slot.assign(std::max(cap, slot.size()), Slot{0, 0, 0});
+      epoch = 1;
+    }
     mask = cap - 1;
   }
   bool insert(uint64_t k) {
-    k += 1;
     for (size_t h = ((k * 0x9E3779B97F4A7C15ull) >> 20) & mask;; h = (h + 1) & mask) {
-      if (!slot[h]) return slot[h] = k, true;
-      if (slot[h] == k) return false;
+      if (slot[h].epoch != epoch) return slot[h] = Slot{k, epoch, 0}, true;
+      if (slot[h].key == k) return false;
     }
   }
 };
+
+// The global interning: string -> id, in first-appearance order, keys viewing
+// storage that outlives the map (the graphs' arenas, or the stream's tables).
+struct InternMap {
+  struct Slot {
+    uint32_t tag, val;  // val ~0u = empty
+  };
+  std::vector<Slot> slot;
+  std::vector<std::string_view> key;
+  size_t mask = 0, n = 0;
+  void grow() {
+    const size_t cap = std::max<size_t>(64, 2 * slot.size());
+    std::vector<Slot> os(cap, Slot{0, ~0u});
+    std::vector<std::string_view> ok(cap);
+    os.swap(slot);
+    ok.swap(key);
+    mask = cap - 1;
+    for (size_t i = 0; i < os.size(); i++) {
+      if (os[i].val == ~0u) continue;
+      size_t j = hash_sv(ok[i]) & mask;
+      while (slot[j].val != ~0u) j = (j + 1) & mask;
+      slot[j] = os[i];
+      key[j] = ok[i];
+    }
+  }
+  // the id of k; absent: make(k) stores it and returns (its id, a view of the stored copy)
+  template <class F>
+  uint32_t intern(std::string_view k, F &&make) {
+    if (2 * (n + 1) > slot.size()) grow();
+    const uint64_t h = hash_sv(k);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      if (slot[i].val == ~0u) {
+        const std::pair<uint32_t, std::string_view> m = make(k);
+        slot[i] = Slot{tag, m.first};
+        key[i] = m.second;
+        n++;
+        return m.first;
+      }
+      if (slot[i].tag == tag && key[i] == k) return slot[i].val;
+    }
+  }
+};
+
+// per-thread maps of parse_graph, reused from graph to graph
+struct ParseMaps {
+  FlatMap gidx, ridx, tabs, labs;
+  FlatSet64 seen;
+  std::vector<std::pair<uint64_t, uint32_t>> keys;
+};
+thread_local ParseMaps t_maps;
 
 // ---- a schema-directed JSON reader (encoding/json semantics for the fields used) ----
 struct Json {
@@ -301,14 +384,6 @@ struct Json {
   }
 };
 
-bool ieq(const std::vector<char> &k, const char *s) {
-  size_t n = strlen(s);
-  if (k.size() != n) return false;
-  for (size_t i = 0; i < n; i++)
-    if (tolower((unsigned char)k[i]) != s[i]) return false;  // encoding/json matches keys case-insensitively
-  return true;
-}
-
 // ", <digits>, __WILDCARD__)" and ", <digits>, <digits>)" (molly.go:74-89): leftmost match, group 1
 bool clock_time(std::string_view s, bool wild, std::string &out) {
   for (size_t i = 0; i + 2 <= s.size(); i++) {
@@ -493,7 +568,9 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   const size_t V = goals.size() + rules.size();
   g.n_goals = (uint32_t)goals.size();
   g.id.reserve(V), g.label.reserve(V), g.table.reserve(V), g.type.reserve(V), g.time.reserve(V);
-  FlatMap gidx, ridx, tabs, labs;
+  g.ltab.reserve(V), g.llab.reserve(V), g.tclass.reserve(V);
+  ParseMaps &M = t_maps;
+  FlatMap &gidx = M.gidx, &ridx = M.ridx, &tabs = M.tabs, &labs = M.labs;
   gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
   auto intern = [&](FlatMap &m, std::vector<Str> &order, Str s) {
     if (order.size() * 2 + 16 > m.mask) {  // grow: rehash the distinct keys seen so far
@@ -541,23 +618,57 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.tclass.push_back(type_class(g.sv(r.f[3])));
   }
   // rank of each node's ID inside the graph (the prefix is common, so unprefixed order == prefixed order)
-  // sorted by the first 8 bytes as a big-endian key (a shorter ID pads with
-  // zero bytes, so the key order agrees with the string order), ties by the whole string
-  std::vector<std::pair<uint64_t, uint32_t>> order(V);
-  for (uint32_t i = 0; i < V; i++) {
+  // sorted by 8-byte big-endian keys taken at offset 0 (a shorter ID pads with
+  // zero bytes, so the key order agrees with the string order); a run of equal
+  // keys is sorted again by the next 8 bytes, and so on
+  std::vector<std::pair<uint64_t, uint32_t>> &order = M.keys;
+  order.resize(V);
+  auto key_at = [&](uint32_t i, size_t o) {
     const std::string_view x = g.sv(g.id[i]);
+    if (x.size() >= o + 8) return __builtin_bswap64(load8(x.data() + o));
     uint64_t k = 0;
-    for (size_t b = 0; b < 8; b++) k = (k << 8) | (b < x.size() ? (uint8_t)x[b] : 0u);
-    order[i] = {k, i};
+    for (size_t b = o; b < x.size(); b++) k |= (uint64_t)(uint8_t)x[b] << (56 - 8 * (b - o));
+    return k;
+  };
+  auto by_key = [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+    return a.first != b.first ? a.first < b.first : a.second < b.second;
+  };
+  for (uint32_t i = 0; i < V; i++) order[i] = {key_at(i, 0), i};
+  std::sort(order.begin(), order.end(), by_key);
+  // runs of equal keys: (begin, end, offset of the next key)
+  std::vector<std::array<uint32_t, 3>> runs;
+  for (uint32_t i = 0; i < V;) {
+    uint32_t j = i + 1;
+    while (j < V && order[j].first == order[i].first) j++;
+    if (j - i > 1) runs.push_back({i, j, 8});
+    i = j;
   }
-  std::sort(order.begin(), order.end(), [&](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
-    if (a.first != b.first) return a.first < b.first;
-    const std::string_view x = g.sv(g.id[a.second]), y = g.sv(g.id[b.second]);
-    return x != y ? x < y : a.second < b.second;
-  });
+  while (!runs.empty()) {
+    const auto r = runs.back();
+    runs.pop_back();
+    bool longer = false;  // some ID of the run goes past the keys read so far
+    for (uint32_t i = r[0]; i < r[1]; i++) {
+      longer |= g.id[order[i].second].len > r[2];
+      order[i].first = key_at(order[i].second, r[2]);
+    }
+    if (!longer) {  // keys equal to the end: IDs that differ only by embedded NUL bytes
+      std::sort(order.begin() + r[0], order.begin() + r[1],
+                [&](const std::pair<uint64_t, uint32_t> &x, const std::pair<uint64_t, uint32_t> &y) {
+                  return g.sv(g.id[x.second]) < g.sv(g.id[y.second]);
+                });
+      continue;
+    }
+    std::sort(order.begin() + r[0], order.begin() + r[1], by_key);
+    for (uint32_t i = r[0]; i < r[1];) {
+      uint32_t j = i + 1;
+      while (j < r[1] && order[j].first == order[i].first) j++;
+      if (j - i > 1) runs.push_back({i, j, r[2] + 8});
+      i = j;
+    }
+  }
   g.rank.assign(V, 0);
   for (uint32_t pos = 0; pos < V; pos++) g.rank[order[pos].second] = pos;
-  FlatSet64 seen;
+  FlatSet64 &seen = M.seen;
   seen.init(edges.size());
   size_t created = 0;
   g.src.reserve(edges.size()), g.dst.reserve(edges.size());
@@ -623,30 +734,29 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
       return fail(m);
     }
   // global interning in graph order (== the sequential first-appearance order)
-  std::unordered_map<std::string, uint32_t> tmap, lmap;
+  // (keys view the graphs' arenas, alive until the ingest is freed)
+  InternMap tmap, lmap;
   std::vector<std::vector<uint32_t>> tre(G), lre(G);
   h->node_off.assign(G + 1, 0);
   h->edge_off.assign(G + 1, 0);
+  auto add = [](std::vector<std::string> &names) {
+    return [&names](std::string_view k) {
+      names.emplace_back(k);
+      return std::pair<uint32_t, std::string_view>((uint32_t)names.size() - 1, k);
+    };
+  };
   for (uint32_t g = 0; g < G; g++) {
     Graph &gr = h->graphs[g];
-    for (Str s : gr.tabs) {
-      auto it = tmap.emplace(std::string(gr.sv(s)), (uint32_t)h->tables.size());
-      if (it.second) h->tables.emplace_back(gr.sv(s));
-      tre[g].push_back(it.first->second);
-    }
-    for (Str s : gr.labs) {
-      auto it = lmap.emplace(std::string(gr.sv(s)), (uint32_t)h->labels.size());
-      if (it.second) h->labels.emplace_back(gr.sv(s));
-      lre[g].push_back(it.first->second);
-    }
+    tre[g].reserve(gr.tabs.size());
+    lre[g].reserve(gr.labs.size());
+    for (Str s : gr.tabs) tre[g].push_back(tmap.intern(gr.sv(s), add(h->tables)));
+    for (Str s : gr.labs) lre[g].push_back(lmap.intern(gr.sv(s), add(h->labels)));
     h->node_off[g + 1] = h->node_off[g] + gr.id.size();
     h->edge_off[g + 1] = h->edge_off[g] + gr.src.size();
   }
-  for (const char *c : {"pre", "post"}) {
-    auto it = tmap.emplace(c, (uint32_t)h->tables.size());
-    if (it.second) h->tables.emplace_back(c);
-    (c[1] == 'r' ? h->table_pre : h->table_post) = it.first->second;
-  }
+  static const char *kPrePost[2] = {"pre", "post"};
+  for (int k = 0; k < 2; k++)
+    (k == 0 ? h->table_pre : h->table_post) = tmap.intern(kPrePost[k], add(h->tables));
   if (h->tables.size() > NEMO_MAX_TABLES) {
     delete h;
     return fail("more than NEMO_MAX_TABLES distinct tables");
@@ -686,8 +796,8 @@ struct nemo_ingest_stream {
   std::vector<uint32_t> order;  // parse order: run 0, failedRuns[0], then runs.json order
   int threads = 1;
   uint32_t next = 0;  // next position in `order`
-  std::unordered_map<std::string, uint32_t> tmap, lmap;
-  std::vector<std::string> tables, labels;
+  InternMap tmap, lmap;  // keys view the strings of tables / labels (a deque: no relocation)
+  std::deque<std::string> tables, labels;
   uint32_t table_pre = 0, table_post = 0;
   bool pre_post = false;
   int64_t run0 = -1;  // position of iteration 0 in `order` (0, or -1: absent)
@@ -757,24 +867,22 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
   for (uint32_t g = 0; g < G; g++)
     if (!gs[g].err.empty()) return fail(gs[g].err);
   std::vector<std::vector<uint32_t>> tre(G), lre(G);
+  auto add = [](std::deque<std::string> &names) {
+    return [&names](std::string_view k) {
+      names.emplace_back(k);
+      return std::pair<uint32_t, std::string_view>((uint32_t)names.size() - 1, std::string_view(names.back()));
+    };
+  };
   for (uint32_t g = 0; g < G; g++) {
-    for (Str x : gs[g].tabs) {
-      auto it = s->tmap.emplace(std::string(gs[g].sv(x)), (uint32_t)s->tables.size());
-      if (it.second) s->tables.emplace_back(gs[g].sv(x));
-      tre[g].push_back(it.first->second);
-    }
-    for (Str x : gs[g].labs) {
-      auto it = s->lmap.emplace(std::string(gs[g].sv(x)), (uint32_t)s->labels.size());
-      if (it.second) s->labels.emplace_back(gs[g].sv(x));
-      lre[g].push_back(it.first->second);
-    }
+    tre[g].reserve(gs[g].tabs.size());
+    lre[g].reserve(gs[g].labs.size());
+    for (Str x : gs[g].tabs) tre[g].push_back(s->tmap.intern(gs[g].sv(x), add(s->tables)));
+    for (Str x : gs[g].labs) lre[g].push_back(s->lmap.intern(gs[g].sv(x), add(s->labels)));
   }
   if (!s->pre_post) {  // fixed from the first chunk on: every chunk's corpus names the same ids
-    for (const char *cn : {"pre", "post"}) {
-      auto it = s->tmap.emplace(cn, (uint32_t)s->tables.size());
-      if (it.second) s->tables.emplace_back(cn);
-      (cn[1] == 'r' ? s->table_pre : s->table_post) = it.first->second;
-    }
+    static const char *kPrePost[2] = {"pre", "post"};
+    for (int k = 0; k < 2; k++)
+      (k == 0 ? s->table_pre : s->table_post) = s->tmap.intern(kPrePost[k], add(s->tables));
     s->pre_post = true;
   }
   if (s->tables.size() > NEMO_MAX_TABLES) return fail("more than NEMO_MAX_TABLES distinct tables");
