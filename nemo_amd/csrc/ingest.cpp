@@ -10,6 +10,10 @@
 // nemo_amd/corpus.py (tests/test_ingest.py checks it array for array).
 // Host code only; no device work.
 #include <emmintrin.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
@@ -33,15 +37,56 @@ struct Str {
   uint32_t off, len;
 };
 
+// a provenance file mapped read-only (page-cache pages, no copy), unmapped with its graph
+struct FileMap {
+  void *p = nullptr;
+  size_t n = 0;
+  FileMap() = default;
+  FileMap(const FileMap &) = delete;
+  FileMap &operator=(const FileMap &) = delete;
+  FileMap(FileMap &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr, o.n = 0; }
+  FileMap &operator=(FileMap &&o) noexcept {
+    if (this != &o) reset(), p = o.p, n = o.n, o.p = nullptr, o.n = 0;
+    return *this;
+  }
+  ~FileMap() { reset(); }
+  void reset() {
+    if (p) munmap(p, n);
+    p = nullptr, n = 0;
+  }
+  // false: the file cannot be opened or read
+  bool open(const char *path) {
+    reset();
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    struct stat st;
+    bool ok = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
+    if (ok && st.st_size > 0) {
+      void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (m == MAP_FAILED) ok = false;
+      else p = m, n = (size_t)st.st_size;
+    }
+    close(fd);
+    return ok;
+  }
+};
+
 struct Graph {
-  std::vector<char> arena;   // decoded strings of this graph
+  // Str offsets below flen are bytes of the mapped file (strings without
+  // escapes), at and above it the arena (decoded strings, clock times)
+  FileMap file;
+  const char *fb = "";
+  uint32_t flen = 0;
+  std::vector<char> arena;
   std::vector<Str> id, label, table, type, time;
   uint32_t n_goals = 0;
   std::vector<uint32_t> src, dst, rank, ltab, llab;
   std::vector<uint8_t> tclass;
   std::vector<Str> tabs, labs;  // local first-appearance order
   std::string err;
-  std::string_view sv(Str s) const { return std::string_view(arena.data() + s.off, s.len); }
+  std::string_view sv(Str s) const {
+    return std::string_view(s.off < flen ? fb + s.off : arena.data() + (s.off - flen), s.len);
+  }
 };
 
 // ---- open-addressing tables (the per-graph maps are hot: one lookup per node and edge) ----
@@ -263,9 +308,9 @@ struct Json {
     while (q < e && *q != '"' && *q != '\\') q++;
     return q;
   }
-  // a string as a view: in place when it has no escapes (base = the buffer the
-  // reader walks, which is the arena), else decoded and appended to `o`
-  bool sview(std::vector<char> &o, const char *base, Str &out) {
+  // a string as a view: in place when it has no escapes (offset from base, the
+  // buffer the reader walks), else decoded and appended to `o` (offset bias + its place in o)
+  bool sview(std::vector<char> &o, const char *base, uint32_t bias, Str &out) {
     ws();
     if (p >= e || *p != '"') return ok = false;
     const char *q = scan(p + 1);
@@ -276,7 +321,7 @@ struct Json {
     }
     const size_t o0 = o.size();
     if (!str(o)) return false;
-    out = Str{(uint32_t)o0, (uint32_t)(o.size() - o0)};
+    out = Str{(uint32_t)(bias + o0), (uint32_t)(o.size() - o0)};
     return true;
   }
   // string into `o` (appended); returns false on error
@@ -420,29 +465,19 @@ inline bool keyis(std::string_view k, const char *s, size_t n) {
 }
 
 void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g) {
-  // the file is read into the arena itself: strings without escapes are views
-  // of it, decoded ones and clock times are appended (reserved: no reallocation)
-  {
-    FILE *f = fopen(path.c_str(), "rb");
-    bool ok = f != nullptr;
-    if (ok) {
-      fseek(f, 0, SEEK_END);
-      const long n = ftell(f);
-      fseek(f, 0, SEEK_SET);
-      const size_t sz = n > 0 ? (size_t)n : 0;
-      g.arena.reserve(3 * sz + 64);
-      g.arena.resize(sz);
-      ok = (sz ? fread(g.arena.data(), 1, sz, f) : 0) == sz;
-      fclose(f);
-    }
-    if (!ok) {
-      g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
-              " provenance of file '" + path + "'";
-      return;
-    }
+  // the file is mapped: strings without escapes are views of it, decoded ones
+  // and clock times go to the arena (reserved: no reallocation, the maps hold views)
+  if (!g.file.open(path.c_str()) || g.file.n >= 0xF0000000u) {
+    g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
+            " provenance of file '" + path + "'";
+    return;
   }
-  const size_t fsz = g.arena.size();
-  const char *base = g.arena.data();
+  const size_t fsz = g.file.n;
+  if (fsz) g.fb = (const char *)g.file.p;
+  g.flen = (uint32_t)fsz;
+  g.arena.reserve(2 * fsz + 64);
+  const char *base = g.fb;
+  const uint32_t bias = g.flen;
   Json j{base, base + fsz};
   struct Rec {
     Str f[4];
@@ -459,7 +494,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     else
       while (j.ok) {
         Str ks;
-        if (!j.sview(g.arena, base, ks)) break;
+        if (!j.sview(g.arena, base, bias, ks)) break;
         const std::string_view key = g.sv(ks);
         j.ws();
         if (j.p >= j.e || *j.p != ':') {
@@ -490,7 +525,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
               else
                 while (j.ok) {
                   Str kst;
-                  if (!j.sview(g.arena, base, kst)) break;
+                  if (!j.sview(g.arena, base, bias, kst)) break;
                   const std::string_view k = g.sv(kst);
                   j.ws();
                   if (j.p >= j.e || *j.p != ':') {
@@ -513,7 +548,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
                   } else if (j.lit("null")) {
                   } else {
                     Str sv;
-                    if (!j.sview(g.arena, base, sv)) break;
+                    if (!j.sview(g.arena, base, bias, sv)) break;
                     if (which == 2) (f == 0 ? ed.first : ed.second) = sv;
                     else r.f[f] = sv;
                   }
@@ -595,7 +630,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
       std::string tm2;
       if (clock_time(lab, false, tm2)) tm = tm2, hit = true;
       if (hit) {
-        t = Str{(uint32_t)g.arena.size(), (uint32_t)tm.size()};
+        t = Str{g.flen + (uint32_t)g.arena.size(), (uint32_t)tm.size()};
         g.arena.insert(g.arena.end(), tm.begin(), tm.end());
       }
     }
@@ -1028,7 +1063,7 @@ extern "C" int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index
   const size_t i = index - h->node_off[g];
   Str st = kind == NEMO_STR_NODE_ID ? gr.id[i] : kind == NEMO_STR_NODE_TYPE ? gr.type[i] : kind == NEMO_STR_NODE_TIME ? gr.time[i] : Str{0, 0};
   if (kind < NEMO_STR_NODE_ID || kind > NEMO_STR_NODE_TIME) return NEMO_ERR_INVALID;
-  *s = gr.arena.data() + st.off;
+  *s = gr.sv(st).data();
   *len = st.len;
   return NEMO_OK;
 }
