@@ -95,6 +95,9 @@ struct nemo_ctx {
   // the multi-entry diff (k_dx.hip): g0's Kahn-order relayout, built with the
   // CSR in every load / rebuild, and the per-call buffers (grow-only)
   nemo::DxPrep dxp{};
+  nemo::DxImg dx_img[3]{};           // walk images of g0 (k_dx.hip), built for the test knob dx_img_key
+  nemo::DxImgScratch dx_its{};
+  int dx_img_key = -1;               // -1: not built for the current load
   bool dx_ok = false;                // relayout allocated: run 0 present, every row fits a window
   int diff_legacy = 0;               // option diff_legacy: one workgroup per entry (k_diff.hip)
   uint32_t diff_window = 0;          // option diff_window (test knob): 0 by size, 1 windowed, 2 tiny windows
@@ -397,6 +400,9 @@ static void release_corpus(nemo_ctx *c) {
   c->d_dmap = nullptr;
   c->d_dumask = nullptr;
   c->dxp = nemo::DxPrep{};
+  for (auto &m : c->dx_img) m = nemo::DxImg{};
+  c->dx_its = nemo::DxImgScratch{};
+  c->dx_img_key = -1;
   c->dx_ok = false;
   c->dx_nu_cap = c->dx_nch_cap = 0;
   c->d_dxpb = c->d_dxsval = c->d_dxlpl = nullptr;
@@ -721,8 +727,15 @@ static int device_load(nemo_ctx *c) {
   // order, both CSRs and the node words; write positions, rows both ways, level bounds
   if (c->dx_ok) {
     const double V0 = c->dxp.V0, E0 = c->dxp.E0;
-    if ((rc = timed(c, "k_dxprep", 16 * E0 + 44 * V0, 0, [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->stream); })))
+    if ((rc = timed(c, "k_dxprep", 16 * E0 + 44 * V0, 0,
+                    [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->dx_its.tsum, c->stream); })))
       return rc;
+    // the walk images for the default windows (read rows and Kahn levels, write records and misses)
+    nemo::dx_img_configs(c->dxp.V0, c->dxp.E0, 0, c->dx_img);
+    if ((rc = timed(c, "k_dximg", 3 * (16 * E0 + 24 * V0), 0,
+                    [&] { nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, c->stream); })))
+      return rc;
+    c->dx_img_key = 0;
   }
   return NEMO_OK;
 }
@@ -1030,6 +1043,15 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
           (rc = dalloc(c, &p.lend, nv)) || (rc = dalloc(c, &p.rp, nv + 1)) || (rc = dalloc(c, &p.fp, nv + 1)) ||
           (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))
+        return rc;
+      for (nemo::DxImg &m : c->dx_img)
+        if ((rc = dalloc(c, &m.nw, 1)) || (rc = dalloc(c, &m.wb, nv + 2)) || (rc = dalloc(c, &m.segb, nv + 2)) ||
+            (rc = dalloc(c, &m.missb, nv + 2)) || (rc = dalloc(c, &m.segs, 2 * nv + 2)) ||
+            (rc = dalloc(c, &m.rec, ne + 4)) || (rc = dalloc(c, &m.miss, ne + 1)))
+          return rc;
+      nemo::DxImgScratch &t = c->dx_its;
+      if ((rc = dalloc(c, &t.fseg, nv + 1)) || (rc = dalloc(c, &t.fmiss, nv + 1)) ||
+          (rc = dalloc(c, &t.tsum, nemo::dx_scan_tiles((uint32_t)std::max(nv, ne) + 1))))
         return rc;
     }
   }
@@ -1412,6 +1434,12 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.missing = c->d_miss;
     a.n_missing = c->d_nmiss;
     a.window = c->diff_window;
+    if (c->dx_img_key != (int)c->diff_window) {  // the test knob changed the windows: rebuild the images
+      nemo::dx_img_configs(c->dxp.V0, c->dxp.E0, c->diff_window, c->dx_img);
+      nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, s);
+      c->dx_img_key = (int)c->diff_window;
+    }
+    for (int k = 0; k < 3; k++) a.img[k] = c->dx_img[k];
     rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0, [&] { nemo::launch_dx(c->dc, a, s); });
   } else {
     nemo::DiffArgs a;

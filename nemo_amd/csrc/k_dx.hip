@@ -35,6 +35,52 @@
 
 namespace nemo {
 
+// ---- device-wide exclusive scan (in place) --------------------------------------------
+// tiles of DSC_TILE entries: tile sums, their scan (one workgroup), then each
+// tile scanned with its offset
+#define DSC_NT 1024
+#define DSC_PER 4
+#define DSC_TILE (DSC_NT * DSC_PER)
+__global__ __launch_bounds__(DSC_NT) void k_scan_tiles(const uint32_t *a, uint32_t n, uint32_t *tsum) {
+  __shared__ uint32_t s_red[DSC_NT / 64];
+  const uint32_t i0 = blockIdx.x * DSC_TILE + threadIdx.x * DSC_PER;
+  uint32_t x = 0;
+#pragma unroll
+  for (int q = 0; q < DSC_PER; q++) x += i0 + q < n ? a[i0 + q] : 0u;
+  uint32_t tot;
+  block_exscan<DSC_NT>(x, &tot, s_red);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(DSC_NT) void k_scan_sums(uint32_t *tsum, uint32_t nt) {
+  __shared__ uint32_t s_red[DSC_NT / 64];
+  block_scan_inplace<DSC_NT, 4>(tsum, nt, s_red);
+}
+__global__ __launch_bounds__(DSC_NT) void k_scan_apply(uint32_t *a, uint32_t n, const uint32_t *tsum) {
+  __shared__ uint32_t s_red[DSC_NT / 64];
+  const uint32_t i0 = blockIdx.x * DSC_TILE + threadIdx.x * DSC_PER;
+  uint32_t x[DSC_PER], sum = 0;
+#pragma unroll
+  for (int q = 0; q < DSC_PER; q++) {
+    x[q] = i0 + q < n ? a[i0 + q] : 0u;
+    sum += x[q];
+  }
+  uint32_t tot;
+  uint32_t ex = block_exscan<DSC_NT>(sum, &tot, s_red) + tsum[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < DSC_PER; q++) {
+    if (i0 + q < n) a[i0 + q] = ex;
+    ex += x[q];
+  }
+}
+uint32_t dx_scan_tiles(uint32_t n) { return (n + DSC_TILE - 1) / DSC_TILE + 1; }
+void launch_scan(uint32_t *a, uint32_t n, uint32_t *tsum, hipStream_t s) {
+  const uint32_t nt = (n + DSC_TILE - 1) / DSC_TILE;
+  if (!nt) return;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(nt), dim3(DSC_NT), 0, s, a, n, tsum);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(DSC_NT), 0, s, tsum, nt);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nt), dim3(DSC_NT), 0, s, a, n, tsum);
+}
+
 // ---- g0 relayout (launch_dx_prep) ---------------------------------------------------
 // pass 1, one thread per position i: node -> position, row lengths (parents in
 // Kahn order, children in reversed Kahn order), level bounds, rule bit
@@ -55,12 +101,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_a(DevCorpus c, DxPrep p) {
   p.lend[i] = gv.lvl[l + 1];
   p.info[i] = (l << 3) | (is_rule(gv.word[v]) ? DXI_RULE : 0u);
 }
-// pass 2, one workgroup: row starts
-__global__ __launch_bounds__(1024) void k_dxp_scan(DxPrep p) {
-  __shared__ uint32_t s_red[16];
-  block_scan_inplace<1024, 16>(p.rp, p.V0 + 1, s_red);
-  block_scan_inplace<1024, 16>(p.fp, p.V0 + 1, s_red);
-}
+// pass 2 (launch_scan): row starts
 // pass 3, one thread per position: rows as walk indices (parents as positions,
 // children as reversed positions), label entries as positions
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_b(DevCorpus c, DxPrep p) {
@@ -75,12 +116,118 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_b(DevCorpus c, DxPrep p) {
   for (uint32_t j = gv.fp[v]; j < gv.fp[v + 1]; j++) p.fc[o++] = V - 1u - p.tpos[gv.fc[j]];
 }
 
-void launch_dx_prep(const DevCorpus &c, const DxPrep &p, hipStream_t s) {
+void launch_dx_prep(const DevCorpus &c, const DxPrep &p, uint32_t *tsum, hipStream_t s) {
   const uint32_t nb = (std::max(p.V0, p.n_r0lab) + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (!nb) return;
   hipLaunchKernelGGL(k_dxp_a, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, p);
-  hipLaunchKernelGGL(k_dxp_scan, dim3(1), dim3(1024), 0, s, p);
+  launch_scan(p.rp, p.V0 + 1, tsum, s);
+  launch_scan(p.fp, p.V0 + 1, tsum, s);
   hipLaunchKernelGGL(k_dxp_b, dim3(nb), dim3(NEMO_BLOCK), 0, s, c, p);
+}
+
+// ---- walk images (launch_dx_img) -------------------------------------------------------
+// windows: greedy in walk order, one workgroup per image; a window ends before
+// W positions or before its links pass EC (every row fits: dx_max_row)
+struct DxImgSet {
+  DxImg m[3];
+};
+__global__ __launch_bounds__(1024) void k_dxi_bounds(DxPrep p, DxImgSet set) {
+  __shared__ uint32_t s_best[3];
+  const DxImg m = set.m[blockIdx.x];
+  const uint32_t V = p.V0, tid = threadIdx.x, lane = lane_id();
+  const uint32_t *rowp = m.rev ? p.fp : p.rp;
+  if (tid < 3) s_best[tid] = 0;
+  __syncthreads();
+  uint32_t b = 0, k = 0;
+  while (b < V) {  // workgroup-uniform
+    const uint32_t nmax = min(m.W, V - b), base = rowp[b];
+    uint32_t best = 0;
+    for (uint32_t t = tid + 1; t <= nmax; t += 1024)
+      if (rowp[b + t] - base <= m.EC) best = max(best, t);
+    for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor(best, d));
+    // three buffers: round k fills k % 3 and clears (k + 1) % 3, last read in round k - 2
+    if (tid == 0) s_best[(k + 1) % 3] = 0;
+    if (lane == 0) atomicMax(&s_best[k % 3], best);
+    __syncthreads();
+    const uint32_t n = max(s_best[k % 3], 1u);
+    if (tid == 0) m.wb[k] = b;
+    b += n;
+    k++;
+  }
+  if (tid == 0) {
+    m.wb[k] = V;
+    m.nw[0] = k;
+  }
+}
+// the window of walk index i: wb[k] <= i < wb[k + 1]
+__device__ __forceinline__ uint32_t dxi_window(const DxImg &m, uint32_t nw, uint32_t i) {
+  uint32_t lo = 0, hi = nw;  // wb[lo] <= i < wb[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (m.wb[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+// per walk index: segment flag (the window's first position or a level's
+// first), links that leave the ring
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_count(DxPrep p, DxImg m, DxImgScratch t) {
+  const uint32_t V = p.V0, i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i > V) return;
+  if (i == V) {
+    t.fseg[V] = 0;
+    t.fmiss[V] = 0;
+    return;
+  }
+  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), w0 = m.wb[k], w1 = m.wb[k + 1];
+  const uint32_t *rowp = m.rev ? p.fp : p.rp, *col = m.rev ? p.fc : p.rc;
+  const uint32_t pos = m.rev ? V - 1u - i : i;
+  const uint32_t lstart = m.rev ? V - p.lend[pos] : p.lbeg[pos];
+  t.fseg[i] = (i == w0 || lstart == i) ? 1u : 0u;
+  uint32_t nm = 0;
+  if (!m.whole)
+    for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) nm += col[j] + m.R < w1 ? 1u : 0u;
+  t.fmiss[i] = nm;
+}
+// per walk index: its segment entry, its links' records and misses; window starts
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_fill(DxPrep p, DxImg m, DxImgScratch t) {
+  const uint32_t V = p.V0, i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (i >= V) return;
+  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), w0 = m.wb[k], w1 = m.wb[k + 1];
+  const uint32_t *rowp = m.rev ? p.fp : p.rp, *col = m.rev ? p.fc : p.rc;
+  const uint32_t base = rowp[w0], sg = t.fseg[i];
+  if (t.fseg[i + 1] != sg) m.segs[sg] = (uint16_t)(rowp[i] - base);
+  if (i == w0) {
+    m.segb[k] = sg;
+    m.missb[k] = t.fmiss[i];
+  }
+  if (i == 0) {
+    m.segb[nw] = t.fseg[V];
+    m.missb[nw] = t.fmiss[V];
+  }
+  const uint32_t own = (m.whole ? i : (i & (m.R - 1u))) << 16;
+  uint32_t o = t.fmiss[i];
+  for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) {
+    const uint32_t x = col[j];
+    const bool far = !m.whole && x + m.R < w1;
+    m.rec[j] = (far ? m.R : (m.whole ? x : (x & (m.R - 1u)))) | own;
+    if (far) m.miss[o++] = make_uint2(x, own >> 16);
+  }
+}
+
+void launch_dx_img(const DxPrep &p, DxImg img[3], const DxImgScratch &t, hipStream_t s) {
+  const uint32_t V = p.V0;
+  if (!V) return;
+  DxImgSet set;
+  for (int k = 0; k < 3; k++) set.m[k] = img[k];
+  hipLaunchKernelGGL(k_dxi_bounds, dim3(3), dim3(1024), 0, s, p, set);
+  const uint32_t nb = (V + 1 + NEMO_BLOCK - 1) / NEMO_BLOCK;
+  for (int k = 0; k < 3; k++) {
+    hipLaunchKernelGGL(k_dxi_count, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
+    launch_scan(t.fseg, V + 1, t.tsum, s);
+    launch_scan(t.fmiss, V + 1, t.tsum, s);
+    hipLaunchKernelGGL(k_dxi_fill, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
+  }
 }
 
 // ---- present bitmaps ------------------------------------------------------------------
@@ -214,8 +361,8 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 
 // ---- the windowed walk ------------------------------------------------------------------
 // MODE 0: reachability, T = u64 (64 sources per bit column), one walker;
-//         blockIdx.y = 0: Fwd* over parents in Kahn order, 1: Bwd* over
-//         children in reversed Kahn order.  value = Good | OR(links).
+//         blockIdx.y = 0: Fwd* over parents in Kahn order (image m0), 1: Bwd*
+//         over children in reversed Kahn order (image m1).  value = Good | OR(links).
 // MODE 2: depth, T = u32, NE walkers (sources NE·blockIdx.x + e), Kahn order
 //         over parents: s = D ? 1 + max(s of links) : 0 (depth + 1 of D nodes;
 //         a non-D parent has s = 0, so the max runs over D parents).  While a
@@ -223,72 +370,58 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 //         max) or DX_IND | r, r = the max so far; s = r + 1.
 // WHOLE: the graph is one window (ring = positions, no wrap, no misses).
 //
-// A window: staging (all waves) -> the walk (waves e < NE) -> finalize (all
-// waves: values to HBM, LP maxima).  Staging writes the window's links as u32
-// records (ring slot of the linked position | ring slot of the owner << 16) in
-// walk order, and the link range of every level segment.  The walk of a level
-// is then one pass over its links, lanes over links: read the record, read the
-// linked value, apply it to the owner's slot with an LDS atomic; a level only
-// reads slots of earlier levels, and a wave's LDS operations complete in
-// order, so no barrier separates the levels.
+// A window (the image's ranges): staging (all waves: the link records and
+// level segments copied to LDS, every position's init value into its ring
+// slot, the links that leave the ring read from HBM and folded into their
+// owners' slots) -> the walk (waves e < NE) -> finalize (all waves: values to
+// HBM, LP maxima).  The walk of a level is one pass over its links, lanes over
+// links: read the linked value, apply it to the owner's slot with an LDS
+// atomic; a level only reads slots of earlier levels, and a wave's LDS
+// operations complete in order, so no barrier separates the levels.
 #define DX_NOTD 0xFFFFFFFFu
 #define DX_IND 0x80000000u
-#define DX_MC 2048u  // ring misses listed per window (beyond: applied one by one)
 template <typename T, int NE>
 struct DxLds {
-  T *ring0;          // NE rings of [R + 2] (stride rs): [R] the identity (sink), [R + 1] a dump slot
+  T *ring0;          // NE rings of [R + 1 + 64] (stride rs): [R] the identity (sink), [R + 1 + lane] dump slots
   uint32_t rs;
-  uint32_t *off;     // [W + 1] absolute row starts of the window's positions
-  uint32_t *lk;      // [EC] links: ring slot of the linked position (R: none) | owner's slot << 16
-  uint16_t *seg;     // [W + 1] first link of each level segment (relative); seg[nseg] = links
-  uint32_t *lpb;     // [NE][W / 32 + 1] depth: LP rules of the window, one bit per position
-  uint2 *miss;       // [DX_MC] (linked walk index, owner's slot) of the links older than the ring
+  uint32_t *lk;      // [EC] link records: ring slot of the linked position (R: none) | owner's slot << 16
+  uint16_t *seg;     // [W + 2] first link of each level segment (relative); seg[nseg] = links
+  uint32_t *lpb;     // [NE][W / 32 + 2] depth: LP rules of the window, one bit per position
 };
 template <typename T, int NE>
-__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC, bool whole) {
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 2u)) + lds_align(4u * (W + 1u)) + lds_align(4u * EC) +
-         lds_align(2u * (W + 1u)) + NE * lds_align(4u * (W / 32u + 1u)) + (whole ? 0u : 8u * DX_MC);
+__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC) {
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + lds_align(4u * EC) + lds_align(2u * (W + 2u)) +
+         NE * lds_align(4u * (W / 32u + 2u));
 }
 template <typename T, int NE>
 __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC) {
   uint8_t *p = (uint8_t *)base;
   DxLds<T, NE> L;
   L.ring0 = (T *)p;
-  L.rs = lds_align((uint32_t)sizeof(T) * (R + 2u)) / (uint32_t)sizeof(T);
-  p += NE * lds_align((uint32_t)sizeof(T) * (R + 2u));
-  L.off = (uint32_t *)p;
-  p += lds_align(4u * (W + 1u));
+  L.rs = lds_align((uint32_t)sizeof(T) * (R + 65u)) / (uint32_t)sizeof(T);
+  p += NE * lds_align((uint32_t)sizeof(T) * (R + 65u));
   L.lk = (uint32_t *)p;
   p += lds_align(4u * EC);
   L.seg = (uint16_t *)p;
-  p += lds_align(2u * (W + 1u));
+  p += lds_align(2u * (W + 2u));
   L.lpb = (uint32_t *)p;
-  p += NE * lds_align(4u * (W / 32u + 1u));
-  L.miss = (uint2 *)p;
   return L;
 }
-struct DxWalkCfg {
-  uint32_t W, R, EC;  // window positions, ring slots, links per window
-  uint32_t whole;     // 1: the whole graph is one window
-};
 
-template <int MODE, int NE, bool WHOLE, int NT, int PS>
-__global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg cfg) {
+template <int MODE, int NE, bool WHOLE, int NT>
+__global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0, DxImg m1) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  // PS positions per thread per staging group (contiguous, so that the level
-  // segments come out in thread order); windowed: W == PS * NT, one group
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_n, s_nmiss, s_red[NT / 64];
   __shared__ uint32_t s_lmax[NE], s_lpn[NE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const uint32_t V = a.p.V0, W = cfg.W, R = cfg.R, EC = cfg.EC, LW = W / 32u + 1u;
   const bool rev = MODE == 0 && blockIdx.y == 1;
+  const DxImg m = rev ? m1 : m0;
+  const uint32_t V = a.p.V0, W = m.W, R = m.R, EC = m.EC, LW = W / 32u + 2u;
   const uint32_t chunk = MODE == 0 ? blockIdx.x : 0u;
   DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC);
-  // walk-order rows (parents in Kahn order / children in reversed order); per
-  // walker e: its source (depth), ring and value array, computed from e (a
+  const uint32_t *rowp = rev ? a.p.fp : a.p.rp;
+  // per walker e: its source (depth), ring and value array, computed from e (a
   // dynamically indexed register array would live in scratch memory)
-  const uint32_t *rowp = rev ? a.p.fp : a.p.rp, *col = rev ? a.p.fc : a.p.rc;
   auto srcu = [&](uint32_t e) -> uint32_t {  // NEMO_NONE: no source, or no LP rule (nothing to walk)
     if (MODE == 0) return 0u;
     const uint32_t u = blockIdx.x * NE + e;
@@ -300,7 +433,6 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
     return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
   };
   auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
-  // the missing value of a link older than the ring, applied to its owner's slot
   auto apply_miss = [&](uint32_t e, uint32_t osl, T val) {
     if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[osl], (unsigned long long)val);
     else atomicMax((uint32_t *)&ringp(e)[osl], DX_IND | (uint32_t)val);
@@ -333,219 +465,181 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
   do {         \
   } while (0)
 #endif
-  for (uint32_t w0 = 0; w0 < V;) {
-    const uint32_t nmax = min(W, V - w0);
-    // ---- staging 1: row starts; the window ends where its links would pass EC ----
-    for (uint32_t k0 = 0; k0 <= nmax; k0 += PS * NT) {
-      uint32_t v[PS];
-#pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q * NT + tid;
-        v[q] = k <= nmax ? rowp[w0 + k] : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q * NT + tid;
-        if (k <= nmax) L.off[k] = v[q];
-      }
-    }
-    if (tid == 0) {
-      s_n = 0;
-      s_nmiss = 0;
-    }
-    for (uint32_t w = tid; w < NE * LW && MODE == 2; w += NT) L.lpb[w] = 0;
-    __syncthreads();
-    {
-      uint32_t best = 0;
-      for (uint32_t k = tid + 1; k <= nmax; k += NT)
-        if (L.off[k] - L.off[0] <= EC) best = max(best, k);
-      for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor(best, d));
-      if (lane == 0) atomicMax(&s_n, best);
-    }
-    __syncthreads();
-    const uint32_t n = s_n, w1 = w0 + n, base = L.off[0], ne = L.off[n] - base;
-    DXT(0);
-    // ---- staging 2: per position: init value into its ring slot (no link of
-    // the window reads those slots: they hold positions older than the ring),
-    // the owner half of its links' records, the level segments (a position
-    // that starts its level starts a segment), depth: the LP bits ----
-    uint32_t nseg = 0;
-    for (uint32_t g0 = 0; g0 < n; g0 += PS * NT) {
-      const uint32_t k0 = g0 + tid * PS;
-      uint32_t lb[PS], st = 0, lp[PS];
-      T ini[PS][NE];
-#pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q;
-        const bool in = k < n;
-        const uint32_t i = w0 + (in ? k : 0u), pos = rev ? V - 1u - i : i;
-        lb[q] = rev ? V - a.p.lend[pos] : a.p.lbeg[pos];  // the walk index where the position's level starts
-        lp[q] = 0;
-        if (MODE == 0) {
-          ini[q][0] = in ? (T)a.gw[(size_t)chunk * V + pos] : (T)0;
-        } else {
-          const bool rule = in && (a.p.info[pos] & DXI_RULE);
-#pragma unroll
-          for (int e = 0; e < NE; e++) {
-            const uint32_t u = srcu(e), b = u & 63u;
-            const uint64_t dv = u != NEMO_NONE && in ? a.dw[(size_t)(u >> 6) * V + pos] : 0ull;
-            const uint64_t lv = u != NEMO_NONE && in ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
-            ini[q][e] = ((dv >> b) & 1ull) ? DX_IND : DX_NOTD;
-            lp[q] |= (rule && ((lv >> b) & 1ull) ? 1u : 0u) << e;
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q;
-        if (k >= n) continue;
-        const uint32_t sl = slot(w0 + k);
-#pragma unroll
-        for (int e = 0; e < NE; e++) ringp(e)[sl] = ini[q][e];
-#pragma unroll
-        for (int e = 0; e < NE; e++)
-          if (MODE == 2 && ((lp[q] >> e) & 1u)) atomicOr(&L.lpb[e * LW + (k >> 5)], 1u << (k & 31u));
-        for (uint32_t j = L.off[k]; j < L.off[k + 1]; j++) ((uint16_t *)&L.lk[j - base])[1] = (uint16_t)sl;
-        st |= (k == 0 || lb[q] == w0 + k ? 1u : 0u) << q;
-      }
-      uint32_t tot;
-      uint32_t o = nseg + block_exscan<NT>((uint32_t)__popc(st), &tot, s_red);
-#pragma unroll
-      for (int q = 0; q < PS; q++)
-        if ((st >> q) & 1u) L.seg[o++] = (uint16_t)(L.off[k0 + q] - base);
-      nseg += tot;
-    }
-    if (tid == 0) L.seg[nseg] = (uint16_t)ne;
-    __syncthreads();
-    DXT(1);
-    // ---- staging 3: the links, one contiguous range of col, in 16-B aligned
-    // chunks: the linked position's ring slot, or, for a link older than the
-    // ring, an entry of the miss list (its final value is in HBM, written by
-    // an earlier window's finalize) ----
+  const uint32_t nw = m.nw[0];
+  for (uint32_t k = 0; k < nw; k++) {
+    const uint32_t w0 = m.wb[k], w1 = m.wb[k + 1], n = w1 - w0;
+    const uint32_t base = rowp[w0], ne = rowp[w1] - base;
+    const uint32_t sg0 = m.segb[k], nseg = m.segb[k + 1] - sg0;
+    const uint32_t ms0 = m.missb[k], nm = m.missb[k + 1] - ms0;
+    // ---- staging: records (16-B chunks of the image), level segments, init
+    // values, and the first round of misses loaded (entry, then value) ----
     {
       const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
-      for (uint32_t cb = c0; cb < c1; cb += 4 * NT) {
-        uint4 v4[4];
+      for (uint32_t cb = c0; cb < c1; cb += 2 * NT) {
+        uint4 v4[2];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < 2; q++) {
           const uint32_t ck = cb + q * NT + tid;
-          v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(col)[ck] : make_uint4(0, 0, 0, 0);
+          v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(m.rec)[ck] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < 2; q++) {
           const uint32_t ck = cb + q * NT + tid;
           const uint32_t qs[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
 #pragma unroll
           for (int b = 0; b < 4; b++) {
             const uint32_t j = 4 * ck + b;
-            const bool in = ck < c1 && j >= base && j < base + ne;
-            const uint32_t x = qs[b];  // walk index of the linked position
-            const bool far = in && !WHOLE && x + R < w1;
-            if (in) ((uint16_t *)&L.lk[j - base])[0] = (uint16_t)(far ? R : slot(x));
-            if (WHOLE) continue;
-            const uint64_t fm = __ballot(far);
-            if (!fm) continue;  // wave-uniform
-            uint32_t mb = 0;
-            if (lane == (uint32_t)(__ffsll((long long)fm) - 1)) mb = atomicAdd(&s_nmiss, (uint32_t)__popcll(fm));
-            mb = __shfl(mb, __ffsll((long long)fm) - 1) + mbcnt(fm);
-            if (!far) continue;
-            const uint32_t osl = ((uint16_t *)&L.lk[j - base])[1];
-            if (mb < DX_MC) {
-              L.miss[mb] = make_uint2(x, osl);
-            } else {  // the list is full: apply it here
-#pragma unroll
-              for (uint32_t e = 0; e < (uint32_t)NE; e++)
-                if (MODE == 0 || srcu(e) != NEMO_NONE)
-                  apply_miss(e, osl, __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            }
+            if (ck < c1 && j >= base && j < base + ne) L.lk[j - base] = qs[b];
           }
         }
       }
     }
-    __syncthreads();
-    if (!WHOLE) {  // the listed misses: their values loaded together, then applied
-      const uint32_t nm = min(s_nmiss, DX_MC);
-      for (uint32_t m0 = 0; m0 < nm; m0 += 4 * NT) {
-        uint2 ms[4];
-        T val[4][NE];
+    for (uint32_t t = tid; t < nseg; t += NT) L.seg[t] = m.segs[sg0 + t];
+    if (tid == 0) L.seg[nseg] = (uint16_t)ne;
+    // init values; depth: the LP bits of 64 consecutive positions by ballot
+    for (uint32_t k0 = 0; k0 < n; k0 += NT) {
+      const uint32_t kk = k0 + tid;
+      const bool in = kk < n;
+      const uint32_t i = w0 + (in ? kk : 0u), pos = rev ? V - 1u - i : i;
+      if (MODE == 0) {
+        if (in) ringp(0)[slot(i)] = (T)a.gw[(size_t)chunk * V + pos];
+      } else {
+        const bool rule = in && (a.p.info[pos] & DXI_RULE);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t m = m0 + q * NT + tid;
-          ms[q] = m < nm ? L.miss[m] : make_uint2(0, R + 1);
-#pragma unroll
-          for (int e = 0; e < NE; e++)
-            val[q][e] = m < nm && (MODE == 0 || srcu(e) != NEMO_NONE)
-                            ? __hip_atomic_load(gvalp(e) + ms[q].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : (T)0;
+        for (int e = 0; e < NE; e++) {
+          const uint32_t u = srcu(e), b = u & 63u;
+          const uint64_t dv = u != NEMO_NONE && in ? a.dw[(size_t)(u >> 6) * V + pos] : 0ull;
+          const uint64_t lv = u != NEMO_NONE && rule ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
+          if (in) ringp(e)[slot(i)] = (T)(((dv >> b) & 1ull) ? DX_IND : DX_NOTD);
+          const uint64_t lb = __ballot(rule && ((lv >> b) & 1ull));
+          if (lane < 2u && ((k0 + wv * 64u) >> 5) + lane < LW)
+            L.lpb[e * LW + ((k0 + wv * 64u) >> 5) + lane] = (uint32_t)(lb >> (32u * lane));
         }
+      }
+    }
+    constexpr int MB = 4;  // misses per thread per round
+    uint2 mr[MB];
+    T mv[MB][NE];
+    auto load_miss = [&](uint32_t r0) {
 #pragma unroll
-        for (int q = 0; q < 4; q++)
+      for (int q = 0; q < MB; q++) {
+        const uint32_t mm = r0 + q * NT + tid;
+        mr[q] = mm < nm ? m.miss[ms0 + mm] : make_uint2(0, R + 1u + lane);
+      }
 #pragma unroll
-          for (int e = 0; e < NE; e++)
-            if (m0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)) apply_miss(e, ms[q].y, val[q][e]);
+      for (int q = 0; q < MB; q++)
+#pragma unroll
+        for (int e = 0; e < NE; e++)
+          mv[q][e] = r0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)
+                         ? __hip_atomic_load(gvalp(e) + mr[q].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : (T)0;
+    };
+    auto apply_misses = [&](uint32_t r0) {
+#pragma unroll
+      for (int q = 0; q < MB; q++)
+#pragma unroll
+        for (int e = 0; e < NE; e++)
+          if (r0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)) apply_miss(e, mr[q].y, mv[q][e]);
+    };
+    if (!WHOLE && nm) load_miss(0);
+    __syncthreads();  // init values are in place before misses fold into them
+    if (!WHOLE && nm) {
+      apply_misses(0);
+      for (uint32_t r0 = MB * NT; r0 < nm; r0 += MB * NT) {
+        load_miss(r0);
+        apply_misses(r0);
       }
       __syncthreads();
     }
-    DXT(2);
+    DXT(1);
     // ---- the walk: wave e < NE walks source e through the window's level
     // segments, lanes over a segment's links.  No barrier or fence between
     // levels: a level reads only slots of earlier levels, and a wave's LDS
-    // operations complete in issue order.  Idle lanes read the sink and write
-    // the dump slot, so the level has no branches ----
+    // operations complete in issue order.  A level's first 256 link records
+    // are read during the level before (they do not depend on it), so a level
+    // costs one LDS round trip: read the linked values, apply them.  Idle
+    // lanes read the sink and apply to a dump slot of their own (no branches,
+    // no two lanes on one slot) ----
     if (wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE)) {
       T *ring = ringp(wv);
-      const uint32_t idle = R | ((R + 1u) << 16);
-      uint32_t lo = L.seg[0], hi = L.seg[nseg > 0 ? 1 : 0];
-      for (uint32_t t = 0; t < nseg; t++) {
-        const uint32_t hn = L.seg[min(t + 2, nseg)];  // the next level's end, read ahead
-        for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
-          uint32_t rc[4];
-          T x[4];
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const uint32_t j = j0 + 64u * q + lane;
-            rc[q] = j < hi ? L.lk[j] : idle;
-          }
-#pragma unroll
-          for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            if (MODE == 0) {
-              atomicOr((unsigned long long *)&ring[rc[q] >> 16], (unsigned long long)x[q]);
-            } else {
-              const uint32_t sv = (uint32_t)x[q] == DX_NOTD ? 0u : ((uint32_t)x[q] & ~DX_IND) + 1u;
-              atomicMax((uint32_t *)&ring[rc[q] >> 16], DX_IND | sv);
-            }
-          }
+      const uint32_t idle = R | ((R + 1u + lane) << 16);
+      auto apply = [&](uint32_t rec, T x) {
+        if (MODE == 0) {
+          atomicOr((unsigned long long *)&ring[rec >> 16], (unsigned long long)x);
+        } else {
+          const uint32_t sv = (uint32_t)x == DX_NOTD ? 0u : ((uint32_t)x & ~DX_IND) + 1u;
+          atomicMax((uint32_t *)&ring[rec >> 16], DX_IND | sv);
         }
+      };
+      // level t: links [lo, hi); hn = the end of level t + 1
+      uint32_t lo = 0, hi = 0, hn = 0;
+      if (nseg) {
+        lo = L.seg[0];
+        hi = L.seg[1];
+        hn = L.seg[min(2u, nseg)];
+      }
+      uint32_t rc[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t j = lo + 64u * q + lane;
+        rc[q] = j < hi ? L.lk[j] : idle;
+      }
+      lo = __builtin_amdgcn_readfirstlane(lo);
+      hi = __builtin_amdgcn_readfirstlane(hi);
+      hn = __builtin_amdgcn_readfirstlane(hn);
+      for (uint32_t t = 0; t < nseg; t++) {
+        T x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
+        // the next level's first records and the end of the level after it
+        uint32_t rn[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t j = hi + 64u * q + lane;
+          rn[q] = j < hn ? L.lk[j] : idle;
+        }
+        const uint32_t hnn = L.seg[min(t + 3u, nseg)];
+#pragma unroll
+        for (int q = 0; q < 4; q++) apply(rc[q], x[q]);
+        // links past the first 256 of the level (wide levels): 512 per step
+        for (uint32_t j0 = lo + 256u; j0 < hi; j0 += 512u) {
+          uint32_t r2[8];
+          T x2[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const uint32_t j = j0 + 64u * q + lane;
+            r2[q] = j < hi ? L.lk[j] : idle;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++) x2[q] = ring[r2[q] & 0xFFFFu];
+#pragma unroll
+          for (int q = 0; q < 8; q++) apply(r2[q], x2[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) rc[q] = rn[q];
         lo = hi;
-        hi = __builtin_amdgcn_readfirstlane(hn);
-        asm volatile("" ::: "memory");
+        hi = hn;
+        hn = __builtin_amdgcn_readfirstlane(hnn);
       }
     }
     DXT(3);
     __syncthreads();
     // ---- finalize: the window's values to HBM; depth: s, the LP maxima, the LP list ----
-    for (uint32_t k0 = 0; k0 < n; k0 += PS * NT) {
+    for (uint32_t kk = tid; kk < n; kk += NT) {
+      const uint32_t i = w0 + kk, sl = slot(i);
+      if (MODE == 0) {
+        gvalp(0)[i] = ringp(0)[sl];
+      } else {
 #pragma unroll
-      for (int q = 0; q < PS; q++) {
-        const uint32_t k = k0 + q * NT + tid;
-        if (k >= n) continue;
-        const uint32_t i = w0 + k, sl = slot(i);
-        if (MODE == 0) {
-          gvalp(0)[i] = ringp(0)[sl];
-        } else {
-#pragma unroll
-          for (int e = 0; e < NE; e++) {
-            const uint32_t u = srcu(e);
-            if (u == NEMO_NONE) continue;
-            const uint32_t r = (uint32_t)ringp(e)[sl];
-            const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
-            gvalp(e)[i] = (T)sv;
-            if ((L.lpb[e * LW + (k >> 5)] >> (k & 31u)) & 1u) {
-              lmax[e] = max(lmax[e], sv);
-              if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
-            }
+        for (int e = 0; e < NE; e++) {
+          const uint32_t u = srcu(e);
+          if (u == NEMO_NONE) continue;
+          const uint32_t r = (uint32_t)ringp(e)[sl];
+          const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
+          gvalp(e)[i] = (T)sv;
+          if ((L.lpb[e * LW + (kk >> 5)] >> (kk & 31u)) & 1u) {
+            lmax[e] = max(lmax[e], sv);
+            if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
           }
         }
       }
@@ -560,7 +654,6 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxWalkCfg
 #ifdef NEMO_STAMPS
     acc[6]++;
 #endif
-    w0 = w1;
   }
 #ifdef NEMO_STAMPS
   const uint32_t stw = 16u * (MODE == 0 ? blockIdx.x * 2u + blockIdx.y : blockIdx.x) + (MODE == 0 ? 0u : 8u);
@@ -686,51 +779,75 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
 }
 
 // ---- launch -----------------------------------------------------------------------------
-template <int MODE, int NE, bool WHOLE, int NT, int PS>
-static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxWalkCfg &cfg, dim3 grid, hipStream_t s) {
+template <int MODE, int NE, bool WHOLE, int NT>
+static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1, dim3 grid,
+                        hipStream_t s) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  const uint32_t bytes = dx_lds_bytes<T, NE>(cfg.W, cfg.R, cfg.EC, cfg.whole != 0);
-  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT, PS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  const uint32_t bytes = dx_lds_bytes<T, NE>(m0.W, m0.R, m0.EC);
+  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)bytes);
-  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT, PS>), grid, dim3(NT), bytes, s, c, a, cfg);
+  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, m0, m1);
 }
 
 #define DX_LDS_MAX (160u * 1024u - 1024u)
-// windowed configurations: W positions, R ring slots (power of two, > W), EC links
-// reachability: 1024 threads, 2 positions each per window; depth: 512 threads, 4 walkers
+// windowed configurations: W positions, R ring slots (power of two, >= 2 W), EC links
+// reachability: 1024 threads, one walker; depth: 512 threads, 4 walkers
 #define DXR_NT 1024
 #define DXD_NT 512
-static const DxWalkCfg kReach = {2 * DXR_NT, 8192, 12288, 0};
-static const DxWalkCfg kDepth = {2 * DXD_NT, 4096, 6144, 0};
+#define DXD_NE 4
+struct DxCfg {
+  uint32_t W, R, EC;
+};
+static const DxCfg kReach = {2048, 8192, 12288};
+static const DxCfg kDepth = {1024, 4096, 6144};
 // test knob (window = 2): windows of the same size, rings barely larger, so most links leave them
-static const DxWalkCfg kTinyR = {2 * DXR_NT, 4096, 12288, 0};
-static const DxWalkCfg kTinyD = {2 * DXD_NT, 2048, 6144, 0};
+static const DxCfg kTinyR = {2048, 4096, 12288};
+static const DxCfg kTinyD = {1024, 2048, 6144};
 
 // every row of g0 must fit one window's links (launch_dx's windowed configurations)
 uint32_t dx_max_row() { return std::min(kReach.EC, kDepth.EC); }
 uint32_t dx_max_row_tiny() { return std::min(kTinyR.EC, kTinyD.EC); }
 
+// image 0: Fwd*, 1: Bwd* (reachability, u64 ring), 2: depth (DXD_NE u32 rings);
+// the whole graph in one window when its image fits LDS (ring slots and link
+// offsets are u16)
+void dx_img_configs(uint32_t V, uint32_t E, uint32_t window, DxImg out[3]) {
+  const bool small = window == 0 && V + 64u <= 0xFFFFu && E <= 0xFFFFu;
+  const uint32_t EC = std::max(E, 1u);
+  const bool wr = small && dx_lds_bytes<uint64_t, 1>(V, V, EC) <= DX_LDS_MAX;
+  const bool wd = small && dx_lds_bytes<uint32_t, DXD_NE>(V, V, EC) <= DX_LDS_MAX;
+  const DxCfg r = window == 2 ? kTinyR : kReach, d = window == 2 ? kTinyD : kDepth;
+  for (int k = 0; k < 3; k++) {
+    DxImg &m = out[k];
+    const bool whole = k < 2 ? wr : wd;
+    const DxCfg &g = k < 2 ? r : d;
+    m.W = whole ? V : g.W;
+    m.R = whole ? V : g.R;
+    m.EC = whole ? EC : g.EC;
+    m.whole = whole ? 1u : 0u;
+    m.rev = k == 1 ? 1u : 0u;
+  }
+}
+
 void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
-  const uint32_t V = a.p.V0, E = a.p.E0;
+  const uint32_t V = a.p.V0;
   if (!V || !a.nu) return;
   const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
   launch_zero(a.lpany, (uint64_t)a.nch * 8u, s);
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
   hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  // reachability: the whole graph in one window when its image fits
-  const DxWalkCfg whole = {V, V, std::max(E, 1u), 1};
-  const bool small = a.window == 0 && V < 0xFFFFu && E <= 0xFFFFu;
-  if (small && dx_lds_bytes<uint64_t, 1>(V, V, whole.EC, true) <= DX_LDS_MAX)
-    walk_launch<0, 1, true, DXR_NT, 8>(c, a, whole, dim3(a.nch, 2), s);
+  if (a.img[0].whole)
+    walk_launch<0, 1, true, DXR_NT>(c, a, a.img[0], a.img[1], dim3(a.nch, 2), s);
   else
-    walk_launch<0, 1, false, DXR_NT, 2>(c, a, a.window == 2 ? kTinyR : kReach, dim3(a.nch, 2), s);
+    walk_launch<0, 1, false, DXR_NT>(c, a, a.img[0], a.img[1], dim3(a.nch, 2), s);
   hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  if (small && dx_lds_bytes<uint32_t, 4>(V, V, whole.EC, true) <= DX_LDS_MAX)
-    walk_launch<2, 4, true, DXD_NT, 8>(c, a, whole, dim3((a.nu + 3) / 4), s);
+  const dim3 gd((a.nu + DXD_NE - 1) / DXD_NE);
+  if (a.img[2].whole)
+    walk_launch<2, DXD_NE, true, DXD_NT>(c, a, a.img[2], a.img[2], gd, s);
   else
-    walk_launch<2, 4, false, DXD_NT, 2>(c, a, a.window == 2 ? kTinyD : kDepth, dim3((a.nu + 3) / 4), s);
+    walk_launch<2, DXD_NE, false, DXD_NT>(c, a, a.img[2], a.img[2], gd, s);
   if (a.n_entries)
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }
