@@ -95,7 +95,7 @@ struct nemo_ctx {
   // the multi-entry diff (k_dx.hip): g0's Kahn-order relayout, built with the
   // CSR in every load / rebuild, and the per-call buffers (grow-only)
   nemo::DxPrep dxp{};
-  nemo::DxImg dx_img[3]{};           // walk images of g0 (k_dx.hip), built for the test knob dx_img_key
+  nemo::DxImg dx_img[2]{};           // walk images of g0 (k_dx.hip), built for the test knob dx_img_key
   nemo::DxImgScratch dx_its{};
   int dx_img_key = -1;               // -1: not built for the current load
   bool dx_ok = false;                // relayout allocated: run 0 present, every row fits a window
@@ -732,7 +732,7 @@ static int device_load(nemo_ctx *c) {
       return rc;
     // the walk images for the default windows (read rows and Kahn levels, write records and misses)
     nemo::dx_img_configs(c->dxp.V0, c->dxp.E0, 0, c->dx_img);
-    if ((rc = timed(c, "k_dximg", 3 * (16 * E0 + 24 * V0), 0,
+    if ((rc = timed(c, "k_dximg", 2 * (16 * E0 + 32 * V0), 0,
                     [&] { nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, c->stream); })))
       return rc;
     c->dx_img_key = 0;
@@ -1045,12 +1045,13 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
           (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))
         return rc;
       for (nemo::DxImg &m : c->dx_img)
-        if ((rc = dalloc(c, &m.nw, 1)) || (rc = dalloc(c, &m.wb, nv + 2)) || (rc = dalloc(c, &m.segb, nv + 2)) ||
-            (rc = dalloc(c, &m.missb, nv + 2)) || (rc = dalloc(c, &m.segs, 2 * nv + 2)) ||
-            (rc = dalloc(c, &m.rec, ne + 4)) || (rc = dalloc(c, &m.miss, ne + 1)))
+        if ((rc = dalloc(c, &m.nw, 1)) || (rc = dalloc(c, &m.wb, nv + 2)) || (rc = dalloc(c, &m.stepb, nv + 2)) ||
+            (rc = dalloc(c, &m.steps, 2 * nv + ne / 256 + 4)) || (rc = dalloc(c, &m.rec, ne + 4)) ||
+            (rc = dalloc(c, &m.moff, nv + 1)) || (rc = dalloc(c, &m.mx, ne + 1)))
           return rc;
       nemo::DxImgScratch &t = c->dx_its;
-      if ((rc = dalloc(c, &t.fseg, nv + 1)) || (rc = dalloc(c, &t.fmiss, nv + 1)) ||
+      if ((rc = dalloc(c, &t.fseg, nv + 1)) || (rc = dalloc(c, &t.segpos, nv + 2)) ||
+          (rc = dalloc(c, &t.fstep, nv + 1)) ||
           (rc = dalloc(c, &t.tsum, nemo::dx_scan_tiles((uint32_t)std::max(nv, ne) + 1))))
         return rc;
     }
@@ -1439,7 +1440,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
       nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, s);
       c->dx_img_key = (int)c->diff_window;
     }
-    for (int k = 0; k < 3; k++) a.img[k] = c->dx_img[k];
+    for (int k = 0; k < 2; k++) a.img[k] = c->dx_img[k];
     rc = timed_on(c, s, "k_diff", bytes, (double)nu * 3 * E0, [&] { nemo::launch_dx(c->dc, a, s); });
   } else {
     nemo::DiffArgs a;

@@ -47,21 +47,26 @@ struct DxPrep {
 
 // A walk image of g0 (k_dx.hip k_dxi_*, built once per load and window
 // configuration): the walk order cut into windows, and per window its links
-// as ring records, its level segments and the links that leave the ring.  The
-// walks stage a window by copying these ranges (no per-window derivation).
+// as ring records, its walk steps (<= 256 links of one level) and, per
+// position, the links that leave the ring.  The walks stage a window by
+// copying these ranges (no per-window derivation).  Image 0: Kahn order over
+// parents (Fwd*, depth), 1: reversed Kahn order over children (Bwd*).
 struct DxImg {
-  uint32_t W, R, EC;         // positions, ring slots (power of two; whole: V0), links per window
+  uint32_t W, R, EC;         // positions, ring slots (power of two, >= 4 W; whole: V0), links per window
   uint32_t whole;            // 1: one window, ring = positions (no misses)
-  uint32_t rev;              // 1: reversed walk order (children rows, Bwd*)
+  uint32_t rev;              // 1: reversed walk order (children rows)
   uint32_t *nw;              // [1] windows
   uint32_t *wb;              // [V0 + 2] first walk index of window k; wb[nw] = V0
-  uint32_t *segb, *missb;    // [V0 + 2] first entry of window k in segs / miss; [nw] = totals
-  uint16_t *segs;            // [2 V0 + 2] level segment starts, as link offsets in the window
+  uint32_t *stepb;           // [V0 + 2] first step of window k; [nw] = total
+  uint32_t *steps;           // [2 V0 + E0 / 256 + 4] first link (in the window) | links << 16
   uint32_t *rec;             // [E0 + 4] per link (walk-order rows): linked ring slot (R: a miss) | owner's slot << 16
-  uint2 *miss;               // [E0 + 1] (linked walk index, owner's slot) of the links older than the ring
+  uint32_t *moff;            // [V0 + 1] first miss of walk index i in mx
+  uint32_t *mx;              // [E0 + 1] walk index linked by each miss
 };
 struct DxImgScratch {
-  uint32_t *fseg, *fmiss;    // [V0 + 1] per position: segment flag / misses -> offsets
+  uint32_t *fseg;            // [V0 + 1] segment flags -> segment numbers
+  uint32_t *segpos;          // [V0 + 2] first walk index of each segment
+  uint32_t *fstep;           // [V0 + 1] steps per segment -> first step
   uint32_t *tsum;            // scan tiles
 };
 
@@ -96,7 +101,7 @@ struct DxArgs {
   uint32_t *missing;         // [2 * cap] (source, rule node)
   uint32_t *n_missing;
   uint32_t window;           // test knob: 0 by size, 1 windowed walks, 2 tiny windows (ring misses)
-  DxImg img[3];              // walk images: Fwd*, Bwd* (reachability), depth
+  DxImg img[2];              // walk images: Kahn order (Fwd*, depth), reversed (Bwd*)
 };
 
 struct PullArgs {
@@ -143,9 +148,9 @@ void launch_dx_prep(const DevCorpus &c, const DxPrep &p, uint32_t *tsum, hipStre
 void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s);
 uint32_t dx_max_row();       // the longest row of g0 the multi-entry diff takes
 uint32_t dx_max_row_tiny();  // the same under the tiny-window test knob
-// window configurations of the three walk images for g0 (V0, E0) under the test knob `window`
-void dx_img_configs(uint32_t V0, uint32_t E0, uint32_t window, DxImg out[3]);
-void launch_dx_img(const DxPrep &p, DxImg img[3], const DxImgScratch &t, hipStream_t s);
+// window configurations of the two walk images for g0 (V0, E0) under the test knob `window`
+void dx_img_configs(uint32_t V0, uint32_t E0, uint32_t window, DxImg out[2]);
+void launch_dx_img(const DxPrep &p, DxImg img[2], const DxImgScratch &t, hipStream_t s);
 uint32_t dx_scan_tiles(uint32_t n);  // tile sums launch_scan needs for n entries
 void launch_scan(uint32_t *a, uint32_t n, uint32_t *tsum, hipStream_t s);  // in-place exclusive scan
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);

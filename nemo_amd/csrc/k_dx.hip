@@ -129,7 +129,7 @@ void launch_dx_prep(const DevCorpus &c, const DxPrep &p, uint32_t *tsum, hipStre
 // windows: greedy in walk order, one workgroup per image; a window ends before
 // W positions or before its links pass EC (every row fits: dx_max_row)
 struct DxImgSet {
-  DxImg m[3];
+  DxImg m[2];
 };
 __global__ __launch_bounds__(1024) void k_dxi_bounds(DxPrep p, DxImgSet set) {
   __shared__ uint32_t s_best[3];
@@ -169,6 +169,13 @@ __device__ __forceinline__ uint32_t dxi_window(const DxImg &m, uint32_t nw, uint
   }
   return lo;
 }
+// A link of window k to walk index x leaves the ring when x + R < end of window
+// k + 1: the walk of window k then never reads a slot that the staging of
+// window k + 1 (running beside it) writes, and with R >= 4 W such an x lies two
+// windows back or more, whose values are in HBM by then.
+__device__ __forceinline__ uint32_t dxi_far_end(const DxImg &m, uint32_t nw, uint32_t k) {
+  return m.wb[min(k + 2u, nw)];
+}
 // per walk index: segment flag (the window's first position or a level's
 // first), links that leave the ring
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_count(DxPrep p, DxImg m, DxImgScratch t) {
@@ -176,57 +183,73 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_count(DxPrep p, DxImg m, DxI
   if (i > V) return;
   if (i == V) {
     t.fseg[V] = 0;
-    t.fmiss[V] = 0;
+    m.moff[V] = 0;
     return;
   }
-  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), w0 = m.wb[k], w1 = m.wb[k + 1];
+  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), w0 = m.wb[k], fe = dxi_far_end(m, nw, k);
   const uint32_t *rowp = m.rev ? p.fp : p.rp, *col = m.rev ? p.fc : p.rc;
   const uint32_t pos = m.rev ? V - 1u - i : i;
   const uint32_t lstart = m.rev ? V - p.lend[pos] : p.lbeg[pos];
   t.fseg[i] = (i == w0 || lstart == i) ? 1u : 0u;
   uint32_t nm = 0;
   if (!m.whole)
-    for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) nm += col[j] + m.R < w1 ? 1u : 0u;
-  t.fmiss[i] = nm;
+    for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) nm += col[j] + m.R < fe ? 1u : 0u;
+  m.moff[i] = nm;
 }
-// per walk index: its segment entry, its links' records and misses; window starts
+// per walk index: its segment's first position, its links' records and misses
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_fill(DxPrep p, DxImg m, DxImgScratch t) {
   const uint32_t V = p.V0, i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
-  if (i >= V) return;
-  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), w0 = m.wb[k], w1 = m.wb[k + 1];
+  if (i >= V) {
+    if (i == V) t.segpos[t.fseg[V]] = V;
+    return;
+  }
+  const uint32_t nw = m.nw[0], k = dxi_window(m, nw, i), fe = dxi_far_end(m, nw, k);
   const uint32_t *rowp = m.rev ? p.fp : p.rp, *col = m.rev ? p.fc : p.rc;
-  const uint32_t base = rowp[w0], sg = t.fseg[i];
-  if (t.fseg[i + 1] != sg) m.segs[sg] = (uint16_t)(rowp[i] - base);
-  if (i == w0) {
-    m.segb[k] = sg;
-    m.missb[k] = t.fmiss[i];
-  }
-  if (i == 0) {
-    m.segb[nw] = t.fseg[V];
-    m.missb[nw] = t.fmiss[V];
-  }
+  if (t.fseg[i + 1] != t.fseg[i]) t.segpos[t.fseg[i]] = i;
   const uint32_t own = (m.whole ? i : (i & (m.R - 1u))) << 16;
-  uint32_t o = t.fmiss[i];
+  uint32_t o = m.moff[i];
   for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) {
     const uint32_t x = col[j];
-    const bool far = !m.whole && x + m.R < w1;
+    const bool far = !m.whole && x + m.R < fe;
     m.rec[j] = (far ? m.R : (m.whole ? x : (x & (m.R - 1u)))) | own;
-    if (far) m.miss[o++] = make_uint2(x, own >> 16);
+    if (far) m.mx[o++] = x;
   }
 }
+// per segment: its walk steps (<= DX_STEP links each; a segment without links has none)
+#define DX_STEP 256u
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_stepcount(DxPrep p, DxImg m, DxImgScratch t) {
+  const uint32_t V = p.V0, sg = blockIdx.x * NEMO_BLOCK + threadIdx.x, ns = t.fseg[V];
+  if (sg > V) return;
+  const uint32_t *rowp = m.rev ? p.fp : p.rp;
+  t.fstep[sg] = sg < ns ? (rowp[t.segpos[sg + 1]] - rowp[t.segpos[sg]] + DX_STEP - 1u) / DX_STEP : 0u;
+}
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_steps(DxPrep p, DxImg m, DxImgScratch t) {
+  const uint32_t V = p.V0, sg = blockIdx.x * NEMO_BLOCK + threadIdx.x, ns = t.fseg[V];
+  if (sg >= ns) return;
+  const uint32_t *rowp = m.rev ? p.fp : p.rp;
+  const uint32_t nw = m.nw[0], a = t.segpos[sg], k = dxi_window(m, nw, a), w0 = m.wb[k];
+  const uint32_t rel = rowp[a] - rowp[w0], cnt = rowp[t.segpos[sg + 1]] - rowp[a];
+  uint32_t o = t.fstep[sg];
+  if (a == w0) m.stepb[k] = o;
+  if (sg == 0) m.stepb[nw] = t.fstep[ns];
+  for (uint32_t r = 0; r * DX_STEP < cnt; r++) m.steps[o++] = (rel + r * DX_STEP) | (min(DX_STEP, cnt - r * DX_STEP) << 16);
+}
 
-void launch_dx_img(const DxPrep &p, DxImg img[3], const DxImgScratch &t, hipStream_t s) {
+void launch_dx_img(const DxPrep &p, DxImg img[2], const DxImgScratch &t, hipStream_t s) {
   const uint32_t V = p.V0;
   if (!V) return;
   DxImgSet set;
-  for (int k = 0; k < 3; k++) set.m[k] = img[k];
-  hipLaunchKernelGGL(k_dxi_bounds, dim3(3), dim3(1024), 0, s, p, set);
+  for (int k = 0; k < 2; k++) set.m[k] = img[k];
+  hipLaunchKernelGGL(k_dxi_bounds, dim3(2), dim3(1024), 0, s, p, set);
   const uint32_t nb = (V + 1 + NEMO_BLOCK - 1) / NEMO_BLOCK;
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < 2; k++) {
     hipLaunchKernelGGL(k_dxi_count, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
     launch_scan(t.fseg, V + 1, t.tsum, s);
-    launch_scan(t.fmiss, V + 1, t.tsum, s);
+    launch_scan(img[k].moff, V + 1, t.tsum, s);
     hipLaunchKernelGGL(k_dxi_fill, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
+    hipLaunchKernelGGL(k_dxi_stepcount, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
+    launch_scan(t.fstep, V + 1, t.tsum, s);
+    hipLaunchKernelGGL(k_dxi_steps, dim3(nb), dim3(NEMO_BLOCK), 0, s, p, img[k], t);
   }
 }
 
@@ -364,46 +387,57 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 //         blockIdx.y = 0: Fwd* over parents in Kahn order (image m0), 1: Bwd*
 //         over children in reversed Kahn order (image m1).  value = Good | OR(links).
 // MODE 2: depth, T = u32, NE walkers (sources NE·blockIdx.x + e), Kahn order
-//         over parents: s = D ? 1 + max(s of links) : 0 (depth + 1 of D nodes;
-//         a non-D parent has s = 0, so the max runs over D parents).  While a
-//         window is walked a ring slot holds DX_NOTD (not in D: absorbs every
-//         max) or DX_IND | r, r = the max so far; s = r + 1.
+//         over parents (image m0): s = D ? 1 + max(s of links) : 0 (depth + 1
+//         of D nodes; a non-D parent has s = 0, so the max runs over D
+//         parents).  While a window is walked a ring slot holds DX_NOTD (not in
+//         D: absorbs every max) or DX_IND | r, r = the max so far; s = r + 1.
 // WHOLE: the graph is one window (ring = positions, no wrap, no misses).
 //
-// A window (the image's ranges): staging (all waves: the link records and
-// level segments copied to LDS, every position's init value into its ring
-// slot, the links that leave the ring read from HBM and folded into their
-// owners' slots) -> the walk (waves e < NE) -> finalize (all waves: values to
-// HBM, LP maxima).  The walk of a level is one pass over its links, lanes over
-// links: read the linked value, apply it to the owner's slot with an LDS
-// atomic; a level only reads slots of earlier levels, and a wave's LDS
-// operations complete in order, so no barrier separates the levels.
+// Windows are pipelined: while the walker waves walk window k, the other
+// ("worker") waves finalize window k - 1 (values to HBM, LP maxima) and stage
+// window k + 1 (its link records and steps copied from the image into the
+// other LDS buffer, every position's init value, with the values of its links
+// that leave the ring folded in from HBM, into its ring slot); one barrier
+// per window.  The image's ring misses make this safe (dxi_far_end).
+//
+// A walk step is <= 256 links of one level, lanes over links: read the linked
+// values, apply them to the owners' slots with LDS atomics.  A step only reads
+// slots of earlier levels and a wave's LDS operations complete in order, so
+// no barrier separates steps; the next step's records are read during the
+// step before, and step descriptors come 64 at a time (one LDS read per 64
+// steps), so a step costs one LDS round trip.
 #define DX_NOTD 0xFFFFFFFFu
 #define DX_IND 0x80000000u
 template <typename T, int NE>
 struct DxLds {
   T *ring0;          // NE rings of [R + 1 + 64] (stride rs): [R] the identity (sink), [R + 1 + lane] dump slots
   uint32_t rs;
-  uint32_t *lk;      // [EC] link records: ring slot of the linked position (R: none) | owner's slot << 16
-  uint16_t *seg;     // [W + 2] first link of each level segment (relative); seg[nseg] = links
-  uint32_t *lpb;     // [NE][W / 32 + 2] depth: LP rules of the window, one bit per position
+  uint32_t *lk;      // [NB][EC] link records of a window
+  uint32_t *st;      // [NB][SC] its steps
+  uint32_t *lpb;     // [NL][NE][LW] depth: LP rules of a window, one bit per position
+  uint32_t SC, LW;
 };
+__host__ __device__ inline uint32_t dx_sc(uint32_t W, uint32_t EC) { return W + EC / DX_STEP + 2u; }
 template <typename T, int NE>
-__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC) {
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + lds_align(4u * EC) + lds_align(2u * (W + 2u)) +
-         NE * lds_align(4u * (W / 32u + 2u));
+__host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC, bool whole) {
+  const uint32_t NB = whole ? 1u : 2u, NL = whole ? 1u : 3u;
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * lds_align(4u * dx_sc(W, EC)) +
+         NL * NE * lds_align(4u * (W / 32u + 2u));
 }
 template <typename T, int NE>
-__device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC) {
+__device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC, bool whole) {
+  const uint32_t NB = whole ? 1u : 2u;
   uint8_t *p = (uint8_t *)base;
   DxLds<T, NE> L;
   L.ring0 = (T *)p;
   L.rs = lds_align((uint32_t)sizeof(T) * (R + 65u)) / (uint32_t)sizeof(T);
   p += NE * lds_align((uint32_t)sizeof(T) * (R + 65u));
   L.lk = (uint32_t *)p;
-  p += lds_align(4u * EC);
-  L.seg = (uint16_t *)p;
-  p += lds_align(2u * (W + 2u));
+  p += NB * lds_align(4u * EC);
+  L.SC = lds_align(4u * dx_sc(W, EC)) / 4u;
+  L.st = (uint32_t *)p;
+  p += NB * 4u * L.SC;
+  L.LW = lds_align(4u * (W / 32u + 2u)) / 4u;
   L.lpb = (uint32_t *)p;
   return L;
 }
@@ -413,12 +447,13 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint32_t s_lmax[NE], s_lpn[NE];
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool rev = MODE == 0 && blockIdx.y == 1;
   const DxImg m = rev ? m1 : m0;
-  const uint32_t V = a.p.V0, W = m.W, R = m.R, EC = m.EC, LW = W / 32u + 2u;
+  const uint32_t V = a.p.V0, W = m.W, R = m.R, EC = m.EC;
   const uint32_t chunk = MODE == 0 ? blockIdx.x : 0u;
-  DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC);
+  DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC, WHOLE);
+  const uint32_t LW = L.LW;
   const uint32_t *rowp = rev ? a.p.fp : a.p.rp;
   // per walker e: its source (depth), ring and value array, computed from e (a
   // dynamically indexed register array would live in scratch memory)
@@ -433,10 +468,6 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
     return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
   };
   auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
-  auto apply_miss = [&](uint32_t e, uint32_t osl, T val) {
-    if (MODE == 0) atomicOr((unsigned long long *)&ringp(e)[osl], (unsigned long long)val);
-    else atomicMax((uint32_t *)&ringp(e)[osl], DX_IND | (uint32_t)val);
-  };
   bool any = MODE == 0;
   for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
   if (!any) return;  // workgroup-uniform
@@ -448,9 +479,146 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
   uint32_t lmax[NE];
 #pragma unroll
   for (int e = 0; e < NE; e++) lmax[e] = 0;
+
+  // ---- staging of window kw by threads [wt0, wt0 + nwt) (whole waves) ----
+  auto stage = [&](uint32_t kw, uint32_t buf, uint32_t lb, uint32_t wt, uint32_t nwt) {
+    const uint32_t w0 = m.wb[kw], w1 = m.wb[kw + 1], n = w1 - w0;
+    const uint32_t base = rowp[w0], ne = rowp[w1] - base;
+    const uint32_t st0 = m.stepb[kw], nst = m.stepb[kw + 1] - st0;
+    uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * L.SC, *lpb = L.lpb + lb * NE * LW;
+    // records, in 16-B chunks of the image
+    const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
+    for (uint32_t cb = c0; cb < c1; cb += 2 * nwt) {
+      uint4 v4[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t ck = cb + q * nwt + wt;
+        v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(m.rec)[ck] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t ck = cb + q * nwt + wt;
+        const uint32_t qs[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t j = 4 * ck + b;
+          if (ck < c1 && j >= base && j < base + ne) lk[j - base] = qs[b];
+        }
+      }
+    }
+    for (uint32_t t = wt; t < nst; t += nwt) st[t] = m.steps[st0 + t];
+    // init values with the misses folded in; depth: the LP bits of 64
+    // consecutive positions by ballot
+    for (uint32_t k0 = 0; k0 < n; k0 += nwt) {
+      const uint32_t kk = k0 + wt;
+      const bool in = kk < n;
+      const uint32_t i = w0 + (in ? kk : 0u), pos = rev ? V - 1u - i : i;
+      const uint32_t mo0 = !WHOLE && in ? m.moff[i] : 0u, mo1 = !WHOLE && in ? m.moff[i + 1] : 0u;
+      if (MODE == 0) {
+        T v = in ? (T)a.gw[(size_t)chunk * V + pos] : (T)0;
+        for (uint32_t mm = mo0; mm < mo1; mm++)
+          v |= __hip_atomic_load(gvalp(0) + m.mx[mm], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (in) ringp(0)[slot(i)] = v;
+      } else {
+        const bool rule = in && (a.p.info[pos] & DXI_RULE);
+        const uint64_t dv = in ? a.dw[(size_t)((blockIdx.x * NE) >> 6) * V + pos] : 0ull;
+        const uint64_t lv = rule ? a.lw[(size_t)((blockIdx.x * NE) >> 6) * V + pos] : 0ull;
+        uint32_t r[NE];
+#pragma unroll
+        for (int e = 0; e < NE; e++) r[e] = 0;
+        for (uint32_t mm = mo0; mm < mo1; mm++) {
+          const uint32_t x = m.mx[mm];
+#pragma unroll
+          for (int e = 0; e < NE; e++)
+            if (srcu(e) != NEMO_NONE)
+              r[e] = max(r[e], __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+          const uint32_t u = srcu(e), b = (blockIdx.x * NE + e) & 63u;
+          const bool d = u != NEMO_NONE && ((dv >> b) & 1ull);
+          if (in) ringp(e)[slot(i)] = d ? (DX_IND | r[e]) : DX_NOTD;
+          const uint64_t lpm = __ballot(u != NEMO_NONE && rule && ((lv >> b) & 1ull));
+          const uint32_t wd = (k0 + (wt & ~63u)) >> 5;
+          if (lane < 2u && wd + lane < LW) lpb[e * LW + wd + lane] = (uint32_t)(lpm >> (32u * lane));
+        }
+      }
+    }
+  };
+  // ---- finalize of window kw: values to HBM; depth: s, the LP maxima, the LP list ----
+  auto finalize = [&](uint32_t kw, uint32_t lb, uint32_t wt, uint32_t nwt) {
+    const uint32_t w0 = m.wb[kw], n = m.wb[kw + 1] - w0;
+    const uint32_t *lpb = L.lpb + lb * NE * LW;
+    for (uint32_t kk = wt; kk < n; kk += nwt) {
+      const uint32_t i = w0 + kk, sl = slot(i);
+      if (MODE == 0) {
+        gvalp(0)[i] = ringp(0)[sl];
+      } else {
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+          const uint32_t u = srcu(e);
+          if (u == NEMO_NONE) continue;
+          const uint32_t r = (uint32_t)ringp(e)[sl];
+          const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
+          gvalp(e)[i] = (T)sv;
+          if ((lpb[e * LW + (kk >> 5)] >> (kk & 31u)) & 1u) {
+            lmax[e] = max(lmax[e], sv);
+            if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
+          }
+        }
+      }
+    }
+  };
+  // ---- the walk of window kw by wave e ----
+  auto walk = [&](uint32_t kw, uint32_t buf, uint32_t e) {
+    const uint32_t nst = __builtin_amdgcn_readfirstlane(m.stepb[kw + 1] - m.stepb[kw]);
+    const uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * L.SC;
+    T *ring = ringp(e);
+    const uint32_t idle = R | ((R + 1u + lane) << 16);
+    auto apply = [&](uint32_t rec, T x) {
+      if (MODE == 0) {
+        atomicOr((unsigned long long *)&ring[rec >> 16], (unsigned long long)x);
+      } else {
+        const uint32_t sv = (uint32_t)x == DX_NOTD ? 0u : ((uint32_t)x & ~DX_IND) + 1u;
+        atomicMax((uint32_t *)&ring[rec >> 16], DX_IND | sv);
+      }
+    };
+    if (!nst) return;
+    // step descriptors 64 at a time (one LDS read per 64 steps, read a batch ahead)
+    uint32_t bat = lane < nst ? st[lane] : 0u;
+    const uint32_t d = __builtin_amdgcn_readlane(bat, 0);
+    uint32_t rc[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) rc[q] = 64u * q + lane < (d >> 16) ? lk[(d & 0xFFFFu) + 64u * q + lane] : idle;
+    // nothing in flight at the loop entry (the compiler's wait counting sees
+    // this wait): a step then waits only for its own reads
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    for (uint32_t b0 = 0; b0 < nst; b0 += 64u) {
+      const uint32_t nbat = b0 + 64u + lane < nst ? st[b0 + 64u + lane] : 0u;
+      const uint32_t ns = min(64u, nst - b0);
+      for (uint32_t s = 0; s < ns; s++) {
+        T x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
+        // the next step's records (0 past the last step)
+        const uint32_t d1 = s + 1u < 64u ? __builtin_amdgcn_readlane(bat, s + 1u) : __builtin_amdgcn_readlane(nbat, 0);
+        uint32_t rn[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) rn[q] = 64u * q + lane < (d1 >> 16) ? lk[(d1 & 0xFFFFu) + 64u * q + lane] : idle;
+#pragma unroll
+        for (int q = 0; q < 4; q++) apply(rc[q], x[q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) rc[q] = rn[q];
+      }
+      bat = nbat;
+    }
+  };
+  const bool walker = wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE);
+  const bool worker = wv >= (uint32_t)NE;
+  const uint32_t wt = tid - NE * 64u, nwt = NT - NE * 64u;
 #ifdef NEMO_STAMPS
-  // diagnostic build: per-workgroup ticks of each phase (wave 0's view), reach at
-  // 16 wg + 0..7, depth at 16 wg + 8..15: S1, S2, S3, walk, finalize, rows, windows, total
+  // diagnostic build: per-workgroup ticks (wave 0's view), reach at 16 wg + 0..7,
+  // depth at 16 wg + 8..15: first staging, -, -, walk, wait for the workers, rows, windows, total
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tk0, tk1, tstart;
 #define DXT(k)          \
   do {                  \
@@ -466,194 +634,36 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
   } while (0)
 #endif
   const uint32_t nw = m.nw[0];
-  for (uint32_t k = 0; k < nw; k++) {
-    const uint32_t w0 = m.wb[k], w1 = m.wb[k + 1], n = w1 - w0;
-    const uint32_t base = rowp[w0], ne = rowp[w1] - base;
-    const uint32_t sg0 = m.segb[k], nseg = m.segb[k + 1] - sg0;
-    const uint32_t ms0 = m.missb[k], nm = m.missb[k + 1] - ms0;
-    // ---- staging: records (16-B chunks of the image), level segments, init
-    // values, and the first round of misses loaded (entry, then value) ----
-    {
-      const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
-      for (uint32_t cb = c0; cb < c1; cb += 2 * NT) {
-        uint4 v4[2];
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-          const uint32_t ck = cb + q * NT + tid;
-          v4[q] = ck < c1 ? reinterpret_cast<const uint4 *>(m.rec)[ck] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-          const uint32_t ck = cb + q * NT + tid;
-          const uint32_t qs[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const uint32_t j = 4 * ck + b;
-            if (ck < c1 && j >= base && j < base + ne) L.lk[j - base] = qs[b];
-          }
-        }
-      }
-    }
-    for (uint32_t t = tid; t < nseg; t += NT) L.seg[t] = m.segs[sg0 + t];
-    if (tid == 0) L.seg[nseg] = (uint16_t)ne;
-    // init values; depth: the LP bits of 64 consecutive positions by ballot
-    for (uint32_t k0 = 0; k0 < n; k0 += NT) {
-      const uint32_t kk = k0 + tid;
-      const bool in = kk < n;
-      const uint32_t i = w0 + (in ? kk : 0u), pos = rev ? V - 1u - i : i;
-      if (MODE == 0) {
-        if (in) ringp(0)[slot(i)] = (T)a.gw[(size_t)chunk * V + pos];
-      } else {
-        const bool rule = in && (a.p.info[pos] & DXI_RULE);
-#pragma unroll
-        for (int e = 0; e < NE; e++) {
-          const uint32_t u = srcu(e), b = u & 63u;
-          const uint64_t dv = u != NEMO_NONE && in ? a.dw[(size_t)(u >> 6) * V + pos] : 0ull;
-          const uint64_t lv = u != NEMO_NONE && rule ? a.lw[(size_t)(u >> 6) * V + pos] : 0ull;
-          if (in) ringp(e)[slot(i)] = (T)(((dv >> b) & 1ull) ? DX_IND : DX_NOTD);
-          const uint64_t lb = __ballot(rule && ((lv >> b) & 1ull));
-          if (lane < 2u && ((k0 + wv * 64u) >> 5) + lane < LW)
-            L.lpb[e * LW + ((k0 + wv * 64u) >> 5) + lane] = (uint32_t)(lb >> (32u * lane));
-        }
-      }
-    }
-    constexpr int MB = 4;  // misses per thread per round
-    uint2 mr[MB];
-    T mv[MB][NE];
-    auto load_miss = [&](uint32_t r0) {
-#pragma unroll
-      for (int q = 0; q < MB; q++) {
-        const uint32_t mm = r0 + q * NT + tid;
-        mr[q] = mm < nm ? m.miss[ms0 + mm] : make_uint2(0, R + 1u + lane);
-      }
-#pragma unroll
-      for (int q = 0; q < MB; q++)
-#pragma unroll
-        for (int e = 0; e < NE; e++)
-          mv[q][e] = r0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)
-                         ? __hip_atomic_load(gvalp(e) + mr[q].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : (T)0;
-    };
-    auto apply_misses = [&](uint32_t r0) {
-#pragma unroll
-      for (int q = 0; q < MB; q++)
-#pragma unroll
-        for (int e = 0; e < NE; e++)
-          if (r0 + q * NT + tid < nm && (MODE == 0 || srcu(e) != NEMO_NONE)) apply_miss(e, mr[q].y, mv[q][e]);
-    };
-    if (!WHOLE && nm) load_miss(0);
-    __syncthreads();  // init values are in place before misses fold into them
-    if (!WHOLE && nm) {
-      apply_misses(0);
-      for (uint32_t r0 = MB * NT; r0 < nm; r0 += MB * NT) {
-        load_miss(r0);
-        apply_misses(r0);
-      }
-      __syncthreads();
-    }
-    DXT(1);
-    // ---- the walk: wave e < NE walks source e through the window's level
-    // segments, lanes over a segment's links.  No barrier or fence between
-    // levels: a level reads only slots of earlier levels, and a wave's LDS
-    // operations complete in issue order.  A level's first 256 link records
-    // are read during the level before (they do not depend on it), so a level
-    // costs one LDS round trip: read the linked values, apply them.  Idle
-    // lanes read the sink and apply to a dump slot of their own (no branches,
-    // no two lanes on one slot) ----
-    if (wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE)) {
-      T *ring = ringp(wv);
-      const uint32_t idle = R | ((R + 1u + lane) << 16);
-      auto apply = [&](uint32_t rec, T x) {
-        if (MODE == 0) {
-          atomicOr((unsigned long long *)&ring[rec >> 16], (unsigned long long)x);
-        } else {
-          const uint32_t sv = (uint32_t)x == DX_NOTD ? 0u : ((uint32_t)x & ~DX_IND) + 1u;
-          atomicMax((uint32_t *)&ring[rec >> 16], DX_IND | sv);
-        }
-      };
-      // level t: links [lo, hi); hn = the end of level t + 1
-      uint32_t lo = 0, hi = 0, hn = 0;
-      if (nseg) {
-        lo = L.seg[0];
-        hi = L.seg[1];
-        hn = L.seg[min(2u, nseg)];
-      }
-      uint32_t rc[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t j = lo + 64u * q + lane;
-        rc[q] = j < hi ? L.lk[j] : idle;
-      }
-      lo = __builtin_amdgcn_readfirstlane(lo);
-      hi = __builtin_amdgcn_readfirstlane(hi);
-      hn = __builtin_amdgcn_readfirstlane(hn);
-      for (uint32_t t = 0; t < nseg; t++) {
-        T x[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
-        // the next level's first records and the end of the level after it
-        uint32_t rn[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t j = hi + 64u * q + lane;
-          rn[q] = j < hn ? L.lk[j] : idle;
-        }
-        const uint32_t hnn = L.seg[min(t + 3u, nseg)];
-#pragma unroll
-        for (int q = 0; q < 4; q++) apply(rc[q], x[q]);
-        // links past the first 256 of the level (wide levels): 512 per step
-        for (uint32_t j0 = lo + 256u; j0 < hi; j0 += 512u) {
-          uint32_t r2[8];
-          T x2[8];
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            const uint32_t j = j0 + 64u * q + lane;
-            r2[q] = j < hi ? L.lk[j] : idle;
-          }
-#pragma unroll
-          for (int q = 0; q < 8; q++) x2[q] = ring[r2[q] & 0xFFFFu];
-#pragma unroll
-          for (int q = 0; q < 8; q++) apply(r2[q], x2[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) rc[q] = rn[q];
-        lo = hi;
-        hi = hn;
-        hn = __builtin_amdgcn_readfirstlane(hnn);
-      }
-    }
+  stage(0, 0, 0, tid, NT);
+  __syncthreads();
+  DXT(0);
+  if (WHOLE) {
+    if (walker) walk(0, 0, wv);
     DXT(3);
     __syncthreads();
-    // ---- finalize: the window's values to HBM; depth: s, the LP maxima, the LP list ----
-    for (uint32_t kk = tid; kk < n; kk += NT) {
-      const uint32_t i = w0 + kk, sl = slot(i);
-      if (MODE == 0) {
-        gvalp(0)[i] = ringp(0)[sl];
-      } else {
-#pragma unroll
-        for (int e = 0; e < NE; e++) {
-          const uint32_t u = srcu(e);
-          if (u == NEMO_NONE) continue;
-          const uint32_t r = (uint32_t)ringp(e)[sl];
-          const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
-          gvalp(e)[i] = (T)sv;
-          if ((L.lpb[e * LW + (kk >> 5)] >> (kk & 31u)) & 1u) {
-            lmax[e] = max(lmax[e], sv);
-            if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
-          }
-        }
-      }
-    }
-    // the values have reached this XCD's L2 before a later window's staging (or
-    // the rows pass) reads them back with L2-served loads, in this workgroup (a
-    // workgroup-scope release fence waits for nothing here, an agent-scope one
-    // writes the whole L2 back: the stores' completion is all that is needed)
-    if (!WHOLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    finalize(0, 0, tid, NT);
     __syncthreads();
-    DXT(4);
+  } else {
+    for (uint32_t k = 0; k < nw; k++) {
+      if (walker) {
+        walk(k, k & 1u, wv);
+      } else if (worker) {
+        if (k > 0) finalize(k - 1, (k - 1) % 3u, wt, nwt);
+        if (k + 1 < nw) stage(k + 1, (k + 1) & 1u, (k + 1) % 3u, wt, nwt);
+        // finalized values reach this XCD's L2 before a later staging reads them
+        // back with L2-served loads (the stores' completion is all that is needed)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      DXT(3);
+      __syncthreads();
+      DXT(4);
 #ifdef NEMO_STAMPS
-    acc[6]++;
+      acc[6]++;
 #endif
+    }
+    finalize(nw - 1, (nw - 1) % 3u, tid, NT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 #ifdef NEMO_STAMPS
   const uint32_t stw = 16u * (MODE == 0 ? blockIdx.x * 2u + blockIdx.y : blockIdx.x) + (MODE == 0 ? 0u : 8u);
@@ -780,52 +790,47 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
 
 // ---- launch -----------------------------------------------------------------------------
 template <int MODE, int NE, bool WHOLE, int NT>
-static void walk_launch(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1, dim3 grid,
-                        hipStream_t s) {
+static void walk_launch(const DevCorpus &c, const DxArgs &a, dim3 grid, hipStream_t s) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  const uint32_t bytes = dx_lds_bytes<T, NE>(m0.W, m0.R, m0.EC);
+  const DxImg &m = a.img[0];
+  const uint32_t bytes = dx_lds_bytes<T, NE>(m.W, m.R, m.EC, WHOLE);
   hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)bytes);
-  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, m0, m1);
+  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, a.img[0], a.img[1]);
 }
 
 #define DX_LDS_MAX (160u * 1024u - 1024u)
-// windowed configurations: W positions, R ring slots (power of two, >= 2 W), EC links
-// reachability: 1024 threads, one walker; depth: 512 threads, 4 walkers
-#define DXR_NT 1024
-#define DXD_NT 512
-#define DXD_NE 4
+// windowed configurations: W positions, R ring slots (power of two, >= 4 W), EC links.
+// Both walks: 1024 threads; reachability one walker (u64 ring), depth two (u32 rings),
+// so that their LDS images match and share the window configuration
+#define DX_NT 1024
+#define DXD_NE 2
 struct DxCfg {
   uint32_t W, R, EC;
 };
-static const DxCfg kReach = {2048, 8192, 12288};
-static const DxCfg kDepth = {1024, 4096, 6144};
-// test knob (window = 2): windows of the same size, rings barely larger, so most links leave them
-static const DxCfg kTinyR = {2048, 4096, 12288};
-static const DxCfg kTinyD = {1024, 2048, 6144};
+static const DxCfg kWin = {2048, 8192, 8192};
+// test knob (window = 2): small windows and rings, so that many links leave them
+static const DxCfg kTiny = {512, 2048, 8192};
 
 // every row of g0 must fit one window's links (launch_dx's windowed configurations)
-uint32_t dx_max_row() { return std::min(kReach.EC, kDepth.EC); }
-uint32_t dx_max_row_tiny() { return std::min(kTinyR.EC, kTinyD.EC); }
+uint32_t dx_max_row() { return kWin.EC; }
+uint32_t dx_max_row_tiny() { return kTiny.EC; }
 
-// image 0: Fwd*, 1: Bwd* (reachability, u64 ring), 2: depth (DXD_NE u32 rings);
-// the whole graph in one window when its image fits LDS (ring slots and link
-// offsets are u16)
-void dx_img_configs(uint32_t V, uint32_t E, uint32_t window, DxImg out[3]) {
+// image 0: Kahn order (Fwd*, depth), 1: reversed (Bwd*); the whole graph in one
+// window when its image fits LDS (ring slots and link offsets are u16)
+void dx_img_configs(uint32_t V, uint32_t E, uint32_t window, DxImg out[2]) {
   const bool small = window == 0 && V + 64u <= 0xFFFFu && E <= 0xFFFFu;
   const uint32_t EC = std::max(E, 1u);
-  const bool wr = small && dx_lds_bytes<uint64_t, 1>(V, V, EC) <= DX_LDS_MAX;
-  const bool wd = small && dx_lds_bytes<uint32_t, DXD_NE>(V, V, EC) <= DX_LDS_MAX;
-  const DxCfg r = window == 2 ? kTinyR : kReach, d = window == 2 ? kTinyD : kDepth;
-  for (int k = 0; k < 3; k++) {
+  const bool whole = small && dx_lds_bytes<uint64_t, 1>(V, V, EC, true) <= DX_LDS_MAX &&
+                     dx_lds_bytes<uint32_t, DXD_NE>(V, V, EC, true) <= DX_LDS_MAX;
+  const DxCfg g = window == 2 ? kTiny : kWin;
+  for (int k = 0; k < 2; k++) {
     DxImg &m = out[k];
-    const bool whole = k < 2 ? wr : wd;
-    const DxCfg &g = k < 2 ? r : d;
     m.W = whole ? V : g.W;
     m.R = whole ? V : g.R;
     m.EC = whole ? EC : g.EC;
     m.whole = whole ? 1u : 0u;
-    m.rev = k == 1 ? 1u : 0u;
+    m.rev = (uint32_t)k;
   }
 }
 
@@ -837,17 +842,13 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   launch_zero(a.lpany, (uint64_t)a.nch * 8u, s);
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
   hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  if (a.img[0].whole)
-    walk_launch<0, 1, true, DXR_NT>(c, a, a.img[0], a.img[1], dim3(a.nch, 2), s);
-  else
-    walk_launch<0, 1, false, DXR_NT>(c, a, a.img[0], a.img[1], dim3(a.nch, 2), s);
+  if (a.img[0].whole) walk_launch<0, 1, true, DX_NT>(c, a, dim3(a.nch, 2), s);
+  else walk_launch<0, 1, false, DX_NT>(c, a, dim3(a.nch, 2), s);
   hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   const dim3 gd((a.nu + DXD_NE - 1) / DXD_NE);
-  if (a.img[2].whole)
-    walk_launch<2, DXD_NE, true, DXD_NT>(c, a, a.img[2], a.img[2], gd, s);
-  else
-    walk_launch<2, DXD_NE, false, DXD_NT>(c, a, a.img[2], a.img[2], gd, s);
+  if (a.img[0].whole) walk_launch<2, DXD_NE, true, DX_NT>(c, a, gd, s);
+  else walk_launch<2, DXD_NE, false, DX_NT>(c, a, gd, s);
   if (a.n_entries)
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }

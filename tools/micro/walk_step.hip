@@ -5,6 +5,9 @@
 //           atomic OR into the owners' slots (k_dx_walk's step)
 //   mode 1: position-parallel: each lane owns a position, ORs the values of its
 //           (up to 4) linked slots into its own value and writes it (gather)
+//   mode 2: as mode 0 with u32 values (ds_or_b32)
+//   mode 3: as mode 0 with plain stores instead of atomics (cost reference only)
+//   mode 4: as mode 0 with owners in runs of 4 consecutive lanes (rows of 4 links)
 //   hipcc -O3 --offload-arch=gfx950 -o tools/micro/bin/walk_step tools/micro/walk_step.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -29,7 +32,45 @@ __global__ __launch_bounds__(256) void k(unsigned long long *out, int mode, int 
   unsigned long long t0, t1;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
   if (tid < 64) {
-    if (mode == 0) {
+    if (mode == 2) {
+      unsigned *r32 = (unsigned *)ring;
+      unsigned rc[4];
+      for (int q = 0; q < 4; q++) rc[q] = q < groups ? rec[64 * q + lane] : (RING | ((RING + 1 + lane) << 16));
+      for (int s = 0; s < steps; s++) {
+        unsigned x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = r32[rc[q] & 0xFFFFu];
+        unsigned rn[4];
+        const unsigned b = ((s + 1) * 256u) & (NREC - 1u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) rn[q] = q < groups ? rec[b + 64 * q + lane] : (RING | ((RING + 1 + lane) << 16));
+#pragma unroll
+        for (int q = 0; q < 4; q++) atomicOr(&r32[rc[q] >> 16], x[q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) rc[q] = rn[q];
+        asm volatile("" ::: "memory");
+      }
+    } else if (mode == 3 || mode == 4) {
+      unsigned rc[4];
+      for (int q = 0; q < 4; q++) rc[q] = q < groups ? rec[64 * q + lane] : (RING | ((RING + 1 + lane) << 16));
+      for (int s = 0; s < steps; s++) {
+        unsigned long long x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = ring[rc[q] & 0xFFFFu];
+        unsigned rn[4];
+        const unsigned b = ((s + 1) * 256u) & (NREC - 1u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) rn[q] = q < groups ? rec[b + 64 * q + lane] : (RING | ((RING + 1 + lane) << 16));
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (mode == 3) ring[rc[q] >> 16] = x[q];
+          else atomicOr(&ring[64u + ((s * 64u + 16u * q + (lane >> 2)) & 2047u)], x[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) rc[q] = rn[q];
+        asm volatile("" ::: "memory");
+      }
+    } else if (mode == 0) {
       unsigned rc[4];
       for (int q = 0; q < 4; q++) rc[q] = q < groups ? rec[64 * q + lane] : (RING | ((RING + 1 + lane) << 16));
       for (int s = 0; s < steps; s++) {
@@ -68,8 +109,8 @@ int main() {
   unsigned long long *d, h[8];
   (void)hipMalloc(&d, sizeof(h));
   const int steps = 20000;
-  for (int mode = 0; mode < 2; mode++)
-    for (int g = 1; g <= (mode == 0 ? 4 : 1); g++) {
+  for (int mode = 0; mode < 5; mode++)
+    for (int g = 1; g <= (mode == 1 ? 1 : 4); g += (mode == 1 ? 1 : 3)) {
       hipLaunchKernelGGL(k, dim3(1), dim3(256), 0, 0, d, mode, g, steps);
       hipError_t e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
       printf("mode %d groups %d: ticks/step %.1f %s\n", mode, g, (double)h[0] / steps, hipGetErrorString(e));
