@@ -252,10 +252,12 @@ struct Json {
   std::vector<char> key;  // scratch for object keys (capacity reused)
 
   void ws() {
+    if (p < e && (unsigned char)*p > ' ') return;  // the common case: no white space
     while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) p++;
   }
   bool lit(const char *s) {
-    size_t n = strlen(s);
+    if (p >= e || *p != *s) return false;
+    const size_t n = strlen(s);
     if ((size_t)(e - p) >= n && !memcmp(p, s, n)) {
       p += n;
       return true;

@@ -401,7 +401,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 // per window.  The image's ring misses make this safe (dxi_far_end).
 //
 // A walk step is <= 256 links of one level, lanes over links: read the linked
-// values, apply them to the owners' slots with LDS atomics.  A step only reads
+// values, apply them to the owners' slots with LDS atomics.  Lane l takes the
+// step's links 4l..4l+3, one per atomic instruction: a row's consecutive links
+// (one owner) go to different instructions, as lanes of one instruction on one
+// slot would be applied one after another.  A step only reads
 // slots of earlier levels and a wave's LDS operations complete in order, so
 // no barrier separates steps; the next step's records are read during the
 // step before, and step descriptors come 64 at a time (one LDS read per 64
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
     const uint32_t d = __builtin_amdgcn_readlane(bat, 0);
     uint32_t rc[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) rc[q] = 64u * q + lane < (d >> 16) ? lk[(d & 0xFFFFu) + 64u * q + lane] : idle;
+    for (int q = 0; q < 4; q++) rc[q] = 4u * lane + q < (d >> 16) ? lk[(d & 0xFFFFu) + 4u * lane + q] : idle;
     // nothing in flight at the loop entry (the compiler's wait counting sees
     // this wait): a step then waits only for its own reads
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
         const uint32_t d1 = s + 1u < 64u ? __builtin_amdgcn_readlane(bat, s + 1u) : __builtin_amdgcn_readlane(nbat, 0);
         uint32_t rn[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) rn[q] = 64u * q + lane < (d1 >> 16) ? lk[(d1 & 0xFFFFu) + 64u * q + lane] : idle;
+        for (int q = 0; q < 4; q++) rn[q] = 4u * lane + q < (d1 >> 16) ? lk[(d1 & 0xFFFFu) + 4u * lane + q] : idle;
 #pragma unroll
         for (int q = 0; q < 4; q++) apply(rc[q], x[q]);
 #pragma unroll

@@ -62,7 +62,10 @@ GROUPS = {
     "k_proto": ["k_proto_lds", "k_proto_sel", "k_pg_init", "k_pg_link", "k_pg_a", "k_pg_b", "k_pg_c", "k_pg_sweep",
                 "k_pg_d", "k_pg_gate"],
     "k_pull": ["k_pull_lds", "k_pull_sel", "k_pull", "k_mwp_count", "k_mwp_scan", "k_mwp_write", "k_scan64"],
-    "k_diff": ["k_dprep_a", "k_dprep_scan", "k_dprep_b", "k_diff_lds", "k_diff", "k_diff_expand"],
+    # the multi-entry kernels (k_dx.hip; k_zero's two small clears are not attributed) and the
+    # one-workgroup-per-entry ones (option diff_legacy)
+    "k_diff": ["k_dx_label", "k_dx_good", "k_dx_walk", "k_dx_leaf", "k_dx_lp", "k_dx_mask",
+               "k_dprep_a", "k_dprep_scan", "k_dprep_b", "k_diff_lds", "k_diff", "k_diff_expand"],
 }
 
 

@@ -1,8 +1,9 @@
 """Diagnostic: per-phase ticks of the multi-entry diff's walks (k_dx_walk) from the stamps build.
 
 usage: python tools/stamps_dx.py [c3|c5] [RUNS] [P_FAULT]
-Reach workgroups (chunk x direction) and depth workgroups (4 sources each): staging 1 (row starts), staging 2
-(positions), staging 3 (links), the walk, finalize, missing rows; windows; total.
+Reach workgroups (chunk x direction) and depth workgroups (2 sources each), wave 0's view: the first window's
+staging, the walks, the waits for the worker waves (finalize k-1 / stage k+1) at the window barriers, the missing
+rows pass; windows; total.
 """
 import os
 import sys
@@ -30,10 +31,10 @@ eng.diffprov(f, DIFF_PER_RUN)
 eng.synchronize()
 nu = len(f)
 nch = (nu + 63) // 64
-nd = (nu + 3) // 4
+nd = (nu + 1) // 2
 n = 16 * max(2 * nch, nd)
 st = eng.debug_copy("stamps", 0, 8 * n).view(np.uint64).reshape(-1, 16).astype(np.int64)
-names = ["stage1", "stage2", "stage3", "walk", "finalize", "rows", "windows", "total"]
+names = ["stage0", "-", "-", "walk", "wait", "rows", "windows", "total"]
 for label, rows, off in (("reach", st[:2 * nch], 0), ("depth", st[:nd], 8)):
     blk = rows[:, off:off + 8]
     print(f"{label}: {len(blk)} workgroups")
