@@ -726,6 +726,7 @@ static int device_load(nemo_ctx *c) {
   // run 0's post graph in Kahn order for the multi-entry diff: read the Kahn
   // order, both CSRs and the node words; write positions, rows both ways, level bounds
   if (c->dx_ok) {
+    c->dxp.err0 = c->dc.err + c->dxp.g0;
     const double V0 = c->dxp.V0, E0 = c->dxp.E0;
     if ((rc = timed(c, "k_dxprep", 16 * E0 + 44 * V0, 0,
                     [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->dx_its.tsum, c->stream); })))
@@ -1040,6 +1041,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       p.E0 = (uint32_t)ne;
       p.r0idx = c->d_r0idx;
       p.n_r0lab = c->n_r0lab;
+      p.err0 = nullptr;  // set in device_load (the error flags are allocated there)
       if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
           (rc = dalloc(c, &p.lend, nv)) || (rc = dalloc(c, &p.rp, nv + 1)) || (rc = dalloc(c, &p.fp, nv + 1)) ||
           (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))

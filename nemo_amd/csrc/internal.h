@@ -42,6 +42,8 @@ struct DxPrep {
   const uint32_t *r0idx;     // [n_r0lab] node of each sorted run-0 goal label
   uint32_t *r0pos;           // [n_r0lab] its position
   uint32_t n_r0lab;
+  const uint32_t *err0;      // g0's load error flag (k_build / k_csr / k_topo): set, the CSR and Kahn
+                             // order may be partial and every relayout kernel does nothing (the load fails)
 };
 #define DXI_RULE 1u   // the position is a rule
 

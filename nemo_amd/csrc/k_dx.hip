@@ -85,6 +85,7 @@ void launch_scan(uint32_t *a, uint32_t n, uint32_t *tsum, hipStream_t s) {
 // pass 1, one thread per position i: node -> position, row lengths (parents in
 // Kahn order, children in reversed Kahn order), level bounds, rule bit
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_a(DevCorpus c, DxPrep p) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const GraphView gv = c.view(p.g0);
   const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (i == 0) {
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_a(DevCorpus c, DxPrep p) {
 // pass 3, one thread per position: rows as walk indices (parents as positions,
 // children as reversed positions), label entries as positions
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_b(DevCorpus c, DxPrep p) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const GraphView gv = c.view(p.g0);
   const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (i < p.n_r0lab) p.r0pos[i] = p.tpos[p.r0idx[i]];
@@ -132,6 +134,7 @@ struct DxImgSet {
   DxImg m[2];
 };
 __global__ __launch_bounds__(1024) void k_dxi_bounds(DxPrep p, DxImgSet set) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   __shared__ uint32_t s_best[3];
   const DxImg m = set.m[blockIdx.x];
   const uint32_t V = p.V0, tid = threadIdx.x, lane = lane_id();
@@ -179,6 +182,7 @@ __device__ __forceinline__ uint32_t dxi_far_end(const DxImg &m, uint32_t nw, uin
 // per walk index: segment flag (the window's first position or a level's
 // first), links that leave the ring
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_count(DxPrep p, DxImg m, DxImgScratch t) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const uint32_t V = p.V0, i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (i > V) return;
   if (i == V) {
@@ -198,6 +202,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_count(DxPrep p, DxImg m, DxI
 }
 // per walk index: its segment's first position, its links' records and misses
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_fill(DxPrep p, DxImg m, DxImgScratch t) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const uint32_t V = p.V0, i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (i >= V) {
     if (i == V) t.segpos[t.fseg[V]] = V;
@@ -218,12 +223,14 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_fill(DxPrep p, DxImg m, DxIm
 // per segment: its walk steps (<= DX_STEP links each; a segment without links has none)
 #define DX_STEP 256u
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_stepcount(DxPrep p, DxImg m, DxImgScratch t) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const uint32_t V = p.V0, sg = blockIdx.x * NEMO_BLOCK + threadIdx.x, ns = t.fseg[V];
   if (sg > V) return;
   const uint32_t *rowp = m.rev ? p.fp : p.rp;
   t.fstep[sg] = sg < ns ? (rowp[t.segpos[sg + 1]] - rowp[t.segpos[sg]] + DX_STEP - 1u) / DX_STEP : 0u;
 }
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dxi_steps(DxPrep p, DxImg m, DxImgScratch t) {
+  if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const uint32_t V = p.V0, sg = blockIdx.x * NEMO_BLOCK + threadIdx.x, ns = t.fseg[V];
   if (sg >= ns) return;
   const uint32_t *rowp = m.rev ? p.fp : p.rp;
