@@ -83,6 +83,7 @@ struct Graph {
   std::vector<uint32_t> src, dst, rank, ltab, llab;
   std::vector<uint8_t> tclass;
   std::vector<Str> tabs, labs;  // local first-appearance order
+  std::vector<uint64_t> labh;   // hash_sv of each of labs (the global interning's shard and slot)
   std::string err;
   std::string_view sv(Str s) const {
     return std::string_view(s.off < flen ? fb + s.off : arena.data() + (s.off - flen), s.len);
@@ -143,8 +144,8 @@ struct FlatMap {
     mask = cap - 1;
   }
   // value of k, inserting v if absent; second = inserted
-  std::pair<uint32_t, bool> emplace(std::string_view k, uint32_t v) {
-    const uint64_t h = hash_sv(k);
+  std::pair<uint32_t, bool> emplace(std::string_view k, uint32_t v) { return emplace_h(k, hash_sv(k), v); }
+  std::pair<uint32_t, bool> emplace_h(std::string_view k, uint64_t h, uint32_t v) {
     const uint32_t tag = (uint32_t)(h >> 32);
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       Slot &sl = slot[i];
@@ -232,6 +233,103 @@ struct InternMap {
       }
       if (slot[i].tag == tag && key[i] == k) return slot[i].val;
     }
+  }
+};
+
+// The global label interning, sharded by hash so that threads intern in
+// parallel with the sequential result.  A label's shard is fixed by its hash;
+// each shard is filled by one thread walking the graphs in order, so an entry
+// is created at the label's first appearance (graph, local index), which is
+// flagged.  One serial pass over the local labels in graph order then numbers
+// the flagged ones: global ids in first-appearance order, as one map would give.
+struct ShardIntern {
+  static constexpr uint32_t NEW = 1u << 31, SH = 25;  // lre entry: NEW | shard << SH | shard index
+  struct Shard {
+    std::vector<uint32_t> tag, val;   // slots: hash tag, shard index (~0u empty)
+    size_t mask = 0;
+    std::vector<std::string_view> key;
+    std::vector<uint64_t> hash;
+    std::vector<uint32_t> gid;        // by shard index: the global id
+    void grow() {
+      const size_t cap = std::max<size_t>(64, 2 * tag.size());
+      tag.assign(cap, 0);
+      val.assign(cap, ~0u);
+      mask = cap - 1;
+      for (uint32_t x = 0; x < key.size(); x++) {
+        size_t i = hash[x] & mask;
+        while (val[i] != ~0u) i = (i + 1) & mask;
+        tag[i] = (uint32_t)(hash[x] >> 32);
+        val[i] = x;
+      }
+    }
+    // the shard index of k, and whether it is new
+    std::pair<uint32_t, bool> intern(std::string_view k, uint64_t h) {
+      if (2 * (key.size() + 1) > tag.size()) grow();
+      const uint32_t t = (uint32_t)(h >> 32);
+      for (size_t i = h & mask;; i = (i + 1) & mask) {
+        if (val[i] == ~0u) {
+          tag[i] = t;
+          val[i] = (uint32_t)key.size();
+          key.push_back(k);
+          hash.push_back(h);
+          gid.push_back(~0u);
+          return {val[i], true};
+        }
+        if (tag[i] == t && key[val[i]] == k) return {val[i], false};
+      }
+    }
+  };
+  std::vector<Shard> sh;  // one per thread of the first merge (fixed from then on)
+  uint64_t count = 0;     // labels numbered so far
+  uint32_t shard_of(uint64_t h) const { return (uint32_t)(((h >> 40) * sh.size()) >> 24); }
+
+  // lre[g][li] = global id of graph g's local label li.  add(view) stores a
+  // new label's name (its index is the global id) and returns the view the
+  // shard keeps from then on (the graphs' arenas may not outlive the call).
+  template <class Add>
+  bool merge(std::vector<Graph> &gs, uint32_t G, int nt, std::vector<std::vector<uint32_t>> &lre, Add &&add) {
+    for (uint32_t g = 0; g < G; g++) lre[g].assign(gs[g].labs.size(), 0);
+    if (sh.empty()) sh.resize((size_t)std::min(64, std::max(1, nt)));
+    const uint32_t S = (uint32_t)sh.size();
+    std::atomic<uint32_t> nexts{0};
+    auto phase_a = [&] {
+      for (uint32_t k; (k = nexts.fetch_add(1)) < S;) {
+        Shard &d = sh[k];
+        for (uint32_t g = 0; g < G; g++) {
+          const Graph &gr = gs[g];
+          for (uint32_t li = 0; li < gr.labh.size(); li++) {
+            const uint64_t h = gr.labh[li];
+            if (shard_of(h) != k) continue;
+            const auto r = d.intern(gr.sv(gr.labs[li]), h);
+            lre[g][li] = (r.second ? NEW : 0u) | (k << SH) | r.first;
+          }
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; i++) pool.emplace_back(phase_a);
+    phase_a();
+    for (auto &t : pool) t.join();
+    for (uint32_t g = 0; g < G; g++)  // first appearances in graph order
+      for (uint32_t &x : lre[g])
+        if (x & NEW) {
+          x &= ~NEW;
+          Shard &d = sh[x >> SH];
+          const uint32_t si = x & ((1u << SH) - 1u);
+          if (count >= 0xFFFFFFFFull || d.key.size() >= (1u << SH)) return false;
+          d.gid[si] = (uint32_t)count++;
+          d.key[si] = add(d.key[si]);
+        }
+    std::atomic<uint32_t> nextg{0};
+    auto phase_c = [&] {
+      for (uint32_t g; (g = nextg.fetch_add(1)) < G;)
+        for (uint32_t &x : lre[g]) x = sh[x >> SH].gid[x & ((1u << SH) - 1u)];
+    };
+    pool.clear();
+    for (int i = 1; i < nt; i++) pool.emplace_back(phase_c);
+    phase_c();
+    for (auto &t : pool) t.join();
+    return true;
   }
 };
 
@@ -618,6 +716,21 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     if (it.second) order.push_back(s);
     return it.first;
   };
+  g.labh.reserve(V);
+  auto intern_label = [&](Str s) {  // the same, keeping each distinct label's hash
+    if (g.labs.size() * 2 + 16 > labs.mask) {
+      labs.init(g.labs.size() * 2 + 16);
+      for (uint32_t i = 0; i < g.labs.size(); i++) labs.emplace_h(g.sv(g.labs[i]), g.labh[i], i);
+    }
+    const std::string_view k = g.sv(s);
+    const uint64_t h = hash_sv(k);
+    auto it = labs.emplace_h(k, h, (uint32_t)g.labs.size());
+    if (it.second) {
+      g.labs.push_back(s);
+      g.labh.push_back(h);
+    }
+    return it.first;
+  };
   for (auto &r : goals) {
     if (!gidx.emplace(g.sv(r.f[0]), (uint32_t)g.id.size()).second) {
       g.err = "Run " + std::to_string(iteration) + ": duplicate goal id run_" + std::to_string(iteration) + "_" +
@@ -639,7 +752,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(Str{0, 0});
     g.time.push_back(t);
     g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
-    g.llab.push_back(intern(labs, g.labs, r.f[1]));
+    g.llab.push_back(intern_label(r.f[1]));
     g.tclass.push_back(0);
   }
   for (auto &r : rules) {
@@ -651,7 +764,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(r.f[3]);
     g.time.push_back(Str{0, 0});
     g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
-    g.llab.push_back(intern(labs, g.labs, r.f[1]));
+    g.llab.push_back(intern_label(r.f[1]));
     g.tclass.push_back(type_class(g.sv(r.f[3])));
   }
   // rank of each node's ID inside the graph (the prefix is common, so unprefixed order == prefixed order)
@@ -772,7 +885,8 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
     }
   // global interning in graph order (== the sequential first-appearance order)
   // (keys view the graphs' arenas, alive until the ingest is freed)
-  InternMap tmap, lmap;
+  InternMap tmap;
+  ShardIntern lmap;
   std::vector<std::vector<uint32_t>> tre(G), lre(G);
   h->node_off.assign(G + 1, 0);
   h->edge_off.assign(G + 1, 0);
@@ -787,9 +901,15 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
     tre[g].reserve(gr.tabs.size());
     lre[g].reserve(gr.labs.size());
     for (Str s : gr.tabs) tre[g].push_back(tmap.intern(gr.sv(s), add(h->tables)));
-    for (Str s : gr.labs) lre[g].push_back(lmap.intern(gr.sv(s), add(h->labels)));
     h->node_off[g + 1] = h->node_off[g] + gr.id.size();
     h->edge_off[g + 1] = h->edge_off[g] + gr.src.size();
+  }
+  if (!lmap.merge(h->graphs, G, nt, lre, [&](std::string_view k) {
+        h->labels.emplace_back(k);
+        return k;  // the arenas live as long as the ingest
+      })) {
+    delete h;
+    return fail("too many distinct labels");
   }
   static const char *kPrePost[2] = {"pre", "post"};
   for (int k = 0; k < 2; k++)
@@ -833,7 +953,8 @@ struct nemo_ingest_stream {
   std::vector<uint32_t> order;  // parse order: run 0, failedRuns[0], then runs.json order
   int threads = 1;
   uint32_t next = 0;  // next position in `order`
-  InternMap tmap, lmap;  // keys view the strings of tables / labels (a deque: no relocation)
+  InternMap tmap;        // keys view the strings of tables / labels (a deque: no relocation)
+  ShardIntern lmap;
   std::deque<std::string> tables, labels;
   uint32_t table_pre = 0, table_post = 0;
   bool pre_post = false;
@@ -912,10 +1033,13 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
   };
   for (uint32_t g = 0; g < G; g++) {
     tre[g].reserve(gs[g].tabs.size());
-    lre[g].reserve(gs[g].labs.size());
     for (Str x : gs[g].tabs) tre[g].push_back(s->tmap.intern(gs[g].sv(x), add(s->tables)));
-    for (Str x : gs[g].labs) lre[g].push_back(s->lmap.intern(gs[g].sv(x), add(s->labels)));
   }
+  if (!s->lmap.merge(gs, G, nt, lre, [&](std::string_view k) {
+        s->labels.emplace_back(k);
+        return std::string_view(s->labels.back());  // the chunk's arenas go away
+      }))
+    return fail("too many distinct labels");
   if (!s->pre_post) {  // fixed from the first chunk on: every chunk's corpus names the same ids
     static const char *kPrePost[2] = {"pre", "post"};
     for (int k = 0; k < 2; k++)
