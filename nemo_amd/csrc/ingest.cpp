@@ -333,8 +333,36 @@ struct ShardIntern {
   }
 };
 
+// Molly's node IDs are "goal<n>" / "rule<n>" with n decimal.  When every ID
+// of a kind in a graph has that shape, n is below a bound and no two of them
+// share n, the ID -> node map of that kind is an array indexed by n; an entry
+// keeps the digit count too, so that "goal07" does not find "goal7".  Anything
+// else takes the hash maps (the results are the same).
+struct NumMap {
+  std::vector<uint32_t> v;     // n -> node | digits << 28 (~0u: none)
+  std::vector<uint32_t> used;  // the n set for this graph (cleared after it)
+  void clear() {
+    for (uint32_t n : used) v[n] = ~0u;
+    used.clear();
+  }
+};
+// n and digit count of "<pfx><digits>" (4-byte prefix, 1..9 digits)
+inline bool id_num(std::string_view s, const char *pfx, uint32_t &n, uint32_t &nd) {
+  if (s.size() < 5 || s.size() > 13 || memcmp(s.data(), pfx, 4)) return false;
+  uint32_t x = 0;
+  for (size_t i = 4; i < s.size(); i++) {
+    const uint32_t d = (uint32_t)(unsigned char)s[i] - '0';
+    if (d > 9) return false;
+    x = x * 10 + d;
+  }
+  n = x;
+  nd = (uint32_t)s.size() - 4;
+  return true;
+}
+
 // per-thread maps of parse_graph, reused from graph to graph
 struct ParseMaps {
+  NumMap gnum, rnum;
   FlatMap gidx, ridx, tabs, labs;
   FlatSet64 seen;
   std::vector<std::pair<uint64_t, uint32_t>> keys;
@@ -731,12 +759,50 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     }
     return it.first;
   };
-  for (auto &r : goals) {
-    if (!gidx.emplace(g.sv(r.f[0]), (uint32_t)g.id.size()).second) {
-      g.err = "Run " + std::to_string(iteration) + ": duplicate goal id run_" + std::to_string(iteration) + "_" +
-              cond + "_" + std::string(g.sv(r.f[0])) + " (Goal.id IS UNIQUE, pre-post-prov.go:68)";
-      return;
+  // the ID -> node maps, numeric when the IDs allow (NumMap), else hashed; a
+  // duplicate ID is the reference's uniqueness error (pre-post-prov.go:68, :129)
+  const uint32_t nbound = (uint32_t)std::min<size_t>(4 * V + 4096, 1u << 27);
+  auto build_ids = [&](const std::vector<Rec> &recs, uint32_t base, const char *pfx, NumMap &nm, FlatMap &hm,
+                       const char *what, const char *cons) -> int {  // 1 numeric, 0 hashed, -1 duplicate
+    bool num = true;
+    if (nm.v.size() < nbound) nm.v.resize(nbound, ~0u);
+    for (uint32_t k = 0; k < recs.size() && num; k++) {
+      uint32_t n, nd;
+      if (!id_num(g.sv(recs[k].f[0]), pfx, n, nd) || n >= nbound) {
+        num = false;
+      } else if (nm.v[n] == ~0u) {
+        nm.v[n] = (base + k) | (nd << 28);
+        nm.used.push_back(n);
+      } else if ((nm.v[n] >> 28) != nd) {
+        num = false;  // "goal7" and "goal07": the hash map tells them apart
+      } else {
+        g.err = "Run " + std::to_string(iteration) + ": duplicate " + what + " id run_" + std::to_string(iteration) +
+                "_" + cond + "_" + std::string(g.sv(recs[k].f[0])) + " (" + cons + ")";
+        return -1;
+      }
     }
+    if (num) return 1;
+    nm.clear();
+    for (uint32_t k = 0; k < recs.size(); k++)
+      if (!hm.emplace(g.sv(recs[k].f[0]), base + k).second) {
+        g.err = "Run " + std::to_string(iteration) + ": duplicate " + what + " id run_" + std::to_string(iteration) +
+                "_" + cond + "_" + std::string(g.sv(recs[k].f[0])) + " (" + cons + ")";
+        return -1;
+      }
+    return 0;
+  };
+  const int gnumk = build_ids(goals, 0, "goal", M.gnum, gidx, "goal", "Goal.id IS UNIQUE, pre-post-prov.go:68");
+  if (gnumk < 0) {
+    M.gnum.clear();
+    return;
+  }
+  const int rnumk = build_ids(rules, (uint32_t)goals.size(), "rule", M.rnum, ridx, "rule",
+                              "Rule.id IS UNIQUE, pre-post-prov.go:129");
+  if (rnumk < 0) {
+    M.gnum.clear(), M.rnum.clear();
+    return;
+  }
+  for (auto &r : goals) {
     Str t = r.f[3];
     if (g.sv(r.f[2]) == "clock") {  // molly.go:74-89
       std::string tm;
@@ -756,11 +822,6 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.tclass.push_back(0);
   }
   for (auto &r : rules) {
-    if (!ridx.emplace(g.sv(r.f[0]), (uint32_t)g.id.size()).second) {
-      g.err = "Run " + std::to_string(iteration) + ": duplicate rule id run_" + std::to_string(iteration) + "_" +
-              cond + "_" + std::string(g.sv(r.f[0])) + " (Rule.id IS UNIQUE, pre-post-prov.go:129)";
-      return;
-    }
     g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(r.f[3]);
     g.time.push_back(Str{0, 0});
     g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
@@ -822,18 +883,29 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   seen.init(edges.size());
   size_t created = 0;
   g.src.reserve(edges.size()), g.dst.reserve(edges.size());
+  auto find_id = [&](std::string_view x, bool goal) -> uint32_t {
+    if ((goal ? gnumk : rnumk) == 0) return (goal ? gidx : ridx).find(x);
+    const NumMap &nm = goal ? M.gnum : M.rnum;
+    uint32_t n, nd;
+    // every ID of the kind has the numeric shape: another string is none of them
+    if (!id_num(x, goal ? "goal" : "rule", n, nd) || n >= nbound) return ~0u;
+    const uint32_t e = nm.v[n];
+    return e != ~0u && (e >> 28) == nd ? (e & ((1u << 28) - 1u)) : ~0u;
+  };
   for (auto &ed : edges) {
     std::string_view f = g.sv(ed.first), t = g.sv(ed.second);
     uint32_t u, v;
-    if (f.find("goal") != std::string_view::npos) {  // strings.Contains(From, "goal") (pre-post-prov.go:173)
-      u = gidx.find(f), v = ridx.find(t);
+    // strings.Contains(From, "goal") (pre-post-prov.go:173)
+    if ((f.size() >= 4 && !memcmp(f.data(), "goal", 4)) || f.find("goal") != std::string_view::npos) {
+      u = find_id(f, true), v = find_id(t, false);
     } else {
-      u = ridx.find(f), v = gidx.find(t);
+      u = find_id(f, false), v = find_id(t, true);
     }
     if (u == ~0u || v == ~0u || !seen.insert(((uint64_t)u << 32) | v)) continue;
     g.src.push_back(u), g.dst.push_back(v);
     created++;
   }
+  M.gnum.clear(), M.rnum.clear();
   if (created != edges.size())
     g.err = "Run " + std::to_string(iteration) + ": inserted number of edges (" + std::to_string(created) +
             ") does not equal number of antecedent provenance edges (" + std::to_string(edges.size()) + ")";
