@@ -304,8 +304,9 @@ int nemo_fetch_pulled(nemo_ctx *ctx, uint32_t slot, uint32_t *src, uint32_t *dst
 /* Every slot at once (one call where the Go side would make one per graph):
  * off[slot] / cnt[slot] (pulled-slot count entries each) locate slot s's edges
  * in src/dst, whose used extent is *n_used (regions are claimed in device
- * order, so they are disjoint but not sorted by slot).  src/dst may be NULL
- * to query *n_used; then cap >= *n_used.                                   */
+ * order, so they are not sorted by slot; they are disjoint, except that diff
+ * entries sharing a label source -- one D mask, one graph -- share one
+ * region).  src/dst may be NULL to query *n_used; then cap >= *n_used.     */
 int nemo_fetch_pulled_all(nemo_ctx *ctx, uint64_t *off, uint32_t *cnt, uint32_t *src, uint32_t *dst, uint64_t cap,
                           uint64_t *n_used);
 

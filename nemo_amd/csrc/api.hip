@@ -111,6 +111,8 @@ struct nemo_ctx {
   // memory asynchronously; the first fetch waits for them
   int pull_which = -1;
   uint32_t pull_slots = 0, pull_slot_cap = 0;
+  uint32_t pull_dslots = 0;              // slots computed: diff entries sharing a label source share one
+  std::vector<uint32_t> pull_map;        // which 2 with shared slots: entry -> computed slot
   uint32_t *d_pck = nullptr;          // big graphs' pull chunk table
   size_t pull_ck_cap = 0;
   uint32_t *d_pcnt = nullptr, *d_psrc = nullptr, *d_pdst = nullptr;
@@ -723,21 +725,9 @@ static int device_load(nemo_ctx *c) {
                   [&] { nemo::launch_csr_big(c->dc, c->big_chunks, c->stream); })))
     return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
-  // run 0's post graph in Kahn order for the multi-entry diff: read the Kahn
-  // order, both CSRs and the node words; write positions, rows both ways, level bounds
-  if (c->dx_ok) {
-    c->dxp.err0 = c->dc.err + c->dxp.g0;
-    const double V0 = c->dxp.V0, E0 = c->dxp.E0;
-    if ((rc = timed(c, "k_dxprep", 16 * E0 + 44 * V0, 0,
-                    [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->dx_its.tsum, c->stream); })))
-      return rc;
-    // the walk images for the default windows (read rows and Kahn levels, write records and misses)
-    nemo::dx_img_configs(c->dxp.V0, c->dxp.E0, 0, c->dx_img);
-    if ((rc = timed(c, "k_dximg", 2 * (16 * E0 + 32 * V0), 0,
-                    [&] { nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, c->stream); })))
-      return rc;
-    c->dx_img_key = 0;
-  }
+  // the multi-entry diff's relayout of run 0's post graph and its walk images
+  // follow the next diffprov, on its stream (they read the graph built here)
+  c->dx_img_key = -1;
   return NEMO_OK;
 }
 
@@ -1041,7 +1031,9 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       p.E0 = (uint32_t)ne;
       p.r0idx = c->d_r0idx;
       p.n_r0lab = c->n_r0lab;
-      p.err0 = nullptr;  // set in device_load (the error flags are allocated there)
+      p.err0 = nullptr;  // set at the first diffprov (the error flags are allocated with the corpus)
+      p.r0lab = c->d_r0lab;
+      p.r0dense = nv < (1ull << 28) ? c->d_r0dense : nullptr;  // positions << 4 must fit
       if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
           (rc = dalloc(c, &p.lend, nv)) || (rc = dalloc(c, &p.rp, nv + 1)) || (rc = dalloc(c, &p.fp, nv + 1)) ||
           (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))
@@ -1318,12 +1310,12 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
   if (!c->ev_up_dsrc) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_dsrc, hipEventDisableTiming));
   else HIPCHK(c, hipEventSynchronize(c->ev_up_dsrc));  // the previous upload has landed
-  if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, 2 * n_failed)) return rg;
+  if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, 3 * n_failed)) return rg;
   // D_f depends on run 0 and on the label source alone (differential-provenance.go:22-43):
   // entries with the same source share one computation.  In the reference mode every
   // entry's source is failedRuns[0] (the in-place ###RUN### substitution of :43), so
   // the whole call is one computation; in the per-run mode each distinct failed run is.
-  uint32_t *src = c->h_dsrc, *emap = c->h_dsrc + n_failed;
+  uint32_t *src = c->h_dsrc, *emap = c->h_dsrc + n_failed, *urep = c->h_dsrc + 2 * n_failed;
   c->dmap.assign(n_failed, 0);
   std::unordered_map<uint32_t, uint32_t> uniq;
   uint32_t nu = 0;
@@ -1336,6 +1328,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     const uint32_t key = d_labels ? 0u : 2 * r + 1;  // label mode: one set for every entry
     auto ins = uniq.emplace(key, nu);
     if (ins.second) {
+      urep[nu] = (uint32_t)e;  // the first entry of each source stands for it (nemo_pull_edges(2))
       src[nu++] = 2 * r + 1;
       src_bytes += d_labels ? 0.0 : 8.0 * (double)(c->node_off[2 * r + 2] - c->node_off[2 * r + 1]);
     }
@@ -1356,7 +1349,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->d_ddepth = nullptr;
     c->d_dtopo = nullptr;
     c->legacy_cap = 0;
-    if ((rc = dalloc(c, &c->d_dsrc, 2 * n_failed))) return rc;
+    if ((rc = dalloc(c, &c->d_dsrc, 3 * n_failed))) return rc;
     if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
     c->diff_cap = (uint32_t)n_failed;
@@ -1393,7 +1386,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   hipStream_t s = c->aux;
-  nemo::launch_to_host(c->d_dsrc, src, 2 * n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
+  nemo::launch_to_host(c->d_dsrc, src, 3 * n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
   nemo::launch_zero(c->d_nmiss, 4, s);
   // HBM lower bound: run 0's post graph once (rows both ways, node word, Kahn
@@ -1413,7 +1406,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.r0hkey = c->d_r0hkey;
     a.r0hval = c->d_r0hval;
     a.r0hmask = c->r0hmask;
-    a.r0dense = c->d_r0dense;
+    a.r0dense = c->dxp.r0dense;
     a.nlab = c->nlab;
     a.pb = c->d_dxpb;
     a.w32 = w32;
@@ -1437,9 +1430,21 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.missing = c->d_miss;
     a.n_missing = c->d_nmiss;
     a.window = c->diff_window;
-    if (c->dx_img_key != (int)c->diff_window) {  // the test knob changed the windows: rebuild the images
+    if (c->dx_img_key < 0) {
+      // g0 in Kahn order (read the Kahn order, both CSRs and the node words;
+      // write positions, rows both ways, level bounds), once per load / rebuild
+      c->dxp.err0 = c->dc.err + c->dxp.g0;
+      if ((rc = timed_on(c, s, "k_dxprep", 16.0 * E0 + 44.0 * V0, 0,
+                         [&] { nemo::launch_dx_prep(c->dc, c->dxp, c->dx_its.tsum, s); })))
+        return rc;
+    }
+    if (c->dx_img_key != (int)c->diff_window) {
+      // the walk images (read rows and Kahn levels, write records, steps and
+      // misses), once per load / rebuild and window configuration (test knob)
       nemo::dx_img_configs(c->dxp.V0, c->dxp.E0, c->diff_window, c->dx_img);
-      nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, s);
+      if ((rc = timed_on(c, s, "k_dximg", 2 * (16.0 * E0 + 32.0 * V0), 0,
+                         [&] { nemo::launch_dx_img(c->dxp, c->dx_img, c->dx_its, s); })))
+        return rc;
       c->dx_img_key = (int)c->diff_window;
     }
     for (int k = 0; k < 2; k++) a.img[k] = c->dx_img[k];
@@ -1860,7 +1865,7 @@ static int pull_launch(nemo_ctx *c) {
   a.src = c->d_psrc;
   a.dst = c->d_pdst;
   a.cap = c->pull_cap;
-  const uint32_t slots = c->pull_slots;
+  const uint32_t slots = c->pull_dslots;
   hipStream_t s = c->stream;
   double V = (double)c->V, E = (double)c->E;
   if (a.which == 2) {
@@ -1905,6 +1910,14 @@ static int pull_sync(nemo_ctx *c) {
     HIPCHK(c, hipEventSynchronize(c->ev_pull));
   }
   c->pull_hint[c->pull_which] = total;
+  if (!c->pull_map.empty()) {  // shared regions: entry e takes its computed slot's (map[e] <= e)
+    for (uint32_t e = c->pull_slots; e-- > 0;) {
+      const uint32_t u = c->pull_map[e];
+      c->h_poff[e] = c->h_poff[u];
+      c->h_pcnt[e] = c->h_pcnt[u];
+    }
+    c->pull_map.clear();
+  }
   c->pull_synced = true;
   return NEMO_OK;
 }
@@ -1920,6 +1933,10 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   c->pull_synced = true;
   if (which == 2 && (rc = join_aux(c))) return rc;  // the D masks
   const uint32_t slots = which == 2 ? c->n_entries : c->G;
+  // diff entries sharing a label source have one D mask, hence one graph: it is
+  // compacted once and their slots share its region (pull_sync expands the table)
+  const bool share = which == 2 && c->n_uniq < c->n_entries;
+  const uint32_t dslots = share ? c->n_uniq : slots;
   if (!c->ev_pull) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pull, hipEventDisableTiming));
   if (!c->h_pcur) HIPCHK(c, hipHostMalloc((void **)&c->h_pcur, sizeof(unsigned long long)));
   if (!c->d_pcur && (rc = dalloc(c, &c->d_pcur, 1))) return rc;
@@ -1944,6 +1961,9 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   }
   c->pull_which = which;
   c->pull_slots = slots;
+  c->pull_dslots = dslots;
+  if (share) c->pull_map = c->dmap;
+  else c->pull_map.clear();
   if (slots == 0) return NEMO_OK;
   nemo::PullArgs a{};
   a.which = (uint32_t)which;
@@ -1953,7 +1973,8 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   if (which == 2) {
     a.mask = c->d_dmask;
     a.mask_stride = c->node_off[g0 + 1] - c->node_off[g0];
-    cap = (uint64_t)slots * (c->edge_off[g0 + 1] - c->edge_off[g0]);  // D is an induced subgraph of g0
+    a.mask_row = share ? c->d_dsrc + 2 * c->n_entries : nullptr;  // diffprov's representative entries
+    cap = (uint64_t)dslots * (c->edge_off[g0 + 1] - c->edge_off[g0]);  // D is an induced subgraph of g0
   } else if (which == 0) {
     cap = c->E;  // every edge
   } else {
@@ -1967,7 +1988,7 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   a.ccnt = nullptr;
   a.maxck = 0;
   const uint64_t vg0 = c->node_off[g0 + 1] - c->node_off[g0];
-  const uint32_t rows = which == 2 ? (vg0 >= NEMO_CSR_BIG ? slots : 0u) : c->dc.n_big;
+  const uint32_t rows = which == 2 ? (vg0 >= NEMO_CSR_BIG ? dslots : 0u) : c->dc.n_big;
   if (rows) {
     a.maxck = (uint32_t)(2 * ((c->bigVmax + 4095) / 4096));
     const size_t need = (size_t)rows * a.maxck;

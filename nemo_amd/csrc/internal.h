@@ -42,6 +42,9 @@ struct DxPrep {
   const uint32_t *r0idx;     // [n_r0lab] node of each sorted run-0 goal label
   uint32_t *r0pos;           // [n_r0lab] its position
   uint32_t n_r0lab;
+  uint32_t *r0dense;         // the dense label table (DxArgs::r0dense; null: none): k_dxp_b writes
+                             // the run-0 labels' entries, a single position as pos << 4
+  const uint32_t *r0lab;     // [n_r0lab] sorted run-0 goal labels
   const uint32_t *err0;      // g0's load error flag (k_build / k_csr / k_topo): set, the CSR and Kahn
                              // order may be partial and every relayout kernel does nothing (the load fails)
 };
@@ -81,8 +84,9 @@ struct DxArgs {
   const uint32_t *ref_labels;  // label mode: [n, label...] of the single source (src unused)
   const uint32_t *r0lab, *r0hkey, *r0hval;
   uint32_t r0hmask;
-  // label -> (first sorted run-0 goal label entry << 4 | min(count, 15)), NEMO_NONE = not a run-0
-  // post-goal label; labels >= nlab are not either (null: the hash table above)
+  // label -> its run-0 position << 4 when it labels one run-0 goal, else (first sorted run-0 goal
+  // label entry << 4 | min(count, 15)); NEMO_NONE = not a run-0 post-goal label; labels >= nlab are
+  // not either (null: the hash table above)
   const uint32_t *r0dense;
   uint32_t nlab;
   uint32_t *pb;              // [nu][w32] present bitmaps over positions
@@ -111,6 +115,7 @@ struct PullArgs {
   uint32_t g0;              // graph of which == 2
   const uint8_t *mask;      // which == 2: D masks of the entries
   uint64_t mask_stride;     // bytes between two entries' masks
+  const uint32_t *mask_row; // which == 2: slot -> the entry whose mask it takes (null: the slot's own)
   uint32_t *cnt;            // [slots] edges of the slot
   uint64_t *off;            // [slots] first edge of the slot in src/dst
   unsigned long long *cursor;  // region allocator (zeroed before the launch)

@@ -644,7 +644,7 @@ __device__ __forceinline__ void pull_slot(const DevCorpus c, const PullArgs a, c
   const GraphView gv = c.view(g);
   if (tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;  // k_pull_lds's graph or diff entry
   if (a.ccnt && gv.V >= NEMO_CSR_BIG) return;             // k_mwp_*'s graph
-  const uint8_t *m = a.mask ? a.mask + (size_t)slot * a.mask_stride : nullptr;
+  const uint8_t *m = a.mask ? a.mask + (size_t)(a.mask_row ? a.mask_row[slot] : slot) * a.mask_stride : nullptr;
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = a.which == 1 ? c.nch[g] : 0u;
   if (threadIdx.x == 0) s_cnt = 0;
@@ -749,7 +749,7 @@ __device__ __forceinline__ bool mwp_slot(const DevCorpus &c, const PullArgs &a, 
   const uint32_t nch = a.which == 1 ? c.nch[s.g] : 0u;
   s.nnc = (gv.V + MWP_CH - 1) / MWP_CH;
   s.nt = s.nnc + (nch + MWP_CH - 1) / MWP_CH;
-  s.m = a.mask ? a.mask + (size_t)s.slot * a.mask_stride : nullptr;
+  s.m = a.mask ? a.mask + (size_t)(a.mask_row ? a.mask_row[s.slot] : s.slot) * a.mask_stride : nullptr;
   return true;
 }
 // edges of node u (raw / simplified / diff row) or of chain k (collapsed edges)
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   PullLds L = pull_carve(dyn, V, gv.E);
   {
     // diff pulls stage the entry's D mask where the others stage the flags
-    const uint8_t *fsrc = which == 2 ? a.mask + (size_t)slot * a.mask_stride : gv.flags;
+    const uint8_t *fsrc = which == 2 ? a.mask + (size_t)(a.mask_row ? a.mask_row[slot] : slot) * a.mask_stride : gv.flags;
     const StageDesc d[3] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}, {fsrc, L.fl, V, ST_U8}};
     stage_lds<3, PULL_BLOCK>(d);
   }

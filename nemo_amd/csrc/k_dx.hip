@@ -109,7 +109,15 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_b(DevCorpus c, DxPrep p) {
   if (*p.err0) return;  // g0 failed to load: its CSR and Kahn order may be partial
   const GraphView gv = c.view(p.g0);
   const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;
-  if (i < p.n_r0lab) p.r0pos[i] = p.tpos[p.r0idx[i]];
+  if (i < p.n_r0lab) {
+    const uint32_t pos = p.tpos[p.r0idx[i]], l = p.r0lab[i];
+    p.r0pos[i] = pos;
+    if (p.r0dense && (i == 0 || p.r0lab[i - 1] != l)) {  // the label's first entry: its dense entry
+      uint32_t n = 1;
+      while (n < 15u && i + n < p.n_r0lab && p.r0lab[i + n] == l) n++;
+      p.r0dense[l] = n == 1u ? pos << 4 : (i << 4) | n;
+    }
+  }
   if (i >= gv.V) return;
   const uint32_t v = gv.topo[i], V = gv.V;
   uint32_t o = p.rp[i];
@@ -294,20 +302,24 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     if (lds) atomicOr(&bm[p >> 5], 1u << (p & 31u));
     else atomicOr(&pb[p >> 5], 1u << (p & 31u));
   };
-  if (a.r0dense) {  // one dense-table load per source goal, then its run-0 positions
+  if (a.r0dense) {  // labels and node words together, one dense-table load per source goal
     for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
-      uint32_t lb[DXL_BATCH], dv[DXL_BATCH];
+      uint32_t lb[DXL_BATCH], wd[DXL_BATCH], dv[DXL_BATCH];
 #pragma unroll
       for (int q = 0; q < DXL_BATCH; q++) {
         const uint32_t x = base + q * NEMO_BLOCK + tid;
-        const bool in = x < hi && (!word || !is_rule(word[x]));
-        lb[q] = in ? lab[x] : NEMO_NONE;
+        lb[q] = x < hi ? lab[x] : NEMO_NONE;
+        wd[q] = x < hi && word ? word[x] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab ? a.r0dense[lb[q]] : NEMO_NONE;
+      for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab && !is_rule(wd[q]) ? a.r0dense[lb[q]] : NEMO_NONE;
 #pragma unroll
       for (int q = 0; q < DXL_BATCH; q++) {
         if (dv[q] == NEMO_NONE) continue;
+        if ((dv[q] & 15u) == 0u) {  // one run-0 goal carries the label
+          mark(dv[q] >> 4);
+          continue;
+        }
         const uint32_t i0 = dv[q] >> 4, cnt = dv[q] & 15u;
         for (uint32_t t = 0; t < cnt; t++) mark(a.p.r0pos[i0 + t]);
         if (cnt == 15u)  // 15 or more entries: the rest of the run
@@ -423,15 +435,14 @@ struct DxLds {
   T *ring0;          // NE rings of [R + 1 + 64] (stride rs): [R] the identity (sink), [R + 1 + lane] dump slots
   uint32_t rs;
   uint32_t *lk;      // [NB][EC] link records of a window
-  uint32_t *st;      // [NB][SC] its steps
+  uint32_t *st;      // [NB][64] its first 64 step descriptors (the rest is read from the image)
   uint32_t *lpb;     // [NL][NE][LW] depth: LP rules of a window, one bit per position
-  uint32_t SC, LW;
+  uint32_t LW;
 };
-__host__ __device__ inline uint32_t dx_sc(uint32_t W, uint32_t EC) { return W + EC / DX_STEP + 2u; }
 template <typename T, int NE>
 __host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC, bool whole) {
   const uint32_t NB = whole ? 1u : 2u, NL = whole ? 1u : 3u;
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * lds_align(4u * dx_sc(W, EC)) +
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * 256u +
          NL * NE * lds_align(4u * (W / 32u + 2u));
 }
 template <typename T, int NE>
@@ -444,9 +455,8 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_
   p += NE * lds_align((uint32_t)sizeof(T) * (R + 65u));
   L.lk = (uint32_t *)p;
   p += NB * lds_align(4u * EC);
-  L.SC = lds_align(4u * dx_sc(W, EC)) / 4u;
   L.st = (uint32_t *)p;
-  p += NB * 4u * L.SC;
+  p += NB * 256u;
   L.LW = lds_align(4u * (W / 32u + 2u)) / 4u;
   L.lpb = (uint32_t *)p;
   return L;
@@ -495,7 +505,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
     const uint32_t w0 = m.wb[kw], w1 = m.wb[kw + 1], n = w1 - w0;
     const uint32_t base = rowp[w0], ne = rowp[w1] - base;
     const uint32_t st0 = m.stepb[kw], nst = m.stepb[kw + 1] - st0;
-    uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * L.SC, *lpb = L.lpb + lb * NE * LW;
+    uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * 64u, *lpb = L.lpb + lb * NE * LW;
     // records, in 16-B chunks of the image
     const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
     for (uint32_t cb = c0; cb < c1; cb += 2 * nwt) {
@@ -516,7 +526,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
         }
       }
     }
-    for (uint32_t t = wt; t < nst; t += nwt) st[t] = m.steps[st0 + t];
+    if (wt < 64u) st[wt] = wt < nst ? m.steps[st0 + wt] : 0u;
     // init values with the misses folded in; depth: the LP bits of 64
     // consecutive positions by ballot
     for (uint32_t k0 = 0; k0 < n; k0 += nwt) {
@@ -581,8 +591,9 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
   };
   // ---- the walk of window kw by wave e ----
   auto walk = [&](uint32_t kw, uint32_t buf, uint32_t e) {
-    const uint32_t nst = __builtin_amdgcn_readfirstlane(m.stepb[kw + 1] - m.stepb[kw]);
-    const uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * L.SC;
+    const uint32_t st0 = __builtin_amdgcn_readfirstlane(m.stepb[kw]);
+    const uint32_t nst = __builtin_amdgcn_readfirstlane(m.stepb[kw + 1]) - st0;
+    const uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * 64u;
     T *ring = ringp(e);
     const uint32_t idle = R | ((R + 1u + lane) << 16);
     auto apply = [&](uint32_t rec, T x) {
@@ -594,8 +605,9 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
       }
     };
     if (!nst) return;
-    // step descriptors 64 at a time (one LDS read per 64 steps, read a batch ahead)
-    uint32_t bat = lane < nst ? st[lane] : 0u;
+    // step descriptors 64 at a time: the first 64 staged in LDS, the next
+    // batches read from the image a batch ahead (in flight while 64 steps run)
+    uint32_t bat = st[lane];
     const uint32_t d = __builtin_amdgcn_readlane(bat, 0);
     uint32_t rc[4];
 #pragma unroll
@@ -604,7 +616,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
     // this wait): a step then waits only for its own reads
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     for (uint32_t b0 = 0; b0 < nst; b0 += 64u) {
-      const uint32_t nbat = b0 + 64u + lane < nst ? st[b0 + 64u + lane] : 0u;
+      const uint32_t nbat = b0 + 64u + lane < nst ? m.steps[st0 + b0 + 64u + lane] : 0u;
       const uint32_t ns = min(64u, nst - b0);
       for (uint32_t s = 0; s < ns; s++) {
         T x[4];
