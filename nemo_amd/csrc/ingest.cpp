@@ -744,6 +744,15 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     if (it.second) order.push_back(s);
     return it.first;
   };
+  // tables repeat in runs (a relation's facts and rules come together): the last one is checked first
+  std::string_view last_tab;
+  uint32_t last_tid = ~0u;
+  auto intern_table = [&](Str s) {
+    const std::string_view k = g.sv(s);
+    if (last_tid != ~0u && k.size() == last_tab.size() && !memcmp(k.data(), last_tab.data(), k.size())) return last_tid;
+    last_tab = k;
+    return last_tid = intern(tabs, g.tabs, s);
+  };
   g.labh.reserve(V);
   auto intern_label = [&](Str s) {  // the same, keeping each distinct label's hash
     if (g.labs.size() * 2 + 16 > labs.mask) {
@@ -817,14 +826,14 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     }
     g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(Str{0, 0});
     g.time.push_back(t);
-    g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
+    g.ltab.push_back(intern_table(r.f[2]));
     g.llab.push_back(intern_label(r.f[1]));
     g.tclass.push_back(0);
   }
   for (auto &r : rules) {
     g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(r.f[3]);
     g.time.push_back(Str{0, 0});
-    g.ltab.push_back(intern(tabs, g.tabs, r.f[2]));
+    g.ltab.push_back(intern_table(r.f[2]));
     g.llab.push_back(intern_label(r.f[1]));
     g.tclass.push_back(type_class(g.sv(r.f[3])));
   }
