@@ -112,12 +112,6 @@ struct nemo_ctx {
   int pull_which = -1;
   uint32_t pull_slots = 0, pull_slot_cap = 0;
   uint32_t pull_dslots = 0;              // slots computed: diff entries sharing a label source share one
-  // the edge pulls run on `side`, forked from `stream` where they are called,
-  // beside what follows them there (k_proto, the hand-over); `stream` joins
-  // them (ev_side) before it next rewrites flags or graphs (guard_staged)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_side = nullptr, ev_side_fork = nullptr;
-  bool side_pending = false;
   std::vector<uint32_t> pull_map;        // which 2 with shared slots: entry -> computed slot
   uint32_t *d_pck = nullptr;          // big graphs' pull chunk table
   size_t pull_ck_cap = 0;
@@ -248,18 +242,9 @@ static hipEvent_t get_event(nemo_ctx *c) {
 }
 
 // Kernels that rewrite node flags must not overtake a staged copy still in flight.
-// `stream` waits for the edge pulls queued on `side` (nemo_ctx::side): before
-// anything rewrites the graphs or flags a pull reads
-static int join_side(nemo_ctx *c) {
-  if (!c->side_pending) return NEMO_OK;
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_side, 0));
-  c->side_pending = false;
-  return NEMO_OK;
-}
-
 static int guard_staged(nemo_ctx *c) {
   if (c->staged) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
-  return join_side(c);
+  return NEMO_OK;
 }
 
 template <class F>
@@ -466,7 +451,6 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   hipStreamSynchronize(c->stream);
   if (c->copy) hipStreamSynchronize(c->copy);
   if (c->aux) hipStreamSynchronize(c->aux);
-  if (c->side) hipStreamSynchronize(c->side);
   release_corpus(c);
   for (auto &p : c->pending) {
     hipEventDestroy(p.a);
@@ -500,9 +484,6 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
   if (c->aux) hipStreamDestroy(c->aux);
-  if (c->side) hipStreamDestroy(c->side);
-  if (c->ev_side) hipEventDestroy(c->ev_side);
-  if (c->ev_side_fork) hipEventDestroy(c->ev_side_fork);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
@@ -757,8 +738,6 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->copy) HIPCHK(c, hipStreamSynchronize(c->copy));
   if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
-  if (c->side) HIPCHK(c, hipStreamSynchronize(c->side));
-  c->side_pending = false;
   release_corpus(c);
   if (in->n_tables > NEMO_MAX_TABLES)
     return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
@@ -1329,7 +1308,6 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   HIPCHK(c, hipSetDevice(c->device));
   c->n_entries = 0;
   if (n_failed == 0 || c->run0 < 0) return NEMO_OK;  // MATCH on run 0 finds nothing
-  if (int rj = join_side(c)) return rj;  // a diff pull may still read the D masks rewritten below
   if (!c->ev_up_dsrc) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_dsrc, hipEventDisableTiming));
   else HIPCHK(c, hipEventSynchronize(c->ev_up_dsrc));  // the previous upload has landed
   if (int rg = hgrow(c, &c->h_dsrc, &c->h_dsrc_cap, 3 * n_failed)) return rg;
@@ -1888,14 +1866,7 @@ static int pull_launch(nemo_ctx *c) {
   a.dst = c->d_pdst;
   a.cap = c->pull_cap;
   const uint32_t slots = c->pull_dslots;
-  if (!c->side) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_side_fork, hipEventDisableTiming));
-  }
-  HIPCHK(c, hipEventRecord(c->ev_side_fork, c->stream));  // the graphs and flags the pull reads
-  HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_side_fork, 0));
-  hipStream_t s = c->side;
+  hipStream_t s = c->stream;
   double V = (double)c->V, E = (double)c->E;
   if (a.which == 2) {
     V = (double)slots * (double)a.mask_stride;
@@ -1903,14 +1874,12 @@ static int pull_launch(nemo_ctx *c) {
   }
   nemo::launch_zero(c->d_pcur, sizeof(unsigned long long), s);
   // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
-  int rc = timed_on(c, s, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
+  int rc = timed(c, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
   if (rc) return rc;
   nemo::launch_to_host(c->h_poff, c->d_poff, slots * 8ull, s);
   nemo::launch_to_host(c->h_pcnt, c->d_pcnt, slots * 4ull, s);
   nemo::launch_to_host(c->h_pcur, c->d_pcur, sizeof(unsigned long long), s);
   HIPCHK(c, hipEventRecord(c->ev_pull, s));
-  HIPCHK(c, hipEventRecord(c->ev_side, s));
-  c->side_pending = true;
   c->pull_synced = false;
   return NEMO_OK;
 }
@@ -1918,7 +1887,6 @@ static int pull_launch(nemo_ctx *c) {
 static int pull_grow(nemo_ctx *c, uint64_t total) {
   if (total <= c->pull_cap) return NEMO_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->side) HIPCHK(c, hipStreamSynchronize(c->side));  // a pull still writing the old buffers
   dfree(c, c->d_psrc);
   dfree(c, c->d_pdst);
   c->d_psrc = c->d_pdst = nullptr;
@@ -2125,7 +2093,6 @@ int nemo_synchronize(nemo_ctx *c) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
-  if (c->side) HIPCHK(c, hipStreamSynchronize(c->side));
   return NEMO_OK;
 }
 
