@@ -726,8 +726,8 @@ static int device_load(nemo_ctx *c) {
     return rc;
   if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
   // the multi-entry diff's relayout of run 0's post graph and its walk images
-  // follow the next diffprov, on its stream (they read the graph built here)
-  c->dx_img_key = -1;
+  // are built by the first diffprov after a load (nemo_rebuild re-derives the
+  // same graph: a relayout built from an earlier Kahn order of it stays valid)
   return NEMO_OK;
 }
 
@@ -1034,7 +1034,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
       p.err0 = nullptr;  // set at the first diffprov (the error flags are allocated with the corpus)
       p.r0lab = c->d_r0lab;
       p.r0dense = nv < (1ull << 28) ? c->d_r0dense : nullptr;  // positions << 4 must fit
-      if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
+      if ((rc = dalloc(c, &p.tpos, nv)) || (rc = dalloc(c, &p.pnode, nv)) || (rc = dalloc(c, &p.info, nv)) || (rc = dalloc(c, &p.lbeg, nv)) ||
           (rc = dalloc(c, &p.lend, nv)) || (rc = dalloc(c, &p.rp, nv + 1)) || (rc = dalloc(c, &p.fp, nv + 1)) ||
           (rc = dalloc(c, &p.rc, ne + 4)) || (rc = dalloc(c, &p.fc, ne + 4)) || (rc = dalloc(c, &p.r0pos, l.size())))
         return rc;

@@ -35,6 +35,7 @@ struct DiffArgs {
 struct DxPrep {
   uint32_t g0, V0, E0;
   uint32_t *tpos;            // [V0] node -> position
+  uint32_t *pnode;           // [V0] position -> node (the Kahn order the relayout was built from)
   uint32_t *info;            // [V0] level << 3 | DXI_RULE
   uint32_t *lbeg, *lend;     // [V0] first position of the position's Kahn level / of the next level
   uint32_t *rp, *rc;         // [V0 + 1], [E0 + 4] parents of position i, as positions

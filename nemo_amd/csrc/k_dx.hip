@@ -95,6 +95,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dxp_a(DevCorpus c, DxPrep p) {
   if (i >= gv.V) return;
   const uint32_t v = gv.topo[i];
   p.tpos[v] = i;
+  p.pnode[i] = v;
   p.rp[i] = gv.rp[v + 1] - gv.rp[v];
   p.fp[gv.V - 1u - i] = gv.fp[v + 1] - gv.fp[v];
   const uint32_t l = c.nlv[gv.n0 + v];
@@ -703,7 +704,6 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
   }
   if (!WHOLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LP lists
   __syncthreads();
-  const GraphView g0 = c.view(a.p.g0);
   constexpr int MB = 8;  // entries per thread per round, loads in flight together
   for (uint32_t e = 0; e < (uint32_t)NE; e++) {
     const uint32_t u = srcu(e), mx = s_lmax[e];
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
         if ((r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u) != mx) continue;
         const uint32_t k = atomicAdd(a.n_missing, 1u);
         a.missing[2 * k] = u;
-        a.missing[2 * k + 1] = g0.topo[pos];
+        a.missing[2 * k + 1] = a.p.pnode[pos];
       }
       continue;
     }
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
         if (m0 + q * NT + tid >= nl || sv[q] != mx) continue;
         const uint32_t k = atomicAdd(a.n_missing, 1u);
         a.missing[2 * k] = u;
-        a.missing[2 * k + 1] = g0.topo[pos[q]];
+        a.missing[2 * k + 1] = a.p.pnode[pos[q]];
       }
     }
   }
