@@ -88,6 +88,20 @@ struct Graph {
   std::string_view sv(Str s) const {
     return std::string_view(s.off < flen ? fb + s.off : arena.data() + (s.off - flen), s.len);
   }
+  // empty again, keeping the vectors' memory (a stream reuses its graphs chunk after chunk:
+  // no fresh pages to fault in)
+  void reset() {
+    file.reset();
+    fb = "";
+    flen = 0;
+    n_goals = 0;
+    for (auto *v : {&id, &label, &table, &type, &time, &tabs, &labs}) v->clear();
+    for (auto *v : {&src, &dst, &rank, &ltab, &llab}) v->clear();
+    arena.clear(), tclass.clear(), labh.clear(), err.clear();
+  }
+};
+struct Rec {  // a goal's or rule's fields: id, label, table, time / type
+  Str f[4];
 };
 
 // ---- open-addressing tables (the per-graph maps are hot: one lookup per node and edge) ----
@@ -360,8 +374,10 @@ inline bool id_num(std::string_view s, const char *pfx, uint32_t &n, uint32_t &n
   return true;
 }
 
-// per-thread maps of parse_graph, reused from graph to graph
+// per-thread maps and lists of parse_graph, reused from graph to graph
 struct ParseMaps {
+  std::vector<Rec> goals, rules;
+  std::vector<std::pair<Str, Str>> edges;
   NumMap gnum, rnum;
   FlatMap gidx, ridx, tabs, labs;
   FlatSet64 seen;
@@ -607,12 +623,10 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   const char *base = g.fb;
   const uint32_t bias = g.flen;
   Json j{base, base + fsz};
-  struct Rec {
-    Str f[4];
-  };
-  std::vector<Rec> goals, rules;
-  std::vector<std::pair<Str, Str>> edges;
-  goals.reserve(fsz / 160), rules.reserve(fsz / 160), edges.reserve(fsz / 64);
+  ParseMaps &M = t_maps;
+  std::vector<Rec> &goals = M.goals, &rules = M.rules;
+  std::vector<std::pair<Str, Str>> &edges = M.edges;
+  goals.clear(), rules.clear(), edges.clear();
   j.ws();
   if (j.lit("null")) {
   } else if (j.p < j.e && *j.p == '{') {
@@ -732,7 +746,6 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   g.n_goals = (uint32_t)goals.size();
   g.id.reserve(V), g.label.reserve(V), g.table.reserve(V), g.type.reserve(V), g.time.reserve(V);
   g.ltab.reserve(V), g.llab.reserve(V), g.tclass.reserve(V);
-  ParseMaps &M = t_maps;
   FlatMap &gidx = M.gidx, &ridx = M.ridx, &tabs = M.tabs, &labs = M.labs;
   gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
   auto intern = [&](FlatMap &m, std::vector<Str> &order, Str s) {
@@ -1043,6 +1056,8 @@ struct nemo_ingest_stream {
   bool have_run0 = false;
   uint64_t r0_nv[2] = {0, 0}, r0_ne[2] = {0, 0};
   std::vector<uint32_t> r0_word, r0_label, r0_rank, r0_src, r0_dst;
+  std::vector<Graph> gpool;                       // the chunks' graphs, reused (Graph::reset)
+  std::vector<std::vector<uint32_t>> tre, lre;    // their table / label ids
   // the chunks' arrays, double-buffered: chunk i stays valid while chunk i+1 is parsed
   struct Chunk {
     std::vector<uint32_t> it, word, label, rank, src, dst;
@@ -1088,7 +1103,8 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
   if (s->next >= R) return NEMO_ERR_NOTFOUND;
   const uint32_t a = s->next, b = std::min<uint32_t>(R, a + chunk), G = 2 * (b - a);
   s->next = b;
-  std::vector<Graph> gs(G);
+  if (s->gpool.size() < G) s->gpool.resize(G);
+  std::vector<Graph> &gs = s->gpool;
   int nt = std::max(1, std::min<int>(s->threads, (int)G));
   std::atomic<uint32_t> nextg{0};
   auto work = [&] {
@@ -1096,6 +1112,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
       const uint32_t r = s->order[a + g / 2];  // file names use the run index (molly.go:59-60)
       const char *cond = g % 2 ? "post" : "pre";
       std::string path = s->dir + "/run_" + std::to_string(r) + "_" + cond + "_provenance.json";
+      gs[g].reset();
       parse_graph(path, s->iteration[r], cond, gs[g]);
     }
   };
@@ -1105,7 +1122,9 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
   for (auto &t : pool) t.join();
   for (uint32_t g = 0; g < G; g++)
     if (!gs[g].err.empty()) return fail(gs[g].err);
-  std::vector<std::vector<uint32_t>> tre(G), lre(G);
+  if (s->tre.size() < G) s->tre.resize(G), s->lre.resize(G);
+  std::vector<std::vector<uint32_t>> &tre = s->tre, &lre = s->lre;
+  for (uint32_t g = 0; g < G; g++) tre[g].clear();
   auto add = [](std::deque<std::string> &names) {
     return [&names](std::string_view k) {
       names.emplace_back(k);
