@@ -598,6 +598,14 @@ uint8_t type_class(std::string_view t) {
   return t == "next" ? NEMO_TYPE_NEXT : t == "async" ? NEMO_TYPE_ASYNC : NEMO_TYPE_OTHER;
 }
 
+// a key's bytes and closing quote as a little-endian word (the in-place key match of parse_graph)
+#define KEY3(a, b) ((uint64_t)(a) | (uint64_t)(b) << 8 | (uint64_t)'"' << 16)
+#define KEY5(a, b, c, d) \
+  ((uint64_t)(a) | (uint64_t)(b) << 8 | (uint64_t)(c) << 16 | (uint64_t)(d) << 24 | (uint64_t)'"' << 32)
+#define KEY6(a, b, c, d, e)                                                                              \
+  ((uint64_t)(a) | (uint64_t)(b) << 8 | (uint64_t)(c) << 16 | (uint64_t)(d) << 24 | (uint64_t)(e) << 32 | \
+   (uint64_t)'"' << 40)
+
 // key k (a view into the arena) equals the lower-case keyword s, case-insensitively
 // (encoding/json matches keys case-insensitively): the exact spelling first
 inline bool keyis(std::string_view k, const char *s, size_t n) {
@@ -666,24 +674,45 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
               if (j.p < j.e && *j.p == '}') j.p++;
               else
                 while (j.ok) {
-                  Str kst;
-                  if (!j.sview(g.arena, base, bias, kst)) break;
-                  const std::string_view k = g.sv(kst);
+                  int f = -1;
+                  // the exact lower-case keys, matched in place (the closing quote included)
+                  if (j.e - j.p >= 9 && *j.p == '"') {
+                    const uint64_t w = load8(j.p + 1);
+                    uint32_t adv = 0;
+                    if (which == 2) {
+                      if ((w & 0xFFFFFFFFFFull) == KEY5('f', 'r', 'o', 'm')) f = 0, adv = 6;
+                      else if ((w & 0xFFFFFFull) == KEY3('t', 'o')) f = 1, adv = 4;
+                    } else if ((w & 0xFFFFFFull) == KEY3('i', 'd')) {
+                      f = 0, adv = 4;
+                    } else if ((w & 0xFFFFFFFFFFFFull) == KEY6('l', 'a', 'b', 'e', 'l')) {
+                      f = 1, adv = 7;
+                    } else if ((w & 0xFFFFFFFFFFFFull) == KEY6('t', 'a', 'b', 'l', 'e')) {
+                      f = 2, adv = 7;
+                    } else if ((w & 0xFFFFFFFFFFull) ==
+                               (which == 0 ? KEY5('t', 'i', 'm', 'e') : KEY5('t', 'y', 'p', 'e'))) {
+                      f = 3, adv = 6;
+                    }
+                    j.p += adv;
+                  }
+                  if (f < 0) {  // any other spelling or key (encoding/json matches keys case-insensitively)
+                    Str kst;
+                    if (!j.sview(g.arena, base, bias, kst)) break;
+                    const std::string_view k = g.sv(kst);
+                    if (which == 2) {
+                      f = keyis(k, "from", 4) ? 0 : keyis(k, "to", 2) ? 1 : -1;
+                    } else {
+                      if (keyis(k, "id", 2)) f = 0;
+                      else if (keyis(k, "label", 5)) f = 1;
+                      else if (keyis(k, "table", 5)) f = 2;
+                      else if (keyis(k, which == 0 ? "time" : "type", 4)) f = 3;
+                    }
+                  }
                   j.ws();
                   if (j.p >= j.e || *j.p != ':') {
                     j.ok = false;
                     break;
                   }
                   j.p++;
-                  int f = -1;
-                  if (which == 2) {
-                    f = keyis(k, "from", 4) ? 0 : keyis(k, "to", 2) ? 1 : -1;
-                  } else {
-                    if (keyis(k, "id", 2)) f = 0;
-                    else if (keyis(k, "label", 5)) f = 1;
-                    else if (keyis(k, "table", 5)) f = 2;
-                    else if (keyis(k, which == 0 ? "time" : "type", 4)) f = 3;
-                  }
                   j.ws();
                   if (f < 0) {
                     j.skip();
