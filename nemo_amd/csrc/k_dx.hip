@@ -581,7 +581,7 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
           if (u == NEMO_NONE) continue;
           const uint32_t r = (uint32_t)ringp(e)[sl];
           const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
-          gvalp(e)[i] = (T)sv;
+          if (!WHOLE) gvalp(e)[i] = (T)sv;  // read back by later windows' misses and the rows pass
           if ((lpb[e * LW + (kk >> 5)] >> (kk & 31u)) & 1u) {
             lmax[e] = max(lmax[e], sv);
             if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
