@@ -471,18 +471,32 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
         eng.simplified_view()
         return vec
 
+    phase = {"load_s": [], "analyse_s": [], "join_wait_s": []}
+
+    def timed_load(eng, c):
+        t = time.perf_counter()
+        eng.load(c)
+        eng.synchronize()
+        phase["load_s"].append(round(time.perf_counter() - t, 3))
+
     def one_pass():
+        for v in phase.values():
+            v.clear()
         vec = np.zeros(2 * T + 4, np.int64)
-        engines[0].load(batches[0])
+        timed_load(engines[0], batches[0])
         for i in range(len(batches)):
             th = None
             if i + 1 < len(batches):
                 nxt = engines[(i + 1) % 2]
-                th = threading.Thread(target=nxt.load, args=(batches[i + 1],))
+                th = threading.Thread(target=timed_load, args=(nxt, batches[i + 1]))
                 th.start()
+            t = time.perf_counter()
             vec += analyse(engines[i % 2], batches[i])
+            phase["analyse_s"].append(round(time.perf_counter() - t, 3))
             if th is not None:
+                t = time.perf_counter()
                 th.join()
+                phase["join_wait_s"].append(round(time.perf_counter() - t, 3))
         torch.cuda.synchronize()
         return E.reduce_interpret(vec.astype(np.uint32), T, batches[0].table_post)
 
@@ -520,6 +534,7 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
                       "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped)",
                       "lib_options": args.set},
            "roofline": None, "cpu_baseline": None, "gen_seconds_rank0": round(gen_s, 2),
+           "pass_phases_rank0": dict(phase),
            "note": "no per-kernel roofline on this line: the resident-batch line (--config c5) carries it"}
     if rank == 0:
         line = json.dumps(out)
