@@ -71,6 +71,10 @@ struct nemo_ctx {
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
   std::vector<void *> allocs;
+  std::unordered_map<void *, size_t> alloc_bytes;  // every live allocation's size (allocs and the cache)
+  // blocks of the previous corpus, kept for the next load (nemo_load_corpus frees
+  // what it did not reuse): reloading a corpus of the same shape allocates nothing
+  std::multimap<size_t, void *> cache;
   uint32_t *d_red = nullptr;
 
   // diff
@@ -200,6 +204,15 @@ static int fail(nemo_ctx *c, int code, const char *fmt, ...) {
     if (e_ != hipSuccess) return fail((c), NEMO_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_));     \
   } while (0)
 
+// the cached blocks (nemo_ctx::cache)
+static void drop_cache(nemo_ctx *c) {
+  for (auto &b : c->cache) {
+    c->alloc_bytes.erase(b.second);
+    hipFree(b.second);
+  }
+  c->cache.clear();
+}
+
 template <class T>
 static int dalloc(nemo_ctx *c, T **p, size_t n) {
   void *q = nullptr;
@@ -207,9 +220,24 @@ static int dalloc(nemo_ctx *c, T **p, size_t n) {
   // whole 16-byte chunks: stage_lds (device.h) loads aligned 16-B chunks, so
   // the chunk holding a buffer's last byte must lie inside the allocation
   const size_t bytes = (n * sizeof(T) + 15) & ~(size_t)15;
-  hipError_t e = hipMalloc(&q, bytes);
-  if (e != hipSuccess)
-    return fail(c, NEMO_ERR_HIP, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+  auto it = c->cache.lower_bound(bytes);  // the smallest cached block that fits, if not much larger
+  if (it != c->cache.end() && it->first <= bytes + bytes / 8 + (1u << 20)) {
+    q = it->second;
+    c->cache.erase(it);
+  } else {
+    // large blocks get a little headroom, so that the next corpus of about the same shape reuses them
+    const size_t want = bytes >= (64u << 20) ? ((bytes + bytes / 32) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1) : bytes;
+    hipError_t e = hipMalloc(&q, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      drop_cache(c);  // no room: the cached blocks go first, then the headroom
+      e = hipMalloc(&q, bytes);
+      if (e != hipSuccess) return fail(c, NEMO_ERR_HIP, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+      c->alloc_bytes[q] = bytes;
+    } else {
+      c->alloc_bytes[q] = want;
+    }
+  }
   c->allocs.push_back(q);
   *p = (T *)q;
   return NEMO_OK;
@@ -230,8 +258,10 @@ static void dfree(nemo_ctx *c, void *p) {
   if (!p) return;
   auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
   if (it != c->allocs.end()) c->allocs.erase(it);
+  c->alloc_bytes.erase(p);
   hipFree(p);
 }
+
 
 static hipEvent_t get_event(nemo_ctx *c) {
   if (!c->ev_pool.empty()) {
@@ -389,7 +419,12 @@ int nemo_ctx_create(int device, nemo_ctx **out) {
 }
 
 static void release_corpus(nemo_ctx *c) {
-  for (void *p : c->allocs) hipFree(p);
+  drop_cache(c);  // blocks no allocation took since the last load
+  for (void *p : c->allocs) {  // kept for the next load
+    auto b = c->alloc_bytes.find(p);
+    if (b != c->alloc_bytes.end()) c->cache.emplace(b->second, p);
+    else hipFree(p);
+  }
   c->allocs.clear();
   c->dc = DevCorpus{};
   c->d_owned = c->d_is_success = nullptr;
@@ -455,6 +490,7 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->copy) hipStreamSynchronize(c->copy);
   if (c->aux) hipStreamSynchronize(c->aux);
   release_corpus(c);
+  drop_cache(c);
   for (auto &p : c->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
