@@ -966,50 +966,14 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   hipStream_t s = c->stream;
   HIPCHK(c, hipMemcpyAsync(no, in->node_off, (G + 1) * 8, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(eo, in->edge_off, (G + 1) * 8, hipMemcpyHostToDevice, s));
-  {
-    // the bulk arrays come from pageable host memory, which the runtime copies
-    // through its staging buffers one copy at a time: 64 MB pieces on a few
-    // host threads and streams keep several in flight (C5 batches: ~15 GB each)
-    std::vector<std::tuple<void *, const void *, size_t>> jobs;
-    auto add = [&](void *d, const void *h, size_t bytes) {
-      for (size_t o = 0; o < bytes; o += (64u << 20))
-        jobs.emplace_back((char *)d + o, (const char *)h + o, std::min<size_t>(64u << 20, bytes - o));
-    };
-    if (V) {
-      add(word, in->node_word, V * 4);
-      add(label, in->label, V * 4);
-      if (rank) add(rank, in->id_rank, V * 4);
-    }
-    if (E) {
-      add(es, in->edge_src, E * 4);
-      add(ed, in->edge_dst, E * 4);
-    }
-    const int nt = (int)std::min<size_t>(jobs.size(), 8);
-    if (nt <= 1) {
-      for (auto &j : jobs)
-        HIPCHK(c, hipMemcpyAsync(std::get<0>(j), std::get<1>(j), std::get<2>(j), hipMemcpyHostToDevice, s));
-    } else {
-      HIPCHK(c, hipStreamSynchronize(s));  // the copies below run beside `stream`, not on it
-      std::atomic<size_t> next{0};
-      std::atomic<int> bad{0};
-      auto work = [&] {
-        hipStream_t st = nullptr;
-        if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-          bad = 1;
-          return;
-        }
-        for (size_t k; (k = next.fetch_add(1)) < jobs.size();)
-          if (hipMemcpyAsync(std::get<0>(jobs[k]), std::get<1>(jobs[k]), std::get<2>(jobs[k]), hipMemcpyHostToDevice,
-                             st) != hipSuccess)
-            bad = 1;
-        if (hipStreamSynchronize(st) != hipSuccess) bad = 1;
-        hipStreamDestroy(st);
-      };
-      std::vector<std::thread> pool;
-      for (int i = 0; i < nt; i++) pool.emplace_back(work);
-      for (auto &t : pool) t.join();
-      if (bad) return fail(c, NEMO_ERR_HIP, "corpus upload failed");
-    }
+  if (V) {
+    HIPCHK(c, hipMemcpyAsync(word, in->node_word, V * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(label, in->label, V * 4, hipMemcpyHostToDevice, s));
+    if (rank) HIPCHK(c, hipMemcpyAsync(rank, in->id_rank, V * 4, hipMemcpyHostToDevice, s));
+  }
+  if (E) {
+    HIPCHK(c, hipMemcpyAsync(es, in->edge_src, E * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(ed, in->edge_dst, E * 4, hipMemcpyHostToDevice, s));
   }
   HIPCHK(c, hipMemcpyAsync(c->d_owned, c->owned.data(), R, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemsetAsync(d.nch, 0, G * 4, s));
