@@ -792,7 +792,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_lp(DxArgs a) {
 
 // ---- D masks by node for every entry ------------------------------------------------
 // thread: one node, DXM_E consecutive entries (entries of one source share its bit word)
-#define DXM_E 8u
+#define DXM_E 32u
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
   const uint32_t V = a.p.V0, v = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (v >= V) return;
