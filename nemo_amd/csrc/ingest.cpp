@@ -355,9 +355,13 @@ struct ShardIntern {
 struct NumMap {
   std::vector<uint32_t> v;     // n -> node | digits << 28 (~0u: none)
   std::vector<uint32_t> used;  // the n set for this graph (cleared after it)
+  uint32_t nd0 = 0, nmax = 0;  // the first ID's digit count, the largest n
+  bool uniform = true;         // every ID has nd0 digits: n order is the IDs' string order
   void clear() {
     for (uint32_t n : used) v[n] = ~0u;
     used.clear();
+    nd0 = nmax = 0;
+    uniform = true;
   }
 };
 // n and digit count of "<pfx><digits>" (4-byte prefix, 1..9 digits)
@@ -823,6 +827,9 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
         num = false;
       } else if (nm.v[n] == ~0u) {
         nm.v[n] = (base + k) | (nd << 28);
+        if (nm.used.empty()) nm.nd0 = nd;
+        nm.uniform &= nd == nm.nd0;
+        nm.nmax = std::max(nm.nmax, n);
         nm.used.push_back(n);
       } else if ((nm.v[n] >> 28) != nd) {
         num = false;  // "goal7" and "goal07": the hash map tells them apart
@@ -879,6 +886,15 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     g.llab.push_back(intern_label(r.f[1]));
     g.tclass.push_back(type_class(g.sv(r.f[3])));
   }
+  if (gnumk == 1 && rnumk == 1 && M.gnum.uniform && M.rnum.uniform) {
+    // "goal<n>" / "rule<n>" with one digit count per kind: string order is
+    // every goal ("g" < "r"), then every rule, each by n -- the arrays in order
+    g.rank.assign(V, 0);
+    uint32_t pos = 0;
+    for (const NumMap *nm : {&M.gnum, &M.rnum})
+      for (uint32_t n = 0; n <= nm->nmax && !nm->used.empty(); n++)
+        if (nm->v[n] != ~0u) g.rank[nm->v[n] & ((1u << 28) - 1u)] = pos++;
+  } else {
   // rank of each node's ID inside the graph (the prefix is common, so unprefixed order == prefixed order)
   // sorted by 8-byte big-endian keys taken at offset 0 (a shorter ID pads with
   // zero bytes, so the key order agrees with the string order); a run of equal
@@ -930,6 +946,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   }
   g.rank.assign(V, 0);
   for (uint32_t pos = 0; pos < V; pos++) g.rank[order[pos].second] = pos;
+  }
   FlatSet64 &seen = M.seen;
   seen.init(edges.size());
   size_t created = 0;
