@@ -367,6 +367,20 @@ struct NumMap {
 // n and digit count of "<pfx><digits>" (4-byte prefix, 1..9 digits)
 inline bool id_num(std::string_view s, const char *pfx, uint32_t &n, uint32_t &nd) {
   if (s.size() < 5 || s.size() > 13 || memcmp(s.data(), pfx, 4)) return false;
+  if (s.size() == 12) {  // eight digits (zero-padded IDs) at once: all in '0'..'9', then combined in pairs
+    uint64_t v;
+    memcpy(&v, s.data() + 4, 8);
+    if ((v & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull ||
+        ((v + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull)
+      return false;
+    v &= 0x0F0F0F0F0F0F0F0Full;
+    v = (v * 2561) >> 8;
+    v = ((v & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+    v = ((v & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+    n = (uint32_t)v;
+    nd = 8;
+    return true;
+  }
   uint32_t x = 0;
   for (size_t i = 4; i < s.size(); i++) {
     const uint32_t d = (uint32_t)(unsigned char)s[i] - '0';
