@@ -19,7 +19,6 @@
 #include <array>
 #include <atomic>
 #include <deque>
-#include <memory>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -76,8 +75,6 @@ struct Graph {
   // Str offsets below flen are bytes of the mapped file (strings without
   // escapes), at and above it the arena (decoded strings, clock times)
   FileMap file;
-  std::unique_ptr<char[]> fbuf;  // or the file read into this buffer (reused from chunk to chunk)
-  size_t fcap = 0;
   const char *fb = "";
   uint32_t flen = 0;
   std::vector<char> arena;
@@ -637,40 +634,16 @@ inline bool keyis(std::string_view k, const char *s, size_t n) {
   return true;
 }
 
-// the whole file into g's reusable buffer (read(2): no mapping to set up and
-// tear down under the process's memory-map lock, no fresh pages once warm)
-bool read_file(const char *path, Graph &g, size_t &n) {
-  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return false;
-  struct stat st;
-  bool ok = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
-  n = ok ? (size_t)st.st_size : 0;
-  if (ok && n > g.fcap) {
-    g.fbuf.reset(new char[n]);
-    g.fcap = n;
-  }
-  for (size_t o = 0; ok && o < n;) {
-    const ssize_t r = ::read(fd, g.fbuf.get() + o, n - o);
-    if (r <= 0) ok = false;
-    else o += (size_t)r;
-  }
-  close(fd);
-  return ok;
-}
-
-void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g, bool via_read = false) {
-  // the file is mapped (or read into a reused buffer): strings without escapes
-  // are views of it, decoded ones and clock times go to the arena (reserved: no
-  // reallocation, the maps hold views)
-  size_t fsz = 0;
-  const bool ok = via_read ? read_file(path.c_str(), g, fsz) : g.file.open(path.c_str());
-  if (!via_read) fsz = g.file.n;
-  if (!ok || fsz >= 0xF0000000u) {
+void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g) {
+  // the file is mapped: strings without escapes are views of it, decoded ones
+  // and clock times go to the arena (reserved: no reallocation, the maps hold views)
+  if (!g.file.open(path.c_str()) || g.file.n >= 0xF0000000u) {
     g.err = "Failed reading " + std::string(cond == std::string("pre") ? "antecedent" : "consequent") +
             " provenance of file '" + path + "'";
     return;
   }
-  if (fsz) g.fb = via_read ? g.fbuf.get() : (const char *)g.file.p;
+  const size_t fsz = g.file.n;
+  if (fsz) g.fb = (const char *)g.file.p;
   g.flen = (uint32_t)fsz;
   g.arena.reserve(2 * fsz + 64);
   const char *base = g.fb;
@@ -1200,7 +1173,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
       const char *cond = g % 2 ? "post" : "pre";
       std::string path = s->dir + "/run_" + std::to_string(r) + "_" + cond + "_provenance.json";
       gs[g].reset();
-      parse_graph(path, s->iteration[r], cond, gs[g], true);
+      parse_graph(path, s->iteration[r], cond, gs[g]);
     }
   };
   std::vector<std::thread> pool;
