@@ -18,7 +18,11 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -250,6 +254,67 @@ struct InternMap {
   }
 };
 
+// n persistent workers (a stream's, so that their per-thread maps and lists
+// stay allocated from chunk to chunk); run(f) runs f once on every worker
+class WorkerPool {
+ public:
+  explicit WorkerPool(int n) {
+    for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  void run(const std::function<void()> &f) {
+    std::unique_lock<std::mutex> l(m_);
+    job_ = &f;
+    left_ = (int)th_.size();
+    gen_++;
+    cv_.notify_all();
+    done_.wait(l, [this] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(m_);
+    for (;;) {
+      cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void()> *f = job_;
+      l.unlock();
+      (*f)();
+      l.lock();
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void()> *job_ = nullptr;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+  bool stop_ = false;
+};
+
+// f on nt threads: the pool's workers, or nt - 1 new threads and the caller
+using Runner = std::function<void(const std::function<void()> &)>;
+inline Runner make_runner(WorkerPool *pool, int nt) {
+  if (pool) return [pool](const std::function<void()> &f) { pool->run(f); };
+  return [nt](const std::function<void()> &f) {
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; i++) th.emplace_back(f);
+    f();
+    for (auto &t : th) t.join();
+  };
+}
+
 // The global label interning, sharded by hash so that threads intern in
 // parallel with the sequential result.  A label's shard is fixed by its hash;
 // each shard is filled by one thread walking the graphs in order, so an entry
@@ -301,7 +366,8 @@ struct ShardIntern {
   // new label's name (its index is the global id) and returns the view the
   // shard keeps from then on (the graphs' arenas may not outlive the call).
   template <class Add>
-  bool merge(std::vector<Graph> &gs, uint32_t G, int nt, std::vector<std::vector<uint32_t>> &lre, Add &&add) {
+  bool merge(std::vector<Graph> &gs, uint32_t G, int nt, const Runner &run, std::vector<std::vector<uint32_t>> &lre,
+             Add &&add) {
     for (uint32_t g = 0; g < G; g++) lre[g].assign(gs[g].labs.size(), 0);
     if (sh.empty()) sh.resize((size_t)std::min(64, std::max(1, nt)));
     const uint32_t S = (uint32_t)sh.size();
@@ -320,10 +386,7 @@ struct ShardIntern {
         }
       }
     };
-    std::vector<std::thread> pool;
-    for (int i = 1; i < nt; i++) pool.emplace_back(phase_a);
-    phase_a();
-    for (auto &t : pool) t.join();
+    run(phase_a);
     for (uint32_t g = 0; g < G; g++)  // first appearances in graph order
       for (uint32_t &x : lre[g])
         if (x & NEW) {
@@ -339,10 +402,7 @@ struct ShardIntern {
       for (uint32_t g; (g = nextg.fetch_add(1)) < G;)
         for (uint32_t &x : lre[g]) x = sh[x >> SH].gid[x & ((1u << SH) - 1u)];
     };
-    pool.clear();
-    for (int i = 1; i < nt; i++) pool.emplace_back(phase_c);
-    phase_c();
-    for (auto &t : pool) t.join();
+    run(phase_c);
     return true;
   }
 };
@@ -1027,10 +1087,8 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
       parse_graph(path, h->iteration[r], cond, h->graphs[g]);
     }
   };
-  std::vector<std::thread> pool;
-  for (int i = 1; i < nt; i++) pool.emplace_back(work);
-  work();
-  for (auto &t : pool) t.join();
+  const Runner run = make_runner(nullptr, nt);
+  run(work);
   for (uint32_t g = 0; g < G; g++)
     if (!h->graphs[g].err.empty()) {
       std::string m = h->graphs[g].err;
@@ -1058,7 +1116,7 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
     h->node_off[g + 1] = h->node_off[g] + gr.id.size();
     h->edge_off[g + 1] = h->edge_off[g] + gr.src.size();
   }
-  if (!lmap.merge(h->graphs, G, nt, lre, [&](std::string_view k) {
+  if (!lmap.merge(h->graphs, G, nt, run, lre, [&](std::string_view k) {
         h->labels.emplace_back(k);
         return k;  // the arenas live as long as the ingest
       })) {
@@ -1088,10 +1146,7 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
       std::copy(gr.dst.begin(), gr.dst.end(), h->dst.begin() + e0);
     }
   };
-  pool.clear();
-  for (int i = 1; i < nt; i++) pool.emplace_back(fill);
-  fill();
-  for (auto &t : pool) t.join();
+  run(fill);
   *out = h;
   return NEMO_OK;
 }
@@ -1117,6 +1172,7 @@ struct nemo_ingest_stream {
   uint64_t r0_nv[2] = {0, 0}, r0_ne[2] = {0, 0};
   std::vector<uint32_t> r0_word, r0_label, r0_rank, r0_src, r0_dst;
   std::vector<Graph> gpool;                       // the chunks' graphs, reused (Graph::reset)
+  std::unique_ptr<WorkerPool> workers;            // the parse / merge / fill threads, kept across chunks
   std::vector<std::vector<uint32_t>> tre, lre;    // their table / label ids
   // the chunks' arrays, double-buffered: chunk i stays valid while chunk i+1 is parsed
   struct Chunk {
@@ -1176,10 +1232,9 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
       parse_graph(path, s->iteration[r], cond, gs[g]);
     }
   };
-  std::vector<std::thread> pool;
-  for (int i = 1; i < nt; i++) pool.emplace_back(work);
-  work();
-  for (auto &t : pool) t.join();
+  if (!s->workers) s->workers.reset(new WorkerPool(s->threads));
+  const Runner run = make_runner(s->workers.get(), nt);
+  run(work);
   for (uint32_t g = 0; g < G; g++)
     if (!gs[g].err.empty()) return fail(gs[g].err);
   if (s->tre.size() < G) s->tre.resize(G), s->lre.resize(G);
@@ -1195,7 +1250,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
     tre[g].reserve(gs[g].tabs.size());
     for (Str x : gs[g].tabs) tre[g].push_back(s->tmap.intern(gs[g].sv(x), add(s->tables)));
   }
-  if (!s->lmap.merge(gs, G, nt, lre, [&](std::string_view k) {
+  if (!s->lmap.merge(gs, G, nt, run, lre, [&](std::string_view k) {
         s->labels.emplace_back(k);
         return std::string_view(s->labels.back());  // the chunk's arenas go away
       }))
@@ -1258,10 +1313,7 @@ extern "C" int nemo_ingest_next(nemo_ingest_stream *s, uint32_t chunk, int with_
       std::copy(gr.dst.begin(), gr.dst.end(), ck.dst.begin() + e0);
     }
   };
-  pool.clear();
-  for (int i = 1; i < nt; i++) pool.emplace_back(fill);
-  fill();
-  for (auto &t : pool) t.join();
+  run(fill);
   if (s->run0 >= a && s->run0 < b) {  // keep run 0 for the chunks after this one
     const uint32_t g0 = gbase + 2 * (uint32_t)(s->run0 - a);
     const uint64_t n0 = ck.node_off[g0], n1 = ck.node_off[g0 + 2], e0 = ck.edge_off[g0], e1 = ck.edge_off[g0 + 2];
