@@ -115,13 +115,39 @@ inline uint64_t load8(const char *p) {
   memcpy(&w, p, 8);
   return w;
 }
+// a == b with short keys compared inline (no memcmp call): up to 16 bytes as two
+// overlapping loads each way, exact bytes only
+inline bool sveq(std::string_view a, std::string_view b) {
+  const size_t n = a.size();
+  if (n != b.size()) return false;
+  const char *x = a.data(), *y = b.data();
+  if (n >= 8) {
+    if (n > 16) return !memcmp(x, y, n);
+    return load8(x) == load8(y) && load8(x + n - 8) == load8(y + n - 8);
+  }
+  if (n >= 4) {
+    uint32_t x0, x1, y0, y1;
+    memcpy(&x0, x, 4), memcpy(&x1, x + n - 4, 4), memcpy(&y0, y, 4), memcpy(&y1, y + n - 4, 4);
+    return x0 == y0 && x1 == y1;
+  }
+  for (size_t i = 0; i < n; i++)
+    if (x[i] != y[i]) return false;
+  return true;
+}
 inline uint64_t hash_sv(std::string_view s) {
   const size_t n = s.size();
   const char *p = s.data();
   uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
-  if (n <= 8) {  // exact bytes (a short key may end a buffer)
+  if (n <= 8) {  // exact bytes (a short key may end a buffer): for a given n these words tell every key apart
     uint64_t w = 0;
-    memcpy(&w, p, n);
+    if (n >= 4) {
+      uint32_t a, b;
+      memcpy(&a, p, 4);
+      memcpy(&b, p + n - 4, 4);
+      w = (uint64_t)a | (uint64_t)b << 32;
+    } else if (n) {
+      w = (uint64_t)(uint8_t)p[0] | (uint64_t)(uint8_t)p[n / 2] << 8 | (uint64_t)(uint8_t)p[n - 1] << 16;
+    }
     h = (h ^ w) * 0xff51afd7ed558ccdull;
   } else if (n <= 16) {
     h = (h ^ load8(p)) * 0xff51afd7ed558ccdull;
@@ -172,7 +198,7 @@ struct FlatMap {
         key[i] = k;
         return {v, true};
       }
-      if (sl.tag == tag && key[i] == k) return {sl.val, false};
+      if (sl.tag == tag && sveq(key[i], k)) return {sl.val, false};
     }
   }
   uint32_t find(std::string_view k) const {
@@ -181,32 +207,33 @@ struct FlatMap {
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       const Slot &sl = slot[i];
       if (sl.epoch != epoch) return ~0u;
-      if (sl.tag == tag && key[i] == k) return sl.val;
+      if (sl.tag == tag && sveq(key[i], k)) return sl.val;
     }
   }
 };
 
-struct FlatSet64 {  // u64 keys, reused like FlatMap
-  struct Slot {
-    uint64_t key;
-    uint32_t epoch, pad;
-  };
-  std::vector<Slot> slot;
+// u64 keys whose bits 28-31 and 60-63 are clear (two u28 node indices), reused
+// like FlatMap: the slot's epoch sits in those bits (8-byte slots)
+struct FlatSet64 {
+  std::vector<uint64_t> slot;
   size_t mask = 0;
-  uint32_t epoch = 0;
+  uint32_t epoch = 0;  // 1..255
+  static uint64_t tagged(uint64_t k, uint32_t e) { return k | (uint64_t)(e & 0xFu) << 28 | (uint64_t)(e >> 4) << 60; }
   void init(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
-    if (cap > slot.size() || ++epoch == 0) {
-      slot.assign(std::max(cap, slot.size()), Slot{0, 0, 0});
+    if (cap > slot.size() || ++epoch == 256) {
+      slot.assign(std::max(cap, slot.size()), 0);  // epoch 0: empty
       epoch = 1;
     }
     mask = cap - 1;
   }
   bool insert(uint64_t k) {
+    const uint64_t t = tagged(k, epoch), em = tagged(0, 0xFFu);
     for (size_t h = ((k * 0x9E3779B97F4A7C15ull) >> 20) & mask;; h = (h + 1) & mask) {
-      if (slot[h].epoch != epoch) return slot[h] = Slot{k, epoch, 0}, true;
-      if (slot[h].key == k) return false;
+      const uint64_t x = slot[h];
+      if ((x & em) != (t & em)) return slot[h] = t, true;
+      if (x == t) return false;
     }
   }
 };
@@ -249,7 +276,7 @@ struct InternMap {
         n++;
         return m.first;
       }
-      if (slot[i].tag == tag && key[i] == k) return slot[i].val;
+      if (slot[i].tag == tag && sveq(key[i], k)) return slot[i].val;
     }
   }
 };
@@ -354,7 +381,7 @@ struct ShardIntern {
           gid.push_back(~0u);
           return {val[i], true};
         }
-        if (tag[i] == t && key[val[i]] == k) return {val[i], false};
+        if (tag[i] == t && sveq(key[val[i]], k)) return {val[i], false};
       }
     }
   };
@@ -471,11 +498,11 @@ struct Json {
   static constexpr int kMaxDepth = 512;
   std::vector<char> key;  // scratch for object keys (capacity reused)
 
-  void ws() {
+  __attribute__((always_inline)) void ws() {
     if (p < e && (unsigned char)*p > ' ') return;  // the common case: no white space
     while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) p++;
   }
-  bool lit(const char *s) {
+  __attribute__((always_inline)) bool lit(const char *s) {
     if (p >= e || *p != *s) return false;
     const size_t n = strlen(s);
     if ((size_t)(e - p) >= n && !memcmp(p, s, n)) {
@@ -519,7 +546,7 @@ struct Json {
     return v;
   }
   // the first '"' or '\\' at or after q (e if none), 16 bytes at a time
-  const char *scan(const char *q) const {
+  __attribute__((always_inline)) const char *scan(const char *q) const {
     const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\');
     while (e - q >= 16) {
       const __m128i x = _mm_loadu_si128((const __m128i *)q);
@@ -532,7 +559,7 @@ struct Json {
   }
   // a string as a view: in place when it has no escapes (offset from base, the
   // buffer the reader walks), else decoded and appended to `o` (offset bias + its place in o)
-  bool sview(std::vector<char> &o, const char *base, uint32_t bias, Str &out) {
+  __attribute__((always_inline)) bool sview(std::vector<char> &o, const char *base, uint32_t bias, Str &out) {
     ws();
     if (p >= e || *p != '"') return ok = false;
     const char *q = scan(p + 1);
@@ -651,13 +678,14 @@ struct Json {
   }
 };
 
-// ", <digits>, __WILDCARD__)" and ", <digits>, <digits>)" (molly.go:74-89): leftmost match, group 1
-bool clock_time(std::string_view s, bool wild, std::string &out) {
+// ", <digits>, __WILDCARD__)" and ", <digits>, <digits>)" (molly.go:74-89):
+// the leftmost match's group 1 as [*d0, *d0 + *dn) of s
+bool clock_time(std::string_view s, bool wild, size_t *d0, size_t *dn) {
   for (size_t i = 0; i + 2 <= s.size(); i++) {
     if (s[i] != ',' || s[i + 1] != ' ') continue;
-    size_t j = i + 2, d0 = j;
+    size_t j = i + 2, a = j;
     while (j < s.size() && isdigit((unsigned char)s[j])) j++;
-    if (j == d0 || j + 2 > s.size() || s[j] != ',' || s[j + 1] != ' ') continue;
+    if (j == a || j + 2 > s.size() || s[j] != ',' || s[j + 1] != ' ') continue;
     size_t k = j + 2;
     if (wild) {
       if (s.substr(k, 13) != "__WILDCARD__)") continue;
@@ -666,7 +694,7 @@ bool clock_time(std::string_view s, bool wild, std::string &out) {
       while (k < s.size() && isdigit((unsigned char)s[k])) k++;
       if (k == k0 || k >= s.size() || s[k] != ')') continue;
     }
-    out.assign(s.data() + d0, j - d0);
+    *d0 = a, *dn = j - a;
     return true;
   }
   return false;
@@ -851,8 +879,10 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   }
   const size_t V = goals.size() + rules.size();
   g.n_goals = (uint32_t)goals.size();
-  g.id.reserve(V), g.label.reserve(V), g.table.reserve(V), g.type.reserve(V), g.time.reserve(V);
-  g.ltab.reserve(V), g.llab.reserve(V), g.tclass.reserve(V);
+  // sized once and written by index (a push_back per field and node was a
+  // capacity check each)
+  g.id.resize(V), g.label.resize(V), g.table.resize(V), g.type.resize(V), g.time.resize(V);
+  g.ltab.resize(V), g.llab.resize(V), g.tclass.resize(V);
   FlatMap &gidx = M.gidx, &ridx = M.ridx, &tabs = M.tabs, &labs = M.labs;
   gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
   auto intern = [&](FlatMap &m, std::vector<Str> &order, Str s) {
@@ -869,7 +899,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   uint32_t last_tid = ~0u;
   auto intern_table = [&](Str s) {
     const std::string_view k = g.sv(s);
-    if (last_tid != ~0u && k.size() == last_tab.size() && !memcmp(k.data(), last_tab.data(), k.size())) return last_tid;
+    if (last_tid != ~0u && sveq(k, last_tab)) return last_tid;
     last_tab = k;
     return last_tid = intern(tabs, g.tabs, s);
   };
@@ -934,31 +964,29 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     M.gnum.clear(), M.rnum.clear();
     return;
   }
-  for (auto &r : goals) {
+  for (uint32_t i = 0; i < goals.size(); i++) {
+    const Rec &r = goals[i];
     Str t = r.f[3];
-    if (g.sv(r.f[2]) == "clock") {  // molly.go:74-89
-      std::string tm;
-      std::string_view lab = g.sv(r.f[1]);
-      bool hit = clock_time(lab, true, tm);
-      std::string tm2;
-      if (clock_time(lab, false, tm2)) tm = tm2, hit = true;
-      if (hit) {
-        t = Str{g.flen + (uint32_t)g.arena.size(), (uint32_t)tm.size()};
-        g.arena.insert(g.arena.end(), tm.begin(), tm.end());
-      }
+    if (g.sv(r.f[2]) == "clock") {  // molly.go:74-89: the two-number match wins over the wildcard one
+      // the time is a substring of the label: a view at the label's offset
+      // (a label is contiguous in the file or in the arena)
+      const std::string_view lab = g.sv(r.f[1]);
+      size_t d0, dn;
+      if (clock_time(lab, false, &d0, &dn) || clock_time(lab, true, &d0, &dn))
+        t = Str{r.f[1].off + (uint32_t)d0, (uint32_t)dn};
     }
-    g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(Str{0, 0});
-    g.time.push_back(t);
-    g.ltab.push_back(intern_table(r.f[2]));
-    g.llab.push_back(intern_label(r.f[1]));
-    g.tclass.push_back(0);
+    g.id[i] = r.f[0], g.label[i] = r.f[1], g.table[i] = r.f[2], g.type[i] = Str{0, 0}, g.time[i] = t;
+    g.ltab[i] = intern_table(r.f[2]);
+    g.llab[i] = intern_label(r.f[1]);
+    g.tclass[i] = 0;
   }
-  for (auto &r : rules) {
-    g.id.push_back(r.f[0]), g.label.push_back(r.f[1]), g.table.push_back(r.f[2]), g.type.push_back(r.f[3]);
-    g.time.push_back(Str{0, 0});
-    g.ltab.push_back(intern_table(r.f[2]));
-    g.llab.push_back(intern_label(r.f[1]));
-    g.tclass.push_back(type_class(g.sv(r.f[3])));
+  for (uint32_t k = 0; k < rules.size(); k++) {
+    const Rec &r = rules[k];
+    const size_t i = goals.size() + k;
+    g.id[i] = r.f[0], g.label[i] = r.f[1], g.table[i] = r.f[2], g.type[i] = r.f[3], g.time[i] = Str{0, 0};
+    g.ltab[i] = intern_table(r.f[2]);
+    g.llab[i] = intern_label(r.f[1]);
+    g.tclass[i] = type_class(g.sv(r.f[3]));
   }
   if (gnumk == 1 && rnumk == 1 && M.gnum.uniform && M.rnum.uniform) {
     // "goal<n>" / "rule<n>" with one digit count per kind: string order is
@@ -1037,8 +1065,18 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   for (auto &ed : edges) {
     std::string_view f = g.sv(ed.first), t = g.sv(ed.second);
     uint32_t u, v;
-    // strings.Contains(From, "goal") (pre-post-prov.go:173)
-    if ((f.size() >= 4 && !memcmp(f.data(), "goal", 4)) || f.find("goal") != std::string_view::npos) {
+    // strings.Contains(From, "goal") (pre-post-prov.go:173); "rule<digits>" holds no "goal"
+    bool from_goal;
+    if (f.size() >= 4 && !memcmp(f.data(), "goal", 4)) {
+      from_goal = true;
+    } else if (f.size() >= 4 && !memcmp(f.data(), "rule", 4)) {
+      size_t i = 4;
+      while (i < f.size() && (uint32_t)(unsigned char)f[i] - '0' <= 9u) i++;
+      from_goal = i < f.size() && f.find("goal", 4) != std::string_view::npos;
+    } else {
+      from_goal = f.find("goal") != std::string_view::npos;
+    }
+    if (from_goal) {
       u = find_id(f, true), v = find_id(t, false);
     } else {
       u = find_id(f, false), v = find_id(t, true);

@@ -54,6 +54,9 @@ def test_random_ingest_matches_python(tmp_path, seed):
     runs[0][2]["goals"].append({"id": "goalc", "label": "clock(a, b, 3, 4)", "table": "clock", "time": "9"})
     runs[0][2]["goals"].append({"id": "goalw", "label": "clock(a, a, 2, __WILDCARD__)", "table": "clock"})
     runs[0][3]["goals"].append({"id": "goalu", "label": "café(\"q\", \\, \U0001F600)", "table": "té"})
+    # the two-number match wins over an earlier wildcard one; an escaped label (decoded copy)
+    runs[0][2]["goals"].append({"id": "goalx", "label": "clock(a, 1, __WILDCARD__) clock(b, 7, 8)", "table": "clock"})
+    runs[0][2]["goals"].append({"id": "goale", "label": "clock(\"q\", r, 11, 12)", "table": "clock"})
     write_dir(str(tmp_path), runs)
     n1 = load_molly_native(str(tmp_path), threads=1)
     n4 = load_molly_native(str(tmp_path), threads=4)
@@ -63,6 +66,7 @@ def test_random_ingest_matches_python(tmp_path, seed):
     r0 = n1.graph_nodes(0)
     times = {n1.node_ids[i]: n1.node_times[i] for i in r0}
     assert times["run_0_pre_goalc"] == "3" and times["run_0_pre_goalw"] == "2"
+    assert times["run_0_pre_goalx"] == "7" and times["run_0_pre_goale"] == "11"
 
 
 @pytest.mark.parametrize("case", ["dangling", "dup_goal", "dup_edge", "bad_json", "missing"])
