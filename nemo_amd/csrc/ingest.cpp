@@ -781,6 +781,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
               else
                 while (j.ok) {
                   int f = -1;
+                  j.ws();  // after ", " (json.dump's separators)
                   // the exact lower-case keys, matched in place (the closing quote included)
                   if (j.e - j.p >= 9 && *j.p == '"') {
                     const uint64_t w = load8(j.p + 1);
