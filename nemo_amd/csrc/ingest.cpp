@@ -387,6 +387,8 @@ struct ShardIntern {
   };
   std::vector<Shard> sh;  // one per thread of the first merge (fixed from then on)
   uint64_t count = 0;     // labels numbered so far
+  std::vector<std::vector<uint32_t>> bli;  // per graph: its local labels grouped by shard
+  std::vector<uint32_t> boff;              // per graph: S + 1 group bounds in bli
   uint32_t shard_of(uint64_t h) const { return (uint32_t)(((h >> 40) * sh.size()) >> 24); }
 
   // lre[g][li] = global id of graph g's local label li.  add(view) stores a
@@ -395,19 +397,39 @@ struct ShardIntern {
   template <class Add>
   bool merge(std::vector<Graph> &gs, uint32_t G, int nt, const Runner &run, std::vector<std::vector<uint32_t>> &lre,
              Add &&add) {
-    for (uint32_t g = 0; g < G; g++) lre[g].assign(gs[g].labs.size(), 0);
     if (sh.empty()) sh.resize((size_t)std::min(64, std::max(1, nt)));
     const uint32_t S = (uint32_t)sh.size();
+    if (bli.size() < G) bli.resize(G);
+    boff.resize((size_t)G * (S + 1));
+    // each graph's labels grouped by shard (in parallel by graph), so that a
+    // shard's thread reads its own labels only
+    std::atomic<uint32_t> nextb{0};
+    auto phase_0 = [&] {
+      uint32_t cur[65];
+      for (uint32_t g; (g = nextb.fetch_add(1)) < G;) {
+        const Graph &gr = gs[g];
+        const uint32_t L = (uint32_t)gr.labh.size();
+        uint32_t *off = &boff[(size_t)g * (S + 1)];
+        std::fill(off, off + S + 1, 0u);
+        for (uint32_t li = 0; li < L; li++) off[shard_of(gr.labh[li]) + 1]++;
+        for (uint32_t k = 0; k < S; k++) off[k + 1] += off[k];
+        std::copy(off, off + S, cur);
+        bli[g].resize(L);
+        for (uint32_t li = 0; li < L; li++) bli[g][cur[shard_of(gr.labh[li])]++] = li;
+        lre[g].resize(L);  // every entry is written by its shard below
+      }
+    };
+    run(phase_0);
     std::atomic<uint32_t> nexts{0};
     auto phase_a = [&] {
       for (uint32_t k; (k = nexts.fetch_add(1)) < S;) {
         Shard &d = sh[k];
         for (uint32_t g = 0; g < G; g++) {
           const Graph &gr = gs[g];
-          for (uint32_t li = 0; li < gr.labh.size(); li++) {
-            const uint64_t h = gr.labh[li];
-            if (shard_of(h) != k) continue;
-            const auto r = d.intern(gr.sv(gr.labs[li]), h);
+          const uint32_t *off = &boff[(size_t)g * (S + 1)];
+          for (uint32_t x = off[k]; x < off[k + 1]; x++) {
+            const uint32_t li = bli[g][x];
+            const auto r = d.intern(gr.sv(gr.labs[li]), gr.labh[li]);
             lre[g][li] = (r.second ? NEW : 0u) | (k << SH) | r.first;
           }
         }
@@ -1094,11 +1116,28 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
 
 }  // namespace
 
+// an output array filled once per call by the worker threads: resize neither
+// keeps nor initialises the contents, so the pages are first touched by the
+// parallel fill (not by a serial zero fill)
+template <class T>
+struct RawBuf {
+  std::unique_ptr<T[]> p;
+  size_t n = 0, cap = 0;
+  void resize(size_t m) {
+    if (m > cap) p.reset(new T[m]), cap = m;
+    n = m;
+  }
+  T *data() const { return p.get(); }
+  size_t size() const { return n; }
+  T *begin() const { return p.get(); }
+  T &operator[](size_t i) { return p[i]; }
+};
+
 struct nemo_ingest {
   std::vector<Graph> graphs;  // 2r = pre, 2r+1 = post
   std::vector<uint32_t> iteration;
   std::vector<uint64_t> node_off, edge_off;
-  std::vector<uint32_t> word, label, rank, src, dst;
+  RawBuf<uint32_t> word, label, rank, src, dst;
   std::vector<std::string> tables, labels;
   uint32_t table_pre = 0, table_post = 0;
 };
@@ -1215,7 +1254,8 @@ struct nemo_ingest_stream {
   std::vector<std::vector<uint32_t>> tre, lre;    // their table / label ids
   // the chunks' arrays, double-buffered: chunk i stays valid while chunk i+1 is parsed
   struct Chunk {
-    std::vector<uint32_t> it, word, label, rank, src, dst;
+    std::vector<uint32_t> it;
+    RawBuf<uint32_t> word, label, rank, src, dst;
     std::vector<uint8_t> own;
     std::vector<uint64_t> node_off, edge_off;
   } buf[2];
