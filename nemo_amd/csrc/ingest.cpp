@@ -351,37 +351,48 @@ inline Runner make_runner(WorkerPool *pool, int nt) {
 struct ShardIntern {
   static constexpr uint32_t NEW = 1u << 31, SH = 25;  // lre entry: NEW | shard << SH | shard index
   struct Shard {
-    std::vector<uint32_t> tag, val;   // slots: hash tag, shard index (~0u empty)
+    // open-addressing slots: hash tag, shard index (~0u empty), and keys of up
+    // to 16 bytes inline (a lookup touches one slot; longer keys compare
+    // against `key`)
+    struct Slot {
+      uint32_t tag, val, len, pad;
+      char b[16];
+    };
+    std::vector<Slot> slot;
     size_t mask = 0;
     std::vector<std::string_view> key;
     std::vector<uint64_t> hash;
     std::vector<uint32_t> gid;        // by shard index: the global id
+    static void put(Slot &sl, uint32_t t, uint32_t v, std::string_view k) {
+      sl.tag = t, sl.val = v, sl.len = (uint32_t)std::min<size_t>(k.size(), 0xFFFFFFFFu);
+      if (k.size() <= 16) memcpy(sl.b, k.data(), k.size());
+    }
     void grow() {
-      const size_t cap = std::max<size_t>(64, 2 * tag.size());
-      tag.assign(cap, 0);
-      val.assign(cap, ~0u);
+      const size_t cap = std::max<size_t>(64, 2 * slot.size());
+      slot.assign(cap, Slot{0, ~0u, 0, 0, {}});
       mask = cap - 1;
       for (uint32_t x = 0; x < key.size(); x++) {
         size_t i = hash[x] & mask;
-        while (val[i] != ~0u) i = (i + 1) & mask;
-        tag[i] = (uint32_t)(hash[x] >> 32);
-        val[i] = x;
+        while (slot[i].val != ~0u) i = (i + 1) & mask;
+        put(slot[i], (uint32_t)(hash[x] >> 32), x, key[x]);
       }
     }
     // the shard index of k, and whether it is new
     std::pair<uint32_t, bool> intern(std::string_view k, uint64_t h) {
-      if (2 * (key.size() + 1) > tag.size()) grow();
+      if (2 * (key.size() + 1) > slot.size()) grow();
       const uint32_t t = (uint32_t)(h >> 32);
       for (size_t i = h & mask;; i = (i + 1) & mask) {
-        if (val[i] == ~0u) {
-          tag[i] = t;
-          val[i] = (uint32_t)key.size();
+        Slot &sl = slot[i];
+        if (sl.val == ~0u) {
+          put(sl, t, (uint32_t)key.size(), k);
           key.push_back(k);
           hash.push_back(h);
           gid.push_back(~0u);
-          return {val[i], true};
+          return {sl.val, true};
         }
-        if (tag[i] == t && sveq(key[val[i]], k)) return {val[i], false};
+        if (sl.tag == t && sl.len == k.size() &&
+            (k.size() <= 16 ? sveq(std::string_view(sl.b, k.size()), k) : sveq(key[sl.val], k)))
+          return {sl.val, false};
       }
     }
   };
