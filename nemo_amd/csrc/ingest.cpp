@@ -170,19 +170,18 @@ inline uint64_t hash_sv(std::string_view s) {
 // string_view -> u32 with hash-tagged slots, reused from graph to graph by one
 // thread: a slot is live only in the epoch that wrote it, so no clearing
 struct FlatMap {
-  struct Slot {
-    uint32_t tag, val, epoch, pad;
+  struct Slot {  // the key's view in the slot: one cache line per probe
+    const char *kp;
+    uint32_t klen, tag, val, epoch;
   };
   std::vector<Slot> slot;
-  std::vector<std::string_view> key;
   size_t mask = 0;
   uint32_t epoch = 0;
   void init(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
     if (cap > slot.size() || ++epoch == 0) {
-      slot.assign(std::max(cap, slot.size()), Slot{0, 0, 0, 0});
-      key.assign(slot.size(), std::string_view());
+      slot.assign(std::max(cap, slot.size()), Slot{nullptr, 0, 0, 0, 0});
       epoch = 1;
     }
     mask = cap - 1;
@@ -194,11 +193,10 @@ struct FlatMap {
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       Slot &sl = slot[i];
       if (sl.epoch != epoch) {
-        sl = Slot{tag, v, epoch, 0};
-        key[i] = k;
+        sl = Slot{k.data(), (uint32_t)k.size(), tag, v, epoch};
         return {v, true};
       }
-      if (sl.tag == tag && sveq(key[i], k)) return {sl.val, false};
+      if (sl.tag == tag && sveq(std::string_view(sl.kp, sl.klen), k)) return {sl.val, false};
     }
   }
   uint32_t find(std::string_view k) const {
@@ -207,7 +205,7 @@ struct FlatMap {
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       const Slot &sl = slot[i];
       if (sl.epoch != epoch) return ~0u;
-      if (sl.tag == tag && sveq(key[i], k)) return sl.val;
+      if (sl.tag == tag && sveq(std::string_view(sl.kp, sl.klen), k)) return sl.val;
     }
   }
 };
