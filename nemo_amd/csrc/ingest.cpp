@@ -75,6 +75,26 @@ struct FileMap {
   }
 };
 
+// an array written in full after each resize (the output arrays, a graph's
+// per-node fields): resize neither keeps nor initialises the contents, so
+// nothing is zero-filled and the output pages are first touched by the
+// parallel fill
+template <class T>
+struct RawBuf {
+  std::unique_ptr<T[]> p;
+  size_t n = 0, cap = 0;
+  void resize(size_t m) {
+    if (m > cap) p.reset(new T[m]), cap = m;
+    n = m;
+  }
+  T *data() const { return p.get(); }
+  size_t size() const { return n; }
+  T *begin() const { return p.get(); }
+  T &operator[](size_t i) { return p[i]; }
+  const T &operator[](size_t i) const { return p[i]; }
+  void clear() { n = 0; }
+};
+
 struct Graph {
   // Str offsets below flen are bytes of the mapped file (strings without
   // escapes), at and above it the arena (decoded strings, clock times)
@@ -82,10 +102,11 @@ struct Graph {
   const char *fb = "";
   uint32_t flen = 0;
   std::vector<char> arena;
-  std::vector<Str> id, label, table, type, time;
+  RawBuf<Str> id, label, table, type, time;  // per node, written in full by parse_graph
   uint32_t n_goals = 0;
-  std::vector<uint32_t> src, dst, rank, ltab, llab;
-  std::vector<uint8_t> tclass;
+  std::vector<uint32_t> src, dst, rank;
+  RawBuf<uint32_t> ltab, llab;
+  RawBuf<uint8_t> tclass;
   std::vector<Str> tabs, labs;  // local first-appearance order
   std::vector<uint64_t> labh;   // hash_sv of each of labs (the global interning's shard and slot)
   std::string err;
@@ -99,8 +120,10 @@ struct Graph {
     fb = "";
     flen = 0;
     n_goals = 0;
-    for (auto *v : {&id, &label, &table, &type, &time, &tabs, &labs}) v->clear();
-    for (auto *v : {&src, &dst, &rank, &ltab, &llab}) v->clear();
+    for (auto *v : {&id, &label, &table, &type, &time}) v->clear();
+    tabs.clear(), labs.clear();
+    for (auto *v : {&src, &dst, &rank}) v->clear();
+    ltab.clear(), llab.clear();
     arena.clear(), tclass.clear(), labh.clear(), err.clear();
   }
 };
@@ -1124,23 +1147,6 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
 }
 
 }  // namespace
-
-// an output array filled once per call by the worker threads: resize neither
-// keeps nor initialises the contents, so the pages are first touched by the
-// parallel fill (not by a serial zero fill)
-template <class T>
-struct RawBuf {
-  std::unique_ptr<T[]> p;
-  size_t n = 0, cap = 0;
-  void resize(size_t m) {
-    if (m > cap) p.reset(new T[m]), cap = m;
-    n = m;
-  }
-  T *data() const { return p.get(); }
-  size_t size() const { return n; }
-  T *begin() const { return p.get(); }
-  T &operator[](size_t i) { return p[i]; }
-};
 
 struct nemo_ingest {
   std::vector<Graph> graphs;  // 2r = pre, 2r+1 = post
