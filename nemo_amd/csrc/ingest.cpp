@@ -102,7 +102,7 @@ struct Graph {
   const char *fb = "";
   uint32_t flen = 0;
   std::vector<char> arena;
-  RawBuf<Str> id, label, table, type, time;  // per node, written in full by parse_graph
+  RawBuf<Str> id, type, time;  // per node (the strings nemo_ingest_string hands out), written in full by parse_graph
   uint32_t n_goals = 0;
   std::vector<uint32_t> src, dst, rank;
   RawBuf<uint32_t> ltab, llab;
@@ -120,7 +120,7 @@ struct Graph {
     fb = "";
     flen = 0;
     n_goals = 0;
-    for (auto *v : {&id, &label, &table, &type, &time}) v->clear();
+    for (auto *v : {&id, &type, &time}) v->clear();
     tabs.clear(), labs.clear();
     for (auto *v : {&src, &dst, &rank}) v->clear();
     ltab.clear(), llab.clear();
@@ -554,6 +554,10 @@ struct Json {
 
   __attribute__((always_inline)) void ws() {
     if (p < e && (unsigned char)*p > ' ') return;  // the common case: no white space
+    if (e - p >= 2 && *p == ' ' && (unsigned char)p[1] > ' ') {  // one space (json.dump's separators)
+      p++;
+      return;
+    }
     while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) p++;
   }
   __attribute__((always_inline)) bool lit(const char *s) {
@@ -936,7 +940,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   g.n_goals = (uint32_t)goals.size();
   // sized once and written by index (a push_back per field and node was a
   // capacity check each)
-  g.id.resize(V), g.label.resize(V), g.table.resize(V), g.type.resize(V), g.time.resize(V);
+  g.id.resize(V), g.type.resize(V), g.time.resize(V);
   g.ltab.resize(V), g.llab.resize(V), g.tclass.resize(V);
   FlatMap &gidx = M.gidx, &ridx = M.ridx, &tabs = M.tabs, &labs = M.labs;
   gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
@@ -1030,7 +1034,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
       if (clock_time(lab, false, &d0, &dn) || clock_time(lab, true, &d0, &dn))
         t = Str{r.f[1].off + (uint32_t)d0, (uint32_t)dn};
     }
-    g.id[i] = r.f[0], g.label[i] = r.f[1], g.table[i] = r.f[2], g.type[i] = Str{0, 0}, g.time[i] = t;
+    g.id[i] = r.f[0], g.type[i] = Str{0, 0}, g.time[i] = t;
     g.ltab[i] = intern_table(r.f[2]);
     g.llab[i] = intern_label(r.f[1]);
     g.tclass[i] = 0;
@@ -1038,7 +1042,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   for (uint32_t k = 0; k < rules.size(); k++) {
     const Rec &r = rules[k];
     const size_t i = goals.size() + k;
-    g.id[i] = r.f[0], g.label[i] = r.f[1], g.table[i] = r.f[2], g.type[i] = r.f[3], g.time[i] = Str{0, 0};
+    g.id[i] = r.f[0], g.type[i] = r.f[3], g.time[i] = Str{0, 0};
     g.ltab[i] = intern_table(r.f[2]);
     g.llab[i] = intern_label(r.f[1]);
     g.tclass[i] = type_class(g.sv(r.f[3]));
