@@ -102,7 +102,9 @@ struct Graph {
   const char *fb = "";
   uint32_t flen = 0;
   std::vector<char> arena;
-  RawBuf<Str> id, type, time;  // per node (the strings nemo_ingest_string hands out), written in full by parse_graph
+  // per node, written in full by parse_graph: the ID, and a goal's time or a
+  // rule's type (the strings nemo_ingest_string hands out)
+  RawBuf<Str> id, tt;
   uint32_t n_goals = 0;
   std::vector<uint32_t> src, dst, rank;
   RawBuf<uint32_t> ltab, llab;
@@ -120,7 +122,7 @@ struct Graph {
     fb = "";
     flen = 0;
     n_goals = 0;
-    for (auto *v : {&id, &type, &time}) v->clear();
+    id.clear(), tt.clear();
     tabs.clear(), labs.clear();
     for (auto *v : {&src, &dst, &rank}) v->clear();
     ltab.clear(), llab.clear();
@@ -940,7 +942,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   g.n_goals = (uint32_t)goals.size();
   // sized once and written by index (a push_back per field and node was a
   // capacity check each)
-  g.id.resize(V), g.type.resize(V), g.time.resize(V);
+  g.id.resize(V), g.tt.resize(V);
   g.ltab.resize(V), g.llab.resize(V), g.tclass.resize(V);
   FlatMap &gidx = M.gidx, &ridx = M.ridx, &tabs = M.tabs, &labs = M.labs;
   gidx.init(goals.size()), ridx.init(rules.size()), tabs.init(64), labs.init(V);
@@ -1034,7 +1036,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
       if (clock_time(lab, false, &d0, &dn) || clock_time(lab, true, &d0, &dn))
         t = Str{r.f[1].off + (uint32_t)d0, (uint32_t)dn};
     }
-    g.id[i] = r.f[0], g.type[i] = Str{0, 0}, g.time[i] = t;
+    g.id[i] = r.f[0], g.tt[i] = t;
     g.ltab[i] = intern_table(r.f[2]);
     g.llab[i] = intern_label(r.f[1]);
     g.tclass[i] = 0;
@@ -1042,7 +1044,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
   for (uint32_t k = 0; k < rules.size(); k++) {
     const Rec &r = rules[k];
     const size_t i = goals.size() + k;
-    g.id[i] = r.f[0], g.type[i] = r.f[3], g.time[i] = Str{0, 0};
+    g.id[i] = r.f[0], g.tt[i] = r.f[3];
     g.ltab[i] = intern_table(r.f[2]);
     g.llab[i] = intern_label(r.f[1]);
     g.tclass[i] = type_class(g.sv(r.f[3]));
@@ -1497,7 +1499,8 @@ extern "C" int nemo_ingest_string(const nemo_ingest *h, int kind, uint64_t index
   const uint32_t g = (uint32_t)(std::upper_bound(h->node_off.begin(), h->node_off.end(), index) - h->node_off.begin() - 1);
   const Graph &gr = h->graphs[g];
   const size_t i = index - h->node_off[g];
-  Str st = kind == NEMO_STR_NODE_ID ? gr.id[i] : kind == NEMO_STR_NODE_TYPE ? gr.type[i] : kind == NEMO_STR_NODE_TIME ? gr.time[i] : Str{0, 0};
+  const bool goal = i < gr.n_goals;
+  Str st = kind == NEMO_STR_NODE_ID ? gr.id[i] : (kind == NEMO_STR_NODE_TIME) == goal ? gr.tt[i] : Str{0, 0};
   if (kind < NEMO_STR_NODE_ID || kind > NEMO_STR_NODE_TIME) return NEMO_ERR_INVALID;
   *s = gr.sv(st).data();
   *len = st.len;
