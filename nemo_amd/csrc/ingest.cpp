@@ -782,6 +782,17 @@ inline bool keyis(std::string_view k, const char *s, size_t n) {
   return true;
 }
 
+// the keys of goals (0), rules (1) and edges (2) in the order Molly and json.dump
+// write them, as the in-place match's (mask, word, advance)
+constexpr uint64_t kPredM[3][4] = {{0xFFFFFFull, 0xFFFFFFFFFFFFull, 0xFFFFFFFFFFFFull, 0xFFFFFFFFFFull},
+                                   {0xFFFFFFull, 0xFFFFFFFFFFFFull, 0xFFFFFFFFFFFFull, 0xFFFFFFFFFFull},
+                                   {0xFFFFFFFFFFull, 0xFFFFFFull, 0, 0}};
+constexpr uint64_t kPredK[3][4] = {
+    {KEY3('i', 'd'), KEY6('l', 'a', 'b', 'e', 'l'), KEY6('t', 'a', 'b', 'l', 'e'), KEY5('t', 'i', 'm', 'e')},
+    {KEY3('i', 'd'), KEY6('l', 'a', 'b', 'e', 'l'), KEY6('t', 'a', 'b', 'l', 'e'), KEY5('t', 'y', 'p', 'e')},
+    {KEY5('f', 'r', 'o', 'm'), KEY3('t', 'o'), 1, 1}};
+constexpr uint32_t kPredA[3][4] = {{4, 7, 7, 6}, {4, 7, 7, 6}, {6, 4, 0, 0}};
+
 void parse_graph(const std::string &path, uint32_t iteration, const char *cond, Graph &g) {
   // the file is mapped: strings without escapes are views of it, decoded ones
   // and clock times go to the arena (reserved: no reallocation, the maps hold views)
@@ -836,6 +847,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
               j.p++;
               Rec r{};
               std::pair<Str, Str> ed{};
+              int nf = 0;  // the field expected next
               j.ws();
               if (j.p < j.e && *j.p == '}') j.p++;
               else
@@ -846,7 +858,9 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
                   if (j.e - j.p >= 9 && *j.p == '"') {
                     const uint64_t w = load8(j.p + 1);
                     uint32_t adv = 0;
-                    if (which == 2) {
+                    if (nf < (which == 2 ? 2 : 4) && (w & kPredM[which][nf]) == kPredK[which][nf]) {
+                      f = nf, adv = kPredA[which][nf];  // the field after the last one (the writers' order)
+                    } else if (which == 2) {
                       if ((w & 0xFFFFFFFFFFull) == KEY5('f', 'r', 'o', 'm')) f = 0, adv = 6;
                       else if ((w & 0xFFFFFFull) == KEY3('t', 'o')) f = 1, adv = 4;
                     } else if ((w & 0xFFFFFFull) == KEY3('i', 'd')) {
@@ -890,6 +904,7 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
                     if (which == 2) (f == 0 ? ed.first : ed.second) = sv;
                     else r.f[f] = sv;
                   }
+                  nf = f + 1;
                   j.ws();
                   if (j.p < j.e && *j.p == ',') {
                     j.p++;
