@@ -52,6 +52,18 @@ class _Handle:
             raise IndexError(i)
         return ctypes.string_at(p, n.value).decode() if n.value else ""
 
+    def strings(self, kind: int, n: int) -> list:
+        """Strings 0..n-1 of a kind (the lookup bound once, its out-arguments reused)."""
+        f = _lib().nemo_ingest_string
+        p, ln = ctypes.c_char_p(), ctypes.c_size_t()
+        bp, bn, h, at = ctypes.byref(p), ctypes.byref(ln), self.h, ctypes.string_at
+        out = []
+        for i in range(n):
+            if f(h, kind, i, bp, bn) != 0:
+                raise IndexError(i)
+            out.append(at(p, ln.value).decode() if ln.value else "")
+        return out
+
 
 class NodeStrings:
     """Lazy per-node string column (node IDs are re-prefixed like molly.go:92)."""
@@ -104,8 +116,8 @@ def load_molly_native(out_dir: str, threads: int = 0) -> Corpus:
                label=arr(cs.label, V), edge_src=arr(cs.edge_src, Ecount), edge_dst=arr(cs.edge_dst, Ecount),
                id_rank=arr(cs.id_rank, V), n_tables=cs.n_tables, table_pre=cs.table_pre, table_post=cs.table_post,
                status=[r.get("status", "") for r in runs],
-               tables=[handle.string(STR_TABLE, i) for i in range(int(L.nemo_ingest_count(h, STR_TABLE)))],
-               labels=[handle.string(STR_LABEL, i) for i in range(int(L.nemo_ingest_count(h, STR_LABEL)))],
+               tables=handle.strings(STR_TABLE, int(L.nemo_ingest_count(h, STR_TABLE))),
+               labels=handle.strings(STR_LABEL, int(L.nemo_ingest_count(h, STR_LABEL))),
                runs=runs)
     c.node_ids = NodeStrings(handle, STR_NODE_ID, c, prefixed=True)
     c.node_types = NodeStrings(handle, STR_NODE_TYPE, c)
