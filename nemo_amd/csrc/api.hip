@@ -1340,6 +1340,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
                          const uint32_t *d_labels, uint64_t labels_cap) {
   if (!c || (!failed_iters && n_failed)) return NEMO_ERR_INVALID;
   if (mode != NEMO_DIFF_REFERENCE && mode != NEMO_DIFF_PER_RUN) return fail(c, NEMO_ERR_INVALID, "unknown diff mode %d", mode);
+  if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_diffprov without a loaded corpus (the last load failed?)");
   if (!c->marked) return fail(c, NEMO_ERR_STATE, "nemo_diffprov before nemo_mark_holds");
   // (the diff kernels read no holds flags: a deferred mark stays fused with the simplification)
   HIPCHK(c, hipSetDevice(c->device));
@@ -1392,6 +1393,10 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->diff_cap = (uint32_t)n_failed;
   }
   if (!dx && n_failed > c->legacy_cap) {  // the one-workgroup-per-entry kernels' scratch
+    for (void *q : {(void *)c->d_dbits, (void *)c->d_dumask, (void *)c->d_ddepth, (void *)c->d_dtopo}) dfree(c, q);
+    c->d_dbits = c->d_dumask = nullptr;
+    c->d_ddepth = nullptr;
+    c->d_dtopo = nullptr;
     if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dumask, n_failed * V0))) return rc;
     if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;

@@ -24,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -41,23 +42,50 @@ struct Str {
   uint32_t off, len;
 };
 
-// a provenance file mapped read-only (page-cache pages, no copy), unmapped with its graph
+// Live mappings of the process: every graph keeps its file mapped while it
+// lives (its strings are views), so a one-shot ingest of many runs would pass
+// the kernel's vm.max_map_count (65530 by default) and mmap would fail.  Past
+// a limit (half the kernel's, or NEMO_INGEST_MAP_LIMIT) a file is read into a
+// heap buffer instead; the parse is the same either way.
+std::atomic<int64_t> g_live_maps{0};
+int64_t map_limit() {
+  static const int64_t lim = [] {
+    if (const char *e = getenv("NEMO_INGEST_MAP_LIMIT")) return (int64_t)atoll(e);
+    int64_t k = 65530;
+    if (FILE *f = fopen("/proc/sys/vm/max_map_count", "r")) {
+      long long v;
+      if (fscanf(f, "%lld", &v) == 1 && v > 0) k = v;
+      fclose(f);
+    }
+    return k / 2;
+  }();
+  return lim;
+}
+
+// a provenance file mapped read-only (page-cache pages, no copy), or read
+// into a heap buffer past the mapping limit; released with its graph
 struct FileMap {
   void *p = nullptr;
   size_t n = 0;
+  std::unique_ptr<char[]> heap;  // the read() fallback (p points into it)
   FileMap() = default;
   FileMap(const FileMap &) = delete;
   FileMap &operator=(const FileMap &) = delete;
-  FileMap(FileMap &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr, o.n = 0; }
+  FileMap(FileMap &&o) noexcept : p(o.p), n(o.n), heap(std::move(o.heap)) { o.p = nullptr, o.n = 0; }
   FileMap &operator=(FileMap &&o) noexcept {
-    if (this != &o) reset(), p = o.p, n = o.n, o.p = nullptr, o.n = 0;
+    if (this != &o) reset(), p = o.p, n = o.n, heap = std::move(o.heap), o.p = nullptr, o.n = 0;
     return *this;
   }
   ~FileMap() { reset(); }
   void reset() {
-    if (p) munmap(p, n);
+    if (p && !heap) {
+      munmap(p, n);
+      g_live_maps.fetch_sub(1, std::memory_order_relaxed);
+    }
+    heap.reset();
     p = nullptr, n = 0;
   }
+  bool mapped() const { return p && !heap; }
   // false: the file cannot be opened or read
   bool open(const char *path) {
     reset();
@@ -66,9 +94,29 @@ struct FileMap {
     struct stat st;
     bool ok = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
     if (ok && st.st_size > 0) {
-      void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-      if (m == MAP_FAILED) ok = false;
-      else p = m, n = (size_t)st.st_size;
+      const size_t sz = (size_t)st.st_size;
+      void *m = MAP_FAILED;
+      if (g_live_maps.fetch_add(1, std::memory_order_relaxed) < map_limit())
+        m = mmap(nullptr, sz, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (m != MAP_FAILED) {
+        p = m, n = sz;
+      } else {  // over the limit, or the kernel refused (ENOMEM at vm.max_map_count)
+        g_live_maps.fetch_sub(1, std::memory_order_relaxed);
+        heap.reset(new char[sz + 64]);
+        size_t got = 0;
+        while (got < sz) {
+          const ssize_t r = ::read(fd, heap.get() + got, sz - got);
+          if (r <= 0) break;
+          got += (size_t)r;
+        }
+        if (got != sz) {
+          heap.reset();
+          ok = false;
+        } else {
+          memset(heap.get() + sz, 0, 64);
+          p = heap.get(), n = sz;
+        }
+      }
     }
     close(fd);
     return ok;
@@ -455,6 +503,7 @@ struct ShardIntern {
     };
     run(phase_0);
     std::atomic<uint32_t> nexts{0};
+    std::atomic<bool> over{false};  // a shard index past SH bits would spill into the shard field
     auto phase_a = [&] {
       for (uint32_t k; (k = nexts.fetch_add(1)) < S;) {
         Shard &d = sh[k];
@@ -464,12 +513,17 @@ struct ShardIntern {
           for (uint32_t x = off[k]; x < off[k + 1]; x++) {
             const uint32_t li = bli[g][x];
             const auto r = d.intern(gr.sv(gr.labs[li]), gr.labh[li]);
+            if (r.first >= (1u << SH)) {
+              over.store(true, std::memory_order_relaxed);
+              return;
+            }
             lre[g][li] = (r.second ? NEW : 0u) | (k << SH) | r.first;
           }
         }
       }
     };
     run(phase_a);
+    if (over.load()) return false;
     for (uint32_t g = 0; g < G; g++)  // first appearances in graph order
       for (uint32_t &x : lre[g])
         if (x & NEW) {
@@ -954,6 +1008,11 @@ void parse_graph(const std::string &path, uint32_t iteration, const char *cond, 
     return;
   }
   const size_t V = goals.size() + rules.size();
+  if (V >= (1u << 28)) {  // the per-graph maps pack node indices in 28 bits (NumMap, FlatSet64)
+    g.err = std::string("Too many nodes (") + std::to_string(V) + ") in " +
+            (cond == std::string("pre") ? "antecedent" : "consequent") + " provenance: " + path;
+    return;
+  }
   g.n_goals = (uint32_t)goals.size();
   // sized once and written by index (a push_back per field and node was a
   // capacity check each)

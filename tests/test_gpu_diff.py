@@ -106,3 +106,28 @@ def test_label_set_mode(eng):
             assert np.array_equal(_rows(eng.missing()), _rows(orc.missing))
         finally:
             eng.set_option("diff_window", 0)
+
+
+def test_failed_load_then_reshaped_reload(eng):
+    """The load-failure class behind round 4's r04l fault (the diff relayout, built at load, indexed a failed
+    g0's Kahn order): load a corpus whose run-0 post graph fails its load, check that diffprov refuses, then
+    load a differently-shaped good corpus into the same context -- the device allocations of the failed load
+    are kept and reused, not zero-filled -- and run the diff against the oracle (pre-post-prov.go:205-210)."""
+    from tests.test_gpu_deep import _inject
+    bad, _ = synth.generate(6, target_nodes=40000, eot=40, body_extra=6, nval=3, nloc=4, p_fault=0.5,
+                            prepend_run0=True)
+    g0 = 2 * bad.run_index(0) + 1
+    eo = bad.edge_off.astype(np.int64)
+    s0, d0 = int(bad.edge_src[eo[g0]]), int(bad.edge_dst[eo[g0]])
+    _inject(bad, g0, [(s0, d0), (s0, d0)])  # duplicates: fewer relationships created than edges listed
+    with pytest.raises(E.NemoError) as ei:
+        eng.load(bad)
+    assert "inserted number of edges" in str(ei.value)
+    with pytest.raises(E.NemoError):
+        eng.diffprov(bad.failed_iters(), DIFF_PER_RUN)
+    good, _ = synth.generate(40, p_fault=0.55, prepend_run0=True, **synth.CONFIGS["c3"])
+    _check_corpus(eng, good, windows=(0, 1))
+    # and back to a deep shape on the same context
+    deep, _ = synth.generate(8, target_nodes=30000, eot=30, body_extra=6, nval=3, nloc=4, p_fault=0.5,
+                             prepend_run0=True, seed=7)
+    _check_corpus(eng, deep, windows=(0, 1))

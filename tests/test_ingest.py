@@ -235,3 +235,36 @@ def test_stream_parses_run0_first(tmp_path, chunk):
         assert pre == _named(one, one.tables, one.labels, 2 * r), it
         assert post == _named(one, one.tables, one.labels, 2 * r + 1), it
     st.close()
+
+
+def test_map_limit_falls_back_to_read(tmp_path):
+    """Every graph keeps its provenance file mapped while it lives, so a one-shot ingest of many runs would
+    pass vm.max_map_count; past a limit the files are read into heap buffers instead.  With the limit
+    lowered to 5 live mappings (NEMO_INGEST_MAP_LIMIT, read once per process: a child process), a 40-run
+    directory (80 files) must ingest to the same arrays and strings as the mapped path."""
+    import subprocess
+    import sys
+    _, _, d = _synth_dir(tmp_path, n_runs=40, nodes=300)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    arrays = ("iteration", "node_off", "edge_off", "node_word", "label", "edge_src", "edge_dst", "id_rank")
+    strings = ("tables", "labels", "status", "node_ids", "node_types", "node_times")
+    out = str(tmp_path / "limited")
+    code = (f"import sys, json, numpy as np; sys.path.insert(0, {root!r})\n"
+            f"from nemo_amd.ingest import load_molly_native\n"
+            f"c = load_molly_native({d!r}, threads=4)\n"
+            f"np.savez({out + '.npz'!r}, **{{k: np.asarray(getattr(c, k)) for k in {arrays!r}}})\n"
+            f"json.dump({{k: list(getattr(c, k)) for k in {strings!r}}}, open({out + '.json'!r}, 'w'))\n")
+    env = dict(os.environ, NEMO_INGEST_MAP_LIMIT="5")
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
+    lim = np.load(out + ".npz")
+    lstr = json.load(open(out + ".json"))
+    ref = load_molly_native(d, threads=4)
+    for k in arrays:
+        assert np.array_equal(np.asarray(getattr(ref, k)), lim[k]), k
+    V = int(ref.node_off[-1])
+    for k in strings:
+        want = list(getattr(ref, k))
+        got = lstr[k]
+        if k.startswith("node_"):
+            want, got = want[:V], got[:V]
+        assert want == got, k
