@@ -61,6 +61,7 @@ struct nemo_ctx {
   uint64_t glob_min_v = 65536;       // graphs with V >= this take k_chains_glob (set before load)
   uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   uint32_t glob_block_force = 0;     // chains_glob_block option (0 = by the number of deep graphs)
+  bool glob_prep_off = false;        // chains_glob_prep option 0: k_chains_glob builds its own H* order (test knob)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
@@ -585,6 +586,14 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->glob_block_force = (uint32_t)value;
     return NEMO_OK;
   }
+  if (!strcmp(name, "chains_glob_stop")) {  // diagnostic (stamps build only; set after the load): k_chains_glob returns after phase k
+    c->dc.glob_stop = value < 0 ? 0u : (uint32_t)value;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "chains_glob_prep")) {  // 0: no k_glob_prep (the per-graph front phases); takes effect at the next load
+    c->glob_prep_off = value == 0;
+    return NEMO_OK;
+  }
   if (!strcmp(name, "chains_glob_min_v")) {  // takes effect at the next nemo_load_corpus
     c->glob_min_v = value < 0 ? ~0ull : (uint64_t)value;
     return NEMO_OK;
@@ -879,6 +888,21 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     d.glob_block = c->glob_block_force ? c->glob_block_force : (n_deep > 512 ? 256u : 512u);
     d.gscratch = nullptr;
     if (words) A(d.gscratch, words);
+    // k_glob_prep's graph list and team scratch (identity ranks only)
+    std::vector<uint32_t> gl;
+    for (uint32_t g = 0; g < G; g++)
+      if (off[g] != ~0ull) gl.push_back(g);
+    uint32_t *dgl = nullptr;
+    A(dgl, gl.size());
+    if (!gl.empty()) HIPCHK(c, hipMemcpy(dgl, gl.data(), gl.size() * 4, hipMemcpyHostToDevice));
+    d.glob_list = dgl;
+    d.n_glob = (uint32_t)gl.size();
+    d.glob_prep = !gl.empty() && !c->has_rank && !c->glob_prep_off;
+    d.team = nullptr;
+    A(d.team, nemo::glob_team_words());
+    int ncu = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    d.n_cu = (uint32_t)std::max(ncu, 8);
   }
   A(d.chain, 5 * V);
   {
@@ -1636,6 +1660,10 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
   if (c->n_entries) {
     HIPCHK(c, hipEventSynchronize(c->ev_diff));
     nu_rows = *c->h_nmiss;
+    // k_dx keeps longest paths as u16 (k_dx.hip DX_VMAX): a longer one is flagged
+    if (c->dx_last && (nu_rows & 0x80000000u))
+      return fail(c, NEMO_ERR_INVALID, "diff graph of run 0: a path longer than 65533 steps (unsupported)");
+    nu_rows &= 0x7FFFFFFFu;
   }
   // rows of the distinct computations (unique index, rule), then one copy per entry
   int rc;

@@ -177,6 +177,12 @@ struct DevCorpus {
   Tier t_ms, t_diff, t_pull;             // the LDS tiers of k_marksimp, k_diff_lds, k_pull_lds
   uint32_t gblock;                       // workgroup size of the global-tier kernels (256, or 1024 for deep corpora)
   uint32_t glob_block;                   // k_chains_glob's workgroup size (256 or 512)
+  uint32_t glob_stop;                    // diagnostic (stamps build): k_chains_glob returns after phase k (0: none)
+  uint32_t glob_prep;                    // 1: k_glob_prep builds the deep graphs' H* order and adjacency (identity ranks)
+  uint32_t n_glob;                       // deep graphs (gs_off != ~0)
+  const uint32_t *glob_list;             // [n_glob] their graph ids
+  uint32_t *team;                        // k_glob_prep's team scratch (barrier counters, phase sums)
+  uint32_t n_cu;                         // compute units of the device
   uint32_t pg_chunks;                    // k_pg_* workgroups per listed graph (by the largest post graph)
   const uint64_t *node_off, *edge_off;
   const uint32_t *word, *label, *rank;  // rank may be null
@@ -399,9 +405,20 @@ __device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
   } while (0)
 // phase accumulators: TICK waits for the wave's outstanding memory operations,
 // so a phase is charged with the latency of the loads it issued
+// diagnostic early exit after phase k of a stamped kernel (per-phase HBM counters)
+#define GSTOP(k)                                   \
+  do {                                             \
+    if (c.glob_stop == (k)) {                      \
+      if (threadIdx.x == 0) c.nch[blockIdx.x] = 0; \
+      return;                                      \
+    }                                              \
+  } while (0)
 #define TICK(t) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory")
 #else
 #define STAMP(k) \
+  do {           \
+  } while (0)
+#define GSTOP(k) \
   do {           \
   } while (0)
 #endif

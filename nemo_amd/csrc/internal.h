@@ -145,6 +145,7 @@ void launch_marksimp(const DevCorpus &c, hipStream_t s);
 void launch_chains(const DevCorpus &c, hipStream_t s);
 void launch_chains_glob(const DevCorpus &c, hipStream_t s);
 uint64_t glob_words(uint64_t V, uint64_t E);  // k_chains_glob scratch of one graph (u32)
+uint32_t glob_team_words();                   // k_glob_prep's team scratch (u32)
 void launch_proto(const DevCorpus &c, hipStream_t s);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s);

@@ -49,13 +49,14 @@ struct GlobScratch {
   uint32_t *ha, *hb, *ta, *tb;  // pointer-jumping buffers (heads, tails)
   uint32_t *S, *A, *va, *vb, *pa, *pb;
   uint32_t *tmp;                // [5 * V] representatives (over child / par)
+  uint32_t *meta;               // [16]: [0] H* node count written by k_glob_prep
   unsigned long long *key;      // up to 2V keys (power-of-two padded chain count)
 };
 
 uint64_t glob_words(uint64_t V, uint64_t E) {
   const uint64_t w = (V + 31) / 32 + 2;
   const uint64_t adj = std::max<uint64_t>(2 * E, 5 * V);  // child + par, or the representatives
-  return 2 * w + 2 * (V + 1) + adj + 2 * (V + 2) + 16 * V + 4 * V + 64;
+  return 2 * w + 2 * (V + 1) + adj + 2 * (V + 2) + 16 * V + 4 * V + 16 + 64;
 }
 
 __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
@@ -98,6 +99,7 @@ __device__ inline GlobScratch glob_carve(uint32_t *p, uint32_t V, uint32_t E) {
   s.vb = s.hb;
   s.pa = s.ta;
   s.pb = s.tb;
+  s.meta = take(16);
   p = (uint32_t *)(((uintptr_t)p + 7) & ~(uintptr_t)7);
   s.key = (unsigned long long *)p;
   return s;
@@ -513,6 +515,275 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 #endif
 }
 
+// ---- k_glob_prep: H* compaction and adjacency by XCD teams ---------------------------
+// The first two phases of the deep-graph chain cover translate between two
+// orders: node order (the CSR, the flags) and H* in Kahn order (the sweeps'
+// compact index).  One workgroup per graph did that with scattered stores
+// into a V-word node -> index map and gathers from it, beside ~600 other
+// graphs doing the same, so every such access went to HBM (C5, r05a:
+// 198 GB of the kernel's 406 GB per launch, 64 of its 218 ms).  Here a team of
+// PT_M workgroups (the blocks of one `blockIdx % 8` class: one XCD under the
+// observed round-robin placement) takes one graph at a time, so the graph's
+// membership bitmap and its compact-node -> H* index map (~2 MB) stay in the
+// team's L2 while it is scattered and gathered.  Correctness does not depend on
+// the placement: team members hand phases over with agent-scope release /
+// acquire barriers.  Identity ID ranks only (corpora with a rank array keep the
+// per-graph phases of k_chains_glob).
+#define PT_TEAMS 8   // teams (blockIdx % 8)
+#define PT_M 32      // workgroups per team
+#define PT_B 1024    // threads per workgroup
+#define PT_CP 8      // Kahn positions per thread and round of the compaction
+#define PT_WORDS 256 // team scratch words: barrier counter + 2 x 3 x PT_M phase sums
+
+// team barrier: every wave's stores drained, one lane releases and arrives,
+// polls the team's counter (relaxed, L1-bypassing loads) and acquires
+__device__ __forceinline__ void team_sync(uint32_t *ctr, uint32_t target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// compact node index (rank among H* nodes in node order) of member y
+__device__ __forceinline__ uint32_t pt_no(const uint2 *hb, uint32_t y) {
+  const uint2 w = hb[y >> 5];
+  return w.y + __popc(w.x & ((1u << (y & 31)) - 1u));
+}
+
+__global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
+  __shared__ uint32_t s_lds[PT_B / 64];
+  __shared__ uint32_t s_base[3];
+  const uint32_t team = blockIdx.x % PT_TEAMS, r = blockIdx.x / PT_TEAMS, tid = threadIdx.x;
+  const uint32_t M = gridDim.x / PT_TEAMS;  // members per team (<= PT_M)
+  uint32_t *ts = c.team + (size_t)team * PT_WORDS, *ctr = ts;
+  uint32_t epoch = 0;
+  for (uint32_t k = team, it = 0; k < c.n_glob; k += PT_TEAMS, it++) {
+    const uint32_t g = c.glob_list[k];
+    if (c.err[g]) continue;  // every member reads the same flag: the whole team skips
+    const GraphView gv = c.view(g);
+    const uint32_t V = gv.V, E = gv.E;
+    GlobScratch S = glob_carve(c.gscratch + c.gs_off[g], V, E);
+    uint2 *hb = reinterpret_cast<uint2 *>(S.bm);  // per 32 nodes: H* bits, H* nodes before the word
+    uint32_t *nolo = S.S;                         // compact node index -> H* (Kahn order) index
+    uint32_t *hs = c.s_a + gv.n0 + g;
+    uint32_t *cnt = ts + 1 + (it & 1) * 3 * PT_M;  // this graph's phase sums (graph parity: the next
+                                                 // graph's writes never meet this graph's late reads)
+    const uint32_t nw = (V + 31) / 32;
+    // ---- P0: membership bitmap in node order (32 nodes per thread: two 16-byte flag loads) ----
+    {
+      const uint32_t a = (uint32_t)((uint64_t)nw * r / M), b = (uint32_t)((uint64_t)nw * (r + 1) / M);
+      uint32_t sum = 0;
+      for (uint32_t w = a + tid; w < b; w += PT_B) {
+        const uint32_t v0 = 32 * w;
+        uint32_t bits = 0;
+        if (v0 + 31 < V) {
+          uint4 fa, fb;
+          __builtin_memcpy(&fa, gv.flags + v0, 16);
+          __builtin_memcpy(&fb, gv.flags + v0 + 16, 16);
+          const uint32_t fw[8] = {fa.x, fa.y, fa.z, fa.w, fb.x, fb.y, fb.z, fb.w};
+#pragma unroll
+          for (int q = 0; q < 32; q++) bits |= ((fw[q >> 2] >> (8 * (q & 3))) & NEMO_F_DELETED ? 1u : 0u) << q;
+        } else {
+          for (uint32_t v = v0; v < V; v++) bits |= (gv.flags[v] & NEMO_F_DELETED ? 1u : 0u) << (v - v0);
+        }
+        hb[w].x = bits;
+        sum += __popc(bits);
+      }
+      uint32_t tot;
+      block_exscan<PT_B>(sum, &tot, s_lds);
+      if (tid == 0) cnt[r] = tot;
+    }
+    team_sync(ctr, ++epoch * M);
+    // ---- P1: word prefixes; H* nodes per Kahn slice ----
+    {
+      if (tid < 64) {
+        uint32_t x = tid < r ? cnt[tid] : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += (uint32_t)__shfl_xor((int)x, d);
+        if (tid == 0) s_base[0] = x;
+      }
+      __syncthreads();
+      const uint32_t a = (uint32_t)((uint64_t)nw * r / M), b = (uint32_t)((uint64_t)nw * (r + 1) / M);
+      uint32_t o = s_base[0];
+      for (uint32_t w0 = a; w0 < b; w0 += PT_B) {
+        const uint32_t w = w0 + tid;
+        const uint32_t bits = w < b ? hb[w].x : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exscan<PT_B>(__popc(bits), &tot, s_lds);
+        if (w < b) hb[w].y = o + ex;
+        o += tot;
+      }
+      const uint32_t pa = (uint32_t)((uint64_t)V * r / M), pb = (uint32_t)((uint64_t)V * (r + 1) / M);
+      uint32_t hc = 0;
+      for (uint32_t p0 = pa + tid * PT_CP; p0 < pb; p0 += PT_B * PT_CP) {
+        uint32_t x[PT_CP];
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) x[q] = p0 + q < pb ? gv.topo[p0 + q] : 0u;
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) hc += p0 + q < pb ? (hb[x[q] >> 5].x >> (x[q] & 31)) & 1u : 0u;
+      }
+      uint32_t tot;
+      block_exscan<PT_B>(hc, &tot, s_lds);
+      if (tid == 0) cnt[PT_M + r] = tot;
+    }
+    team_sync(ctr, ++epoch * M);
+    // ---- P2: compaction of the Kahn slice (H* index, node, rule flag, compact rank, the
+    // node -> index map, full degrees prefixed within the slice) ----
+    {
+      if (tid < 64) {
+        uint32_t x = tid < r ? cnt[PT_M + tid] : 0u, t = tid < M ? cnt[PT_M + tid] : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          x += (uint32_t)__shfl_xor((int)x, d);
+          t += (uint32_t)__shfl_xor((int)t, d);
+        }
+        if (tid == 0) {
+          s_base[0] = x;
+          if (r == 0) S.meta[0] = t;
+        }
+      }
+      __syncthreads();
+      const uint32_t pa = (uint32_t)((uint64_t)V * r / M), pb = (uint32_t)((uint64_t)V * (r + 1) / M);
+      uint32_t i = s_base[0], oc = 0, op = 0;
+      for (uint32_t b0 = pa; b0 < pb; b0 += PT_B * PT_CP) {
+        const uint32_t p0 = b0 + tid * PT_CP;
+        uint32_t x[PT_CP], hx[PT_CP], cl = 0;
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) x[q] = p0 + q < pb ? gv.topo[p0 + q] : 0u;
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) {
+          const uint2 w = hb[x[q] >> 5];
+          const bool h = p0 + q < pb && ((w.x >> (x[q] & 31)) & 1u);
+          hx[q] = h ? w.y + __popc(w.x & ((1u << (x[q] & 31)) - 1u)) : GNIL;
+          cl += h ? 1u : 0u;
+        }
+        uint32_t wd[PT_CP], dc[PT_CP], dp[PT_CP], sc = 0, sp = 0;
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) {
+          const bool h = hx[q] != GNIL;
+          wd[q] = h ? gv.word[x[q]] : 0u;
+          dc[q] = h ? gv.fp[x[q] + 1] - gv.fp[x[q]] : 0u;
+          dp[q] = h ? gv.rp[x[q] + 1] - gv.rp[x[q]] : 0u;
+          sc += dc[q];
+          sp += dp[q];
+        }
+        uint32_t tot, tc, tp;
+        uint32_t j = i + block_exscan<PT_B>(cl, &tot, s_lds);
+        uint32_t ec = oc + block_exscan<PT_B>(sc, &tc, s_lds), ep = op + block_exscan<PT_B>(sp, &tp, s_lds);
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) {
+          if (hx[q] == GNIL) continue;
+          hs[j] = x[q];
+          S.rule[j] = is_rule(wd[q]) ? 1u : 0u;
+          S.crank[j] = hx[q];
+          nolo[hx[q]] = j;
+          S.ccoff[j] = ec;  // within the slice; P3 adds the slices before it
+          S.pcoff[j] = ep;
+          ec += dc[q];
+          ep += dp[q];
+          j++;
+        }
+        i += tot;
+        oc += tc;
+        op += tp;
+      }
+      if (tid == 0) {
+        cnt[2 * PT_M + r] = oc;
+        cnt[r] = op;  // P0's slot: its last readers passed the barrier before P2
+      }
+    }
+    team_sync(ctr, ++epoch * M);
+    // ---- P3: the H* adjacency in H* indices, rows laid out by full degree; the slice's
+    // rows at its offsets (the row pointers made global) ----
+    {
+      if (tid < 64) {
+        uint32_t l = tid < r ? cnt[PT_M + tid] : 0u, oc = tid < r ? cnt[2 * PT_M + tid] : 0u,
+                 op = tid < r ? cnt[tid] : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          l += (uint32_t)__shfl_xor((int)l, d);
+          oc += (uint32_t)__shfl_xor((int)oc, d);
+          op += (uint32_t)__shfl_xor((int)op, d);
+        }
+        if (tid == 0) {
+          s_base[0] = l;
+          s_base[1] = oc;
+          s_base[2] = op;
+        }
+      }
+      __syncthreads();
+      const uint32_t lo = s_base[0], hi = lo + cnt[PT_M + r], cb = s_base[1], pb = s_base[2];
+      if (r == M - 1 && tid == 0) {
+        S.ccoff[hi] = cb + cnt[2 * PT_M + r];
+        S.pcoff[hi] = pb + cnt[r];
+      }
+      auto rows = [&](const uint32_t *ptr, const uint32_t *col, uint32_t *off, uint32_t *endp, uint32_t *out,
+                      uint32_t ob) {
+        for (uint32_t i0 = lo + tid; i0 < hi; i0 += PT_B * GA_N) {
+          uint32_t x[GA_N], a[GA_N], e[GA_N], o[GA_N], k[GA_N];
+#pragma unroll
+          for (int q = 0; q < GA_N; q++) {
+            const uint32_t i = i0 + q * PT_B;
+            x[q] = i < hi ? hs[i] : 0u;
+            o[q] = i < hi ? off[i] + ob : 0u;
+            k[q] = 0;
+          }
+#pragma unroll
+          for (int q = 0; q < GA_N; q++) {
+            a[q] = ptr[x[q]];
+            e[q] = i0 + q * PT_B < hi ? ptr[x[q] + 1] : a[q];
+          }
+          for (uint32_t t = 0;; t += GA_F) {
+            bool more = false;
+            uint32_t y[GA_N][GA_F];
+#pragma unroll
+            for (int q = 0; q < GA_N; q++)
+#pragma unroll
+              for (int h = 0; h < GA_F; h++) y[q][h] = a[q] + t + h < e[q] ? col[a[q] + t + h] : GNIL;
+            uint2 w[GA_N][GA_F];
+#pragma unroll
+            for (int q = 0; q < GA_N; q++)
+#pragma unroll
+              for (int h = 0; h < GA_F; h++) w[q][h] = y[q][h] != GNIL ? hb[y[q][h] >> 5] : make_uint2(0, 0);
+            uint32_t m[GA_N][GA_F];
+#pragma unroll
+            for (int q = 0; q < GA_N; q++)
+#pragma unroll
+              for (int h = 0; h < GA_F; h++) {
+                const uint32_t yy = y[q][h] & 31u;
+                m[q][h] = (w[q][h].x >> yy) & 1u ? nolo[w[q][h].y + __popc(w[q][h].x & ((1u << yy) - 1u))] : GNIL;
+              }
+#pragma unroll
+            for (int q = 0; q < GA_N; q++) {
+#pragma unroll
+              for (int h = 0; h < GA_F; h++)
+                if (m[q][h] != GNIL) out[o[q] + k[q]++] = m[q][h];
+              more |= a[q] + t + GA_F < e[q];
+            }
+            if (!__any(more)) break;
+          }
+#pragma unroll
+          for (int q = 0; q < GA_N; q++) {
+            const uint32_t i = i0 + q * PT_B;
+            if (i >= hi) continue;
+            off[i] = o[q];
+            endp[i] = o[q] + k[q];
+          }
+        }
+      };
+      rows(gv.fp, gv.fc, S.ccoff, S.cend, S.child, cb);
+      rows(gv.rp, gv.rc, S.pcoff, S.pend, S.par, pb);
+    }
+  }
+}
+
 template <int GB>
 __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   static_assert(GS_WN % GB == 0, "whole window nodes per thread");
@@ -535,200 +806,210 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     s_fail = 0;
   }
   STAMP(0);
-  // ---- H* in level order, compact ID ranks ------------------------------------
-  // a stream compaction of the Kahn order (level-sorted already) by the H*
-  // flag: block scans over CP positions per thread, no counter atomics
-  for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
-  // every node's compact index, GNIL outside H* (a coalesced pass): the
-  // adjacency then tests a neighbour's membership and maps it with one gather
-  // With identity ID ranks (no rank array) the rank bitmap is the H* flag in
-  // node order, stored a word per half-wave (no scattered atomics)
+  // With k_glob_prep (identity ranks) the H* compaction, the compact ranks and the
+  // adjacency are done: only the H* node count is read here.
   const bool idrank = gv.rank == nullptr;
-  // (each thread 32 consecutive nodes: their flags in two 16-byte loads, the
-  // map in eight 16-byte stores, the bitmap word built in a register)
-  for (uint32_t v0 = 32 * tid; v0 < V; v0 += 32 * GB) {
-    uint32_t bits = 0;
-    if (v0 + 31 < V) {
-      uint4 fa, fb;
-      __builtin_memcpy(&fa, f + v0, 16);
-      __builtin_memcpy(&fb, f + v0 + 16, 16);
-      const uint32_t fw[8] = {fa.x, fa.y, fa.z, fa.w, fb.x, fb.y, fb.z, fb.w};
-#pragma unroll
-      for (int k = 0; k < 32; k++) bits |= ((fw[k >> 2] >> (8 * (k & 3))) & NEMO_F_DELETED ? 1u : 0u) << k;
-      const uint4 nil = make_uint4(GNIL, GNIL, GNIL, GNIL);
-#pragma unroll
-      for (int k = 0; k < 8; k++) __builtin_memcpy(hidx + v0 + 4 * k, &nil, 16);
-    } else {
-      for (uint32_t v = v0; v < V; v++) {
-        bits |= (f[v] & NEMO_F_DELETED ? 1u : 0u) << (v - v0);
-        hidx[v] = GNIL;
-      }
-    }
-    if (idrank) S.bm[v0 >> 5] = bits;
-  }
-  __syncthreads();
   uint32_t n = 0;
-  for (uint32_t base = 0; base < V; base += GB * CP) {
-    const uint32_t p0 = base + tid * CP;
-    uint32_t x[CP], cl = 0;
-    bool h[CP];
-#pragma unroll
-    for (int q = 0; q < CP; q++) x[q] = p0 + q < V ? gv.topo[p0 + q] : 0u;
-#pragma unroll
-    for (int q = 0; q < CP; q++) {
-      h[q] = p0 + q < V && (f[x[q]] & NEMO_F_DELETED);
-      cl += h[q] ? 1u : 0u;
+  if (c.glob_prep) {
+    n = S.meta[0];
+  } else {
+    // ---- H* in level order, compact ID ranks ------------------------------------
+    // a stream compaction of the Kahn order (level-sorted already) by the H*
+    // flag: block scans over CP positions per thread, no counter atomics
+    for (uint32_t w = tid; w < nw; w += GB) S.bm[w] = 0;
+    // every node's compact index, GNIL outside H* (a coalesced pass): the
+    // adjacency then tests a neighbour's membership and maps it with one gather
+    // With identity ID ranks (no rank array) the rank bitmap is the H* flag in
+    // node order, stored a word per half-wave (no scattered atomics)
+    // (each thread 32 consecutive nodes: their flags in two 16-byte loads, the
+    // map in eight 16-byte stores, the bitmap word built in a register)
+    for (uint32_t v0 = 32 * tid; v0 < V; v0 += 32 * GB) {
+      uint32_t bits = 0;
+      if (v0 + 31 < V) {
+        uint4 fa, fb;
+        __builtin_memcpy(&fa, f + v0, 16);
+        __builtin_memcpy(&fb, f + v0 + 16, 16);
+        const uint32_t fw[8] = {fa.x, fa.y, fa.z, fa.w, fb.x, fb.y, fb.z, fb.w};
+  #pragma unroll
+        for (int k = 0; k < 32; k++) bits |= ((fw[k >> 2] >> (8 * (k & 3))) & NEMO_F_DELETED ? 1u : 0u) << k;
+        const uint4 nil = make_uint4(GNIL, GNIL, GNIL, GNIL);
+  #pragma unroll
+        for (int k = 0; k < 8; k++) __builtin_memcpy(hidx + v0 + 4 * k, &nil, 16);
+      } else {
+        for (uint32_t v = v0; v < V; v++) {
+          bits |= (f[v] & NEMO_F_DELETED ? 1u : 0u) << (v - v0);
+          hidx[v] = GNIL;
+        }
+      }
+      if (idrank) S.bm[v0 >> 5] = bits;
     }
-    uint32_t tot;
-    uint32_t i = block_exscan<GB>(cl, &tot, s_lds) + n;
-#pragma unroll
-    for (int q = 0; q < CP; q++) {
-      if (p0 + q >= V || !h[q]) continue;
-      hs[i] = x[q];
-      hidx[x[q]] = i;
-      S.rule[i] = is_rule(gv.word[x[q]]) ? 1u : 0u;
-      const uint32_t r = gv.rank_of(x[q]);
-      S.crank[i] = r;
-      if (!idrank) atomicOr(&S.bm[r >> 5], 1u << (r & 31));
-      i++;
+    __syncthreads();
+    for (uint32_t base = 0; base < V; base += GB * CP) {
+      const uint32_t p0 = base + tid * CP;
+      uint32_t x[CP], cl = 0;
+      bool h[CP];
+  #pragma unroll
+      for (int q = 0; q < CP; q++) x[q] = p0 + q < V ? gv.topo[p0 + q] : 0u;
+  #pragma unroll
+      for (int q = 0; q < CP; q++) {
+        h[q] = p0 + q < V && (f[x[q]] & NEMO_F_DELETED);
+        cl += h[q] ? 1u : 0u;
+      }
+      uint32_t tot;
+      uint32_t i = block_exscan<GB>(cl, &tot, s_lds) + n;
+  #pragma unroll
+      for (int q = 0; q < CP; q++) {
+        if (p0 + q >= V || !h[q]) continue;
+        hs[i] = x[q];
+        hidx[x[q]] = i;
+        S.rule[i] = is_rule(gv.word[x[q]]) ? 1u : 0u;
+        const uint32_t r = gv.rank_of(x[q]);
+        S.crank[i] = r;
+        if (!idrank) atomicOr(&S.bm[r >> 5], 1u << (r & 31));
+        i++;
+      }
+      n += tot;
     }
-    n += tot;
   }
   __syncthreads();
   if (n == 0) {
     if (tid == 0) c.nch[g] = 0;
     return;
   }
-  // (GU entries per thread and round below: each round's loads, then its
-  // gathers, in flight together)
-  for (uint32_t w0 = tid; w0 < nw; w0 += GB * GU) {
-    uint32_t x[GU];
-#pragma unroll
-    for (int q = 0; q < GU; q++) x[q] = w0 + q * GB < nw ? S.bm[w0 + q * GB] : 0u;
-#pragma unroll
-    for (int q = 0; q < GU; q++)
-      if (w0 + q * GB < nw) S.bmpre[w0 + q * GB] = __popc(x[q]);
-  }
-  __syncthreads();
-  block_scan_inplace<GB, 16>(S.bmpre, nw, s_lds);
-  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
-    uint32_t r[GU], bp_[GU], bw[GU];
-#pragma unroll
-    for (int q = 0; q < GU; q++) r[q] = i0 + q * GB < n ? S.crank[i0 + q * GB] : 0u;
-#pragma unroll
-    for (int q = 0; q < GU; q++) {
-      bp_[q] = S.bmpre[r[q] >> 5];
-      bw[q] = S.bm[r[q] >> 5];
+  if (!c.glob_prep) {
+    // (GU entries per thread and round below: each round's loads, then its
+    // gathers, in flight together)
+    for (uint32_t w0 = tid; w0 < nw; w0 += GB * GU) {
+      uint32_t x[GU];
+  #pragma unroll
+      for (int q = 0; q < GU; q++) x[q] = w0 + q * GB < nw ? S.bm[w0 + q * GB] : 0u;
+  #pragma unroll
+      for (int q = 0; q < GU; q++)
+        if (w0 + q * GB < nw) S.bmpre[w0 + q * GB] = __popc(x[q]);
     }
-#pragma unroll
-    for (int q = 0; q < GU; q++)
-      if (i0 + q * GB < n) S.crank[i0 + q * GB] = bp_[q] + __popc(bw[q] & ((1u << (r[q] & 31)) - 1u));
-  }
-  STAMP(1);
-  // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
-  // From the graph's own CSR rows, one H* node per thread: a row's children
-  // (or parents) in batches of GA_B with their loads in flight together, no
-  // atomics.  Each H* row is laid out by the node's full degree (one scan of
-  // the degrees, no counting pass over the neighbours' flags); the H*
-  // entries fill its front and cend / pend mark where they stop.  (Counting
-  // and scattering the whole edge list with cursor atomics cost a
-  // latency-bound pass over all E edges per direction; walking four nodes'
-  // rows in lockstep, one entry per row and step, was slower: the step count
-  // is the longest of the rows.)
-  auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t j00, uint32_t *out) -> uint32_t {
-    uint32_t k = 0;
-    const uint32_t j1 = ptr[x + 1];
-    for (uint32_t j = j00; j < j1; j += GA_B) {
-      uint32_t y[GA_B];
-#pragma unroll
-      for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
-      uint32_t hy[GA_B];
-#pragma unroll
-      for (int q = 0; q < GA_B; q++) hy[q] = j + q < j1 ? hidx[y[q]] : GNIL;
-#pragma unroll
-      for (int q = 0; q < GA_B; q++)
-        if (hy[q] != GNIL) out[k++] = hy[q];
-    }
-    return k;
-  };
-  for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
-    uint32_t x[GU];
-#pragma unroll
-    for (int q = 0; q < GU; q++) x[q] = i0 + q * GB < n ? hs[i0 + q * GB] : 0u;
-#pragma unroll
-    for (int q = 0; q < GU; q++) {
-      const uint32_t i = i0 + q * GB;
-      const uint32_t fa = gv.fp[x[q]], fb = gv.fp[x[q] + 1], ra = gv.rp[x[q]], rb = gv.rp[x[q] + 1];
-      if (i < n) {
-        S.ccoff[i] = fb - fa;
-        S.pcoff[i] = rb - ra;
+    __syncthreads();
+    block_scan_inplace<GB, 16>(S.bmpre, nw, s_lds);
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      uint32_t r[GU], bp_[GU], bw[GU];
+  #pragma unroll
+      for (int q = 0; q < GU; q++) r[q] = i0 + q * GB < n ? S.crank[i0 + q * GB] : 0u;
+  #pragma unroll
+      for (int q = 0; q < GU; q++) {
+        bp_[q] = S.bmpre[r[q] >> 5];
+        bw[q] = S.bm[r[q] >> 5];
       }
+  #pragma unroll
+      for (int q = 0; q < GU; q++)
+        if (i0 + q * GB < n) S.crank[i0 + q * GB] = bp_[q] + __popc(bw[q] & ((1u << (r[q] & 31)) - 1u));
     }
-  }
-  if (tid == 0) {
-    S.ccoff[n] = 0;
-    S.pcoff[n] = 0;
-  }
-  __syncthreads();
-  block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
-  block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
-  // the rows written GA_N nodes per thread at a time: their bounds, first
-  // GA_F entries and those entries' compact indices each a round of loads in
-  // flight together (one node at a time was a chain of three dependent
-  // round trips per node and direction); longer rows finish by themselves
-  auto hrows = [&](const uint32_t *ptr, const uint32_t *col, const uint32_t *off, uint32_t *endp, uint32_t *out) {
-    for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) {
-      uint32_t x[GA_N], a[GA_N], b[GA_N], o[GA_N], k[GA_N];
-#pragma unroll
-      for (int q = 0; q < GA_N; q++) {
+    STAMP(1);
+    GSTOP(1);
+    // ---- H* adjacency (rows in any order: every consumer takes a max/min) ---------
+    // From the graph's own CSR rows, one H* node per thread: a row's children
+    // (or parents) in batches of GA_B with their loads in flight together, no
+    // atomics.  Each H* row is laid out by the node's full degree (one scan of
+    // the degrees, no counting pass over the neighbours' flags); the H*
+    // entries fill its front and cend / pend mark where they stop.  (Counting
+    // and scattering the whole edge list with cursor atomics cost a
+    // latency-bound pass over all E edges per direction; walking four nodes'
+    // rows in lockstep, one entry per row and step, was slower: the step count
+    // is the longest of the rows.)
+    auto hrow = [&](const uint32_t *ptr, const uint32_t *col, uint32_t x, uint32_t j00, uint32_t *out) -> uint32_t {
+      uint32_t k = 0;
+      const uint32_t j1 = ptr[x + 1];
+      for (uint32_t j = j00; j < j1; j += GA_B) {
+        uint32_t y[GA_B];
+  #pragma unroll
+        for (int q = 0; q < GA_B; q++) y[q] = j + q < j1 ? col[j + q] : 0u;
+        uint32_t hy[GA_B];
+  #pragma unroll
+        for (int q = 0; q < GA_B; q++) hy[q] = j + q < j1 ? hidx[y[q]] : GNIL;
+  #pragma unroll
+        for (int q = 0; q < GA_B; q++)
+          if (hy[q] != GNIL) out[k++] = hy[q];
+      }
+      return k;
+    };
+    for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
+      uint32_t x[GU];
+  #pragma unroll
+      for (int q = 0; q < GU; q++) x[q] = i0 + q * GB < n ? hs[i0 + q * GB] : 0u;
+  #pragma unroll
+      for (int q = 0; q < GU; q++) {
         const uint32_t i = i0 + q * GB;
-        x[q] = i < n ? hs[i] : 0u;
-        o[q] = i < n ? off[i] : 0u;
-        k[q] = 0;
-      }
-#pragma unroll
-      for (int q = 0; q < GA_N; q++) {
-        a[q] = ptr[x[q]];
-        b[q] = i0 + q * GB < n ? ptr[x[q] + 1] : a[q];
-      }
-      uint32_t y[GA_N][GA_F], hy[GA_N][GA_F];
-#pragma unroll
-      for (int q = 0; q < GA_N; q++)
-#pragma unroll
-        for (int h = 0; h < GA_F; h++) y[q][h] = a[q] + h < b[q] ? col[a[q] + h] : 0u;
-#if GA_BM
-      // identity ranks: S.bm is the H* flag in node order (119 KB per 1M-node
-      // graph, cache-resident), so only members' compact indices are gathered
-      if (idrank) {
-        uint32_t w[GA_N][GA_F];
-#pragma unroll
-        for (int q = 0; q < GA_N; q++)
-#pragma unroll
-          for (int h = 0; h < GA_F; h++) w[q][h] = a[q] + h < b[q] ? S.bm[y[q][h] >> 5] : 0u;
-#pragma unroll
-        for (int q = 0; q < GA_N; q++)
-#pragma unroll
-          for (int h = 0; h < GA_F; h++) hy[q][h] = (w[q][h] >> (y[q][h] & 31)) & 1u ? hidx[y[q][h]] : GNIL;
-      } else
-#endif
-#pragma unroll
-      for (int q = 0; q < GA_N; q++)
-#pragma unroll
-        for (int h = 0; h < GA_F; h++) hy[q][h] = a[q] + h < b[q] ? hidx[y[q][h]] : GNIL;
-#pragma unroll
-      for (int q = 0; q < GA_N; q++) {
-#pragma unroll
-        for (int h = 0; h < GA_F; h++)
-          if (hy[q][h] != GNIL) out[o[q] + k[q]++] = hy[q][h];
-        if (b[q] > a[q] + GA_F) k[q] += hrow(ptr, col, x[q], a[q] + GA_F, out + o[q] + k[q]);
-        if (i0 + q * GB < n) endp[i0 + q * GB] = o[q] + k[q];
+        const uint32_t fa = gv.fp[x[q]], fb = gv.fp[x[q] + 1], ra = gv.rp[x[q]], rb = gv.rp[x[q] + 1];
+        if (i < n) {
+          S.ccoff[i] = fb - fa;
+          S.pcoff[i] = rb - ra;
+        }
       }
     }
-  };
-  hrows(gv.fp, gv.fc, S.ccoff, S.cend, S.child);
-  hrows(gv.rp, gv.rc, S.pcoff, S.pend, S.par);
-  __syncthreads();
+    if (tid == 0) {
+      S.ccoff[n] = 0;
+      S.pcoff[n] = 0;
+    }
+    __syncthreads();
+    block_scan_inplace<GB, 16>(S.ccoff, n + 1, s_lds);
+    block_scan_inplace<GB, 16>(S.pcoff, n + 1, s_lds);
+    // the rows written GA_N nodes per thread at a time: their bounds, first
+    // GA_F entries and those entries' compact indices each a round of loads in
+    // flight together (one node at a time was a chain of three dependent
+    // round trips per node and direction); longer rows finish by themselves
+    auto hrows = [&](const uint32_t *ptr, const uint32_t *col, const uint32_t *off, uint32_t *endp, uint32_t *out) {
+      for (uint32_t i0 = tid; i0 < n; i0 += GB * GA_N) {
+        uint32_t x[GA_N], a[GA_N], b[GA_N], o[GA_N], k[GA_N];
+  #pragma unroll
+        for (int q = 0; q < GA_N; q++) {
+          const uint32_t i = i0 + q * GB;
+          x[q] = i < n ? hs[i] : 0u;
+          o[q] = i < n ? off[i] : 0u;
+          k[q] = 0;
+        }
+  #pragma unroll
+        for (int q = 0; q < GA_N; q++) {
+          a[q] = ptr[x[q]];
+          b[q] = i0 + q * GB < n ? ptr[x[q] + 1] : a[q];
+        }
+        uint32_t y[GA_N][GA_F], hy[GA_N][GA_F];
+  #pragma unroll
+        for (int q = 0; q < GA_N; q++)
+  #pragma unroll
+          for (int h = 0; h < GA_F; h++) y[q][h] = a[q] + h < b[q] ? col[a[q] + h] : 0u;
+  #if GA_BM
+        // identity ranks: S.bm is the H* flag in node order (119 KB per 1M-node
+        // graph, cache-resident), so only members' compact indices are gathered
+        if (idrank) {
+          uint32_t w[GA_N][GA_F];
+  #pragma unroll
+          for (int q = 0; q < GA_N; q++)
+  #pragma unroll
+            for (int h = 0; h < GA_F; h++) w[q][h] = a[q] + h < b[q] ? S.bm[y[q][h] >> 5] : 0u;
+  #pragma unroll
+          for (int q = 0; q < GA_N; q++)
+  #pragma unroll
+            for (int h = 0; h < GA_F; h++) hy[q][h] = (w[q][h] >> (y[q][h] & 31)) & 1u ? hidx[y[q][h]] : GNIL;
+        } else
+  #endif
+  #pragma unroll
+        for (int q = 0; q < GA_N; q++)
+  #pragma unroll
+          for (int h = 0; h < GA_F; h++) hy[q][h] = a[q] + h < b[q] ? hidx[y[q][h]] : GNIL;
+  #pragma unroll
+        for (int q = 0; q < GA_N; q++) {
+  #pragma unroll
+          for (int h = 0; h < GA_F; h++)
+            if (hy[q][h] != GNIL) out[o[q] + k[q]++] = hy[q][h];
+          if (b[q] > a[q] + GA_F) k[q] += hrow(ptr, col, x[q], a[q] + GA_F, out + o[q] + k[q]);
+          if (i0 + q * GB < n) endp[i0 + q * GB] = o[q] + k[q];
+        }
+      }
+    };
+    hrows(gv.fp, gv.fc, S.ccoff, S.cend, S.child);
+    hrows(gv.rp, gv.rc, S.pcoff, S.pend, S.par);
+    __syncthreads();
+  }
   STAMP(2);
+  GSTOP(2);
   // ---- up (forward) and down/nxt (backward): windowed single-wave sweeps -----------
 #ifdef NEMO_STAMPS
   unsigned long long *gst = c.stamps ? c.stamps + 16 * (size_t)blockIdx.x : nullptr;
@@ -738,6 +1019,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   glob_sweep<true, GB>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
   glob_sweep<false, GB>(S, n, hs, nlv, &s_fail, s_gs, s_lds, gst);
   STAMP(3);
+  GSTOP(3);
   uint32_t mu = 0, ml = 0;
   for (uint32_t b0 = 0; b0 < n; b0 += 16 * GB) {  // four quads of consecutive nodes per thread and round
     int32_t u[16], d[16];
@@ -831,6 +1113,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
   __syncthreads();
   STAMP(4);
+  GSTOP(4);
   // ---- prefix ranks per up-level: roots by ID rank, then groups by po(bp) -----------
   for (uint32_t k = 0; k <= maxup; k++) {
     const uint32_t a = S.uoff[k], b = S.uoff[k + 1];
@@ -929,6 +1212,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     __syncthreads();
   }
   STAMP(5);
+  GSTOP(5);
   // ---- preorder of the representatives: pre(v) = up(v) + sum of off over v and its bp
   // ancestors, off = sizes of the earlier siblings (sizes laid out in (level, po) order).
   // Subtree sizes bottom-up, then ONE top-down pass over the up-levels adds each
@@ -1014,6 +1298,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     __syncthreads();
   }
   STAMP(6);
+  GSTOP(6);
   // one representative per accepted path (the witness whose best parent does not continue into it)
   // (GU nodes per thread per round, each round's gathers in flight together)
   for (uint32_t i0 = 0; i0 < n; i0 += GB * GU) {
@@ -1054,6 +1339,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   __syncthreads();
   const uint32_t nch = s_nch;
   STAMP(7);
+  GSTOP(7);
   // ---- acceptance order (len desc, preorder asc) -------------------------------------
   // pre = va + up is the representative's preorder index (unique, < n): the chains
   // laid out by it are already in preorder; a stable LSD counting sort by
@@ -1115,6 +1401,7 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     kb = t;
   }
   STAMP(8);
+  GSTOP(8);
   uint32_t *out = c.chain + 5 * gv.n0;
   for (uint32_t p0 = tid; p0 < nch; p0 += GB * GU) {
     uint32_t q[GU], h[GU], t[GU], l[GU], hh[GU], tt[GU];
@@ -1149,8 +1436,17 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   }
 }
 
+uint32_t glob_team_words() { return PT_TEAMS * PT_WORDS; }
+
 void launch_chains_glob(const DevCorpus &c, hipStream_t s) {
   if (!c.gscratch) return;
+  if (c.glob_prep) {
+    launch_zero(c.team, PT_TEAMS * PT_WORDS * sizeof(uint32_t), s);
+    // every member of a team must be resident at once (team barriers): one
+    // 1024-thread workgroup per CU, at most the device's CUs
+    const uint32_t m = std::max(1u, std::min<uint32_t>(PT_M, c.n_cu / PT_TEAMS));
+    hipLaunchKernelGGL(k_glob_prep, dim3(PT_TEAMS * m), dim3(PT_B), 0, s, c);
+  }
   if (c.glob_block == 512)
     hipLaunchKernelGGL(k_chains_glob<512>, dim3(c.G), dim3(512), 0, s, c);
   else

@@ -403,22 +403,26 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 }
 
 // ---- the windowed walk ------------------------------------------------------------------
-// MODE 0: reachability, T = u64 (64 sources per bit column), one walker;
-//         blockIdx.y = 0: Fwd* over parents in Kahn order (image m0), 1: Bwd*
-//         over children in reversed Kahn order (image m1).  value = Good | OR(links).
-// MODE 2: depth, T = u32, NE walkers (sources NE·blockIdx.x + e), Kahn order
-//         over parents (image m0): s = D ? 1 + max(s of links) : 0 (depth + 1
-//         of D nodes; a non-D parent has s = 0, so the max runs over D
-//         parents).  While a window is walked a ring slot holds DX_NOTD (not in
-//         D: absorbs every max) or DX_IND | r, r = the max so far; s = r + 1.
+// MODE 0: Bwd* reachability, T = u64 (64 sources per bit column), one walker,
+//         over children in reversed Kahn order (image m1); value = Good | OR(links).
+//         When the walk is done the workgroup also writes the chunk's leaf
+//         candidates LC(x) = B(x) & ~OR(B of x's children) for goals x.
+// MODE 2: longest paths from Good, T = u32, NE walkers (sources NE·bx + e), Kahn
+//         order over parents (image m0):
+//           val(v) = max(Good(v), max over parents p of c(val(p))), c(x) = x + (x > 0)
+//         so val(v) = 1 + the longest path from a Good goal to v, and 0 off
+//         Fwd*(Good).  For v in D = Fwd* ∩ Bwd* this is depth(v) + 1, the reference's
+//         depth (:82-98): every path from a Good goal to a D node stays in D, and a
+//         D node without a D parent is a Good goal.  The walk needs no D and no Fwd*
+//         walk: it runs beside the Bwd* walk (one launch, k_dx_walks).
 // WHOLE: the graph is one window (ring = positions, no wrap, no misses).
 //
 // Windows are pipelined: while the walker waves walk window k, the other
-// ("worker") waves finalize window k - 1 (values to HBM, LP maxima) and stage
-// window k + 1 (its link records and steps copied from the image into the
-// other LDS buffer, every position's init value, with the values of its links
-// that leave the ring folded in from HBM, into its ring slot); one barrier
-// per window.  The image's ring misses make this safe (dxi_far_end).
+// ("worker") waves finalize window k - 1 (values to HBM) and stage window k + 1
+// (its link records and steps copied from the image into the other LDS buffer,
+// every position's init value, with the values of its links that leave the
+// ring folded in from HBM, into its ring slot); one barrier per window.  The
+// image's ring misses make this safe (dxi_far_end).
 //
 // A walk step is <= 256 links of one level, lanes over links: read the linked
 // values, apply them to the owners' slots with LDS atomics.  Lane l takes the
@@ -429,25 +433,21 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_good(DxArgs a) {
 // no barrier separates steps; the next step's records are read during the
 // step before, and step descriptors come 64 at a time (one LDS read per 64
 // steps), so a step costs one LDS round trip.
-#define DX_NOTD 0xFFFFFFFFu
-#define DX_IND 0x80000000u
 template <typename T, int NE>
 struct DxLds {
   T *ring0;          // NE rings of [R + 1 + 64] (stride rs): [R] the identity (sink), [R + 1 + lane] dump slots
   uint32_t rs;
   uint32_t *lk;      // [NB][EC] link records of a window
   uint32_t *st;      // [NB][64] its first 64 step descriptors (the rest is read from the image)
-  uint32_t *lpb;     // [NL][NE][LW] depth: LP rules of a window, one bit per position
-  uint32_t LW;
 };
 template <typename T, int NE>
 __host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_t EC, bool whole) {
-  const uint32_t NB = whole ? 1u : 2u, NL = whole ? 1u : 3u;
-  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * 256u +
-         NL * NE * lds_align(4u * (W / 32u + 2u));
+  const uint32_t NB = whole ? 1u : 2u;
+  (void)W;
+  return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * 256u;
 }
 template <typename T, int NE>
-__device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_t R, uint32_t EC, bool whole) {
+__device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t R, uint32_t EC, bool whole) {
   const uint32_t NB = whole ? 1u : 2u;
   uint8_t *p = (uint8_t *)base;
   DxLds<T, NE> L;
@@ -457,56 +457,41 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t W, uint32_
   L.lk = (uint32_t *)p;
   p += NB * lds_align(4u * EC);
   L.st = (uint32_t *)p;
-  p += NB * 256u;
-  L.LW = lds_align(4u * (W / 32u + 2u)) / 4u;
-  L.lpb = (uint32_t *)p;
   return L;
 }
+#define DX_VMAX 0xFFFEu  // longest val kept (u16 per source and position); past it the call fails
 
 template <int MODE, int NE, bool WHOLE, int NT>
-__global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0, DxImg m1) {
+__device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1,
+                                        uint32_t bx, uint8_t *dyn) {
   using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
-  extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_lmax[NE], s_lpn[NE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool rev = MODE == 0 && blockIdx.y == 1;
-  const DxImg m = rev ? m1 : m0;
-  const uint32_t V = a.p.V0, W = m.W, R = m.R, EC = m.EC;
-  const uint32_t chunk = MODE == 0 ? blockIdx.x : 0u;
-  DxLds<T, NE> L = dx_carve<T, NE>(dyn, W, R, EC, WHOLE);
-  const uint32_t LW = L.LW;
+  constexpr bool rev = MODE == 0;
+  const DxImg &m = rev ? m1 : m0;
+  const uint32_t V = a.p.V0, R = m.R, EC = m.EC;
+  const uint32_t chunk = MODE == 0 ? bx : (bx * NE) >> 6;
+  DxLds<T, NE> L = dx_carve<T, NE>(dyn, R, EC, WHOLE);
   const uint32_t *rowp = rev ? a.p.fp : a.p.rp;
-  // per walker e: its source (depth), ring and value array, computed from e (a
+  // per walker e: its source (MODE 2), ring and value array, computed from e (a
   // dynamically indexed register array would live in scratch memory)
-  auto srcu = [&](uint32_t e) -> uint32_t {  // NEMO_NONE: no source, or no LP rule (nothing to walk)
+  auto srcu = [&](uint32_t e) -> uint32_t {  // NEMO_NONE: no source
     if (MODE == 0) return 0u;
-    const uint32_t u = blockIdx.x * NE + e;
-    return u < a.nu && ((a.lpany[u >> 6] >> (u & 63u)) & 1ull) ? u : NEMO_NONE;
+    const uint32_t u = bx * NE + e;
+    return u < a.nu ? u : NEMO_NONE;
   };
   auto ringp = [&](uint32_t e) -> T * { return L.ring0 + (size_t)e * L.rs; };
-  auto gvalp = [&](uint32_t e) -> T * {
-    if (MODE == 0) return (T *)((rev ? a.bw : a.fw) + (size_t)chunk * V);
-    return (T *)(a.sval + (size_t)min(blockIdx.x * NE + e, a.nu - 1u) * V);
+  uint64_t *const bwv = a.bw + (size_t)chunk * V;
+  auto sval = [&](uint32_t e) -> uint16_t * {
+    return reinterpret_cast<uint16_t *>(a.sval) + (size_t)min(bx * NE + e, a.nu - 1u) * V;
   };
   auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
-  bool any = MODE == 0;
-  for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
-  if (!any) return;  // workgroup-uniform
-  if (tid < (uint32_t)NE) {
-    ringp(tid)[R] = MODE == 0 ? (T)0 : (T)DX_NOTD;  // the sink reads as "no value": OR 0, depth s = 0
-    s_lmax[tid] = 0;
-    s_lpn[tid] = 0;
-  }
-  uint32_t lmax[NE];
-#pragma unroll
-  for (int e = 0; e < NE; e++) lmax[e] = 0;
-
+  if (tid < (uint32_t)NE) ringp(tid)[R] = (T)0;  // the sink reads as "no value": OR 0, max 0
   // ---- staging of window kw by threads [wt0, wt0 + nwt) (whole waves) ----
-  auto stage = [&](uint32_t kw, uint32_t buf, uint32_t lb, uint32_t wt, uint32_t nwt) {
+  auto stage = [&](uint32_t kw, uint32_t buf, uint32_t wt, uint32_t nwt) {
     const uint32_t w0 = m.wb[kw], w1 = m.wb[kw + 1], n = w1 - w0;
     const uint32_t base = rowp[w0], ne = rowp[w1] - base;
     const uint32_t st0 = m.stepb[kw], nst = m.stepb[kw + 1] - st0;
-    uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * 64u, *lpb = L.lpb + lb * NE * LW;
+    uint32_t *lk = L.lk + buf * EC, *st = L.st + buf * 64u;
     // records, in 16-B chunks of the image
     const uint32_t c0 = base >> 2, c1 = (base + ne + 3u) >> 2;
     for (uint32_t cb = c0; cb < c1; cb += 2 * nwt) {
@@ -528,67 +513,56 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
       }
     }
     if (wt < 64u) st[wt] = wt < nst ? m.steps[st0 + wt] : 0u;
-    // init values with the misses folded in; depth: the LP bits of 64
-    // consecutive positions by ballot
+    // init values (Good) with the misses folded in
     for (uint32_t k0 = 0; k0 < n; k0 += nwt) {
       const uint32_t kk = k0 + wt;
       const bool in = kk < n;
       const uint32_t i = w0 + (in ? kk : 0u), pos = rev ? V - 1u - i : i;
       const uint32_t mo0 = !WHOLE && in ? m.moff[i] : 0u, mo1 = !WHOLE && in ? m.moff[i + 1] : 0u;
+      const uint64_t gd = in ? a.gw[(size_t)chunk * V + pos] : 0ull;
       if (MODE == 0) {
-        T v = in ? (T)a.gw[(size_t)chunk * V + pos] : (T)0;
+        T v = (T)gd;
         for (uint32_t mm = mo0; mm < mo1; mm++)
-          v |= __hip_atomic_load(gvalp(0) + m.mx[mm], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v |= __hip_atomic_load(bwv + m.mx[mm], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (in) ringp(0)[slot(i)] = v;
       } else {
-        const bool rule = in && (a.p.info[pos] & DXI_RULE);
-        const uint64_t dv = in ? a.dw[(size_t)((blockIdx.x * NE) >> 6) * V + pos] : 0ull;
-        const uint64_t lv = rule ? a.lw[(size_t)((blockIdx.x * NE) >> 6) * V + pos] : 0ull;
         uint32_t r[NE];
 #pragma unroll
-        for (int e = 0; e < NE; e++) r[e] = 0;
+        for (int e = 0; e < NE; e++) r[e] = (uint32_t)((gd >> ((bx * NE + e) & 63u)) & 1ull);
         for (uint32_t mm = mo0; mm < mo1; mm++) {
           const uint32_t x = m.mx[mm];
 #pragma unroll
           for (int e = 0; e < NE; e++)
-            if (srcu(e) != NEMO_NONE)
-              r[e] = max(r[e], __hip_atomic_load(gvalp(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (srcu(e) != NEMO_NONE) {
+              const uint32_t v = __hip_atomic_load(sval(e) + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              r[e] = max(r[e], v + (v ? 1u : 0u));
+            }
         }
 #pragma unroll
-        for (int e = 0; e < NE; e++) {
-          const uint32_t u = srcu(e), b = (blockIdx.x * NE + e) & 63u;
-          const bool d = u != NEMO_NONE && ((dv >> b) & 1ull);
-          if (in) ringp(e)[slot(i)] = d ? (DX_IND | r[e]) : DX_NOTD;
-          const uint64_t lpm = __ballot(u != NEMO_NONE && rule && ((lv >> b) & 1ull));
-          const uint32_t wd = (k0 + (wt & ~63u)) >> 5;
-          if (lane < 2u && wd + lane < LW) lpb[e * LW + wd + lane] = (uint32_t)(lpm >> (32u * lane));
-        }
+        for (int e = 0; e < NE; e++)
+          if (in) ringp(e)[slot(i)] = r[e];
       }
     }
   };
-  // ---- finalize of window kw: values to HBM; depth: s, the LP maxima, the LP list ----
-  auto finalize = [&](uint32_t kw, uint32_t lb, uint32_t wt, uint32_t nwt) {
+  // ---- finalize of window kw: values to HBM ----
+  auto finalize = [&](uint32_t kw, uint32_t wt, uint32_t nwt) {
     const uint32_t w0 = m.wb[kw], n = m.wb[kw + 1] - w0;
-    const uint32_t *lpb = L.lpb + lb * NE * LW;
+    bool over = false;
     for (uint32_t kk = wt; kk < n; kk += nwt) {
       const uint32_t i = w0 + kk, sl = slot(i);
       if (MODE == 0) {
-        gvalp(0)[i] = ringp(0)[sl];
+        if (!WHOLE) bwv[i] = ringp(0)[sl];
       } else {
 #pragma unroll
         for (int e = 0; e < NE; e++) {
-          const uint32_t u = srcu(e);
-          if (u == NEMO_NONE) continue;
-          const uint32_t r = (uint32_t)ringp(e)[sl];
-          const uint32_t sv = r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u;
-          if (!WHOLE) gvalp(e)[i] = (T)sv;  // read back by later windows' misses and the rows pass
-          if ((lpb[e * LW + (kk >> 5)] >> (kk & 31u)) & 1u) {
-            lmax[e] = max(lmax[e], sv);
-            if (!WHOLE) a.lplist[(size_t)u * V + atomicAdd(&s_lpn[e], 1u)] = i;
-          }
+          if (srcu(e) == NEMO_NONE) continue;
+          const uint32_t v = (uint32_t)ringp(e)[sl];
+          over |= v > DX_VMAX;
+          sval(e)[i] = (uint16_t)min(v, (uint32_t)DX_VMAX);
         }
       }
     }
+    if (MODE == 2 && __any(over) && lane == 0) atomicOr(a.n_missing, 0x80000000u);
   };
   // ---- the walk of window kw by wave e ----
   auto walk = [&](uint32_t kw, uint32_t buf, uint32_t e) {
@@ -598,12 +572,8 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
     T *ring = ringp(e);
     const uint32_t idle = R | ((R + 1u + lane) << 16);
     auto apply = [&](uint32_t rec, T x) {
-      if (MODE == 0) {
-        atomicOr((unsigned long long *)&ring[rec >> 16], (unsigned long long)x);
-      } else {
-        const uint32_t sv = (uint32_t)x == DX_NOTD ? 0u : ((uint32_t)x & ~DX_IND) + 1u;
-        atomicMax((uint32_t *)&ring[rec >> 16], DX_IND | sv);
-      }
+      if (MODE == 0) atomicOr((unsigned long long *)&ring[rec >> 16], (unsigned long long)x);
+      else atomicMax((uint32_t *)&ring[rec >> 16], (uint32_t)x + ((uint32_t)x ? 1u : 0u));
     };
     if (!nst) return;
     // step descriptors 64 at a time: the first 64 staged in LDS, the next
@@ -636,197 +606,151 @@ __global__ __launch_bounds__(NT) void k_dx_walk(DevCorpus c, DxArgs a, DxImg m0,
       bat = nbat;
     }
   };
+  bool any = MODE == 0;
+  for (uint32_t e = 0; e < (uint32_t)NE; e++) any |= srcu(e) != NEMO_NONE;
+  if (!any) return;  // workgroup-uniform
   const bool walker = wv < (uint32_t)NE && (MODE == 0 || srcu(wv) != NEMO_NONE);
   const bool worker = wv >= (uint32_t)NE;
   const uint32_t wt = tid - NE * 64u, nwt = NT - NE * 64u;
-#ifdef NEMO_STAMPS
-  // diagnostic build: per-workgroup ticks (wave 0's view), reach at 16 wg + 0..7,
-  // depth at 16 wg + 8..15: first staging, -, -, walk, wait for the workers, rows, windows, total
-  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tk0, tk1, tstart;
-#define DXT(k)          \
-  do {                  \
-    TICK(tk1);          \
-    acc[k] += tk1 - tk0; \
-    tk0 = tk1;          \
-  } while (0)
-  TICK(tk0);
-  tstart = tk0;
-#else
-#define DXT(k) \
-  do {         \
-  } while (0)
-#endif
   const uint32_t nw = m.nw[0];
-  stage(0, 0, 0, tid, NT);
+  stage(0, 0, tid, NT);
   __syncthreads();
-  DXT(0);
   if (WHOLE) {
     if (walker) walk(0, 0, wv);
-    DXT(3);
     __syncthreads();
-    finalize(0, 0, tid, NT);
-    __syncthreads();
+    finalize(0, tid, NT);
   } else {
     for (uint32_t k = 0; k < nw; k++) {
       if (walker) {
         walk(k, k & 1u, wv);
       } else if (worker) {
-        if (k > 0) finalize(k - 1, (k - 1) % 3u, wt, nwt);
-        if (k + 1 < nw) stage(k + 1, (k + 1) & 1u, (k + 1) % 3u, wt, nwt);
+        if (k > 0) finalize(k - 1, wt, nwt);
+        if (k + 1 < nw) stage(k + 1, (k + 1) & 1u, wt, nwt);
         // finalized values reach this XCD's L2 before a later staging reads them
         // back with L2-served loads (the stores' completion is all that is needed)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      DXT(3);
       __syncthreads();
-      DXT(4);
-#ifdef NEMO_STAMPS
-      acc[6]++;
-#endif
     }
-    finalize(nw - 1, (nw - 1) % 3u, tid, NT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    finalize(nw - 1, tid, NT);
   }
-#ifdef NEMO_STAMPS
-  const uint32_t stw = 16u * (MODE == 0 ? blockIdx.x * 2u + blockIdx.y : blockIdx.x) + (MODE == 0 ? 0u : 8u);
-  if (tid == 0 && c.stamps)
-    for (int k = 0; k < 5; k++) c.stamps[stw + k] = acc[k];
-  if (tid == 0 && c.stamps) c.stamps[stw + 6] = acc[6];
-#endif
-  if (MODE != 2) return;
-  // missing rows: LP rules at the maximal depth, depth + 1 == maxLen (:82-98)
-#pragma unroll
-  for (int e = 0; e < NE; e++) {
-    uint32_t m = lmax[e];
-    for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d));
-    if (lane == 0 && m) atomicMax(&s_lmax[e], m);
-  }
-  if (!WHOLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LP lists
+  if (MODE != 0) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  constexpr int MB = 8;  // entries per thread per round, loads in flight together
-  for (uint32_t e = 0; e < (uint32_t)NE; e++) {
-    const uint32_t u = srcu(e), mx = s_lmax[e];
-    if (u == NEMO_NONE || mx == 0) continue;
-    if (WHOLE) {  // the whole graph is in LDS: values in the ring, LP bits in lpb
-      const T *ring = ringp(e);
-      for (uint32_t pos = tid; pos < V; pos += NT) {
-        if (!((L.lpb[e * LW + (pos >> 5)] >> (pos & 31u)) & 1u)) continue;
-        const uint32_t r = (uint32_t)ring[pos];
-        if ((r == DX_NOTD ? 0u : (r & ~DX_IND) + 1u) != mx) continue;
-        const uint32_t k = atomicAdd(a.n_missing, 1u);
-        a.missing[2 * k] = u;
-        a.missing[2 * k + 1] = a.p.pnode[pos];
-      }
-      continue;
+  // leaf candidates of the chunk: goals in Bwd* none of whose children is (a D
+  // goal's children are all in Fwd*, so its D children are its Bwd* children)
+  uint64_t *lc = a.lw + (size_t)chunk * V;
+  for (uint32_t i = tid; i < V; i += NT) {  // i: reversed walk index, its row = the children
+    const uint32_t pos = V - 1u - i;
+    uint64_t w = 0;
+    if (!(a.p.info[pos] & DXI_RULE)) {
+      const uint64_t b = WHOLE ? (uint64_t)ringp(0)[i] : __hip_atomic_load(bwv + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t ch = 0;
+      if (b)
+        for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) {
+          const uint32_t x = a.p.fc[j];
+          ch |= WHOLE ? (uint64_t)ringp(0)[x] : __hip_atomic_load(bwv + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      w = b & ~ch;
     }
-    const uint32_t nl = s_lpn[e], *list = a.lplist + (size_t)u * V;
-    const T *gv = gvalp(e);
-    for (uint32_t m0 = 0; m0 < nl; m0 += MB * NT) {
-      uint32_t pos[MB], sv[MB];
-#pragma unroll
-      for (int q = 0; q < MB; q++) {
-        const uint32_t m = m0 + q * NT + tid;
-        pos[q] = m < nl ? __hip_atomic_load(list + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < MB; q++)
-        sv[q] = m0 + q * NT + tid < nl ? __hip_atomic_load(gv + pos[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-      for (int q = 0; q < MB; q++) {
-        if (m0 + q * NT + tid >= nl || sv[q] != mx) continue;
-        const uint32_t k = atomicAdd(a.n_missing, 1u);
-        a.missing[2 * k] = u;
-        a.missing[2 * k + 1] = a.p.pnode[pos[q]];
-      }
-    }
+    lc[pos] = w;
+    if (WHOLE) bwv[i] = ringp(0)[i];
   }
-#ifdef NEMO_STAMPS
-  DXT(5);
-  if (tid == 0 && c.stamps) {
-    c.stamps[stw + 5] = acc[5];
-    c.stamps[stw + 7] = tk0 - tstart;
-  }
-#endif
-#undef DXT
 }
 
-// ---- D and D-leaf goals: one thread per (position, chunk) ----------------------------
-// D = F & B; a D goal is a leaf when no child is in D (:82-98, leaf = D goal
-// with D-out-degree 0).  Children of position p: the reversed-order row of
-// V-1-p, as reversed positions.
-__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_leaf(DxArgs a) {
-  const uint32_t c = blockIdx.y, V = a.p.V0;
-  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
-  if (pos >= V) return;
-  const uint64_t *F = a.fw + (size_t)c * V, *B = a.bw + (size_t)c * V;
-  const uint32_t r = V - 1u - pos;
-  const uint64_t d = F[pos] & B[r];
-  a.dw[(size_t)c * V + pos] = d;
-  if (a.p.info[pos] & DXI_RULE) return;  // k_dx_lp writes the rules' word
-  uint64_t dc = 0;
-  if (d)
-    for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) {
-      const uint32_t x = a.p.fc[j];  // reversed position of a child
-      dc |= F[V - 1u - x] & B[x];
-    }
-  a.lw[(size_t)c * V + pos] = d & ~dc;
+// One launch for both walks: blocks [0, nch) walk Bwd* of their chunk, the rest
+// the longest paths of NE sources each.
+template <int NE, bool WHOLE, int NT>
+__global__ __launch_bounds__(NT) void k_dx_walks(DevCorpus c, DxArgs a, DxImg m0, DxImg m1) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  if (blockIdx.x < a.nch) dx_walk<0, 1, WHOLE, NT>(c, a, m0, m1, blockIdx.x, dyn);
+  else dx_walk<2, NE, WHOLE, NT>(c, a, m0, m1, blockIdx.x - a.nch, dyn);
 }
-// LP rules: D rules with a D-leaf goal child; the chunk's summary of sources with any
+
+// ---- LP rules and the longest LP path per source ------------------------------------
+// LP rule r of source u: r in D_u with a D_u-leaf goal child; D_u(r) = val_u(r) > 0 and
+// B_u(r).  maxLen_u = max val_u over them (:82-98; maxlen is zeroed per call).
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_lp(DxArgs a) {
   const uint32_t c = blockIdx.y, V = a.p.V0;
   const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (pos >= V) return;
   uint64_t lp = 0;
-  if (pos < V && (a.p.info[pos] & DXI_RULE)) {
-    const uint64_t d = a.dw[(size_t)c * V + pos];
-    const uint64_t *Lw = a.lw + (size_t)c * V;
+  if (a.p.info[pos] & DXI_RULE) {
     const uint32_t r = V - 1u - pos;
-    if (d)
-      for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) lp |= Lw[V - 1u - a.p.fc[j]];
-    lp &= d;
-    a.lw[(size_t)c * V + pos] = lp;
+    const uint64_t b = a.bw[(size_t)c * V + r];
+    uint64_t ol = 0;
+    if (b)
+      for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) ol |= a.lw[(size_t)c * V + (V - 1u - a.p.fc[j])];
+    uint64_t cand = b & ol;
+    const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
+    uint32_t *maxlen = a.lplist;
+    while (cand) {
+      const uint32_t e = (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1ull;
+      const uint32_t u = 64u * c + e;
+      const uint32_t v = sv[(size_t)u * V + pos];
+      if (!v) continue;
+      lp |= 1ull << e;
+      atomicMax(maxlen + u, v);
+    }
   }
-  for (int d = 32; d >= 1; d >>= 1) lp |= __shfl_xor(lp, d);
-  if (lane_id() == 0 && lp) atomicOr((unsigned long long *)&a.lpany[c], (unsigned long long)lp);
+  a.dw[(size_t)c * V + pos] = lp;
+}
+// missing rows: LP rules at the maximal depth, val == maxLen
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_emit(DxArgs a) {
+  const uint32_t c = blockIdx.y, V = a.p.V0;
+  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if (pos >= V) return;
+  uint64_t lp = a.dw[(size_t)c * V + pos];
+  const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
+  while (lp) {
+    const uint32_t e = (uint32_t)__builtin_ctzll(lp);
+    lp &= lp - 1ull;
+    const uint32_t u = 64u * c + e;
+    if (sv[(size_t)u * V + pos] != a.lplist[u]) continue;
+    const uint32_t k = atomicAdd(a.n_missing, 1u) & 0x7FFFFFFFu;
+    a.missing[2 * k] = u;
+    a.missing[2 * k + 1] = a.p.pnode[pos];
+  }
 }
 
 // ---- D masks by node for every entry ------------------------------------------------
-// thread: one node, DXM_E consecutive entries (entries of one source share its bit word)
+// D_u(v) = val_u(v) > 0 and B_u(v).  Thread: one node, DXM_E consecutive entries.
 #define DXM_E 32u
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
   const uint32_t V = a.p.V0, v = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (v >= V) return;
   const uint32_t pos = a.p.tpos[v];
   const uint32_t e0 = blockIdx.y * DXM_E, e1 = min(a.n_entries, e0 + DXM_E);
+  const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
   uint32_t lc = NEMO_NONE;
   uint64_t w = 0;
   for (uint32_t e = e0; e < e1; e++) {
     const uint32_t u = a.map[e], c = u >> 6;
     if (c != lc) {
-      w = a.dw[(size_t)c * V + pos];
+      w = a.bw[(size_t)c * V + (V - 1u - pos)];
       lc = c;
     }
-    a.mask[(size_t)e * V + v] = (uint8_t)((w >> (u & 63u)) & 1ull);
+    a.mask[(size_t)e * V + v] = (uint8_t)(((w >> (u & 63u)) & 1ull) && sv[(size_t)u * V + pos] != 0);
   }
 }
 
 // ---- launch -----------------------------------------------------------------------------
-template <int MODE, int NE, bool WHOLE, int NT>
-static void walk_launch(const DevCorpus &c, const DxArgs &a, dim3 grid, hipStream_t s) {
-  using T = typename std::conditional<MODE == 0, uint64_t, uint32_t>::type;
+template <int NE, bool WHOLE, int NT>
+static void walks_launch(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   const DxImg &m = a.img[0];
-  const uint32_t bytes = dx_lds_bytes<T, NE>(m.W, m.R, m.EC, WHOLE);
-  hipFuncSetAttribute((const void *)k_dx_walk<MODE, NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)bytes);
-  hipLaunchKernelGGL((k_dx_walk<MODE, NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, a.img[0], a.img[1]);
+  const uint32_t bytes =
+      std::max(dx_lds_bytes<uint64_t, 1>(m.W, m.R, m.EC, WHOLE), dx_lds_bytes<uint32_t, NE>(m.W, m.R, m.EC, WHOLE));
+  hipFuncSetAttribute((const void *)k_dx_walks<NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  const dim3 grid(a.nch + (a.nu + NE - 1) / NE);
+  hipLaunchKernelGGL((k_dx_walks<NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, a.img[0], a.img[1]);
 }
 
 #define DX_LDS_MAX (160u * 1024u - 1024u)
 // windowed configurations: W positions, R ring slots (power of two, >= 4 W), EC links.
-// Both walks: 1024 threads; reachability one walker (u64 ring), depth two (u32 rings),
-// so that their LDS images match and share the window configuration
+// 1024 threads: the Bwd* walk one walker (u64 ring), the longest paths two or
+// four (u32 rings; four when the whole graph's image fits LDS with them)
 #define DX_NT 1024
-#define DXD_NE 2
 struct DxCfg {
   uint32_t W, R, EC;
 };
@@ -838,13 +762,13 @@ static const DxCfg kTiny = {512, 2048, 8192};
 uint32_t dx_max_row() { return kWin.EC; }
 uint32_t dx_max_row_tiny() { return kTiny.EC; }
 
-// image 0: Kahn order (Fwd*, depth), 1: reversed (Bwd*); the whole graph in one
+// image 0: Kahn order (longest paths), 1: reversed (Bwd*); the whole graph in one
 // window when its image fits LDS (ring slots and link offsets are u16)
 void dx_img_configs(uint32_t V, uint32_t E, uint32_t window, DxImg out[2]) {
   const bool small = window == 0 && V + 64u <= 0xFFFFu && E <= 0xFFFFu;
   const uint32_t EC = std::max(E, 1u);
   const bool whole = small && dx_lds_bytes<uint64_t, 1>(V, V, EC, true) <= DX_LDS_MAX &&
-                     dx_lds_bytes<uint32_t, DXD_NE>(V, V, EC, true) <= DX_LDS_MAX;
+                     dx_lds_bytes<uint32_t, 2>(V, V, EC, true) <= DX_LDS_MAX;
   const DxCfg g = window == 2 ? kTiny : kWin;
   for (int k = 0; k < 2; k++) {
     DxImg &m = out[k];
@@ -861,16 +785,18 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   if (!V || !a.nu) return;
   const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
-  launch_zero(a.lpany, (uint64_t)a.nch * 8u, s);
+  launch_zero(a.lplist, (uint64_t)a.nu * 4u, s);  // maxLen per source
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
   hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  if (a.img[0].whole) walk_launch<0, 1, true, DX_NT>(c, a, dim3(a.nch, 2), s);
-  else walk_launch<0, 1, false, DX_NT>(c, a, dim3(a.nch, 2), s);
-  hipLaunchKernelGGL(k_dx_leaf, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  const DxImg &m = a.img[0];
+  if (m.whole) {
+    if (dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) walks_launch<4, true, DX_NT>(c, a, s);
+    else walks_launch<2, true, DX_NT>(c, a, s);
+  } else {
+    walks_launch<2, false, DX_NT>(c, a, s);
+  }
   hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  const dim3 gd((a.nu + DXD_NE - 1) / DXD_NE);
-  if (a.img[0].whole) walk_launch<2, DXD_NE, true, DX_NT>(c, a, gd, s);
-  else walk_launch<2, DXD_NE, false, DX_NT>(c, a, gd, s);
+  hipLaunchKernelGGL(k_dx_emit, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   if (a.n_entries)
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }

@@ -286,17 +286,20 @@ def test_build_heavy_indegree_redo(eng):
     _check(eng, corpus)
 
 
+@pytest.mark.parametrize("prep", [1, 0])
 @pytest.mark.parametrize("block", [256, 512])
 @pytest.mark.parametrize("kind", ["random", "synthetic", "branchy"])
-def test_chains_glob_tier(kind, block):
+def test_chains_glob_tier(kind, block, prep):
     # k_chains_glob (deep-graph tier, scratch in HBM) on every graph of small corpora, at both
-    # workgroup sizes
+    # workgroup sizes, with the H* order and adjacency built by the XCD teams of k_glob_prep
+    # (identity-rank corpora) and by k_chains_glob's own front phases
     import random as _r
     from tests.small import random_prov
     e = E.Engine(0)
     try:
         e.set_option("chains_glob_min_v", 0)
         e.set_option("chains_glob_block", block)
+        e.set_option("chains_glob_prep", prep)
         if kind == "random":
             for seed in range(12):
                 corpus, _ = random_corpus(300 + seed, max_nodes=16)
