@@ -407,7 +407,11 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
     mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
     R = args.runs_total // world
     base = rank * R
-    B = max(1, min(args.batch_runs, R))
+    # batches of near-equal size (1000 runs at --batch-runs 160: seven of 143, not six of 160 and one of 40),
+    # so that each reload reuses the previous batch's device allocations (nemo_ctx::cache takes blocks at most
+    # 1/8 larger than asked; a 40-run batch between 160-run ones cost a 3.5 s re-allocation per pass)
+    nb = -(-R // max(1, min(args.batch_runs, R)))
+    B = -(-R // nb)
     t0 = time.time()
     batches = []
     for a in range(0, R, B):
@@ -518,6 +522,9 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
         elapsed = float(t.item())
     runs = sum(int((c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)).sum()) for c in batches)
     total = runs * world
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg.get("cpu_runs"):
+        cpu = cpu_baseline(args, cfg, gen, None, None, None, None, mode)  # its bounded sample of the same shape
     Vn = sum(int(c.node_off[-1]) for c in batches)
     E_ = sum(int(c.edge_off[-1]) for c in batches)
     out = {"metric": METRIC, "value": round(total * args.steps / elapsed, 2), "unit": "runs/s", "n_gpus": world,
@@ -533,7 +540,7 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
                       "failed_runs_rank0": len(fail_all), "diff_mode": args.diff_mode,
                       "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped)",
                       "lib_options": args.set},
-           "roofline": None, "cpu_baseline": None, "gen_seconds_rank0": round(gen_s, 2),
+           "roofline": None, "cpu_baseline": cpu, "gen_seconds_rank0": round(gen_s, 2),
            "pass_phases_rank0": dict(phase),
            "note": "no per-kernel roofline on this line: the resident-batch line (--config c5) carries it"}
     if rank == 0:

@@ -111,8 +111,8 @@ struct nemo_ctx {
   uint32_t diff_window = 0;          // option diff_window (test knob): 0 by size, 1 windowed, 2 tiny windows
   uint32_t g0_maxdeg = 0;
   uint32_t dx_nu_cap = 0, dx_nch_cap = 0;
-  uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr, *d_dxlpl = nullptr;
-  uint64_t *d_dxw = nullptr, *d_dxlp = nullptr;  // [5][nch][V0] Good, F, B, D, L|LP; [nch] LP summary
+  uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr, *d_dxlpl = nullptr, *d_dxfb = nullptr;
+  uint64_t *d_dxw = nullptr;  // [4][nch][V0] Good / LP, B, D, leaf candidates
   bool dx_last = false;              // the last diffprov ran the multi-entry kernels
 
   // pulls: per-slot (offset, count) and the region cursor come back to pinned
@@ -446,8 +446,8 @@ static void release_corpus(nemo_ctx *c) {
   c->dx_img_key = -1;
   c->dx_ok = false;
   c->dx_nu_cap = c->dx_nch_cap = 0;
-  c->d_dxpb = c->d_dxsval = c->d_dxlpl = nullptr;
-  c->d_dxw = c->d_dxlp = nullptr;
+  c->d_dxpb = c->d_dxsval = c->d_dxlpl = c->d_dxfb = nullptr;
+  c->d_dxw = nullptr;
   c->n_uniq = 0;
   c->dmap.clear();
   c->aux_pending = false;
@@ -1429,16 +1429,16 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   }
   const uint32_t nch = (nu + 63) / 64, w32 = (uint32_t)((V0 + 31) / 32);
   if (dx && (nu > c->dx_nu_cap || nch > c->dx_nch_cap)) {
-    for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxlpl, (void *)c->d_dxw, (void *)c->d_dxlp})
+    for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxlpl, (void *)c->d_dxw, (void *)c->d_dxfb})
       dfree(c, q);
-    c->d_dxpb = c->d_dxsval = c->d_dxlpl = nullptr;
-    c->d_dxw = c->d_dxlp = nullptr;
+    c->d_dxpb = c->d_dxsval = c->d_dxlpl = c->d_dxfb = nullptr;
+    c->d_dxw = nullptr;
     c->dx_nu_cap = c->dx_nch_cap = 0;
     if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
-    if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dxw, 5 * (size_t)nch * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dxlp, (size_t)nch))) return rc;
+    if ((rc = dalloc(c, &c->d_dxsval, ((size_t)nu * V0 + 1) / 2))) return rc;  // u16
+    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu))) return rc;
+    if ((rc = dalloc(c, &c->d_dxw, 4 * (size_t)nch * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dxfb, 8 * (size_t)nch * V0))) return rc;  // 32 bytes per position and chunk
     c->dx_nu_cap = nu;
     c->dx_nch_cap = nch;
   }
@@ -1479,17 +1479,16 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     uint64_t maxsrc = d_labels ? labels_cap : 0;
     for (uint32_t u = 0; u < nu && !d_labels; u++)
       maxsrc = std::max<uint64_t>(maxsrc, c->node_off[src[u] + 1] - c->node_off[src[u]]);
-    a.lab_per = 4096;
+    a.lab_per = 8192;  // one workgroup per source up to 8192 nodes: its bitmap stored whole, no atomics
     a.lab_split = (uint32_t)std::max<uint64_t>(1, (maxsrc + a.lab_per - 1) / a.lab_per);
     const size_t plane = (size_t)nch * V0;
     a.gw = c->d_dxw;
-    a.fw = a.gw + plane;
-    a.bw = a.fw + plane;
+    a.bw = a.gw + plane;
     a.dw = a.bw + plane;
     a.lw = a.dw + plane;
-    a.lpany = c->d_dxlp;
-    a.sval = c->d_dxsval;
-    a.lplist = c->d_dxlpl;
+    a.fb = reinterpret_cast<uint8_t *>(c->d_dxfb);
+    a.sval = reinterpret_cast<uint16_t *>(c->d_dxsval);
+    a.maxlen = c->d_dxlpl;
     a.mask = c->d_dmask;
     a.map = c->d_dmap;
     a.n_entries = (uint32_t)n_failed;

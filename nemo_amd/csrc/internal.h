@@ -94,14 +94,13 @@ struct DxArgs {
   uint32_t w32;              // ceil(V0 / 32)
   uint32_t lab_per;          // source nodes per k_dx_label workgroup
   uint32_t lab_split;        // workgroups per source (1: LDS bitmap stored whole)
-  uint64_t *gw;              // [nch][V0] Good bits by position
-  uint64_t *fw;              // [nch][V0] Fwd*(Good) by position
+  uint64_t *gw;              // [nch][V0] Good bits by position; after the walks: LP rules (k_dx_lp)
   uint64_t *bw;              // [nch][V0] Bwd*(Good) by REVERSED position (V0 - 1 - pos)
-  uint64_t *dw;              // [nch][V0] D = F & B by position
-  uint64_t *lw;              // [nch][V0] D-leaf goals | LP rules (rules with a D-leaf child) by position
-  uint64_t *lpany;           // [nch] sources with at least one LP rule
-  uint32_t *sval;            // [nu][V0] depth + 1 of D nodes (0 elsewhere) by position
-  uint32_t *lplist;          // [nu][V0] the LP rules' positions of each source (windowed depth walks)
+  uint64_t *dw;              // [nch][V0] D = Fwd* & Bwd* by position (k_dx_lp)
+  uint64_t *lw;              // [nch][V0] leaf candidates: Bwd* goals without a Bwd* child, by position
+  uint8_t *fb;               // [nch][64 / NE][V0] Fwd* bits of the NE sources of longest-path workgroup g
+  uint16_t *sval;            // [nu][V0] val = 1 + the longest path from Good (0 off Fwd*) by position
+  uint32_t *maxlen;          // [nu] the longest LP val of each source (zeroed per call)
   uint8_t *mask;             // [n_entries][V0] D masks by node (output)
   const uint32_t *map;       // [n_entries] entry -> source
   uint32_t n_entries;

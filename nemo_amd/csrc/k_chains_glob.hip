@@ -531,9 +531,16 @@ __device__ __forceinline__ void glob_sweep(GlobScratch &S, const uint32_t n, con
 // per-graph phases of k_chains_glob).
 #define PT_TEAMS 8   // teams (blockIdx % 8)
 #define PT_M 32      // workgroups per team
-#define PT_B 1024    // threads per workgroup
-#define PT_CP 8      // Kahn positions per thread and round of the compaction
+#ifndef PT_B
+#define PT_B 512     // threads per workgroup (1024 spilled registers)
+#endif
+#define PT_CP 4      // Kahn positions per thread and round of the compaction
 #define PT_WORDS 256 // team scratch words: barrier counter + 2 x 3 x PT_M phase sums
+#define PT_GN 2      // H* nodes per thread and round of the adjacency
+#ifndef PT_F
+#define PT_F 4       // ... and row entries per node and load round
+#endif
+#define PT_RB 512    // LDS entries per wave and node slot for assembling adjacency ranges
 
 // team barrier: every wave's stores drained, one lane releases and arrives,
 // polls the team's counter (relaxed, L1-bypassing loads) and acquires
@@ -560,6 +567,7 @@ __device__ __forceinline__ uint32_t pt_no(const uint2 *hb, uint32_t y) {
 __global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
   __shared__ uint32_t s_lds[PT_B / 64];
   __shared__ uint32_t s_base[3];
+  __shared__ uint32_t s_rbuf[PT_B / 64][PT_GN * PT_RB];
   const uint32_t team = blockIdx.x % PT_TEAMS, r = blockIdx.x / PT_TEAMS, tid = threadIdx.x;
   const uint32_t M = gridDim.x / PT_TEAMS;  // members per team (<= PT_M)
   uint32_t *ts = c.team + (size_t)team * PT_WORDS, *ctr = ts;
@@ -572,6 +580,9 @@ __global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
     GlobScratch S = glob_carve(c.gscratch + c.gs_off[g], V, E);
     uint2 *hb = reinterpret_cast<uint2 *>(S.bm);  // per 32 nodes: H* bits, H* nodes before the word
     uint32_t *nolo = S.S;                         // compact node index -> H* (Kahn order) index
+    uint32_t *rb = S.ta;                          // rule bits in node order
+    // P2 -> P3: each H* node's CSR row bounds, in H* order (the sweeps' buffers, free until then)
+    uint32_t *cst = reinterpret_cast<uint32_t *>(S.up), *pst = reinterpret_cast<uint32_t *>(S.down);
     uint32_t *hs = c.s_a + gv.n0 + g;
     uint32_t *cnt = ts + 1 + (it & 1) * 3 * PT_M;  // this graph's phase sums (graph parity: the next
                                                  // graph's writes never meet this graph's late reads)
@@ -595,6 +606,22 @@ __global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
         }
         hb[w].x = bits;
         sum += __popc(bits);
+        // rule bits of the same 32 nodes (node words streamed here, not gathered in Kahn order in P2)
+        uint32_t rbits = 0;
+        if (v0 + 31 < V) {
+#pragma unroll
+          for (int q4 = 0; q4 < 8; q4++) {
+            uint4 w4;
+            __builtin_memcpy(&w4, gv.word + v0 + 4 * q4, 16);
+            rbits |= (is_rule(w4.x) ? 1u : 0u) << (4 * q4);
+            rbits |= (is_rule(w4.y) ? 1u : 0u) << (4 * q4 + 1);
+            rbits |= (is_rule(w4.z) ? 1u : 0u) << (4 * q4 + 2);
+            rbits |= (is_rule(w4.w) ? 1u : 0u) << (4 * q4 + 3);
+          }
+        } else {
+          for (uint32_t v = v0; v < V; v++) rbits |= (is_rule(gv.word[v]) ? 1u : 0u) << (v - v0);
+        }
+        rb[w] = rbits;
       }
       uint32_t tot;
       block_exscan<PT_B>(sum, &tot, s_lds);
@@ -651,46 +678,67 @@ __global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
       }
       __syncthreads();
       const uint32_t pa = (uint32_t)((uint64_t)V * r / M), pb = (uint32_t)((uint64_t)V * (r + 1) / M);
+      const uint32_t wv = tid >> 6, lane = lane_id();
       uint32_t i = s_base[0], oc = 0, op = 0;
+      // wave wv takes 64 * PT_CP consecutive positions, lane-interleaved (position
+      // c0 + 64 q + lane), so each store instruction below writes consecutive H*
+      // indices: whole lines, not one dword per line and lane
       for (uint32_t b0 = pa; b0 < pb; b0 += PT_B * PT_CP) {
-        const uint32_t p0 = b0 + tid * PT_CP;
-        uint32_t x[PT_CP], hx[PT_CP], cl = 0;
+        const uint32_t c0 = b0 + wv * 64u * PT_CP;
+        uint32_t x[PT_CP], hx[PT_CP];
 #pragma unroll
-        for (int q = 0; q < PT_CP; q++) x[q] = p0 + q < pb ? gv.topo[p0 + q] : 0u;
+        for (int q = 0; q < PT_CP; q++) {
+          const uint32_t p = c0 + 64u * q + lane;
+          x[q] = p < pb ? gv.topo[p] : 0u;
+        }
 #pragma unroll
         for (int q = 0; q < PT_CP; q++) {
           const uint2 w = hb[x[q] >> 5];
-          const bool h = p0 + q < pb && ((w.x >> (x[q] & 31)) & 1u);
+          const bool h = c0 + 64u * q + lane < pb && ((w.x >> (x[q] & 31)) & 1u);
           hx[q] = h ? w.y + __popc(w.x & ((1u << (x[q] & 31)) - 1u)) : GNIL;
-          cl += h ? 1u : 0u;
         }
-        uint32_t wd[PT_CP], dc[PT_CP], dp[PT_CP], sc = 0, sp = 0;
+        uint32_t rl[PT_CP], fa[PT_CP], fb[PT_CP], ra[PT_CP], rb2[PT_CP];
 #pragma unroll
         for (int q = 0; q < PT_CP; q++) {
           const bool h = hx[q] != GNIL;
-          wd[q] = h ? gv.word[x[q]] : 0u;
-          dc[q] = h ? gv.fp[x[q] + 1] - gv.fp[x[q]] : 0u;
-          dp[q] = h ? gv.rp[x[q] + 1] - gv.rp[x[q]] : 0u;
-          sc += dc[q];
-          sp += dp[q];
+          rl[q] = h ? (rb[x[q] >> 5] >> (x[q] & 31)) & 1u : 0u;
+          fa[q] = h ? gv.fp[x[q]] : 0u;
+          fb[q] = h ? gv.fp[x[q] + 1] : 0u;
+          ra[q] = h ? gv.rp[x[q]] : 0u;
+          rb2[q] = h ? gv.rp[x[q] + 1] : 0u;
         }
-        uint32_t tot, tc, tp;
-        uint32_t j = i + block_exscan<PT_B>(cl, &tot, s_lds);
-        uint32_t ec = oc + block_exscan<PT_B>(sc, &tc, s_lds), ep = op + block_exscan<PT_B>(sp, &tp, s_lds);
+        // offsets within the wave in (q, lane) order, then the waves' bases
+        uint32_t jq[PT_CP], cq[PT_CP], pq[PT_CP], wn = 0, wc = 0, wp = 0;
+#pragma unroll
+        for (int q = 0; q < PT_CP; q++) {
+          uint32_t t;
+          jq[q] = wn + wave_exscan(hx[q] != GNIL ? 1u : 0u, &t);
+          wn += t;
+          cq[q] = wc + wave_exscan(fb[q] - fa[q], &t);
+          wc += t;
+          pq[q] = wp + wave_exscan(rb2[q] - ra[q], &t);
+          wp += t;
+        }
+        uint32_t tn, tc, tp;
+        const uint32_t bn = __builtin_amdgcn_readfirstlane(block_exscan<PT_B>(lane == 0 ? wn : 0u, &tn, s_lds));
+        const uint32_t bc = __builtin_amdgcn_readfirstlane(block_exscan<PT_B>(lane == 0 ? wc : 0u, &tc, s_lds));
+        const uint32_t bp = __builtin_amdgcn_readfirstlane(block_exscan<PT_B>(lane == 0 ? wp : 0u, &tp, s_lds));
 #pragma unroll
         for (int q = 0; q < PT_CP; q++) {
           if (hx[q] == GNIL) continue;
+          const uint32_t j = i + bn + jq[q];
           hs[j] = x[q];
-          S.rule[j] = is_rule(wd[q]) ? 1u : 0u;
+          S.rule[j] = rl[q];
           S.crank[j] = hx[q];
           nolo[hx[q]] = j;
-          S.ccoff[j] = ec;  // within the slice; P3 adds the slices before it
-          S.pcoff[j] = ep;
-          ec += dc[q];
-          ep += dp[q];
-          j++;
+          S.ccoff[j] = oc + bc + cq[q];  // within the slice; P3 adds the slices before it
+          S.pcoff[j] = op + bp + pq[q];
+          cst[j] = fa[q];
+          S.cend[j] = fb[q];
+          pst[j] = ra[q];
+          S.pend[j] = rb2[q];
         }
-        i += tot;
+        i += tn;
         oc += tc;
         op += tp;
       }
@@ -724,62 +772,83 @@ __global__ __launch_bounds__(PT_B) void k_glob_prep(DevCorpus c) {
         S.ccoff[hi] = cb + cnt[2 * PT_M + r];
         S.pcoff[hi] = pb + cnt[r];
       }
-      auto rows = [&](const uint32_t *ptr, const uint32_t *col, uint32_t *off, uint32_t *endp, uint32_t *out,
+      // rows of 64 consecutive H* nodes (a wave, one node per lane) fill one range
+      // of the adjacency (full-degree layout): assembled in LDS and stored whole
+      // (one dword per lane into a different line per row was a partial-line
+      // write each); a range past PT_RB entries is stored directly
+      uint32_t *rbuf = s_rbuf[tid >> 6];
+      const uint32_t lane = lane_id();
+      auto rows = [&](const uint32_t *st, const uint32_t *col, uint32_t *off, uint32_t *endp, uint32_t *out,
                       uint32_t ob) {
-        for (uint32_t i0 = lo + tid; i0 < hi; i0 += PT_B * GA_N) {
-          uint32_t x[GA_N], a[GA_N], e[GA_N], o[GA_N], k[GA_N];
+        for (uint32_t i0 = lo + tid; __any(i0 < hi); i0 += PT_B * PT_GN) {
+          uint32_t a[PT_GN], e[PT_GN], o[PT_GN], k[PT_GN], rs[PT_GN], rl[PT_GN];
 #pragma unroll
-          for (int q = 0; q < GA_N; q++) {
+          for (int q = 0; q < PT_GN; q++) {
             const uint32_t i = i0 + q * PT_B;
-            x[q] = i < hi ? hs[i] : 0u;
+            a[q] = i < hi ? st[i] : 0u;
+            e[q] = i < hi ? endp[i] : 0u;  // the row's CSR end (P2), replaced by its H* end below
             o[q] = i < hi ? off[i] + ob : 0u;
             k[q] = 0;
           }
 #pragma unroll
-          for (int q = 0; q < GA_N; q++) {
-            a[q] = ptr[x[q]];
-            e[q] = i0 + q * PT_B < hi ? ptr[x[q] + 1] : a[q];
+          for (int q = 0; q < PT_GN; q++) {  // the wave's range: [first active lane's row, last one's end)
+            uint32_t ee = i0 + q * PT_B < hi ? o[q] + (e[q] - a[q]) : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) ee = max(ee, (uint32_t)__shfl_xor((int)ee, d));
+            rs[q] = __builtin_amdgcn_readfirstlane(o[q]);
+            rl[q] = ee > rs[q] ? ee - rs[q] : 0u;
+            if (rl[q] <= PT_RB)
+              for (uint32_t t = lane; t < rl[q]; t += 64) rbuf[q * PT_RB + t] = GNIL;
           }
-          for (uint32_t t = 0;; t += GA_F) {
+          wsync();
+          for (uint32_t t = 0;; t += PT_F) {
             bool more = false;
-            uint32_t y[GA_N][GA_F];
+            uint32_t y[PT_GN][PT_F];
 #pragma unroll
-            for (int q = 0; q < GA_N; q++)
+            for (int q = 0; q < PT_GN; q++)
 #pragma unroll
-              for (int h = 0; h < GA_F; h++) y[q][h] = a[q] + t + h < e[q] ? col[a[q] + t + h] : GNIL;
-            uint2 w[GA_N][GA_F];
+              for (int h = 0; h < PT_F; h++) y[q][h] = a[q] + t + h < e[q] ? col[a[q] + t + h] : GNIL;
+            uint2 w[PT_GN][PT_F];
 #pragma unroll
-            for (int q = 0; q < GA_N; q++)
+            for (int q = 0; q < PT_GN; q++)
 #pragma unroll
-              for (int h = 0; h < GA_F; h++) w[q][h] = y[q][h] != GNIL ? hb[y[q][h] >> 5] : make_uint2(0, 0);
-            uint32_t m[GA_N][GA_F];
+              for (int h = 0; h < PT_F; h++) w[q][h] = y[q][h] != GNIL ? hb[y[q][h] >> 5] : make_uint2(0, 0);
+            uint32_t m[PT_GN][PT_F];
 #pragma unroll
-            for (int q = 0; q < GA_N; q++)
+            for (int q = 0; q < PT_GN; q++)
 #pragma unroll
-              for (int h = 0; h < GA_F; h++) {
+              for (int h = 0; h < PT_F; h++) {
                 const uint32_t yy = y[q][h] & 31u;
                 m[q][h] = (w[q][h].x >> yy) & 1u ? nolo[w[q][h].y + __popc(w[q][h].x & ((1u << yy) - 1u))] : GNIL;
               }
 #pragma unroll
-            for (int q = 0; q < GA_N; q++) {
+            for (int q = 0; q < PT_GN; q++) {
 #pragma unroll
-              for (int h = 0; h < GA_F; h++)
-                if (m[q][h] != GNIL) out[o[q] + k[q]++] = m[q][h];
-              more |= a[q] + t + GA_F < e[q];
+              for (int h = 0; h < PT_F; h++)
+                if (m[q][h] != GNIL) {
+                  if (rl[q] <= PT_RB) rbuf[q * PT_RB + o[q] + k[q] - rs[q]] = m[q][h];
+                  else out[o[q] + k[q]] = m[q][h];
+                  k[q]++;
+                }
+              more |= a[q] + t + PT_F < e[q];
             }
             if (!__any(more)) break;
           }
+          wsync();
 #pragma unroll
-          for (int q = 0; q < GA_N; q++) {
+          for (int q = 0; q < PT_GN; q++) {
+            if (rl[q] <= PT_RB)
+              for (uint32_t t = lane; t < rl[q]; t += 64) out[rs[q] + t] = rbuf[q * PT_RB + t];
             const uint32_t i = i0 + q * PT_B;
             if (i >= hi) continue;
             off[i] = o[q];
             endp[i] = o[q] + k[q];
           }
+          wsync();
         }
       };
-      rows(gv.fp, gv.fc, S.ccoff, S.cend, S.child, cb);
-      rows(gv.rp, gv.rc, S.pcoff, S.pend, S.par, pb);
+      rows(cst, gv.fc, S.ccoff, S.cend, S.child, cb);
+      rows(pst, gv.rc, S.pcoff, S.pend, S.par, pb);
     }
   }
 }
@@ -1176,6 +1245,75 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       __syncthreads();
       continue;
     }
+    if (mp + 1 + 2 * (b - a) <= LW) {
+      // the level's group counters, its members' cranks and their po(bp) in LDS
+      // (the sweeps' memory): device-scope atomics run at the memory side, and a
+      // level's histogram and cursors were ~2 per node of them
+      uint32_t *lcnt = lw, *lgrp = lw + mp + 1, *lbpo = lgrp + (b - a);
+      for (uint32_t w = tid; w <= mp; w += GB) lcnt[w] = 0;
+      __syncthreads();
+      for (uint32_t j0 = a + tid; j0 < b; j0 += GB * GU) {
+        uint32_t i[GU], bpi[GU], bpo[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < b ? S.ub[j0 + q * GB] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) bpi[q] = j0 + q * GB < b ? S.bp[i[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          if (j0 + q * GB >= b || bpi[q] != MULTI) continue;
+          uint32_t best = GNIL, bo = GNIL;
+          for (uint32_t qq = S.pcoff[i[q]]; qq < S.pend[i[q]]; qq++) {
+            const uint32_t p = S.par[qq];
+            if ((uint32_t)S.up[p] == k - 1 && S.po[p] < bo) {
+              best = p;
+              bo = S.po[p];
+            }
+          }
+          bpi[q] = best;
+          S.bp[i[q]] = best;
+        }
+#pragma unroll
+        for (int q = 0; q < GU; q++) bpo[q] = j0 + q * GB < b ? S.po[bpi[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          if (j0 + q * GB >= b) continue;
+          lbpo[j0 + q * GB - a] = bpo[q];
+          atomicAdd(&lcnt[bpo[q]], 1u);
+        }
+      }
+      __syncthreads();
+      block_scan_inplace<GB>(lcnt, mp + 1, s_lds);  // group bases
+      for (uint32_t j0 = a + tid; j0 < b; j0 += GB * GU) {
+        uint32_t i[GU], cr[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < b ? S.ub[j0 + q * GB] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) cr[q] = j0 + q * GB < b ? S.crank[i[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++)
+          if (j0 + q * GB < b) lgrp[atomicAdd(&lcnt[lbpo[j0 + q * GB - a]], 1u)] = cr[q];
+      }
+      __syncthreads();  // lcnt[q] = end of group q = base of group q + 1
+      for (uint32_t j0 = a + tid; j0 < b; j0 += GB * GU) {
+        uint32_t i[GU], cr[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < b ? S.ub[j0 + q * GB] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) cr[q] = j0 + q * GB < b ? S.crank[i[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          if (j0 + q * GB >= b) continue;
+          const uint32_t bo = lbpo[j0 + q * GB - a];
+          const uint32_t base = bo ? lcnt[bo - 1] : 0u, end = lcnt[bo];
+          uint32_t r = 0;
+          for (uint32_t qq = base; qq < end; qq++) r += lgrp[qq] < cr[q];
+          S.po[i[q]] = base + r;
+          S.fpos[i[q]] = base;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     for (uint32_t w = tid; w <= mp; w += GB) S.cnt[w] = 0;
     __syncthreads();
     for (uint32_t j = a + tid; j < b; j += GB) {
@@ -1223,12 +1361,48 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
   uint32_t *va = S.va, *hd = S.hb, *tl = S.ta;
   for (uint32_t i = tid; i < n; i += GB) S.S[i] = 1;
   __syncthreads();
+  // subtree sizes bottom-up: a level's sizes summed into its parents' slots in
+  // LDS (indexed by the parent's po, dense in [0, size of the level above)),
+  // then the parents' sizes stored; levels above past the LDS take device atomics
   for (uint32_t k = maxup; k >= 1; k--) {
-    for (uint32_t j = S.uoff[k] + tid; j < S.uoff[k + 1]; j += GB) {
-      const uint32_t i = S.ub[j];
-      atomicAdd(&S.S[S.bp[i]], S.S[i]);
+    const uint32_t a = S.uoff[k], b = S.uoff[k + 1], pa = S.uoff[k - 1], mp = a - pa;
+    if (mp <= LW) {
+      for (uint32_t w = tid; w < mp; w += GB) lw[w] = 0;
+      __syncthreads();
+      for (uint32_t j0 = a + tid; j0 < b; j0 += GB * GU) {
+        uint32_t i[GU], p[GU], sz[GU], po[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < b ? S.ub[j0 + q * GB] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) {
+          p[q] = j0 + q * GB < b ? S.bp[i[q]] : 0u;
+          sz[q] = j0 + q * GB < b ? S.S[i[q]] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < GU; q++) po[q] = j0 + q * GB < b ? S.po[p[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++)
+          if (j0 + q * GB < b) atomicAdd(&lw[po[q]], sz[q]);
+      }
+      __syncthreads();
+      for (uint32_t j0 = pa + tid; j0 < a; j0 += GB * GU) {
+        uint32_t i[GU], po[GU];
+#pragma unroll
+        for (int q = 0; q < GU; q++) i[q] = j0 + q * GB < a ? S.ub[j0 + q * GB] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++) po[q] = j0 + q * GB < a ? S.po[i[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < GU; q++)
+          if (j0 + q * GB < a) S.S[i[q]] = 1u + lw[po[q]];
+      }
+      __syncthreads();
+    } else {
+      for (uint32_t j = a + tid; j < b; j += GB) {
+        const uint32_t i = S.ub[j];
+        atomicAdd(&S.S[S.bp[i]], S.S[i]);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
     uint32_t k[GU], po[GU], sz[GU], base[GU];

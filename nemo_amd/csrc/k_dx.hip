@@ -7,17 +7,19 @@
 //   D_u    = Fwd*(Good_u) ∩ Bwd*(Good_u)                (:22-32, APOC export)
 //   missing_u = D_u rules with a D_u-leaf goal child at maximal depth (:82-98)
 // Reachability is the same sweep for every source, so one bit per source in a
-// u64 word carries 64 sources through one Kahn-order walk (a "chunk").  Depth
-// (the longest path from a D root) is per source; it runs four sources per
-// workgroup, one walking wave each, over the same staged graph windows.
+// u64 word carries 64 sources through one reversed-Kahn-order walk (a
+// "chunk").  The depth of a D rule is 1 + the longest path from a Good goal
+// (k_dx_walk, MODE 2): per source, two or four sources per workgroup, one
+// walking wave each, over the same staged graph windows; it needs neither D
+// nor a Fwd* walk (its non-zero values are Fwd*), so it runs beside Bwd*.
 //
 // Kernels per call (launch_dx):
 //   k_dx_label   present bitmaps: g0 positions whose label a source holds
 //   k_dx_good    Good words per chunk (64 bitmaps transposed by ballots)
-//   k_dx_walk<0> Fwd* and Bwd* (grid chunks x 2: forward / reversed walk)
-//   k_dx_leaf    D = F & B, D-leaf goals
-//   k_dx_lp      LP rules (D rules with a D-leaf child), chunks' LP summary
-//   k_dx_walk<2> depth per source, the maximal LP depth, missing rows
+//   k_dx_walks   Bwd* per chunk (+ leaf candidates) and the longest paths per
+//                source, one launch
+//   k_dx_lp      D = Fwd* & Bwd*, LP rules, the longest LP path per source
+//   k_dx_emit    missing rows (LP rules at that length)
 //   k_dx_mask    D masks by node for every entry (entries -> sources)
 // g0's Kahn-order relayout (k_dxp_*) is built with the CSR in every load /
 // rebuild (launch_dx_prep), since it depends on the graph alone.
@@ -276,7 +278,7 @@ void launch_dx_img(const DxPrep &p, DxImg img[2], const DxImgScratch &t, hipStre
 // are gathered in LDS and stored whole (one workgroup per source) or ORed in
 // by word; larger ones take global atomics.
 #define DXL_LDS 4096u
-#define DXL_BATCH 8
+#define DXL_BATCH 24  // source nodes per thread and round (all their loads in flight together)
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) {
   __shared__ uint32_t bm[DXL_LDS];
   const uint32_t u = blockIdx.y, tid = threadIdx.x;
@@ -304,13 +306,33 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     else atomicOr(&pb[p >> 5], 1u << (p & 31u));
   };
   if (a.r0dense) {  // labels and node words together, one dense-table load per source goal
+    // (four consecutive nodes per thread and 16-byte load when the slice allows)
+    const bool vec = ((((uintptr_t)(lab + lo)) | (word ? (uintptr_t)(word + lo) : 0u)) & 15u) == 0u;
     for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
       uint32_t lb[DXL_BATCH], wd[DXL_BATCH], dv[DXL_BATCH];
+      if (vec) {
 #pragma unroll
-      for (int q = 0; q < DXL_BATCH; q++) {
-        const uint32_t x = base + q * NEMO_BLOCK + tid;
-        lb[q] = x < hi ? lab[x] : NEMO_NONE;
-        wd[q] = x < hi && word ? word[x] : 0u;
+        for (int g4 = 0; g4 < DXL_BATCH / 4; g4++) {
+          const uint32_t x = base + 4 * (g4 * NEMO_BLOCK + tid);
+          uint4 l4 = make_uint4(NEMO_NONE, NEMO_NONE, NEMO_NONE, NEMO_NONE), w4 = make_uint4(0, 0, 0, 0);
+          if (x + 3 < hi) {
+            l4 = *reinterpret_cast<const uint4 *>(lab + x);
+            if (word) w4 = *reinterpret_cast<const uint4 *>(word + x);
+          } else {
+            if (x < hi) l4.x = lab[x], w4.x = word ? word[x] : 0u;
+            if (x + 1 < hi) l4.y = lab[x + 1], w4.y = word ? word[x + 1] : 0u;
+            if (x + 2 < hi) l4.z = lab[x + 2], w4.z = word ? word[x + 2] : 0u;
+          }
+          lb[4 * g4] = l4.x, lb[4 * g4 + 1] = l4.y, lb[4 * g4 + 2] = l4.z, lb[4 * g4 + 3] = l4.w;
+          wd[4 * g4] = w4.x, wd[4 * g4 + 1] = w4.y, wd[4 * g4 + 2] = w4.z, wd[4 * g4 + 3] = w4.w;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < DXL_BATCH; q++) {
+          const uint32_t x = base + q * NEMO_BLOCK + tid;
+          lb[q] = x < hi ? lab[x] : NEMO_NONE;
+          wd[q] = x < hi && word ? word[x] : 0u;
+        }
       }
 #pragma unroll
       for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab && !is_rule(wd[q]) ? a.r0dense[lb[q]] : NEMO_NONE;
@@ -460,6 +482,7 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t R, uint32_
   return L;
 }
 #define DX_VMAX 0xFFFEu  // longest val kept (u16 per source and position); past it the call fails
+#define DXP_B 256        // k_dx_lp: threads per workgroup
 
 template <int MODE, int NE, bool WHOLE, int NT>
 __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1,
@@ -469,21 +492,25 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   constexpr bool rev = MODE == 0;
   const DxImg &m = rev ? m1 : m0;
   const uint32_t V = a.p.V0, R = m.R, EC = m.EC;
-  const uint32_t chunk = MODE == 0 ? bx : (bx * NE) >> 6;
+  // MODE 2: workgroup bx takes sources 64 chunk + NE g + e (e < NE, NE g + e < 64) of its chunk
+  constexpr uint32_t GPC = (64u + NE - 1u) / NE;  // workgroups per chunk
+  const uint32_t chunk = MODE == 0 ? bx : bx / GPC, grp = MODE == 0 ? 0u : bx % GPC;
   DxLds<T, NE> L = dx_carve<T, NE>(dyn, R, EC, WHOLE);
   const uint32_t *rowp = rev ? a.p.fp : a.p.rp;
   // per walker e: its source (MODE 2), ring and value array, computed from e (a
   // dynamically indexed register array would live in scratch memory)
   auto srcu = [&](uint32_t e) -> uint32_t {  // NEMO_NONE: no source
     if (MODE == 0) return 0u;
-    const uint32_t u = bx * NE + e;
-    return u < a.nu ? u : NEMO_NONE;
+    const uint32_t b = grp * NE + e, u = 64u * chunk + b;
+    return b < 64u && u < a.nu ? u : NEMO_NONE;
   };
   auto ringp = [&](uint32_t e) -> T * { return L.ring0 + (size_t)e * L.rs; };
   uint64_t *const bwv = a.bw + (size_t)chunk * V;
   auto sval = [&](uint32_t e) -> uint16_t * {
-    return reinterpret_cast<uint16_t *>(a.sval) + (size_t)min(bx * NE + e, a.nu - 1u) * V;
+    return a.sval + (size_t)min(64u * chunk + min(grp * NE + e, 63u), a.nu - 1u) * V;
   };
+  // this workgroup's Fwd* byte plane (bit e: source 64 chunk + NE grp + e), MODE 2
+  uint8_t *const fbp = a.fb + ((size_t)chunk * GPC + grp) * V;
   auto slot = [&](uint32_t i) -> uint32_t { return WHOLE ? i : (i & (R - 1u)); };
   if (tid < (uint32_t)NE) ringp(tid)[R] = (T)0;  // the sink reads as "no value": OR 0, max 0
   // ---- staging of window kw by threads [wt0, wt0 + nwt) (whole waves) ----
@@ -528,7 +555,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
       } else {
         uint32_t r[NE];
 #pragma unroll
-        for (int e = 0; e < NE; e++) r[e] = (uint32_t)((gd >> ((bx * NE + e) & 63u)) & 1ull);
+        for (int e = 0; e < NE; e++) r[e] = grp * NE + e < 64u ? (uint32_t)((gd >> (grp * NE + e)) & 1ull) : 0u;
         for (uint32_t mm = mo0; mm < mo1; mm++) {
           const uint32_t x = m.mx[mm];
 #pragma unroll
@@ -553,13 +580,16 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
       if (MODE == 0) {
         if (!WHOLE) bwv[i] = ringp(0)[sl];
       } else {
+        uint32_t fbits = 0;
 #pragma unroll
         for (int e = 0; e < NE; e++) {
           if (srcu(e) == NEMO_NONE) continue;
           const uint32_t v = (uint32_t)ringp(e)[sl];
           over |= v > DX_VMAX;
           sval(e)[i] = (uint16_t)min(v, (uint32_t)DX_VMAX);
+          fbits |= (v ? 1u : 0u) << e;
         }
+        fbp[i] = (uint8_t)fbits;
       }
     }
     if (MODE == 2 && __any(over) && lane == 0) atomicOr(a.n_missing, 0x80000000u);
@@ -667,71 +697,108 @@ __global__ __launch_bounds__(NT) void k_dx_walks(DevCorpus c, DxArgs a, DxImg m0
   else dx_walk<2, NE, WHOLE, NT>(c, a, m0, m1, blockIdx.x - a.nch, dyn);
 }
 
-// ---- LP rules and the longest LP path per source ------------------------------------
-// LP rule r of source u: r in D_u with a D_u-leaf goal child; D_u(r) = val_u(r) > 0 and
-// B_u(r).  maxLen_u = max val_u over them (:82-98; maxlen is zeroed per call).
-__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_lp(DxArgs a) {
-  const uint32_t c = blockIdx.y, V = a.p.V0;
-  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
-  if (pos >= V) return;
-  uint64_t lp = 0;
-  if (a.p.info[pos] & DXI_RULE) {
-    const uint32_t r = V - 1u - pos;
-    const uint64_t b = a.bw[(size_t)c * V + r];
-    uint64_t ol = 0;
-    if (b)
-      for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) ol |= a.lw[(size_t)c * V + (V - 1u - a.p.fc[j])];
-    uint64_t cand = b & ol;
-    const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
-    uint32_t *maxlen = a.lplist;
-    while (cand) {
-      const uint32_t e = (uint32_t)__builtin_ctzll(cand);
-      cand &= cand - 1ull;
-      const uint32_t u = 64u * c + e;
-      const uint32_t v = sv[(size_t)u * V + pos];
-      if (!v) continue;
-      lp |= 1ull << e;
-      atomicMax(maxlen + u, v);
+// ---- D, LP rules and the longest LP path per source ----------------------------------
+// D_u(v) = Fwd*_u(v) and Bwd*_u(v) (the walks' planes); LP rule r of source u: r in D_u
+// with a D_u-leaf goal child (a leaf candidate child, k_dx_walk).  maxLen_u = max val_u
+// over them (:82-98), reduced per workgroup in LDS before one global max per source.
+// the values of up to 8 set bits of m at position pos, their loads in flight together
+__device__ __forceinline__ uint32_t dx_vals8(const DxArgs &a, uint32_t c, uint32_t pos, uint64_t &m, uint32_t (&e)[8],
+                                             uint32_t (&v)[8]) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    e[k] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+    if (m) {
+      m &= m - 1ull;
+      n++;
     }
   }
-  a.dw[(size_t)c * V + pos] = lp;
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = e[k] < 64u ? a.sval[(size_t)(64u * c + e[k]) * a.p.V0 + pos] : 0u;
+  return n;
 }
-// missing rows: LP rules at the maximal depth, val == maxLen
+
+template <int NE>
+__global__ __launch_bounds__(DXP_B) void k_dx_lp(DxArgs a, uint32_t per) {
+  __shared__ uint32_t s_max[64];
+  const uint32_t c = blockIdx.y, V = a.p.V0, tid = threadIdx.x;
+  if (tid < 64) s_max[tid] = 0;
+  __syncthreads();
+  for (uint32_t pos = blockIdx.x * DXP_B * per + tid; pos < min(V, (blockIdx.x + 1) * DXP_B * per); pos += DXP_B) {
+    constexpr uint32_t GPC = (64u + NE - 1u) / NE;
+    uint64_t f = 0;
+    const uint8_t *fb = a.fb + (size_t)c * GPC * V + pos;
+#pragma unroll
+    for (uint32_t g = 0; g < GPC; g++) f |= (uint64_t)fb[(size_t)g * V] << (g * NE);
+    const uint32_t r = V - 1u - pos;
+    const uint64_t d = f & a.bw[(size_t)c * V + r];
+    a.dw[(size_t)c * V + pos] = d;
+    uint64_t lp = 0;
+    if (d && (a.p.info[pos] & DXI_RULE)) {
+      uint64_t ol = 0;
+      for (uint32_t j = a.p.fp[r]; j < a.p.fp[r + 1]; j++) ol |= a.lw[(size_t)c * V + (V - 1u - a.p.fc[j])];
+      lp = d & ol;
+      for (uint64_t m = lp; m;) {
+        uint32_t e[8], v[8];
+        dx_vals8(a, c, pos, m, e, v);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          if (e[k] < 64u) atomicMax(&s_max[e[k]], v[k]);
+      }
+    }
+    a.gw[(size_t)c * V + pos] = lp;
+  }
+  __syncthreads();
+  if (tid < 64 && s_max[tid]) atomicMax(a.maxlen + 64u * c + tid, s_max[tid]);
+}
+// missing rows: LP rules at the maximal depth, val == maxLen.  Eight threads per
+// position, eight sources each: one round of value loads per thread
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_emit(DxArgs a) {
   const uint32_t c = blockIdx.y, V = a.p.V0;
-  const uint32_t pos = blockIdx.x * NEMO_BLOCK + threadIdx.x;
-  if (pos >= V) return;
-  uint64_t lp = a.dw[(size_t)c * V + pos];
-  const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
-  while (lp) {
-    const uint32_t e = (uint32_t)__builtin_ctzll(lp);
-    lp &= lp - 1ull;
-    const uint32_t u = 64u * c + e;
-    if (sv[(size_t)u * V + pos] != a.lplist[u]) continue;
-    const uint32_t k = atomicAdd(a.n_missing, 1u) & 0x7FFFFFFFu;
-    a.missing[2 * k] = u;
-    a.missing[2 * k + 1] = a.p.pnode[pos];
+  const uint32_t t = blockIdx.x * NEMO_BLOCK + threadIdx.x, pos = t >> 3, sub = t & 7u;
+  // (no early return: every lane takes part in the wave's append)
+  uint64_t lp = pos < V ? a.gw[(size_t)c * V + pos] & (0xFFull << (8u * sub)) : 0ull;
+  uint32_t e[8], v[8], ml[8], hit = 0;
+  if (!__any(lp != 0ull)) return;  // wave-uniform
+  dx_vals8(a, c, pos, lp, e, v);  // at most eight bits: one round
+#pragma unroll
+  for (int k = 0; k < 8; k++) ml[k] = e[k] < 64u ? a.maxlen[64u * c + e[k]] : 0u;
+#pragma unroll
+  for (int k = 0; k < 8; k++) hit |= (e[k] < 64u && v[k] == ml[k] ? 1u : 0u) << k;
+  // one append per wave (a counter taking one atomic per row serialised the rows)
+  uint32_t tot;
+  const uint32_t ex = wave_exscan((uint32_t)__popc(hit), &tot);
+  if (!tot) return;
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd(a.n_missing, tot);
+  uint32_t q = ((__builtin_amdgcn_readfirstlane(base) & 0x7FFFFFFFu) + ex);
+  const uint32_t node = hit ? a.p.pnode[pos] : 0u;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (!((hit >> k) & 1u)) continue;
+    a.missing[2 * q] = 64u * c + e[k];
+    a.missing[2 * q + 1] = node;
+    q++;
   }
 }
 
 // ---- D masks by node for every entry ------------------------------------------------
-// D_u(v) = val_u(v) > 0 and B_u(v).  Thread: one node, DXM_E consecutive entries.
+// thread: one node, DXM_E consecutive entries (entries of one source share its bit word)
 #define DXM_E 32u
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
   const uint32_t V = a.p.V0, v = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (v >= V) return;
   const uint32_t pos = a.p.tpos[v];
   const uint32_t e0 = blockIdx.y * DXM_E, e1 = min(a.n_entries, e0 + DXM_E);
-  const uint16_t *sv = reinterpret_cast<const uint16_t *>(a.sval);
   uint32_t lc = NEMO_NONE;
   uint64_t w = 0;
   for (uint32_t e = e0; e < e1; e++) {
     const uint32_t u = a.map[e], c = u >> 6;
     if (c != lc) {
-      w = a.bw[(size_t)c * V + (V - 1u - pos)];
+      w = a.dw[(size_t)c * V + pos];
       lc = c;
     }
-    a.mask[(size_t)e * V + v] = (uint8_t)(((w >> (u & 63u)) & 1ull) && sv[(size_t)u * V + pos] != 0);
+    a.mask[(size_t)e * V + v] = (uint8_t)((w >> (u & 63u)) & 1ull);
   }
 }
 
@@ -742,7 +809,7 @@ static void walks_launch(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   const uint32_t bytes =
       std::max(dx_lds_bytes<uint64_t, 1>(m.W, m.R, m.EC, WHOLE), dx_lds_bytes<uint32_t, NE>(m.W, m.R, m.EC, WHOLE));
   hipFuncSetAttribute((const void *)k_dx_walks<NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  const dim3 grid(a.nch + (a.nu + NE - 1) / NE);
+  const dim3 grid(a.nch * (1u + (64u + NE - 1u) / NE));
   hipLaunchKernelGGL((k_dx_walks<NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, a.img[0], a.img[1]);
 }
 
@@ -785,18 +852,27 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   if (!V || !a.nu) return;
   const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
-  launch_zero(a.lplist, (uint64_t)a.nu * 4u, s);  // maxLen per source
+  launch_zero(a.maxlen, (uint64_t)a.nu * 4u, s);
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
   hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   const DxImg &m = a.img[0];
-  if (m.whole) {
-    if (dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) walks_launch<4, true, DX_NT>(c, a, s);
-    else walks_launch<2, true, DX_NT>(c, a, s);
+  // positions per k_dx_lp thread: enough workgroups for the chip, few enough that the
+  // per-workgroup maxima leave few global atomics per source
+  const uint32_t per = std::max(1u, (uint32_t)(((uint64_t)V * a.nch + DXP_B * 2048ull - 1) / (DXP_B * 2048ull)));
+  const dim3 glp((V + DXP_B * per - 1) / (DXP_B * per), a.nch);
+  // the most longest-path walkers whose rings fit LDS (one round of workgroups over the CUs)
+  if (m.whole && dx_lds_bytes<uint32_t, 6>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) {
+    walks_launch<6, true, DX_NT>(c, a, s);
+    hipLaunchKernelGGL(k_dx_lp<6>, glp, dim3(DXP_B), 0, s, a, per);
+  } else if (m.whole && dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) {
+    walks_launch<4, true, DX_NT>(c, a, s);
+    hipLaunchKernelGGL(k_dx_lp<4>, glp, dim3(DXP_B), 0, s, a, per);
   } else {
-    walks_launch<2, false, DX_NT>(c, a, s);
+    if (m.whole) walks_launch<2, true, DX_NT>(c, a, s);
+    else walks_launch<2, false, DX_NT>(c, a, s);
+    hipLaunchKernelGGL(k_dx_lp<2>, glp, dim3(DXP_B), 0, s, a, per);
   }
-  hipLaunchKernelGGL(k_dx_lp, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  hipLaunchKernelGGL(k_dx_emit, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_dx_emit, dim3((8 * V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   if (a.n_entries)
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }
