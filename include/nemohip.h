@@ -172,6 +172,12 @@ int nemo_set_timing(nemo_ctx *ctx, int enable);
  * the reference's "inserted number of edges" message (pre-post-prov.go:208-210).
  * Cycles fail with NEMO_ERR_CYCLE.  Host arrays may be freed on return.     */
 int nemo_load_corpus(nemo_ctx *ctx, const nemo_corpus *corpus);
+/* Page-lock (hipHostRegister) / release a caller-owned host buffer, so that
+ * nemo_load_corpus uploads it by DMA instead of through the runtime's staging
+ * copies: for corpora loaded more than once (a batch of a pass over a corpus
+ * larger than HBM).  No reference counterpart (Neo4j reads its own store).  */
+int nemo_host_register(const void *ptr, uint64_t bytes);
+int nemo_host_unregister(const void *ptr);
 /* Re-run the device part of the load (CSR + topo) on the resident corpus.    */
 int nemo_rebuild(nemo_ctx *ctx);
 uint64_t nemo_num_nodes(const nemo_ctx *ctx);

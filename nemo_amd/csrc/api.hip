@@ -375,6 +375,16 @@ extern "C" {
 
 int nemo_abi_version(void) { return NEMOHIP_ABI_VERSION; }
 
+int nemo_host_register(const void *ptr, uint64_t bytes) {
+  if (!ptr || !bytes) return NEMO_ERR_INVALID;
+  return hipHostRegister(const_cast<void *>(ptr), (size_t)bytes, hipHostRegisterDefault) == hipSuccess ? NEMO_OK
+                                                                                                       : NEMO_ERR_HIP;
+}
+int nemo_host_unregister(const void *ptr) {
+  if (!ptr) return NEMO_ERR_INVALID;
+  return hipHostUnregister(const_cast<void *>(ptr)) == hipSuccess ? NEMO_OK : NEMO_ERR_HIP;
+}
+
 // Run sharding: longest-processing-time-first over the runs'
 // node + edge counts (both graphs), ties by run index; each run goes to the
 // least-loaded part so far (ties by part index).  Deterministic, so every

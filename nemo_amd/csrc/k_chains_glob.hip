@@ -1145,10 +1145,13 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
     for (uint32_t i = tid; i < n; i += GB) S.ub[atomicAdd(&S.cnt[S.up[i]], 1u)] = i;
   }
   // best parent fixed up front where only one parent has up == up(v) - 1
+  // (GU nodes per thread and round, the first BP_K parents of each read together,
+  // then their up values: two rounds of loads in flight instead of a chain per parent)
   constexpr uint32_t MULTI = 0xFFFFFFFEu;
+  constexpr int BP_K = 3;
   for (uint32_t i0 = tid; i0 < n; i0 += GB * GU) {
     int32_t k[GU];
-    uint32_t r0[GU], r1[GU], p0[GU], cand[GU], cn[GU];
+    uint32_t r0[GU], r1[GU], cand[GU], cn[GU], pp[GU][BP_K];
 #pragma unroll
     for (int q = 0; q < GU; q++) {
       const uint32_t i = i0 + q * GB;
@@ -1158,19 +1161,31 @@ __global__ __launch_bounds__(GB, 1024 / GB) void k_chains_glob(DevCorpus c) {
       r1[q] = in ? S.pend[i] : 0u;
     }
 #pragma unroll
-    for (int q = 0; q < GU; q++) p0[q] = k[q] > 0 && r1[q] > r0[q] ? S.par[r0[q]] : GNIL;
+    for (int q = 0; q < GU; q++)
+#pragma unroll
+      for (int h = 0; h < BP_K; h++) pp[q][h] = k[q] > 0 && r0[q] + h < r1[q] ? S.par[r0[q] + h] : GNIL;
+    int32_t uu[GU][BP_K];
+#pragma unroll
+    for (int q = 0; q < GU; q++)
+#pragma unroll
+      for (int h = 0; h < BP_K; h++) uu[q][h] = pp[q][h] != GNIL ? S.up[pp[q][h]] : -2;
 #pragma unroll
     for (int q = 0; q < GU; q++) {
-      const int32_t u0 = p0[q] != GNIL ? S.up[p0[q]] : -2;
-      cn[q] = p0[q] != GNIL && u0 == k[q] - 1 ? 1u : 0u;
-      cand[q] = cn[q] ? p0[q] : GNIL;
+      cn[q] = 0;
+      cand[q] = GNIL;
+#pragma unroll
+      for (int h = 0; h < BP_K; h++)
+        if (pp[q][h] != GNIL && uu[q][h] == k[q] - 1) {
+          cn[q]++;
+          cand[q] = pp[q][h];
+        }
     }
 #pragma unroll
     for (int q = 0; q < GU; q++) {
       const uint32_t i = i0 + q * GB;
       if (i >= n) continue;
       if (k[q] > 0)
-        for (uint32_t j = r0[q] + 1; j < r1[q]; j++) {  // the rest of the row (rare)
+        for (uint32_t j = r0[q] + BP_K; j < r1[q]; j++) {  // the rest of the row (rare)
           const uint32_t pj = S.par[j];
           if (S.up[pj] == k[q] - 1) {
             cn[q]++;

@@ -296,6 +296,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     n = s.V;
   }
   uint32_t *pb = a.pb + (size_t)u * a.w32;
+  if (blockIdx.x == 0 && tid == 0) a.maxlen[u] = 0;  // k_dx_lp's maxima (two launches later)
   if (lds) {
     for (uint32_t w = tid; w < a.w32; w += NEMO_BLOCK) bm[w] = 0;
     __syncthreads();
@@ -664,11 +665,12 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     }
     finalize(nw - 1, tid, NT);
   }
-  if (MODE != 0) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   // leaf candidates of the chunk: goals in Bwd* none of whose children is (a D
-  // goal's children are all in Fwd*, so its D children are its Bwd* children)
+  // goal's children are all in Fwd*, so its D children are its Bwd* children).
+  // Whole graphs: from the ring, here; windowed walks: k_dx_lc over the grid (one
+  // workgroup re-reading a 1M-node graph's rows from HBM was the walks' long pole)
+  if (MODE != 0 || !WHOLE) return;
+  __syncthreads();
   uint64_t *lc = a.lw + (size_t)chunk * V;
   for (uint32_t i = tid; i < V; i += NT) {  // i: reversed walk index, its row = the children
     const uint32_t pos = V - 1u - i;
@@ -686,6 +688,32 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     lc[pos] = w;
     if (WHOLE) bwv[i] = ringp(0)[i];
   }
+}
+
+// leaf candidates after windowed walks: one thread per (position, chunk)
+__global__ __launch_bounds__(NEMO_BLOCK) void k_dx_lc(DxArgs a) {
+  const uint32_t c = blockIdx.y, V = a.p.V0;
+  const uint32_t i = blockIdx.x * NEMO_BLOCK + threadIdx.x;  // reversed walk index: its row = the children
+  if (i >= V) return;
+  const uint32_t pos = V - 1u - i;
+  const uint64_t *bw = a.bw + (size_t)c * V;
+  uint64_t w = 0;
+  if (!(a.p.info[pos] & DXI_RULE)) {
+    const uint64_t b = bw[i];
+    uint64_t ch = 0;
+    if (b) {
+      const uint32_t j0 = a.p.fp[i], j1 = a.p.fp[i + 1];
+      for (uint32_t j = j0; j < j1; j += 4) {
+        uint64_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = j + q < j1 ? bw[a.p.fc[j + q]] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; q++) ch |= v[q];
+      }
+    }
+    w = b & ~ch;
+  }
+  a.lw[(size_t)c * V + pos] = w;
 }
 
 // One launch for both walks: blocks [0, nch) walk Bwd* of their chunk, the rest
@@ -852,7 +880,6 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   if (!V || !a.nu) return;
   const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
-  launch_zero(a.maxlen, (uint64_t)a.nu * 4u, s);
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
   hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   const DxImg &m = a.img[0];
@@ -868,8 +895,12 @@ void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
     walks_launch<4, true, DX_NT>(c, a, s);
     hipLaunchKernelGGL(k_dx_lp<4>, glp, dim3(DXP_B), 0, s, a, per);
   } else {
-    if (m.whole) walks_launch<2, true, DX_NT>(c, a, s);
-    else walks_launch<2, false, DX_NT>(c, a, s);
+    if (m.whole) {
+      walks_launch<2, true, DX_NT>(c, a, s);
+    } else {
+      walks_launch<2, false, DX_NT>(c, a, s);
+      hipLaunchKernelGGL(k_dx_lc, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+    }
     hipLaunchKernelGGL(k_dx_lp<2>, glp, dim3(DXP_B), 0, s, a, per);
   }
   hipLaunchKernelGGL(k_dx_emit, dim3((8 * V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);

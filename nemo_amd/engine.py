@@ -71,6 +71,8 @@ def lib():
             "nemo_set_timing": ([vp, i32], i32),
             "nemo_set_option": ([vp, ctypes.c_char_p, ctypes.c_int64], i32),
             "nemo_load_corpus": ([vp, vp], i32),
+            "nemo_host_register": ([vp, u64], i32),
+            "nemo_host_unregister": ([vp], i32),
             "nemo_rebuild": ([vp], i32),
             "nemo_num_nodes": ([vp], u64),
             "nemo_num_edges": ([vp], u64),
@@ -117,6 +119,26 @@ def lib():
 
 def _p(a: Optional[np.ndarray]):
     return None if a is None or a.size == 0 else a.ctypes.data
+
+
+def pin_corpus(corpus: Corpus) -> list:
+    """Page-lock a corpus' large host arrays (nemo_host_register) so that every nemo_load_corpus of it
+    uploads by DMA; returns the registered arrays for unpin_corpus."""
+    L = lib()
+    pinned = []
+    for k in ("node_word", "label", "edge_src", "edge_dst", "id_rank"):
+        a = getattr(corpus, k, None)
+        if a is None or a.size == 0 or not a.flags["C_CONTIGUOUS"]:
+            continue
+        if L.nemo_host_register(a.ctypes.data, a.nbytes) == 0:
+            pinned.append(a)
+    return pinned
+
+
+def unpin_corpus(pinned: list) -> None:
+    L = lib()
+    for a in pinned:
+        L.nemo_host_unregister(a.ctypes.data)
 
 
 class Engine:
