@@ -58,13 +58,13 @@ GROUPS = {
     "k_marksimp": ["k_marksimp"],
     "k_mark": ["k_mark", "k_mw_mark_z", "k_mw_mark_a", "k_mw_mark_b"],
     "k_simplify": ["k_simplify_flags", "k_mw_simplify_1", "k_mw_simplify_2", "k_mw_simplify_3", "k_mw_simplify_4"],
-    "k_chains": ["k_chains", "k_chains_sel", "k_chains_list", "k_chains_big", "k_chains_glob"],
+    "k_chains": ["k_chains", "k_chains_sel", "k_chains_list", "k_chains_big", "k_glob_prep", "k_chains_glob"],
     "k_proto": ["k_proto_lds", "k_proto_sel", "k_pg_init", "k_pg_link", "k_pg_a", "k_pg_b", "k_pg_c", "k_pg_sweep",
                 "k_pg_d", "k_pg_gate"],
     "k_pull": ["k_pull_lds", "k_pull_sel", "k_pull", "k_mwp_count", "k_mwp_scan", "k_mwp_write", "k_scan64"],
     # the multi-entry kernels (k_dx.hip; k_zero's two small clears are not attributed) and the
     # one-workgroup-per-entry ones (option diff_legacy)
-    "k_diff": ["k_dx_label", "k_dx_good", "k_dx_walk", "k_dx_leaf", "k_dx_lp", "k_dx_mask",
+    "k_diff": ["k_dx_label", "k_dx_good", "k_dx_walks", "k_dx_lc", "k_dx_lp", "k_dx_emit", "k_dx_mask",
                "k_dprep_a", "k_dprep_scan", "k_dprep_b", "k_diff_lds", "k_diff", "k_diff_expand"],
 }
 
