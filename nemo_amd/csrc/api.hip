@@ -109,6 +109,7 @@ struct nemo_ctx {
   bool dx_ok = false;                // relayout allocated: run 0 present, every row fits a window
   int diff_legacy = 0;               // option diff_legacy: one workgroup per entry (k_diff.hip)
   uint32_t diff_window = 0;          // option diff_window (test knob): 0 by size, 1 windowed, 2 tiny windows
+  uint32_t diff_unfused = 0;         // option diff_fuse 0 (test knob): whole-graph walks hand LP rules to k_dx_lp / k_dx_emit
   uint32_t g0_maxdeg = 0;
   uint32_t dx_nu_cap = 0, dx_nch_cap = 0;
   uint32_t *d_dxpb = nullptr, *d_dxsval = nullptr, *d_dxlpl = nullptr, *d_dxfb = nullptr;
@@ -598,6 +599,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "chains_glob_stop")) {  // diagnostic (stamps build only; set after the load): k_chains_glob returns after phase k
     c->dc.glob_stop = value < 0 ? 0u : (uint32_t)value;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "diff_fuse")) {  // test knob: 0 runs k_dx_lp / k_dx_emit after whole-graph walks too
+    c->diff_unfused = value == 0;
     return NEMO_OK;
   }
   if (!strcmp(name, "chains_glob_prep")) {  // 0: no k_glob_prep (the per-graph front phases); takes effect at the next load
@@ -1446,7 +1451,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->dx_nu_cap = c->dx_nch_cap = 0;
     if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
     if ((rc = dalloc(c, &c->d_dxsval, ((size_t)nu * V0 + 1) / 2))) return rc;  // u16
-    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu))) return rc;
+    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu + nch))) return rc;  // maxima, then the chunks' walk flags
     if ((rc = dalloc(c, &c->d_dxw, 4 * (size_t)nch * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxfb, 8 * (size_t)nch * V0))) return rc;  // 32 bytes per position and chunk
     c->dx_nu_cap = nu;
@@ -1499,12 +1504,16 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.fb = reinterpret_cast<uint8_t *>(c->d_dxfb);
     a.sval = reinterpret_cast<uint16_t *>(c->d_dxsval);
     a.maxlen = c->d_dxlpl;
+    a.wflag = c->d_dxlpl + c->dx_nu_cap;
     a.mask = c->d_dmask;
     a.map = c->d_dmap;
     a.n_entries = (uint32_t)n_failed;
     a.missing = c->d_miss;
     a.n_missing = c->d_nmiss;
     a.window = c->diff_window;
+    a.legacy_lp = c->diff_unfused;
+    a.urep = c->d_dsrc + 2 * n_failed;
+    a.own_mask = nu == n_failed ? 1u : 0u;
     if (c->dx_img_key < 0) {
       // g0 in Kahn order (read the Kahn order, both CSRs and the node words;
       // write positions, rows both ways, level bounds), once per load / rebuild

@@ -96,11 +96,19 @@ struct DxArgs {
   uint32_t lab_split;        // workgroups per source (1: LDS bitmap stored whole)
   uint64_t *gw;              // [nch][V0] Good bits by position; after the walks: LP rules (k_dx_lp)
   uint64_t *bw;              // [nch][V0] Bwd*(Good) by REVERSED position (V0 - 1 - pos)
-  uint64_t *dw;              // [nch][V0] D = Fwd* & Bwd* by position (k_dx_lp)
+  uint64_t *dw;              // [nch][V0] D = Fwd* & Bwd* by position (k_dx_lp; k_dx_mask reads fb & bw)
   uint64_t *lw;              // [nch][V0] leaf candidates: Bwd* goals without a Bwd* child, by position
   uint8_t *fb;               // [nch][64 / NE][V0] Fwd* bits of the NE sources of longest-path workgroup g
   uint16_t *sval;            // [nu][V0] val = 1 + the longest path from Good (0 off Fwd*) by position
   uint32_t *maxlen;          // [nu] the longest LP val of each source (zeroed per call)
+  uint32_t *wflag;           // [nch] Bwd* walk of the chunk done (whole-graph walks; zeroed per call)
+  uint32_t ne;               // sources per longest-path workgroup of the walks launched (k_dx_mask)
+  uint32_t fuse;             // 1: the longest-path workgroups also take LP rules, maxLen and the missing
+                             // rows (whole-graph walks; k_dx_lp / k_dx_emit not launched)
+  uint32_t legacy_lp;        // test knob (option diff_fuse 0): no fusion
+  const uint32_t *urep;      // [nu] each source's first entry
+  uint32_t own_mask;         // 1: one entry per source and fused walks: the longest-path workgroups
+                             // write the D masks (k_dx_mask not launched)
   uint8_t *mask;             // [n_entries][V0] D masks by node (output)
   const uint32_t *map;       // [n_entries] entry -> source
   uint32_t n_entries;

@@ -21,6 +21,13 @@
 //   k_dx_lp      D = Fwd* & Bwd*, LP rules, the longest LP path per source
 //   k_dx_emit    missing rows (LP rules at that length)
 //   k_dx_mask    D masks by node for every entry (entries -> sources)
+// When g0 fits LDS whole (C3), k_dx_walks also does k_dx_lp's, k_dx_emit's and
+// (one entry per source) k_dx_mask's work: the chunk's Bwd* workgroup computes
+// the leaf candidates and, per rule, the OR of its children's, publishes them
+// with Bwd* (agent-scope release + flag), and each longest-path workgroup, whose
+// NE sources' values sit in its LDS over every position, waits for that flag and
+// finishes its sources alone (LP rules, maxLen as an LDS maximum, missing rows,
+// masks): label, good, walks per call.
 // g0's Kahn-order relayout (k_dxp_*) is built with the CSR in every load /
 // rebuild (launch_dx_prep), since it depends on the graph alone.
 //
@@ -32,6 +39,8 @@
 // its owner's init at staging.  Then one wave per source walks the window's
 // levels: each level is one step of independent lanes (no barrier, a wave's
 // LDS operations complete in order), value = init op (ring values of links).
+#include <atomic>
+
 #include "device.h"
 #include "internal.h"
 
@@ -296,7 +305,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     n = s.V;
   }
   uint32_t *pb = a.pb + (size_t)u * a.w32;
-  if (blockIdx.x == 0 && tid == 0) a.maxlen[u] = 0;  // k_dx_lp's maxima (two launches later)
+  if (blockIdx.x == 0 && tid == 0) {
+    a.maxlen[u] = 0;  // k_dx_lp's maxima (two launches later)
+    if (u < a.nch) a.wflag[u] = 0;  // the chunks' Bwd* flags (k_dx_walks)
+  }
   if (lds) {
     for (uint32_t w = tid; w < a.w32; w += NEMO_BLOCK) bm[w] = 0;
     __syncthreads();
@@ -469,6 +481,12 @@ __host__ __device__ inline uint32_t dx_lds_bytes(uint32_t W, uint32_t R, uint32_
   (void)W;
   return NE * lds_align((uint32_t)sizeof(T) * (R + 65u)) + NB * lds_align(4u * EC) + NB * 256u;
 }
+// the fused Bwd* workgroup's extra LDS past its own image: leaf candidates (u64) and rule
+// flags (u8), by reversed walk index
+__host__ __device__ inline uint32_t dx_fuse_bytes(uint32_t V, uint32_t EC) {
+  (void)EC;
+  return lds_align(8u * V) + lds_align(V);
+}
 template <typename T, int NE>
 __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t R, uint32_t EC, bool whole) {
   const uint32_t NB = whole ? 1u : 2u;
@@ -484,6 +502,11 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t R, uint32_
 }
 #define DX_VMAX 0xFFFEu  // longest val kept (u16 per source and position); past it the call fails
 #define DXP_B 256        // k_dx_lp: threads per workgroup
+#define DXF_K 6          // positions per thread and round of the leaf-candidate and fused LP passes
+
+template <int NE, int NT>
+__device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a, uint32_t chunk, uint32_t grp,
+                                            const uint32_t *ring0, uint32_t rs, uint8_t *lpb);
 
 template <int MODE, int NE, bool WHOLE, int NT>
 __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1,
@@ -587,7 +610,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
           if (srcu(e) == NEMO_NONE) continue;
           const uint32_t v = (uint32_t)ringp(e)[sl];
           over |= v > DX_VMAX;
-          sval(e)[i] = (uint16_t)min(v, (uint32_t)DX_VMAX);
+          if (!WHOLE || !a.fuse) sval(e)[i] = (uint16_t)min(v, (uint32_t)DX_VMAX);  // fused: values stay in LDS
           fbits |= (v ? 1u : 0u) << e;
         }
         fbp[i] = (uint8_t)fbits;
@@ -644,12 +667,32 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   const bool worker = wv >= (uint32_t)NE;
   const uint32_t wt = tid - NE * 64u, nwt = NT - NE * 64u;
   const uint32_t nw = m.nw[0];
+  STAMP(0);
   stage(0, 0, tid, NT);
   __syncthreads();
+  // fused Bwd* workgroup: its spare LDS (the launch's LDS is sized for the longest-path
+  // workgroups) takes the leaf candidates and the rule flags, by reversed walk index
+  const uint32_t fz0 = dx_lds_bytes<T, NE>(m.W, R, EC, true);
+  uint64_t *const lcl = (uint64_t *)(dyn + fz0);
+  uint8_t *const rl = (uint8_t *)(dyn + fz0 + lds_align(8u * V));
   if (WHOLE) {
-    if (walker) walk(0, 0, wv);
+    STAMP(1);
+    if (walker) {
+      walk(0, 0, wv);
+    } else if (MODE == 0 && a.fuse) {  // the idle waves fetch the rule flags while wave 0 walks
+      for (uint32_t i = tid - 64u; i < V; i += NT - 64u) {
+        rl[i] = (uint8_t)(a.p.info[V - 1u - i] & DXI_RULE);
+        lcl[i] = 0;
+      }
+    }
     __syncthreads();
-    finalize(0, tid, NT);
+    STAMP(2);
+    if (MODE == 0 || !a.fuse) finalize(0, tid, NT);  // fused: the values stay in LDS, D overwrites Fwd*
+    STAMP(3);
+    if (MODE == 2 && a.fuse) {  // the link records are dead: their LDS holds the LP bytes
+      dx_lp_fused<NE, NT>(c, a, chunk, grp, (const uint32_t *)L.ring0, L.rs, (uint8_t *)L.lk);
+      return;
+    }
   } else {
     for (uint32_t k = 0; k < nw; k++) {
       if (walker) {
@@ -671,23 +714,235 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   // workgroup re-reading a 1M-node graph's rows from HBM was the walks' long pole)
   if (MODE != 0 || !WHOLE) return;
   __syncthreads();
-  uint64_t *lc = a.lw + (size_t)chunk * V;
-  for (uint32_t i = tid; i < V; i += NT) {  // i: reversed walk index, its row = the children
-    const uint32_t pos = V - 1u - i;
-    uint64_t w = 0;
-    if (!(a.p.info[pos] & DXI_RULE)) {
-      const uint64_t b = WHOLE ? (uint64_t)ringp(0)[i] : __hip_atomic_load(bwv + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint64_t ch = 0;
-      if (b)
-        for (uint32_t j = rowp[i]; j < rowp[i + 1]; j++) {
-          const uint32_t x = a.p.fc[j];
-          ch |= WHOLE ? (uint64_t)ringp(0)[x] : __hip_atomic_load(bwv + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      w = b & ~ch;
+  if (a.fuse) {
+    // leaf candidates LC(x) = B(x) & ~OR B(children) of goals, then per rule the OR of its
+    // children's LC (the longest-path workgroups' LP test: a D rule with an LC child), all
+    // from LDS; the rules' words go to HBM (lw by position) with Bwd*
+    const uint64_t *rg = (const uint64_t *)ringp(0);
+    // over the links of the whole-graph image (still in LDS: owner's slot << 16 | child's
+    // slot, slots = reversed walk indices) with LDS atomics, then per index
+    uint64_t *const rw = (uint64_t *)ringp(0);
+    const uint32_t *lk = L.lk, E0 = a.p.E0;
+    for (uint32_t j = tid; j < E0; j += NT) {  // goals: the OR of their children's B
+      const uint32_t rec = lk[j], o = rec >> 16, x = rec & 0xFFFFu;
+      if (!rl[o]) {
+        const uint64_t v = rw[x];
+        if (v) atomicOr((unsigned long long *)&lcl[o], (unsigned long long)v);
+      }
     }
-    lc[pos] = w;
-    if (WHOLE) bwv[i] = ringp(0)[i];
+    __syncthreads();
+    for (uint32_t i = tid; i < V; i += NT) {  // LC, Bwd* to HBM; the ring is free after this
+      const uint64_t b = rw[i];
+      bwv[i] = b;
+      lcl[i] = rl[i] ? 0ull : b & ~lcl[i];
+      rw[i] = 0;
+    }
+    __syncthreads();
+    STAMP(4);
+    for (uint32_t j = tid; j < E0; j += NT) {  // rules: the OR of their children's LC, in the ring
+      const uint32_t rec = lk[j], o = rec >> 16, x = rec & 0xFFFFu;
+      if (rl[o]) {
+        const uint64_t v = lcl[x];
+        if (v) atomicOr((unsigned long long *)&rw[o], (unsigned long long)v);
+      }
+    }
+    __syncthreads();
+    uint64_t *olw = a.lw + (size_t)chunk * V;
+    for (uint32_t i = tid; i < V; i += NT) olw[V - 1u - i] = rw[i];
+    // publish Bwd* and the rules' words to the chunk's longest-path workgroups: every
+    // wave's stores reach L2, then one lane writes the XCD's L2 back and sets the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    STAMP(5);
+    return;
   }
+  uint64_t *lc = a.lw + (size_t)chunk * V;
+  const T *rg = ringp(0);
+  // DXF_K indices per thread and round, the rows' loads in flight together, then the
+  // children's ring slots four children at a time
+  for (uint32_t base = 0; base < V; base += DXF_K * NT) {
+    uint32_t j0[DXF_K], j1[DXF_K];
+    uint64_t b[DXF_K], ch[DXF_K];
+    bool goal[DXF_K];
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {  // i: reversed walk index, its row = the children
+      const uint32_t i = base + k * NT + tid;
+      const bool in = i < V;
+      goal[k] = in && !(a.p.info[V - 1u - min(i, V - 1u)] & DXI_RULE);
+      j0[k] = in ? rowp[i] : 0u;
+      j1[k] = in ? rowp[i + 1] : 0u;
+      b[k] = in ? (uint64_t)rg[i] : 0ull;
+      ch[k] = 0;
+      if (in) bwv[i] = b[k];
+    }
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++)
+      if (!goal[k] || !b[k]) j1[k] = j0[k];
+    for (;;) {
+      bool more = false;
+#pragma unroll
+      for (int k = 0; k < DXF_K; k++) more |= j0[k] < j1[k];
+      if (!more) break;
+      uint32_t x[DXF_K][4];
+#pragma unroll
+      for (int k = 0; k < DXF_K; k++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[k][q] = j0[k] + q < j1[k] ? a.p.fc[j0[k] + q] : R;  // R: the sink (0)
+#pragma unroll
+      for (int k = 0; k < DXF_K; k++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) ch[k] |= (uint64_t)rg[x[k][q]];
+        j0[k] = min(j0[k] + 4u, j1[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {
+      const uint32_t i = base + k * NT + tid;
+      if (i < V) lc[V - 1u - i] = goal[k] ? b[k] & ~ch[k] : 0ull;
+    }
+  }
+}
+
+// Whole-graph walks, fused: a longest-path workgroup holds its NE sources' values over
+// every position, so once its chunk's Bwd* workgroup has published Bwd* and the leaf
+// candidates it finds the sources' LP rules (D rules with a leaf-candidate child),
+// maxLen (an LDS maximum: no other workgroup holds these sources) and the missing rows
+// (LP rules with val == maxLen) itself, in place of k_dx_lp and k_dx_emit.  Its Fwd*
+// byte plane is overwritten with D (k_dx_mask reads D there).
+template <int NE, int NT>
+__device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a, uint32_t chunk, uint32_t grp,
+                                            const uint32_t *ring0, uint32_t rs, uint8_t *lpb) {
+  (void)c;
+  __shared__ uint32_t s_max[NE];
+  const uint32_t tid = threadIdx.x, V = a.p.V0, sh = grp * NE;
+  constexpr uint32_t NM = (1u << NE) - 1u;
+  uint32_t live = 0;  // this workgroup's sources (bit e: source 64 chunk + NE grp + e)
+#pragma unroll
+  for (int e = 0; e < NE; e++) live |= (sh + e < 64u && 64u * chunk + sh + e < a.nu ? 1u : 0u) << e;
+  if (tid < (uint32_t)NE) s_max[tid] = 0;
+  if (tid == 0) {  // one lane polls the chunk's flag, then one acquire for the workgroup
+    while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  STAMP(4);
+  // D by position: in LDS past the LP bytes when this workgroup writes its sources' masks
+  const bool own = a.own_mask != 0u;
+  uint8_t *const dl = lpb + ((V + 15u) & ~15u);
+  // lw: the chunk's rules' leaf-child words (the Bwd* workgroup, fused form)
+  const uint64_t *bw = a.bw + (size_t)chunk * V, *lw = a.lw + (size_t)chunk * V;
+  // D of the sources over the Fwd* plane, for k_dx_mask
+  uint8_t *dpl = a.fb + ((size_t)chunk * ((64u + NE - 1u) / NE) + grp) * V;
+  uint32_t mx[NE];
+#pragma unroll
+  for (int e = 0; e < NE; e++) mx[e] = 0;
+  bool over = false;
+  // DXF_K positions per thread and round, every round's loads in flight together: the rule
+  // flag, the Bwd* word and the rule's leaf-child word (the chunk's Bwd* workgroup)
+  for (uint32_t base = 0; base < V; base += DXF_K * NT) {
+    uint32_t inf[DXF_K];
+    uint64_t b[DXF_K], o[DXF_K];
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {
+      const uint32_t p = min(base + k * NT + tid, V - 1u);  // clamped, unconditional: all loads in flight
+      inf[k] = a.p.info[p];
+      b[k] = bw[V - 1u - p];
+      o[k] = lw[p];
+    }
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {
+      const uint32_t pos = base + k * NT + tid;
+      if (pos >= V) continue;
+      uint32_t f = 0;
+#pragma unroll
+      for (int e = 0; e < NE; e++) {
+        const uint32_t v = ring0[(size_t)e * rs + pos];
+        over |= v > DX_VMAX;
+        f |= (v ? 1u : 0u) << e;
+      }
+      const uint32_t d = f & live & (uint32_t)(b[k] >> sh) & NM;
+      if (own) dl[pos] = (uint8_t)d;
+      else dpl[pos] = (uint8_t)d;
+      const uint32_t lp = (inf[k] & DXI_RULE) ? d & (uint32_t)(o[k] >> sh) & NM : 0u;
+#pragma unroll
+      for (int e = 0; e < NE; e++)
+        if ((lp >> e) & 1u) mx[e] = max(mx[e], ring0[(size_t)e * rs + pos]);
+      lpb[pos] = (uint8_t)lp;
+    }
+  }
+  // maxima: the wave's, then one LDS atomic per wave and source
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    uint32_t x = mx[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    if (lane_id() == 0 && x) atomicMax(&s_max[e], x);
+  }
+  if (__any(over) && lane_id() == 0) atomicOr(a.n_missing, 0x80000000u);
+  __syncthreads();
+  STAMP(5);
+  if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = min(s_max[tid], (uint32_t)DX_VMAX);
+  // one entry per source: the D masks by node, consecutive nodes per wave (coalesced bytes)
+  if (own) {
+    uint32_t ent[NE];
+#pragma unroll
+    for (int e = 0; e < NE; e++) ent[e] = ((live >> e) & 1u) ? a.urep[64u * chunk + sh + e] : 0u;
+    for (uint32_t base = 0; base < V; base += DXF_K * NT) {
+      uint32_t tp[DXF_K];  // every position loaded before the byte stores (which may alias)
+#pragma unroll
+      for (int k = 0; k < DXF_K; k++) tp[k] = a.p.tpos[min(base + k * NT + tid, V - 1u)];
+#pragma unroll
+      for (int k = 0; k < DXF_K; k++) {
+        const uint32_t v = base + k * NT + tid;
+        if (v >= V) continue;
+        const uint32_t d = dl[tp[k]];
+#pragma unroll
+        for (int e = 0; e < NE; e++)
+          if ((live >> e) & 1u) a.mask[(size_t)ent[e] * V + v] = (uint8_t)((d >> e) & 1u);
+      }
+    }
+  }
+  // the rows: counted per thread, one block scan and one global atomic per workgroup
+  __shared__ uint32_t s_scan[NT / 64], s_base;
+  auto hits = [&](uint32_t pos) -> uint32_t {
+    const uint32_t lp = lpb[pos];
+    uint32_t h = 0;
+    if (lp) {
+#pragma unroll
+      for (int e = 0; e < NE; e++)
+        if (((lp >> e) & 1u) && ring0[(size_t)e * rs + pos] == s_max[e]) h |= 1u << e;
+    }
+    return h;
+  };
+  uint32_t cnt = 0;
+  for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
+  uint32_t tot;
+  uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
+  if (!tot) return;  // workgroup-uniform
+  if (tid == 0) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
+  __syncthreads();
+  q += s_base;
+  for (uint32_t pos = tid; pos < V && cnt; pos += NT) {
+    const uint32_t h = hits(pos);
+    if (!h) continue;
+    const uint32_t node = a.p.pnode[pos];
+#pragma unroll
+    for (int e = 0; e < NE; e++) {
+      if (!((h >> e) & 1u)) continue;
+      a.missing[2 * q] = 64u * chunk + sh + e;
+      a.missing[2 * q + 1] = node;
+      q++;
+      cnt--;
+    }
+  }
+  STAMP(6);
 }
 
 // leaf candidates after windowed walks: one thread per (position, chunk)
@@ -811,23 +1066,29 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_emit(DxArgs a) {
 }
 
 // ---- D masks by node for every entry ------------------------------------------------
-// thread: one node, DXM_E consecutive entries (entries of one source share its bit word)
-#define DXM_E 32u
+// thread: one node, DXM_E consecutive entries, all their loads in flight together.
+// D: after fused walks the source's bit of its longest-path workgroup's D byte plane
+// (dx_lp_fused), else its bit of the chunk's D word (k_dx_lp)
+#define DXM_E 32
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_mask(DxArgs a) {
   const uint32_t V = a.p.V0, v = blockIdx.x * NEMO_BLOCK + threadIdx.x;
   if (v >= V) return;
-  const uint32_t pos = a.p.tpos[v];
-  const uint32_t e0 = blockIdx.y * DXM_E, e1 = min(a.n_entries, e0 + DXM_E);
-  uint32_t lc = NEMO_NONE;
-  uint64_t w = 0;
-  for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t u = a.map[e], c = u >> 6;
-    if (c != lc) {
-      w = a.dw[(size_t)c * V + pos];
-      lc = c;
+  const uint32_t pos = a.p.tpos[v], gpc = (64u + a.ne - 1u) / a.ne;
+  const uint32_t e0 = blockIdx.y * DXM_E, n = min(a.n_entries - e0, (uint32_t)DXM_E);
+  uint32_t bit[DXM_E];
+#pragma unroll
+  for (int k = 0; k < DXM_E; k++) {
+    const uint32_t u = (uint32_t)k < n ? a.map[e0 + k] : 0u, c = u >> 6, b = u & 63u;
+    if (a.fuse) {
+      const uint32_t g = b / a.ne;
+      bit[k] = (uint32_t)a.fb[((size_t)c * gpc + g) * V + pos] >> (b - g * a.ne);
+    } else {
+      bit[k] = (uint32_t)(a.dw[(size_t)c * V + pos] >> b);
     }
-    a.mask[(size_t)e * V + v] = (uint8_t)((w >> (u & 63u)) & 1ull);
   }
+#pragma unroll
+  for (int k = 0; k < DXM_E; k++)
+    if ((uint32_t)k < n) a.mask[(size_t)(e0 + k) * V + v] = (uint8_t)(bit[k] & 1u);
 }
 
 // ---- launch -----------------------------------------------------------------------------
@@ -836,7 +1097,16 @@ static void walks_launch(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
   const DxImg &m = a.img[0];
   const uint32_t bytes =
       std::max(dx_lds_bytes<uint64_t, 1>(m.W, m.R, m.EC, WHOLE), dx_lds_bytes<uint32_t, NE>(m.W, m.R, m.EC, WHOLE));
-  hipFuncSetAttribute((const void *)k_dx_walks<NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  // per instantiation and device: the attribute call (host time before the launch) only when
+  // the size grows
+  static std::atomic<uint32_t> set[64];
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::atomic<uint32_t> &st = set[dev & 63];
+  if (bytes > st.load()) {
+    hipFuncSetAttribute((const void *)k_dx_walks<NE, WHOLE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    st.store(bytes);
+  }
   const dim3 grid(a.nch * (1u + (64u + NE - 1u) / NE));
   hipLaunchKernelGGL((k_dx_walks<NE, WHOLE, NT>), grid, dim3(NT), bytes, s, c, a, a.img[0], a.img[1]);
 }
@@ -875,36 +1145,52 @@ void dx_img_configs(uint32_t V, uint32_t E, uint32_t window, DxImg out[2]) {
   }
 }
 
-void launch_dx(const DevCorpus &c, const DxArgs &a, hipStream_t s) {
+void launch_dx(const DevCorpus &c, const DxArgs &a_in, hipStream_t s) {
+  DxArgs a = a_in;
   const uint32_t V = a.p.V0;
   if (!V || !a.nu) return;
   const uint32_t nbv = (V + NEMO_BLOCK - 1) / NEMO_BLOCK;
   if (a.lab_split > 1 || a.w32 > DXL_LDS) launch_zero(a.pb, (uint64_t)a.nu * a.w32 * 4u, s);
   hipLaunchKernelGGL(k_dx_label, dim3(a.lab_split, a.nu), dim3(NEMO_BLOCK), 0, s, c, a);
-  hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
   const DxImg &m = a.img[0];
   // positions per k_dx_lp thread: enough workgroups for the chip, few enough that the
   // per-workgroup maxima leave few global atomics per source
   const uint32_t per = std::max(1u, (uint32_t)(((uint64_t)V * a.nch + DXP_B * 2048ull - 1) / (DXP_B * 2048ull)));
   const dim3 glp((V + DXP_B * per - 1) / (DXP_B * per), a.nch);
   // the most longest-path walkers whose rings fit LDS (one round of workgroups over the CUs)
-  if (m.whole && dx_lds_bytes<uint32_t, 6>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) {
+  // whole graphs: the longest-path workgroups finish the call's LP rules and missing rows
+  // (their LP and D bytes over the dead link records), the Bwd* workgroup's rows and
+  // leaf candidates in the LDS the longest-path workgroups' rings leave it
+  const uint32_t ne = dx_lds_bytes<uint32_t, 6>(m.W, m.R, m.EC, true) <= DX_LDS_MAX   ? 6u
+                      : dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true) <= DX_LDS_MAX ? 4u
+                                                                                       : 2u;
+  const uint32_t bwd = dx_lds_bytes<uint64_t, 1>(m.W, m.R, m.EC, true);
+  const uint32_t lds = std::max(bwd, ne == 6   ? dx_lds_bytes<uint32_t, 6>(m.W, m.R, m.EC, true)
+                                     : ne == 4 ? dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true)
+                                               : dx_lds_bytes<uint32_t, 2>(m.W, m.R, m.EC, true));
+  a.fuse = m.whole && 2u * ((V + 15u) & ~15u) <= 4u * m.EC && bwd + dx_fuse_bytes(V, m.EC) <= lds && !a.legacy_lp ? 1u : 0u;
+  hipLaunchKernelGGL(k_dx_good, dim3((V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  if (m.whole && ne == 6) {
+    a.ne = 6;
     walks_launch<6, true, DX_NT>(c, a, s);
-    hipLaunchKernelGGL(k_dx_lp<6>, glp, dim3(DXP_B), 0, s, a, per);
-  } else if (m.whole && dx_lds_bytes<uint32_t, 4>(m.W, m.R, m.EC, true) <= DX_LDS_MAX) {
+    if (!a.fuse) hipLaunchKernelGGL(k_dx_lp<6>, glp, dim3(DXP_B), 0, s, a, per);
+  } else if (m.whole && ne == 4) {
+    a.ne = 4;
     walks_launch<4, true, DX_NT>(c, a, s);
-    hipLaunchKernelGGL(k_dx_lp<4>, glp, dim3(DXP_B), 0, s, a, per);
+    if (!a.fuse) hipLaunchKernelGGL(k_dx_lp<4>, glp, dim3(DXP_B), 0, s, a, per);
   } else {
+    a.ne = 2;
     if (m.whole) {
       walks_launch<2, true, DX_NT>(c, a, s);
     } else {
       walks_launch<2, false, DX_NT>(c, a, s);
       hipLaunchKernelGGL(k_dx_lc, dim3(nbv, a.nch), dim3(NEMO_BLOCK), 0, s, a);
     }
-    hipLaunchKernelGGL(k_dx_lp<2>, glp, dim3(DXP_B), 0, s, a, per);
+    if (!a.fuse) hipLaunchKernelGGL(k_dx_lp<2>, glp, dim3(DXP_B), 0, s, a, per);
   }
-  hipLaunchKernelGGL(k_dx_emit, dim3((8 * V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
-  if (a.n_entries)
+  if (!a.fuse)
+    hipLaunchKernelGGL(k_dx_emit, dim3((8 * V + NEMO_BLOCK - 1) / NEMO_BLOCK, a.nch), dim3(NEMO_BLOCK), 0, s, a);
+  if (a.n_entries && !(a.fuse && a.own_mask))
     hipLaunchKernelGGL(k_dx_mask, dim3(nbv, (a.n_entries + DXM_E - 1) / DXM_E), dim3(NEMO_BLOCK), 0, s, a);
 }
 

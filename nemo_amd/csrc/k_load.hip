@@ -52,6 +52,9 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 #define BLD_BLOCK 256  // k_build workgroup size (512: 3.91 ms against 3.66 at C3)
 #endif
 #define BLD_OCC(B) ((B) == 256 ? 4 : 6)  // waves per SIMD the register budget is cut for
+#ifndef BLD_SQ
+#define BLD_SQ 4    // rows per thread and round of the row sort (even)
+#endif
 #ifndef BLD_KB
 #define BLD_KB 4    // Kahn: children of a node processed per round
 #endif
@@ -101,20 +104,19 @@ __device__ __forceinline__ void sort_net16(uint32_t *x) {
 // rows' LDS reads issued together and the entries sorted in registers (a row
 // longer than RS: insertion sort in LDS); reverse rows (dir 0) also count the
 // relationships created (pre-post-prov.go:150-210: distinct, goal<->rule).
-template <int RS, int B>
+template <int RS, int B, int NQ>
 __device__ __forceinline__ uint32_t sort_row_pair(uint16_t *col, const uint32_t *s_rule, uint32_t E, uint32_t V,
-                                                  int dir, uint32_t v0, const uint32_t (&a)[2],
-                                                  const uint32_t (&n)[2]) {
-  uint32_t x[2][RS], created = 0;
+                                                  int dir, uint32_t v0, const uint32_t *a, const uint32_t *n) {
+  uint32_t x[NQ][RS], created = 0;
 #pragma unroll
-  for (int q = 0; q < 2; q++)
+  for (int q = 0; q < NQ; q++)
 #pragma unroll
     for (int i = 0; i < RS; i++) {
       const uint32_t y = col[min(a[q] + i, E - 1u)];  // clamped, unconditional: all reads in flight together
       x[q][i] = (uint32_t)i < n[q] ? y : 0xFFFFu;
     }
 #pragma unroll
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < NQ; q++) {
     const uint32_t v = v0 + q * B, b = a[q] + n[q];
     if (n[q] <= (uint32_t)RS) {
       if (n[q] >= 2) {
@@ -334,22 +336,32 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     // sort every row; two rows per thread at a time with all their LDS reads
     // issued together, the entries sorted in registers (a latency chain of a
     // few LDS round trips instead of one per entry)
-    for (uint32_t v0 = tid; v0 < V; v0 += 2 * B) {
-      uint32_t a[2], n[2];
+    for (uint32_t v0 = tid; v0 < V; v0 += BLD_SQ * B) {
+      uint32_t a[BLD_SQ], n[BLD_SQ];
 #pragma unroll
-      for (int q = 0; q < 2; q++) {
+      for (int q = 0; q < BLD_SQ; q++) {
         const uint32_t v = v0 + q * B;
         a[q] = v < V && v ? ptr[v - 1] : 0u;
         n[q] = v < V ? ptr[v] - a[q] : 0u;
       }
+      uint32_t nmax = 0;
+#pragma unroll
+      for (int q = 0; q < BLD_SQ; q++) nmax = max(nmax, n[q]);
       // rows of at most four entries everywhere in the wave (most reverse rows,
-      // goals' forward rows): the 4-key network; else the 8-key one
-      if (!__any(n[0] > 4u || n[1] > 4u))
-        created += sort_row_pair<4, B>(col, s_rule, E, V, dir, v0, a, n);
-      else if (!__any(n[0] > 8u || n[1] > 8u))
-        created += sort_row_pair<8, B>(col, s_rule, E, V, dir, v0, a, n);
-      else  // a row past eight entries in the wave: the 16-key network (an LDS insertion sort held the wave)
-        created += sort_row_pair<16, B>(col, s_rule, E, V, dir, v0, a, n);
+      // goals' forward rows): the 4-key network over all BLD_SQ rows; else the
+      // 8-key one two rows at a time
+      if (!__any(nmax > 4u)) {
+        created += sort_row_pair<4, B, BLD_SQ>(col, s_rule, E, V, dir, v0, a, n);
+      } else {
+#pragma unroll
+        for (int h = 0; h < BLD_SQ; h += 2) {
+          const uint32_t v = v0 + h * B;
+          if (!__any(n[h] > 8u || n[h + 1] > 8u))
+            created += sort_row_pair<8, B, 2>(col, s_rule, E, V, dir, v, a + h, n + h);
+          else  // a row past eight entries in the wave: the 16-key network (an LDS insertion sort held the wave)
+            created += sort_row_pair<16, B, 2>(col, s_rule, E, V, dir, v, a + h, n + h);
+        }
+      }
     }
     __syncthreads();
     if (dir == 0) STAMP(6);

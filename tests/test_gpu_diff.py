@@ -8,6 +8,8 @@ the label source; D = Fwd*(Good) ∩ Bwd*(Good); missing = D rules with a D-leaf
 The walks are exercised in their three forms: the whole of run 0's post graph in one LDS window (small
 graphs), Kahn-order windows with a ring of recent values (diff_window=1), and tiny windows whose ring most
 links leave (diff_window=2), so that the values of earlier windows are read back from HBM at staging.
+Whole-graph walks finish the LP rules and missing rows in their longest-path workgroups (the default) or
+hand them to k_dx_lp / k_dx_emit (option diff_fuse 0); both are checked.
 Sources come in 64-wide chunks: corpora with more than 64 failed runs take several.
 """
 import numpy as np
@@ -33,15 +35,17 @@ def _rows(m):
     return m[np.lexsort((m[:, 1], m[:, 0]))]
 
 
-def _device(eng, corpus, f, mode, window=0, legacy=0):
+def _device(eng, corpus, f, mode, window=0, legacy=0, fuse=1):
     eng.set_option("diff_window", window)
     eng.set_option("diff_legacy", legacy)
+    eng.set_option("diff_fuse", fuse)
     try:
         eng.diffprov(f, mode)
         return eng.diff_masks(len(f)), _rows(eng.missing())
     finally:
         eng.set_option("diff_window", 0)
         eng.set_option("diff_legacy", 0)
+        eng.set_option("diff_fuse", 1)
 
 
 def _check_corpus(eng, corpus, windows=(0, 1, 2)):
@@ -57,6 +61,9 @@ def _check_corpus(eng, corpus, windows=(0, 1, 2)):
             assert np.array_equal(m, want_m), f"D masks differ (mode {mode}, window {w}): " \
                 f"{int((m != want_m).any(1).sum())} of {len(f)} entries"
             assert np.array_equal(r, want_r), f"missing rows differ (mode {mode}, window {w})"
+        if 0 in windows:  # whole-graph walks with LP rules and missing rows in k_dx_lp / k_dx_emit
+            um, ur = _device(eng, corpus, f, mode, fuse=0)
+            assert np.array_equal(um, want_m) and np.array_equal(ur, want_r), f"unfused walks differ (mode {mode})"
         lm, lr = _device(eng, corpus, f, mode, legacy=1)
         assert np.array_equal(lm, want_m) and np.array_equal(lr, want_r), "legacy kernels differ"
 

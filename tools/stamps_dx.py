@@ -1,9 +1,9 @@
-"""Diagnostic: per-phase ticks of the multi-entry diff's walks (k_dx_walk) from the stamps build.
+"""Diagnostic: per-phase ticks (s_memtime) of the whole-graph walks (k_dx_walks) from the stamps build.
 
-usage: python tools/stamps_dx.py [c3|c5] [RUNS] [P_FAULT]
-Reach workgroups (chunk x direction) and depth workgroups (2 sources each), wave 0's view: the first window's
-staging, the walks, the waits for the worker waves (finalize k-1 / stage k+1) at the window barriers, the missing
-rows pass; windows; total.
+usage: python tools/stamps_dx.py [RUNS] [P_FAULT] [FUSE]
+Bwd* workgroups (one per 64-source chunk): stage, walk, finalize, leaf candidates, publish.
+Longest-path workgroups: stage, walk, finalize, wait for the chunk's Bwd*, LP pass, missing rows.
+Ticks from each workgroup's start; the launch's first start is the origin of "start".
 """
 import os
 import sys
@@ -19,25 +19,29 @@ E.LIB_PATH = os.path.join(os.path.dirname(E.LIB_PATH), "libnemohip_stamps.so")
 from nemo_amd.corpus import DIFF_PER_RUN  # noqa: E402
 from tools import synth  # noqa: E402
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
-runs = int(sys.argv[2]) if len(sys.argv) > 2 else (10000 if cfg == "c3" else 64)
-pf = float(sys.argv[3]) if len(sys.argv) > 3 else (0.15 if cfg == "c3" else 0.6)
-corpus, _ = synth.generate(runs, p_fault=pf, prepend_run0=True, **synth.CONFIGS[cfg])
+runs = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+pf = float(sys.argv[2]) if len(sys.argv) > 2 else 0.15
+fuse = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+corpus, _ = synth.generate(runs, p_fault=pf, prepend_run0=True, **synth.CONFIGS["c3"])
 f = corpus.failed_iters()
 eng = E.Engine(0)
 eng.load(corpus)
 eng.mark()
-eng.diffprov(f, DIFF_PER_RUN)
+eng.set_option("diff_fuse", fuse)
+for _ in range(3):
+    eng.diffprov(f, DIFF_PER_RUN)
 eng.synchronize()
 nu = len(f)
 nch = (nu + 63) // 64
-nd = (nu + 1) // 2
-n = 16 * max(2 * nch, nd)
-st = eng.debug_copy("stamps", 0, 8 * n).view(np.uint64).reshape(-1, 16).astype(np.int64)
-names = ["stage0", "-", "-", "walk", "wait", "rows", "windows", "total"]
-for label, rows, off in (("reach", st[:2 * nch], 0), ("depth", st[:nd], 8)):
-    blk = rows[:, off:off + 8]
-    print(f"{label}: {len(blk)} workgroups")
+nb = nch * (1 + 11)
+st = eng.debug_copy("stamps", 0, 8 * 16 * nb).view(np.uint64).reshape(-1, 16).astype(np.int64)
+t0 = st[:, 0].min()
+for label, rows, names in (("bwd", st[:nch], ["stage", "walk", "finalize", "lc", "publish"]),
+                           ("depth", st[nch:nb], ["stage", "walk", "finalize", "wait", "lp", "rows"])):
+    rows = rows[rows[:, 0] > 0]
+    print(f"{label}: {len(rows)} workgroups; start median {np.median(rows[:, 0] - t0):.0f} max {(rows[:, 0] - t0).max()}")
+    d = np.diff(rows[:, :len(names) + 1], axis=1)
     for i, nm in enumerate(names):
-        print(f"  {nm:9s} median {np.median(blk[:, i]):14.0f}  max {blk[:, i].max():14.0f}")
+        print(f"  {nm:9s} median {np.median(d[:, i]):10.0f}  max {d[:, i].max():10.0f}")
+    print(f"  end       median {np.median(rows[:, len(names)] - t0):10.0f}  max {(rows[:, len(names)] - t0).max()}")
 eng.close()
