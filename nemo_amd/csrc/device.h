@@ -403,6 +403,15 @@ __device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
       c.stamps[16 * (size_t)blockIdx.x + (k)] = t_;                                       \
     }                                                                                     \
   } while (0)
+// the same for a 2-D grid (block index x + y * gridDim.x)
+#define STAMP2(k)                                                                               \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && c.stamps) {                                                         \
+      unsigned long long t_;                                                                    \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+      c.stamps[16 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + (k)] = t_;                  \
+    }                                                                                           \
+  } while (0)
 // phase accumulators: TICK waits for the wave's outstanding memory operations,
 // so a phase is charged with the latency of the loads it issued
 // diagnostic early exit after phase k of a stamped kernel (per-phase HBM counters)
@@ -417,6 +426,9 @@ __device__ __forceinline__ void stage_lds(const StageDesc (&d)[ND]) {
 #else
 #define STAMP(k) \
   do {           \
+  } while (0)
+#define STAMP2(k) \
+  do {            \
   } while (0)
 #define GSTOP(k) \
   do {           \

@@ -305,6 +305,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     n = s.V;
   }
   uint32_t *pb = a.pb + (size_t)u * a.w32;
+  STAMP2(10);
   if (blockIdx.x == 0 && tid == 0) {
     a.maxlen[u] = 0;  // k_dx_lp's maxima (two launches later)
     if (u < a.nch) a.wflag[u] = 0;  // the chunks' Bwd* flags (k_dx_walks)
@@ -347,8 +348,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
           wd[q] = x < hi && word ? word[x] : 0u;
         }
       }
+      STAMP2(11);
 #pragma unroll
       for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab && !is_rule(wd[q]) ? a.r0dense[lb[q]] : NEMO_NONE;
+      STAMP2(12);
 #pragma unroll
       for (int q = 0; q < DXL_BATCH; q++) {
         if (dv[q] == NEMO_NONE) continue;
@@ -401,11 +404,13 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     }
   }
   if (!lds) return;
+  STAMP2(13);
   __syncthreads();
   for (uint32_t w = tid; w < a.w32; w += NEMO_BLOCK) {
     if (a.lab_split == 1) pb[w] = bm[w];
     else if (bm[w]) atomicOr(&pb[w], bm[w]);
   }
+  STAMP2(14);
 }
 
 // ---- Good words: chunk c's 64 bitmaps transposed, one wave per 64 positions ----------
@@ -733,7 +738,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     __syncthreads();
     for (uint32_t i = tid; i < V; i += NT) {  // LC, Bwd* to HBM; the ring is free after this
       const uint64_t b = rw[i];
-      bwv[i] = b;
+      __hip_atomic_store(bwv + i, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
       lcl[i] = rl[i] ? 0ull : b & ~lcl[i];
       rw[i] = 0;
     }
@@ -748,16 +753,13 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     }
     __syncthreads();
     uint64_t *olw = a.lw + (size_t)chunk * V;
-    for (uint32_t i = tid; i < V; i += NT) olw[V - 1u - i] = rw[i];
-    // publish Bwd* and the rules' words to the chunk's longest-path workgroups: every
-    // wave's stores reach L2, then one lane writes the XCD's L2 back and sets the flag
+    for (uint32_t i = tid; i < V; i += NT)
+      __hip_atomic_store(olw + (V - 1u - i), rw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // publish (write-through payload): every storing wave drains its stores, then one lane
+    // sets the flag with an agent-scope atomic store; the readers acquire
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(5);
     return;
   }
@@ -836,8 +838,6 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   // D by position: in LDS past the LP bytes when this workgroup writes its sources' masks
   const bool own = a.own_mask != 0u;
   uint8_t *const dl = lpb + ((V + 15u) & ~15u);
-  // lw: the chunk's rules' leaf-child words (the Bwd* workgroup, fused form)
-  const uint64_t *bw = a.bw + (size_t)chunk * V, *lw = a.lw + (size_t)chunk * V;
   // D of the sources over the Fwd* plane, for k_dx_mask
   uint8_t *dpl = a.fb + ((size_t)chunk * ((64u + NE - 1u) / NE) + grp) * V;
   uint32_t mx[NE];
@@ -846,6 +846,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   bool over = false;
   // DXF_K positions per thread and round, every round's loads in flight together: the rule
   // flag, the Bwd* word and the rule's leaf-child word (the chunk's Bwd* workgroup)
+  const uint64_t *bw = a.bw + (size_t)chunk * V, *lw = a.lw + (size_t)chunk * V;
   for (uint32_t base = 0; base < V; base += DXF_K * NT) {
     uint32_t inf[DXF_K];
     uint64_t b[DXF_K], o[DXF_K];
@@ -889,6 +890,24 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   __syncthreads();
   STAMP(5);
   if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = min(s_max[tid], (uint32_t)DX_VMAX);
+  // the rows: counted per thread, one block scan and one global atomic per workgroup, whose
+  // round trip the mask pass covers
+  __shared__ uint32_t s_scan[NT / 64], s_base;
+  auto hits = [&](uint32_t pos) -> uint32_t {
+    const uint32_t lp = lpb[pos];
+    uint32_t h = 0;
+    if (lp) {
+#pragma unroll
+      for (int e = 0; e < NE; e++)
+        if (((lp >> e) & 1u) && ring0[(size_t)e * rs + pos] == s_max[e]) h |= 1u << e;
+    }
+    return h;
+  };
+  uint32_t cnt = 0;
+  for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
+  uint32_t tot;
+  uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
+  if (tid == 0 && tot) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
   // one entry per source: the D masks by node, consecutive nodes per wave (coalesced bytes)
   if (own) {
     uint32_t ent[NE];
@@ -909,24 +928,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
       }
     }
   }
-  // the rows: counted per thread, one block scan and one global atomic per workgroup
-  __shared__ uint32_t s_scan[NT / 64], s_base;
-  auto hits = [&](uint32_t pos) -> uint32_t {
-    const uint32_t lp = lpb[pos];
-    uint32_t h = 0;
-    if (lp) {
-#pragma unroll
-      for (int e = 0; e < NE; e++)
-        if (((lp >> e) & 1u) && ring0[(size_t)e * rs + pos] == s_max[e]) h |= 1u << e;
-    }
-    return h;
-  };
-  uint32_t cnt = 0;
-  for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
-  uint32_t tot;
-  uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
   if (!tot) return;  // workgroup-uniform
-  if (tid == 0) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
   __syncthreads();
   q += s_base;
   for (uint32_t pos = tid; pos < V && cnt; pos += NT) {

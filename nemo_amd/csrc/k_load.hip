@@ -53,7 +53,7 @@ __device__ void sort_row(uint32_t *r, uint32_t n) {
 #endif
 #define BLD_OCC(B) ((B) == 256 ? 4 : 6)  // waves per SIMD the register budget is cut for
 #ifndef BLD_SQ
-#define BLD_SQ 4    // rows per thread and round of the row sort (even)
+#define BLD_SQ 2    // rows per thread and round of the row sort (even; 4: no faster at C3, 128 VGPRs)
 #endif
 #ifndef BLD_KB
 #define BLD_KB 4    // Kahn: children of a node processed per round

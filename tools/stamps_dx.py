@@ -45,3 +45,17 @@ for label, rows, names in (("bwd", st[:nch], ["stage", "walk", "finalize", "lc",
         print(f"  {nm:9s} median {np.median(d[:, i]):10.0f}  max {d[:, i].max():10.0f}")
     print(f"  end       median {np.median(rows[:, len(names)] - t0):10.0f}  max {(rows[:, len(names)] - t0).max()}")
 eng.close()
+# k_dx_label (slots 10-14 of its block index x + y * gridDim.x): start, loads issued+landed (tick at first
+# use is after the wait), dense lookups, marks, bitmap store
+eng = E.Engine(0)
+eng.load(corpus)
+eng.mark()
+eng.diffprov(f, DIFF_PER_RUN)
+eng.synchronize()
+st = eng.debug_copy("stamps", 0, 8 * 16 * nu).view(np.uint64).reshape(-1, 16).astype(np.int64)[:, 10:15]
+st = st[st[:, 0] > 0]
+d = np.diff(st, axis=1)
+print(f"label: {len(st)} workgroups")
+for i, nm in enumerate(["loads", "dense", "marks", "store"]):
+    print(f"  {nm:9s} median {np.median(d[:, i]):10.0f}  max {d[:, i].max():10.0f}")
+eng.close()
