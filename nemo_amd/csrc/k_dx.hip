@@ -320,7 +320,19 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
     else atomicOr(&pb[p >> 5], 1u << (p & 31u));
   };
   if (a.r0dense) {  // labels and node words together, one dense-table load per source goal
-    // (four consecutive nodes per thread and 16-byte load when the slice allows)
+    // (four consecutive nodes per thread and 16-byte load when the slice allows; vectorising a
+    // misaligned slice after a head of up to three nodes measured no faster)
+    auto mark_dense = [&](uint32_t lbv, uint32_t dvv) {
+      if (dvv == NEMO_NONE) return;
+      if ((dvv & 15u) == 0u) {  // one run-0 goal carries the label
+        mark(dvv >> 4);
+        return;
+      }
+      const uint32_t i0 = dvv >> 4, cnt = dvv & 15u;
+      for (uint32_t t = 0; t < cnt; t++) mark(a.p.r0pos[i0 + t]);
+      if (cnt == 15u)  // 15 or more entries: the rest of the run
+        for (uint32_t i = i0 + 15u; i < a.p.n_r0lab && a.r0lab[i] == lbv; i++) mark(a.p.r0pos[i]);
+    };
     const bool vec = ((((uintptr_t)(lab + lo)) | (word ? (uintptr_t)(word + lo) : 0u)) & 15u) == 0u;
     for (uint32_t base = lo; base < hi; base += DXL_BATCH * NEMO_BLOCK) {
       uint32_t lb[DXL_BATCH], wd[DXL_BATCH], dv[DXL_BATCH];
@@ -353,17 +365,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) 
       for (int q = 0; q < DXL_BATCH; q++) dv[q] = lb[q] < a.nlab && !is_rule(wd[q]) ? a.r0dense[lb[q]] : NEMO_NONE;
       STAMP2(12);
 #pragma unroll
-      for (int q = 0; q < DXL_BATCH; q++) {
-        if (dv[q] == NEMO_NONE) continue;
-        if ((dv[q] & 15u) == 0u) {  // one run-0 goal carries the label
-          mark(dv[q] >> 4);
-          continue;
-        }
-        const uint32_t i0 = dv[q] >> 4, cnt = dv[q] & 15u;
-        for (uint32_t t = 0; t < cnt; t++) mark(a.p.r0pos[i0 + t]);
-        if (cnt == 15u)  // 15 or more entries: the rest of the run
-          for (uint32_t i = i0 + 15u; i < a.p.n_r0lab && a.r0lab[i] == lb[q]; i++) mark(a.p.r0pos[i]);
-      }
+      for (int q = 0; q < DXL_BATCH; q++) mark_dense(lb[q], dv[q]);
     }
   }
   for (uint32_t base = lo; base < hi && !a.r0dense; base += DXL_BATCH * NEMO_BLOCK) {
@@ -827,6 +829,14 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
 #pragma unroll
   for (int e = 0; e < NE; e++) live |= (sh + e < 64u && 64u * chunk + sh + e < a.nu ? 1u : 0u) << e;
   if (tid < (uint32_t)NE) s_max[tid] = 0;
+  // the first round's static loads (rule flags, node positions) before the wait
+  uint32_t pinf[DXF_K], ptp[DXF_K];
+#pragma unroll
+  for (int k = 0; k < DXF_K; k++) {
+    const uint32_t p = min(k * NT + tid, V - 1u);
+    pinf[k] = a.p.info[p];
+    ptp[k] = a.own_mask ? a.p.tpos[p] : 0u;
+  }
   if (tid == 0) {  // one lane polls the chunk's flag, then one acquire for the workgroup
     while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
       __builtin_amdgcn_s_sleep(2);
@@ -853,7 +863,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
 #pragma unroll
     for (int k = 0; k < DXF_K; k++) {
       const uint32_t p = min(base + k * NT + tid, V - 1u);  // clamped, unconditional: all loads in flight
-      inf[k] = a.p.info[p];
+      inf[k] = base == 0 ? pinf[k] : a.p.info[p];
       b[k] = bw[V - 1u - p];
       o[k] = lw[p];
     }
@@ -916,7 +926,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
     for (uint32_t base = 0; base < V; base += DXF_K * NT) {
       uint32_t tp[DXF_K];  // every position loaded before the byte stores (which may alias)
 #pragma unroll
-      for (int k = 0; k < DXF_K; k++) tp[k] = a.p.tpos[min(base + k * NT + tid, V - 1u)];
+      for (int k = 0; k < DXF_K; k++) tp[k] = base == 0 ? ptp[k] : a.p.tpos[min(base + k * NT + tid, V - 1u)];
 #pragma unroll
       for (int k = 0; k < DXF_K; k++) {
         const uint32_t v = base + k * NT + tid;
