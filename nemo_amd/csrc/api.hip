@@ -170,6 +170,13 @@ struct nemo_ctx {
   // staged simplification results: pinned host copies made on `copy`
   hipStream_t copy = nullptr;
   hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
+  // the simplified pull on `aux` (option pull_aux 1; off by default: beside k_proto_lds it made
+  // the C3 step 8.3 -> 9.0 ms): it waits for the end of nemo_simplify (ev_simp) only, so it runs
+  // beside the protos and hand-over kernels of `stream`; anything that rewrites its inputs
+  // first waits for ev_auxpull
+  hipEvent_t ev_simp = nullptr, ev_auxpull = nullptr;
+  bool pull_aux_pending = false;
+  uint32_t pull_on_aux = 0;
   bool staged = false;
   uint64_t staged_n = 0, staged_cap = 0, chht_hint = 0;
   bool pairs_wide = false;    // some graph has >= 65536 nodes: u32 pairs
@@ -279,6 +286,10 @@ static hipEvent_t get_event(nemo_ctx *c) {
 // Kernels that rewrite node flags must not overtake a staged copy still in flight.
 static int guard_staged(nemo_ctx *c) {
   if (c->staged) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
+  if (c->pull_aux_pending) {  // a pull on `aux` still reads the graphs, flags and chains
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_auxpull, 0));
+    c->pull_aux_pending = false;
+  }
   return NEMO_OK;
 }
 
@@ -530,7 +541,7 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   for (void *h : {(void *)c->h_red, (void *)c->h_tab, (void *)c->h_nmiss, (void *)c->h_mrows, (void *)c->h_mask,
                   (void *)c->h_tpre, (void *)c->h_tpost, (void *)c->h_tasync})
     if (h) hipHostFree(h);
-  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc})
+  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc, c->ev_simp, c->ev_auxpull})
     if (e) hipEventDestroy(e);
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
@@ -582,6 +593,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "stage_sdma")) {
     c->stage_sdma = value > 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "pull_aux")) {  // 0: pulls on the context's stream, after everything queued before them
+    c->pull_on_aux = value != 0;
     return NEMO_OK;
   }
   if (!strcmp(name, "stage_cus")) {  // takes effect when the copy stream is created (first stage)
@@ -1217,6 +1232,8 @@ int nemo_simplify(nemo_ctx *c) {
   // reads: flags 1 + Kahn level 4 + node word 4 (+ ID rank 4) per node, the edge list 8 per edge
   rc = timed(c, "k_chains", (c->has_rank ? 13 : 9) * V + 8 * E, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
   if (rc) return rc;
+  if ((rc = ensure_event(c, &c->ev_simp))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev_simp, c->stream));  // a simplified pull on `aux` starts here
   c->simplified = true;
   c->protos_done = false;
   return NEMO_OK;
@@ -1955,6 +1972,14 @@ static int pull_launch(nemo_ctx *c) {
   a.cap = c->pull_cap;
   const uint32_t slots = c->pull_dslots;
   hipStream_t s = c->stream;
+  // the simplified pull reads what nemo_simplify left (graphs, flags, chains): on `aux`, behind
+  // the end of the simplification only, it overlaps the protos and hand-over kernels of `stream`
+  const bool on_aux = a.which == 1 && c->pull_on_aux && c->ev_simp;
+  if (on_aux) {
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_simp, 0));
+    s = c->aux;
+  }
   double V = (double)c->V, E = (double)c->E;
   if (a.which == 2) {
     V = (double)slots * (double)a.mask_stride;
@@ -1962,12 +1987,17 @@ static int pull_launch(nemo_ctx *c) {
   }
   nemo::launch_zero(c->d_pcur, sizeof(unsigned long long), s);
   // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
-  int rc = timed(c, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
+  int rc = timed_on(c, s, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
   if (rc) return rc;
   nemo::launch_to_host(c->h_poff, c->d_poff, slots * 8ull, s);
   nemo::launch_to_host(c->h_pcnt, c->d_pcnt, slots * 4ull, s);
   nemo::launch_to_host(c->h_pcur, c->d_pcur, sizeof(unsigned long long), s);
   HIPCHK(c, hipEventRecord(c->ev_pull, s));
+  if (on_aux) {
+    if ((rc = ensure_event(c, &c->ev_auxpull))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_auxpull, s));
+    c->pull_aux_pending = true;
+  }
   c->pull_synced = false;
   return NEMO_OK;
 }
