@@ -722,9 +722,17 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   if (MODE != 0 || !WHOLE) return;
   __syncthreads();
   if (a.fuse) {
+    // two hand-offs to the chunk's longest-path workgroups (write-through stores, a drain per
+    // storing wave, an agent-scope flag): Bwd* right after the walk (flag 1: they form D and
+    // the masks meanwhile), then the rules' leaf-child words (flag 2)
+    for (uint32_t i = tid; i < V; i += NT)
+      __hip_atomic_store(bwv + i, (uint64_t)ringp(0)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // leaf candidates LC(x) = B(x) & ~OR B(children) of goals, then per rule the OR of its
     // children's LC (the longest-path workgroups' LP test: a D rule with an LC child), all
-    // from LDS; the rules' words go to HBM (lw by position) with Bwd*
+    // from LDS; the rules' words go to HBM (lw by position)
     const uint64_t *rg = (const uint64_t *)ringp(0);
     // over the links of the whole-graph image (still in LDS: owner's slot << 16 | child's
     // slot, slots = reversed walk indices) with LDS atomics, then per index
@@ -738,9 +746,8 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
       }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < V; i += NT) {  // LC, Bwd* to HBM; the ring is free after this
+    for (uint32_t i = tid; i < V; i += NT) {  // LC; the ring is free after this
       const uint64_t b = rw[i];
-      __hip_atomic_store(bwv + i, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
       lcl[i] = rl[i] ? 0ull : b & ~lcl[i];
       rw[i] = 0;
     }
@@ -761,7 +768,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     // sets the flag with an agent-scope atomic store; the readers acquire
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(5);
     return;
   }
@@ -813,11 +820,12 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
 }
 
 // Whole-graph walks, fused: a longest-path workgroup holds its NE sources' values over
-// every position, so once its chunk's Bwd* workgroup has published Bwd* and the leaf
-// candidates it finds the sources' LP rules (D rules with a leaf-candidate child),
-// maxLen (an LDS maximum: no other workgroup holds these sources) and the missing rows
-// (LP rules with val == maxLen) itself, in place of k_dx_lp and k_dx_emit.  Its Fwd*
-// byte plane is overwritten with D (k_dx_mask reads D there).
+// every position.  Once its chunk's Bwd* workgroup has published Bwd* (flag 1) it forms D
+// and (one entry per source) writes the D masks; once the rules' leaf-child words follow
+// (flag 2) it finds the sources' LP rules (D rules with a leaf-candidate child), maxLen (an
+// LDS maximum: no other workgroup holds these sources) and the missing rows (LP rules with
+// val == maxLen), in place of k_dx_lp, k_dx_emit and k_dx_mask.  Without its own masks its
+// Fwd* byte plane is overwritten with D (k_dx_mask reads D there).
 template <int NE, int NT>
 __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a, uint32_t chunk, uint32_t grp,
                                             const uint32_t *ring0, uint32_t rs, uint8_t *lpb) {
@@ -837,36 +845,32 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
     pinf[k] = a.p.info[p];
     ptp[k] = a.own_mask ? a.p.tpos[p] : 0u;
   }
-  if (tid == 0) {  // one lane polls the chunk's flag, then one acquire for the workgroup
-    while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-      __builtin_amdgcn_s_sleep(2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  // one lane polls the chunk's flag until it reaches `want`, then one acquire for the workgroup
+  auto wait_flag = [&](uint32_t want) {
+    if (tid == 0) {
+      while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  };
+  wait_flag(1);  // Bwd*
   STAMP(4);
-  // D by position: in LDS past the LP bytes when this workgroup writes its sources' masks
+  // D by position, in LDS past the LP bytes (and over the Fwd* plane for k_dx_mask when the
+  // masks are not written here)
   const bool own = a.own_mask != 0u;
   uint8_t *const dl = lpb + ((V + 15u) & ~15u);
-  // D of the sources over the Fwd* plane, for k_dx_mask
   uint8_t *dpl = a.fb + ((size_t)chunk * ((64u + NE - 1u) / NE) + grp) * V;
   uint32_t mx[NE];
 #pragma unroll
   for (int e = 0; e < NE; e++) mx[e] = 0;
   bool over = false;
-  // DXF_K positions per thread and round, every round's loads in flight together: the rule
-  // flag, the Bwd* word and the rule's leaf-child word (the chunk's Bwd* workgroup)
   const uint64_t *bw = a.bw + (size_t)chunk * V, *lw = a.lw + (size_t)chunk * V;
-  for (uint32_t base = 0; base < V; base += DXF_K * NT) {
-    uint32_t inf[DXF_K];
-    uint64_t b[DXF_K], o[DXF_K];
+  for (uint32_t base = 0; base < V; base += DXF_K * NT) {  // DXF_K positions per thread, loads together
+    uint64_t b[DXF_K];
 #pragma unroll
-    for (int k = 0; k < DXF_K; k++) {
-      const uint32_t p = min(base + k * NT + tid, V - 1u);  // clamped, unconditional: all loads in flight
-      inf[k] = base == 0 ? pinf[k] : a.p.info[p];
-      b[k] = bw[V - 1u - p];
-      o[k] = lw[p];
-    }
+    for (int k = 0; k < DXF_K; k++) b[k] = bw[V - 1u - min(base + k * NT + tid, V - 1u)];
 #pragma unroll
     for (int k = 0; k < DXF_K; k++) {
       const uint32_t pos = base + k * NT + tid;
@@ -879,46 +883,14 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
         f |= (v ? 1u : 0u) << e;
       }
       const uint32_t d = f & live & (uint32_t)(b[k] >> sh) & NM;
-      if (own) dl[pos] = (uint8_t)d;
-      else dpl[pos] = (uint8_t)d;
-      const uint32_t lp = (inf[k] & DXI_RULE) ? d & (uint32_t)(o[k] >> sh) & NM : 0u;
-#pragma unroll
-      for (int e = 0; e < NE; e++)
-        if ((lp >> e) & 1u) mx[e] = max(mx[e], ring0[(size_t)e * rs + pos]);
-      lpb[pos] = (uint8_t)lp;
+      dl[pos] = (uint8_t)d;
+      if (!own) dpl[pos] = (uint8_t)d;
     }
-  }
-  // maxima: the wave's, then one LDS atomic per wave and source
-#pragma unroll
-  for (int e = 0; e < NE; e++) {
-    uint32_t x = mx[e];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-    if (lane_id() == 0 && x) atomicMax(&s_max[e], x);
   }
   if (__any(over) && lane_id() == 0) atomicOr(a.n_missing, 0x80000000u);
   __syncthreads();
-  STAMP(5);
-  if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = min(s_max[tid], (uint32_t)DX_VMAX);
-  // the rows: counted per thread, one block scan and one global atomic per workgroup, whose
-  // round trip the mask pass covers
-  __shared__ uint32_t s_scan[NT / 64], s_base;
-  auto hits = [&](uint32_t pos) -> uint32_t {
-    const uint32_t lp = lpb[pos];
-    uint32_t h = 0;
-    if (lp) {
-#pragma unroll
-      for (int e = 0; e < NE; e++)
-        if (((lp >> e) & 1u) && ring0[(size_t)e * rs + pos] == s_max[e]) h |= 1u << e;
-    }
-    return h;
-  };
-  uint32_t cnt = 0;
-  for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
-  uint32_t tot;
-  uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
-  if (tid == 0 && tot) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
-  // one entry per source: the D masks by node, consecutive nodes per wave (coalesced bytes)
+  // one entry per source: the D masks by node, consecutive nodes per wave (coalesced bytes),
+  // while the Bwd* workgroup computes the leaf candidates
   if (own) {
     uint32_t ent[NE];
 #pragma unroll
@@ -938,6 +910,56 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
       }
     }
   }
+  wait_flag(2);  // the rules' leaf-child words
+  // LP = D rules with a leaf-candidate child; their longest val per source
+  for (uint32_t base = 0; base < V; base += DXF_K * NT) {
+    uint32_t inf[DXF_K];
+    uint64_t o[DXF_K];
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {
+      const uint32_t p = min(base + k * NT + tid, V - 1u);  // clamped, unconditional: all loads in flight
+      inf[k] = base == 0 ? pinf[k] : a.p.info[p];
+      o[k] = lw[p];
+    }
+#pragma unroll
+    for (int k = 0; k < DXF_K; k++) {
+      const uint32_t pos = base + k * NT + tid;
+      if (pos >= V) continue;
+      const uint32_t lp = (inf[k] & DXI_RULE) ? dl[pos] & (uint32_t)(o[k] >> sh) & NM : 0u;
+#pragma unroll
+      for (int e = 0; e < NE; e++)
+        if ((lp >> e) & 1u) mx[e] = max(mx[e], ring0[(size_t)e * rs + pos]);
+      lpb[pos] = (uint8_t)lp;
+    }
+  }
+  // maxima: the wave's, then one LDS atomic per wave and source
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    uint32_t x = mx[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    if (lane_id() == 0 && x) atomicMax(&s_max[e], x);
+  }
+  __syncthreads();
+  STAMP(5);
+  if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = min(s_max[tid], (uint32_t)DX_VMAX);
+  // the rows: counted per thread, one block scan and one global atomic per workgroup
+  __shared__ uint32_t s_scan[NT / 64], s_base;
+  auto hits = [&](uint32_t pos) -> uint32_t {
+    const uint32_t lp = lpb[pos];
+    uint32_t h = 0;
+    if (lp) {
+#pragma unroll
+      for (int e = 0; e < NE; e++)
+        if (((lp >> e) & 1u) && ring0[(size_t)e * rs + pos] == s_max[e]) h |= 1u << e;
+    }
+    return h;
+  };
+  uint32_t cnt = 0;
+  for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
+  uint32_t tot;
+  uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
+  if (tid == 0 && tot) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
   if (!tot) return;  // workgroup-uniform
   __syncthreads();
   q += s_base;
