@@ -977,8 +977,12 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
 
 void launch_build(const DevCorpus &c, hipStream_t s) {
   if (!c.bld_bytes) return;
-  hipFuncSetAttribute((const void *)k_build<BLD_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.bld_bytes);
-  hipLaunchKernelGGL(k_build<BLD_BLOCK>, dim3(c.G), dim3(BLD_BLOCK), c.bld_bytes, s, c);
+#ifndef BLD_PAD
+#define BLD_PAD 0  // diagnostic: extra LDS per workgroup (fewer workgroups per CU)
+#endif
+  hipFuncSetAttribute((const void *)k_build<BLD_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)(c.bld_bytes + BLD_PAD));
+  hipLaunchKernelGGL(k_build<BLD_BLOCK>, dim3(c.G), dim3(BLD_BLOCK), c.bld_bytes + BLD_PAD, s, c);
 }
 void launch_load(const DevCorpus &c, hipStream_t s) {
   if (!c.G) return;
