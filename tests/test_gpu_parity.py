@@ -538,3 +538,16 @@ def test_node_context(devices):
                 e.set_stream(0)
     finally:
         e.close()
+
+
+def test_pull_on_aux_stream(eng):
+    """Option pull_aux 1: the simplified pull runs on the diff stream behind the end of the simplification
+    (beside the protos); the pulled edges, the protos and every other output still equal the oracle's."""
+    from tools import synth
+    corpus, _ = synth.generate(40, p_fault=0.5, prepend_run0=True, **synth.CONFIGS["c3"])
+    eng.set_option("pull_aux", 1)
+    try:
+        _check(eng, corpus)
+        _check(eng, corpus, mode=DIFF_PER_RUN)  # twice on one context: the second load joins the first pull
+    finally:
+        eng.set_option("pull_aux", 0)
