@@ -175,6 +175,11 @@ struct nemo_ctx {
   // beside the protos and hand-over kernels of `stream`; anything that rewrites its inputs
   // first waits for ev_auxpull
   hipEvent_t ev_simp = nullptr, ev_auxpull = nullptr;
+  // the hand-over kernels of nemo_stage_simplified on `aux` (option stage_aux, default on):
+  // behind everything `stream` has queued so far, beside the triggers and pulls queued after
+  hipEvent_t ev_stage = nullptr;
+  uint32_t stage_on_aux = 1;
+  hipStream_t stage_stream = nullptr;
   bool pull_aux_pending = false;
   uint32_t pull_on_aux = 0;
   bool staged = false;
@@ -541,7 +546,7 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   for (void *h : {(void *)c->h_red, (void *)c->h_tab, (void *)c->h_nmiss, (void *)c->h_mrows, (void *)c->h_mask,
                   (void *)c->h_tpre, (void *)c->h_tpost, (void *)c->h_tasync})
     if (h) hipHostFree(h);
-  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc, c->ev_simp, c->ev_auxpull})
+  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc, c->ev_simp, c->ev_auxpull, c->ev_stage})
     if (e) hipEventDestroy(e);
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
@@ -593,6 +598,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "stage_sdma")) {
     c->stage_sdma = value > 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "stage_aux")) {  // 0: the hand-over kernels on the context's stream
+    c->stage_on_aux = value != 0;
     return NEMO_OK;
   }
   if (!strcmp(name, "pull_aux")) {  // 0: pulls on the context's stream, after everything queued before them
@@ -1854,7 +1863,7 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
 // (node flags, pairs) on the copy stream.
 static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
   int rc;
-  hipStream_t s = c->stream;
+  hipStream_t s = c->stage_stream ? c->stage_stream : c->stream;
   const uint64_t pw = c->pairs_wide ? 2 : 1;  // u32 words per pair
   if (pw * cap > c->d_chht_cap) {
     HIPCHK(c, hipStreamSynchronize(s));
@@ -1866,11 +1875,11 @@ static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
   }
   const uint64_t sbytes = 4 * ((c->V + 15) / 16);  // 2-bit node state
   if (!c->d_state && (rc = dalloc(c, &c->d_state, sbytes / 4 + 1))) return rc;
-  rc = timed(c, "k_chain_pairs", 4.0 * pw * (double)cap + 20.0 * c->G, 0,
-             [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, c->pairs_wide ? 1 : 0, s); });
+  rc = timed_on(c, s, "k_chain_pairs", 4.0 * pw * (double)cap + 20.0 * c->G, 0,
+                [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, c->pairs_wide ? 1 : 0, s); });
   if (rc) return rc;
-  rc = timed(c, "k_pack_state", (double)c->V + (double)sbytes, 0,
-             [&] { nemo::launch_pack_state(c->dc.flags, c->d_state, c->V, s); });
+  rc = timed_on(c, s, "k_pack_state", (double)c->V + (double)sbytes, 0,
+                [&] { nemo::launch_pack_state(c->dc.flags, c->d_state, c->V, s); });
   if (rc) return rc;
   if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, sbytes + 16))) return rc;
   if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, pw * cap + 2))) return rc;
@@ -1925,7 +1934,15 @@ int nemo_stage_simplified(nemo_ctx *c) {
   c->staged = false;
   if (!c->d_choff && (rc = dalloc(c, &c->d_choff, (size_t)c->G + 1))) return rc;
   if ((rc = hgrow(c, &c->h_choff, &c->h_choff_cap, (uint64_t)c->G + 1))) return rc;
-  rc = timed(c, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
+  if (c->stage_on_aux) {  // read-only on the analysis: `stream` goes on to the triggers and pulls
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    if ((rc = ensure_event(c, &c->ev_stage))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_stage, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_stage, 0));
+    s = c->aux;
+  }
+  c->stage_stream = s;
+  rc = timed_on(c, s, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
   if (rc) return rc;
   // the pair count is only known on the device: stage at the last count seen
   // (no host round trip); nemo_simplified_view re-stages if it was too small
