@@ -287,7 +287,9 @@ void launch_dx_img(const DxPrep &p, DxImg img[2], const DxImgScratch &t, hipStre
 // are gathered in LDS and stored whole (one workgroup per source) or ORed in
 // by word; larger ones take global atomics.
 #define DXL_LDS 4096u
+#ifndef DXL_BATCH
 #define DXL_BATCH 24  // source nodes per thread and round (all their loads in flight together)
+#endif
 __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_label(DevCorpus c, DxArgs a) {
   __shared__ uint32_t bm[DXL_LDS];
   const uint32_t u = blockIdx.y, tid = threadIdx.x;
