@@ -1244,6 +1244,11 @@ extern "C" int nemo_ingest_molly(const char *out_dir, const uint32_t *iterations
     return NEMO_ERR_LOAD;
   };
   if (!out_dir || !out || (n_runs && !iterations)) return NEMO_ERR_INVALID;
+  // the calling thread parses too: its per-thread maps (up to ~4V + 4096 words per kind)
+  // are released on the way out, as the helper threads' are when they exit
+  struct ReleaseMaps {
+    ~ReleaseMaps() { t_maps = ParseMaps(); }
+  } release_maps;
   auto *h = new nemo_ingest();
   h->iteration.assign(iterations, iterations + n_runs);
   const uint32_t G = 2 * n_runs;
