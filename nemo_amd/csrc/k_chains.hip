@@ -1212,8 +1212,19 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_chains_sel(DevCorpus c) {
   wave_append(need, g, sel + 1, sel);
 }
 
+// The first tier's H* cap: at 1280 its LDS image is 31.7 KB, so five workgroups share a CU
+// (with the register budget cut to five waves per SIMD: 96 VGPRs, 52 B of spills); the chain
+// cover's level loops are latency-bound, and at C3 this took k_chains 2.01 -> 1.72 ms against
+// 1664 (41 KB, four per CU).  Larger H* go to k_chains_list (2048) as before.
+#ifndef CH_HCAP
+#define CH_HCAP 1280
+#endif
+#ifndef CH_WPE
+#define CH_WPE 5
+#endif
+#define CH_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CH_WPE)))
 template <int HCAP, int UCAP>
-__global__ __launch_bounds__(NEMO_BLOCK) void k_chains(DevCorpus c) {
+__global__ __launch_bounds__(NEMO_BLOCK) CH_WPE_ATTR void k_chains(DevCorpus c) {
   chains_graph<HCAP, UCAP>(c, blockIdx.x);
 }
 
@@ -1232,7 +1243,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 #define CHAINS_GRID 1024u
 void launch_chains(const DevCorpus &c, hipStream_t s) {
   if (!c.G) return;
-  hipLaunchKernelGGL((k_chains<1664, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  hipLaunchKernelGGL((k_chains<CH_HCAP, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
   launch_zero(c.sel + c.G + 1, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_chains_sel, dim3((c.G + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
   hipLaunchKernelGGL((k_chains_list<2048, 512>), dim3(std::min(c.G, CHAINS_GRID)), dim3(NEMO_BLOCK), 0, s, c);
