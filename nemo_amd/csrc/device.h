@@ -260,13 +260,14 @@ __host__ __device__ __forceinline__ uint32_t hash_label(uint32_t x) {
   x *= 0x9E3779B1u;
   return x ^ (x >> 15);
 }
-// k_proto_lds's chains (head, tail) held in LDS: graphs with more run the global tier
-__host__ __device__ __forceinline__ uint32_t proto_chain_cap(uint32_t v) { return v / 8u + 16u; }
-// k_proto_lds's image: chain (head, tail) pairs, table bitsets, u16 node bytes,
-// per-level edge offsets, the forward edges in source Kahn order (u32 pairs)
+// k_proto_lds's chains (head, tail) held in registers, PROTO_CHQ per thread of its
+// PROTO_BLOCK: graphs with more run the global tier
+#define PROTO_CHQ 4
+__host__ __device__ __forceinline__ uint32_t proto_chain_cap(uint32_t) { return PROTO_CHQ * 512u; }
+// k_proto_lds's image: table bitsets, u16 node bytes, per-level edge offsets, the
+// forward edges in source Kahn order (u32 pairs): 39 KB at C3, four workgroups per CU
 __host__ __device__ __forceinline__ uint32_t lds_tier_bytes(uint32_t v, uint32_t e, uint32_t l, uint32_t words) {
-  return 2u * lds_align(2u * proto_chain_cap(v)) + lds_align(8u * words) + lds_align(2u * (v + 1u)) +
-         lds_align(2u * (l + 1u)) + lds_align(4u * e);
+  return lds_align(8u * words) + lds_align(2u * (v + 1u)) + lds_align(2u * (l + 1u)) + lds_align(4u * e);
 }
 
 __device__ __forceinline__ bool lds_fits(const DevCorpus &c, uint32_t V, uint32_t E, uint32_t nlev) {
@@ -287,7 +288,6 @@ __host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t
 }
 
 struct ProtoLds {
-  uint16_t *chd, *ctl;  // chain head, chain tail (bit 15: reach pushed)
   uint32_t *words;      // 2 * c.words u32 of table bitsets
   uint16_t *ab;         // per node: flags byte | PB_* byte << 8 (u32-packed pairs for atomics)
   uint16_t *elo;        // per Kahn level: first edge of e2[] whose source is on it
@@ -297,12 +297,9 @@ struct ProtoLds {
 // Carve k_proto_lds's dynamic LDS for a graph of V nodes / E edges / L levels.
 __device__ __forceinline__ ProtoLds proto_carve(void *base, uint32_t V, uint32_t E, uint32_t L, uint32_t words,
                                                 uint32_t chain_cap) {
+  (void)chain_cap;
   uint8_t *p = (uint8_t *)base;
   ProtoLds g;
-  g.chd = (uint16_t *)p;
-  p += lds_align(2u * chain_cap);
-  g.ctl = (uint16_t *)p;
-  p += lds_align(2u * chain_cap);
   g.words = (uint32_t *)p;
   p += lds_align(8u * words);
   g.ab = (uint16_t *)p;

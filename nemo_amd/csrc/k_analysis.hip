@@ -637,9 +637,13 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
     stage_lds<1, PROTO_BLOCK>(d);
   }
   for (uint32_t l = tid; l <= L; l += PROTO_BLOCK) P.elo[l] = l < L ? (uint16_t)c.posoff[gv.n0 + gv.lvl[l]] : (uint16_t)E;
-  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-    P.chd[k] = (uint16_t)c.chain[5 * (gv.n0 + k)];
-    P.ctl[k] = (uint16_t)c.chain[5 * (gv.n0 + k) + 1];
+  // chain k = tid + q PROTO_BLOCK in registers: head | tail << 16 (bit 31: PCH_DONE << 16)
+  static_assert(PROTO_BLOCK == 512, "proto_chain_cap assumes 512 threads");
+  uint32_t chp[PROTO_CHQ];
+#pragma unroll
+  for (int q = 0; q < PROTO_CHQ; q++) {
+    const uint32_t k = tid + q * PROTO_BLOCK;
+    chp[q] = k < nch ? (c.chain[5 * (gv.n0 + k)] & 0xFFFFu) | (c.chain[5 * (gv.n0 + k) + 1] << 16) : 0u;
   }
   // node bytes; missingFrom's table set (prototype.go:143-147): the tables of the REG / HEAD rules
   for (uint32_t v = tid; v < V; v += PROTO_BLOCK) {
@@ -680,8 +684,9 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
     if (!XRULE(as) && !XDEL(as) && !(XSB(as) & PB_NR) && XRULEISH(ad)) SET(d, PB_R1);
   })
   __syncthreads();
-  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK)
-    if (XSB(ab[P.chd[k]]) & PB_R1) SET(P.ctl[k], PB_R1T);
+#pragma unroll
+  for (int q = 0; q < PROTO_CHQ; q++)
+    if (tid + q * PROTO_BLOCK < nch && (XSB(ab[chp[q] & 0xFFFFu]) & PB_R1)) SET(chp[q] >> 16, PB_R1T);
   __syncthreads();
   STAMP(3);
   // G2 below R1 REG rules and below the tails of chains with an R1 head; the
@@ -701,9 +706,11 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
       atomicOr(&s_s[t >> 5], 1u << (t & 31));
     }
   }
-  for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-    const uint32_t h = P.chd[k];
-    if ((XSB(ab[h]) & PB_R1) && (XSB(ab[P.ctl[k]]) & PB_ADDT)) {
+#pragma unroll
+  for (int q = 0; q < PROTO_CHQ; q++) {
+    if (tid + q * PROTO_BLOCK >= nch) continue;
+    const uint32_t h = chp[q] & 0xFFFFu;
+    if ((XSB(ab[h]) & PB_R1) && (XSB(ab[chp[q] >> 16]) & PB_ADDT)) {
       const uint32_t t = table_of(gv.word[h]);
       atomicOr(&s_s[t >> 5], 1u << (t & 31));
     }
@@ -717,10 +724,11 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
       const bool act = XRULE(as) ? ((XREG(as) && (sb & PB_RCH)) || (sb & PB_RCHT)) : (!XDEL(as) && (sb & (PB_G2 | PB_RCH)));
       if (act && (XRULE(as) ? !XDEL(ad) : XRULEISH(ad))) SET(d, PB_RCH);
     })
-    for (uint32_t k = tid; k < nch; k += PROTO_BLOCK) {
-      const uint32_t t = P.ctl[k];
-      if ((t & PCH_DONE) || !(XSB(ab[P.chd[k]]) & PB_RCH)) continue;
-      P.ctl[k] = (uint16_t)(t | PCH_DONE);
+#pragma unroll
+    for (int q = 0; q < PROTO_CHQ; q++) {
+      const uint32_t t = chp[q] >> 16;
+      if (tid + q * PROTO_BLOCK >= nch || (t & PCH_DONE) || !(XSB(ab[chp[q] & 0xFFFFu]) & PB_RCH)) continue;
+      chp[q] |= PCH_DONE << 16;
       SET(t, PB_RCHT);
     }
     __syncthreads();
