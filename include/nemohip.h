@@ -160,7 +160,15 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *   "stage_sdma"        request nemo_stage_simplified's runtime copies as NoCU
  *                       (SDMA) copies (1) or plain D2H copies (0, default)
  *   "stage_cus"         CUs the copy stream's blit kernels may use (default 8,
- *                       0 = all); set before the first nemo_stage_simplified */
+ *                       0 = all); set before the first nemo_stage_simplified
+ *   "stage_aux"         nemo_stage_simplified's hand-over kernels on the diff
+ *                       stream behind the analysis queued so far (1, default)
+ *                       or on the context's stream (0)
+ *   "pull_aux"          the simplified pull on the diff stream behind the end of
+ *                       nemo_simplify (1) or on the context's stream (0, default)
+ *   "diff_fuse"         whole-graph diff walks finish LP rules, missing rows and
+ *                       one-entry masks themselves (1, default) or hand them to
+ *                       separate kernels (0; test knob) */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);
