@@ -724,8 +724,8 @@ static void set_lds_tier(nemo_ctx *c) {
   c->dc.t_diff = fit_tier(c, 16384, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t e, uint32_t l, uint32_t) {
     return diff_lds_bytes(v, e, l);
   });
-  // k_pull_lds: forward u16 CSR + per-node counts + flags
-  c->dc.t_pull = fit_tier(c, 16384, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t e, uint32_t, uint32_t) {
+  // k_pull_lds: forward u16 CSR + liveness bitmap (per-node counts in registers: 24 nodes per thread)
+  c->dc.t_pull = fit_tier(c, 24u * 256u, 65535, NO_LEVEL_CAP, [](uint32_t v, uint32_t e, uint32_t, uint32_t) {
     return pull_lds_bytes(v, e);
   });
   c->tierV = c->tierE = 0;  // k_marksimp's graphs (the deferred markConditionHolds)

@@ -284,7 +284,7 @@ __host__ __device__ __forceinline__ uint32_t diff_lds_bytes(uint32_t v, uint32_t
   return 2u * lds_align(2u * (v + 1u)) + 2u * lds_align(2u * e) + lds_align(4u * ((v + 31u) / 32u)) + lds_align(v);
 }
 __host__ __device__ __forceinline__ uint32_t pull_lds_bytes(uint32_t v, uint32_t e) {
-  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(2u * v) + lds_align(v);
+  return lds_align(2u * (v + 1u)) + lds_align(2u * e) + lds_align(8u * ((v + 63u) / 64u));
 }
 
 struct ProtoLds {

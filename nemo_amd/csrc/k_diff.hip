@@ -888,13 +888,16 @@ __global__ __launch_bounds__(B) void k_pull(DevCorpus c, PullArgs a) {
 
 // k_pull over the LDS graph tier (raw / simplified graphs, and the diff
 // entries over run 0's graph, D mask in place of the flags): the forward rows
-// and the flags staged in LDS (the reverse rows are read from HBM for the
-// chain heads only), per-node output offsets from one block scan, the same
-// order as k_pull.  The image is ~5V + 2E bytes, so four workgroups share a CU.
+// and a liveness bitmap staged in LDS (the reverse rows are read from HBM for
+// the chain heads only).  Thread t owns nodes k * PULL_BLOCK + t: their edge
+// counts, then their in-wave output offsets, stay in registers (u16 pairs),
+// and one wave scans the per-(k, wave) totals, so the output order is k_pull's.
+// The image is ~2V + 2E bytes (26 KB at C3): six workgroups share a CU.
 #define PULL_BLOCK 256
+#define PULL_K 24  // nodes per thread: the tier's node cap is PULL_K * PULL_BLOCK
 struct PullLds {
-  uint16_t *fp, *fc, *cnt;
-  uint8_t *fl;
+  uint16_t *fp, *fc;
+  uint32_t *bits;  // node v alive = bit v (which 1: KEPT and not DELETED; which 2: D mask)
 };
 __device__ __forceinline__ PullLds pull_carve(void *base, uint32_t V, uint32_t E) {
   uint8_t *p = (uint8_t *)base;
@@ -903,41 +906,61 @@ __device__ __forceinline__ PullLds pull_carve(void *base, uint32_t V, uint32_t E
   p += lds_align(2u * (V + 1u));
   L.fc = (uint16_t *)p;
   p += lds_align(2u * E);
-  L.cnt = (uint16_t *)p;
-  p += lds_align(2u * V);
-  L.fl = p;
+  L.bits = (uint32_t *)p;
   return L;
 }
 
 __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a) {
+  constexpr uint32_t NW = PULL_BLOCK / 64;
+  static_assert(PULL_K * NW <= 128 && PULL_K % 2 == 0, "one wave scans the (k, wave) totals, two per lane");
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_lds[PULL_BLOCK / 64];
-  __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_lds[NW];
+  __shared__ uint32_t s_pre[PULL_K * NW];
+  __shared__ uint32_t s_cnt, s_nn;
   __shared__ unsigned long long s_base;
-  const uint32_t which = a.which, slot = blockIdx.x, tid = threadIdx.x;
+  const uint32_t which = a.which, slot = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t g = which == 2 ? a.g0 : slot;
   if (c.err[g]) return;  // k_pull writes the empty slot
   const GraphView gv = c.view(g);
   if (!tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V;
   PullLds L = pull_carve(dyn, V, gv.E);
-  {
-    // diff pulls stage the entry's D mask where the others stage the flags
+  if (which != 0 && V) {
+    // diff pulls read the entry's D mask where the others read the flags
     const uint8_t *fsrc = which == 2 ? a.mask + (size_t)(a.mask_row ? a.mask_row[slot] : slot) * a.mask_stride : gv.flags;
-    const StageDesc d[3] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}, {fsrc, L.fl, V, ST_U8}};
-    stage_lds<3, PULL_BLOCK>(d);
+    uint32_t f[PULL_K];
+#pragma unroll
+    for (int k = 0; k < PULL_K; k++) f[k] = fsrc[min(k * PULL_BLOCK + tid, V - 1u)];  // unconditional: one wait
+#pragma unroll
+    for (int k = 0; k < PULL_K; k++) {
+      if (k * PULL_BLOCK >= V) break;
+      const bool al = which == 1 ? (f[k] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT : f[k] != 0u;
+      const uint64_t m = __ballot(al && k * PULL_BLOCK + tid < V);
+      const uint32_t n0 = k * PULL_BLOCK + 64u * w;
+      if (lane == 0 && n0 < V) *reinterpret_cast<uint64_t *>(L.bits + (n0 >> 5)) = m;
+    }
+  }
+  {
+    const StageDesc d[2] = {{gv.fp, L.fp, V + 1, ST_U16}, {gv.fc, L.fc, gv.E, ST_U16}};
+    stage_lds<2, PULL_BLOCK>(d);
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  const uint8_t *fl = L.fl;
-#define ALIVE(v) \
-  (which == 0 || (which == 1 ? (fl[v] & (NEMO_F_KEPT | NEMO_F_DELETED)) == NEMO_F_KEPT : fl[v] != 0))
-  uint16_t *cnt = L.cnt;  // per-node edge counts -> output offsets
-  for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
+  const uint32_t *bits = L.bits;
+#define ALIVE(v) (which == 0 || ((bits[(v) >> 5] >> ((v) & 31u)) & 1u))
+  uint32_t cp[PULL_K / 2];  // per node k: in-wave output offset (u16 halves)
+#pragma unroll
+  for (int k = 0; k < PULL_K; k++) {
+    if (k * PULL_BLOCK >= V) break;
+    const uint32_t u = k * PULL_BLOCK + tid;
     uint32_t n = 0;
-    if (ALIVE(u))
+    if (u < V && ALIVE(u))
       for (uint32_t j = L.fp[u]; j < L.fp[u + 1]; j++) n += ALIVE(L.fc[j]);
-    cnt[u] = (uint16_t)n;
+    uint32_t tot;
+    const uint32_t ex = wave_exscan(n, &tot);
+    if (lane == 0) s_pre[k * NW + w] = tot;
+    if (k & 1) cp[k >> 1] |= ex << 16;
+    else cp[k >> 1] = ex;
   }
   const uint32_t *ch = c.chain + 5 * gv.n0;
   const uint32_t nch = which == 1 ? c.nch[g] : 0u;
@@ -948,22 +971,35 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
     for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) nc += ALIVE(L.fc[j]);
   }
   for (int d = 32; d >= 1; d >>= 1) nc += __shfl_xor(nc, d);
-  if (lane_id() == 0 && nc) atomicAdd(&s_cnt, nc);
+  if (lane == 0 && nc) atomicAdd(&s_cnt, nc);
   __syncthreads();
-  const uint32_t nn = block_scan_inplace<PULL_BLOCK>(cnt, V, s_lds);
-  if (tid == 0) {
-    const uint32_t tot = nn + s_cnt;
-    const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)tot);
-    s_base = base;
-    a.off[slot] = base;
-    a.cnt[slot] = tot;
+  if (w == 0) {
+    // (k, wave) totals in node order -> exclusive offsets; then the graph's region
+    const uint32_t nk = ((V + PULL_BLOCK - 1) / PULL_BLOCK) * NW, i0 = 2u * lane;
+    const uint32_t x0 = i0 < nk ? s_pre[i0] : 0u, x1 = i0 + 1u < nk ? s_pre[i0 + 1u] : 0u;
+    uint32_t nn;
+    const uint32_t ex = wave_exscan(x0 + x1, &nn);
+    if (i0 < nk) s_pre[i0] = ex;
+    if (i0 + 1u < nk) s_pre[i0 + 1u] = ex + x0;
+    if (lane == 0) {
+      const uint32_t tot = nn + s_cnt;
+      const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)tot);
+      s_base = base;
+      s_nn = nn;
+      a.off[slot] = base;
+      a.cnt[slot] = tot;
+    }
   }
   __syncthreads();
   const uint64_t base = s_base;
+  const uint32_t nn = s_nn;
   if (base + nn + s_cnt > a.cap) return;
-  for (uint32_t u = tid; u < V; u += PULL_BLOCK) {
-    if (!ALIVE(u)) continue;
-    uint64_t o = base + cnt[u];
+#pragma unroll
+  for (int k = 0; k < PULL_K; k++) {
+    if (k * PULL_BLOCK >= V) break;
+    const uint32_t u = k * PULL_BLOCK + tid;
+    if (u >= V || !ALIVE(u)) continue;
+    uint64_t o = base + s_pre[k * NW + w] + ((cp[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
     for (uint32_t j = L.fp[u]; j < L.fp[u + 1]; j++) {
       const uint32_t v = L.fc[j];
       if (!ALIVE(v)) continue;
