@@ -1041,6 +1041,52 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
 #undef ALIVE
 }
 
+// Raw pulls (which 0) over the LDS graph tier: every edge survives, so a graph's
+// region is its forward CSR verbatim (CSR edge j -> base + j): no staging, no
+// counts, no LDS, so the CU holds as many workgroups as registers allow.
+#define PULLR_BATCH 8
+__global__ __launch_bounds__(PULL_BLOCK) void k_pull_raw(DevCorpus c, PullArgs a) {
+  __shared__ unsigned long long s_base;
+  const uint32_t g = blockIdx.x, tid = threadIdx.x;
+  if (c.err[g]) return;  // k_pull writes the empty slot
+  const GraphView gv = c.view(g);
+  if (!tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;
+  const uint32_t V = gv.V, E = gv.E;
+  if (tid == 0) {
+    const unsigned long long base = atomicAdd(a.cursor, (unsigned long long)E);
+    s_base = base;
+    a.off[g] = base;
+    a.cnt[g] = E;
+  }
+  __syncthreads();
+  const uint64_t base = s_base;
+  if (base + E > a.cap) return;
+  uint32_t *src = a.src + base, *dst = a.dst + base;
+  for (uint32_t j0 = 0; j0 < E; j0 += PULLR_BATCH * PULL_BLOCK) {
+    uint32_t y[PULLR_BATCH];
+#pragma unroll
+    for (int q = 0; q < PULLR_BATCH; q++) y[q] = gv.fc[min(j0 + q * PULL_BLOCK + tid, E - 1u)];
+#pragma unroll
+    for (int q = 0; q < PULLR_BATCH; q++)
+      if (j0 + q * PULL_BLOCK + tid < E) dst[j0 + q * PULL_BLOCK + tid] = y[q];
+  }
+  for (uint32_t u0 = 0; u0 < V; u0 += PULLR_BATCH * PULL_BLOCK) {
+    uint32_t lo[PULLR_BATCH], hi[PULLR_BATCH];
+#pragma unroll
+    for (int q = 0; q < PULLR_BATCH; q++) {
+      const uint32_t u = min(u0 + q * PULL_BLOCK + tid, V - 1u);
+      lo[q] = gv.fp[u];
+      hi[q] = gv.fp[u + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < PULLR_BATCH; q++) {
+      const uint32_t u = u0 + q * PULL_BLOCK + tid;
+      if (u < V)
+        for (uint32_t j = lo[q]; j < hi[q]; j++) src[j] = u;
+    }
+  }
+}
+
 // ---- small-result hand-over -------------------------------------------------------
 // Copies device results straight into pinned host memory with a kernel: the
 // stores cross PCIe from the CUs, so these small copies never queue behind
@@ -1261,7 +1307,9 @@ void launch_diff_expand(uint8_t *mask, const uint8_t *umask, const uint32_t *map
   hipLaunchKernelGGL(k_diff_expand, dim3(gx, n_entries), dim3(NEMO_BLOCK), 0, s, mask, umask, map, V0);
 }
 void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
-  if (c.t_pull.bytes && slots) {
+  if (c.t_pull.bytes && slots && a.which == 0) {
+    hipLaunchKernelGGL(k_pull_raw, dim3(slots), dim3(PULL_BLOCK), 0, s, c, a);
+  } else if (c.t_pull.bytes && slots) {
     const uint32_t bytes = c.t_pull.bytes;
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
