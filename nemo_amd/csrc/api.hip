@@ -63,6 +63,7 @@ struct nemo_ctx {
   uint32_t glob_block_force = 0;     // chains_glob_block option (0 = by the number of deep graphs)
   bool glob_prep_off = false;        // chains_glob_prep option 0: k_chains_glob builds its own H* order (test knob)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
+  uint32_t ms_rest = 0, pull_rest = 0;  // graphs past k_marksimp's / k_pull_lds's tiers (their global grids skipped at 0)
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
   uint64_t bigVmax = 0;              // the largest of them
@@ -729,12 +730,18 @@ static void set_lds_tier(nemo_ctx *c) {
     return pull_lds_bytes(v, e);
   });
   c->tierV = c->tierE = 0;  // k_marksimp's graphs (the deferred markConditionHolds)
-  for (uint32_t g = 0; g < c->G && c->dc.t_ms.bytes; g++) {
+  c->ms_rest = c->pull_rest = 0;  // graphs the per-graph global-tier kernels must take (none: not launched)
+  for (uint32_t g = 0; g < c->G; g++) {
     const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
-    if (v <= c->dc.t_ms.v && e <= c->dc.t_ms.e) {
+    const bool ms = tier_fits(c->dc.t_ms, (uint32_t)std::min<uint64_t>(v, ~0u), (uint32_t)std::min<uint64_t>(e, ~0u), 0);
+    if (ms) {
       c->tierV += (double)v;
       c->tierE += (double)e;
+    } else if (v < NEMO_CSR_BIG) {
+      c->ms_rest++;
     }
+    if (!tier_fits(c->dc.t_pull, (uint32_t)std::min<uint64_t>(v, ~0u), (uint32_t)std::min<uint64_t>(e, ~0u), 0))
+      c->pull_rest++;
   }
 }
 
@@ -1210,7 +1217,8 @@ int nemo_mark_holds(nemo_ctx *c) {
   int rc = guard_staged(c);
   if (rc) return rc;
   const bool defer = c->dc.t_ms.bytes != 0;
-  rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, defer, c->stream); });
+  rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E,
+             [&] { nemo::launch_mark(c->dc, defer, c->stream, !defer || c->ms_rest); });
   if (rc) return rc;
   c->mark_pending = defer;
   c->marked = true;
@@ -1229,7 +1237,8 @@ int nemo_simplify(nemo_ctx *c) {
     const double V = c->tierV, E = c->tierE, Vg = (double)c->V - V, Eg = (double)c->E - E;
     rc = timed(c, "k_marksimp", 8 * E + 5 * V, 5 * E, [&] { nemo::launch_marksimp(c->dc, c->stream); });
     if (rc) return rc;
-    rc = timed(c, "k_simplify", 8 * Eg + 14 * Vg, 2 * Eg, [&] { nemo::launch_simplify(c->dc, true, c->stream); });
+    rc = timed(c, "k_simplify", 8 * Eg + 14 * Vg, 2 * Eg,
+               [&] { nemo::launch_simplify(c->dc, true, c->stream, c->ms_rest != 0); });
     if (rc) return rc;
     c->mark_pending = false;
   } else {
@@ -2004,7 +2013,12 @@ static int pull_launch(nemo_ctx *c) {
   }
   nemo::launch_zero(c->d_pcur, sizeof(unsigned long long), s);
   // algorithmic bytes: the read side (node flags, both row pointers, columns, masks)
-  int rc = timed_on(c, s, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, s); });
+  uint32_t rest = c->pull_rest;
+  if (a.which == 2) {
+    const uint64_t v0 = c->node_off[a.g0 + 1] - c->node_off[a.g0], e0 = c->edge_off[a.g0 + 1] - c->edge_off[a.g0];
+    rest = !tier_fits(c->dc.t_pull, (uint32_t)std::min<uint64_t>(v0, ~0u), (uint32_t)std::min<uint64_t>(e0, ~0u), 0);
+  }
+  int rc = timed_on(c, s, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, rest, s); });
   if (rc) return rc;
   nemo::launch_to_host(c->h_poff, c->d_poff, slots * 8ull, s);
   nemo::launch_to_host(c->h_pcnt, c->d_pcnt, slots * 4ull, s);

@@ -146,8 +146,9 @@ void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
 void launch_topo(const DevCorpus &c, hipStream_t s);
 void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s);
-void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s);
-void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s);
+// per_graph false: no graph below NEMO_CSR_BIG is past the skipped tier (host count), so only the big-graph kernels run
+void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
+void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
 void launch_marksimp(const DevCorpus &c, hipStream_t s);
 void launch_chains(const DevCorpus &c, hipStream_t s);
 void launch_chains_glob(const DevCorpus &c, hipStream_t s);
@@ -169,7 +170,8 @@ void dx_img_configs(uint32_t V0, uint32_t E0, uint32_t window, DxImg out[2]);
 void launch_dx_img(const DxPrep &p, DxImg img[2], const DxImgScratch &t, hipStream_t s);
 uint32_t dx_scan_tiles(uint32_t n);  // tile sums launch_scan needs for n entries
 void launch_scan(uint32_t *a, uint32_t n, uint32_t *tsum, hipStream_t s);  // in-place exclusive scan
-void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s);
+// rest: graphs (which 0/1) or g0 (which 2) past k_pull_lds's LDS tier, counted on the host
+void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, uint32_t rest, hipStream_t s);
 void launch_chain_pairs(const DevCorpus &c, const uint64_t *off, uint32_t *out, uint64_t cap, int wide,
                         hipStream_t s);
 void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStream_t s);

@@ -982,9 +982,10 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_reduce(DevCorpus c, const uint8_
 }
 
 static dim3 mw_grid(const DevCorpus &c) { return dim3(std::max(1u, c.pg_chunks), std::min(c.n_big, 65535u)); }
-void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph) {
   const int sk = skip_tier ? 1 : 0;
-  if (c.gblock == 1024)
+  if (!per_graph) {
+  } else if (c.gblock == 1024)
     hipLaunchKernelGGL(k_mark<1024>, dim3(c.G), dim3(1024), 0, s, c, sk);
   else
     hipLaunchKernelGGL(k_mark<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, sk);
@@ -993,9 +994,10 @@ void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s) {
   hipLaunchKernelGGL(k_mw_mark_a, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
   hipLaunchKernelGGL(k_mw_mark_b, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
 }
-void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s) {
+void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph) {
   const int sk = skip_tier ? 1 : 0;
-  if (c.gblock == 1024)
+  if (!per_graph) {
+  } else if (c.gblock == 1024)
     hipLaunchKernelGGL(k_simplify_flags<1024>, dim3(c.G), dim3(1024), 0, s, c, sk);
   else
     hipLaunchKernelGGL(k_simplify_flags<NEMO_BLOCK>, dim3(c.G), dim3(NEMO_BLOCK), 0, s, c, sk);

@@ -920,7 +920,13 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
   __shared__ unsigned long long s_base;
   const uint32_t which = a.which, slot = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t g = which == 2 ? a.g0 : slot;
-  if (c.err[g]) return;  // k_pull writes the empty slot
+  if (c.err[g]) {  // the empty slot (k_pull, which also writes it, runs only when the host sees graphs past the tier)
+    if (tid == 0) {
+      a.cnt[slot] = 0;
+      a.off[slot] = 0;
+    }
+    return;
+  }
   const GraphView gv = c.view(g);
   if (!tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V;
@@ -1048,7 +1054,13 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
 __global__ __launch_bounds__(PULL_BLOCK) void k_pull_raw(DevCorpus c, PullArgs a) {
   __shared__ unsigned long long s_base;
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
-  if (c.err[g]) return;  // k_pull writes the empty slot
+  if (c.err[g]) {
+    if (tid == 0) {
+      a.cnt[g] = 0;
+      a.off[g] = 0;
+    }
+    return;
+  }
   const GraphView gv = c.view(g);
   if (!tier_fits(c.t_pull, gv.V, gv.E, gv.nlev)) return;
   const uint32_t V = gv.V, E = gv.E;
@@ -1306,7 +1318,7 @@ void launch_diff_expand(uint8_t *mask, const uint8_t *umask, const uint32_t *map
   const uint32_t gx = (uint32_t)std::min<uint64_t>(64, (V0 + NEMO_BLOCK - 1) / NEMO_BLOCK);
   hipLaunchKernelGGL(k_diff_expand, dim3(gx, n_entries), dim3(NEMO_BLOCK), 0, s, mask, umask, map, V0);
 }
-void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStream_t s) {
+void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, uint32_t rest, hipStream_t s) {
   if (c.t_pull.bytes && slots && a.which == 0) {
     hipLaunchKernelGGL(k_pull_raw, dim3(slots), dim3(PULL_BLOCK), 0, s, c, a);
   } else if (c.t_pull.bytes && slots) {
@@ -1314,17 +1326,23 @@ void launch_pull(const DevCorpus &c, const PullArgs &a, uint32_t slots, hipStrea
     hipFuncSetAttribute((const void *)k_pull_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k_pull_lds, dim3(slots), dim3(PULL_BLOCK), bytes, s, c, a);
   }
+  // k_pull's selection and grid only when the host counted graphs past the LDS
+  // tier (`rest`; errors write their empty slots in the LDS kernels too)
+  const bool global = !c.t_pull.bytes || rest;
   uint32_t grid = slots;
-  if (a.which != 2) {
-    if (!slots) return;
+  if (!slots) return;
+  if (!global) {
+  } else if (a.which != 2) {
     launch_zero(c.sel, sizeof(uint32_t), s);
     hipLaunchKernelGGL(k_pull_sel, dim3((slots + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c, slots);
     grid = std::min(slots, PULL_GRID);
   }
-  if (c.gblock == 1024)
-    hipLaunchKernelGGL(k_pull<1024>, dim3(grid), dim3(1024), 0, s, c, a);
-  else
-    hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c, a);
+  if (global) {
+    if (c.gblock == 1024)
+      hipLaunchKernelGGL(k_pull<1024>, dim3(grid), dim3(1024), 0, s, c, a);
+    else
+      hipLaunchKernelGGL(k_pull<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c, a);
+  }
   if (!a.ccnt) return;
   const uint32_t rows = a.which == 2 ? slots : c.n_big;
   if (!rows) return;
