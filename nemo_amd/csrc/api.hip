@@ -63,6 +63,7 @@ struct nemo_ctx {
   uint32_t glob_block_force = 0;     // chains_glob_block option (0 = by the number of deep graphs)
   bool glob_prep_off = false;        // chains_glob_prep option 0: k_chains_glob builds its own H* order (test knob)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
+  bool diff_on_aux = true;           // diff kernels on `aux` beside the simplification (option diff_aux)
   uint32_t ms_rest = 0, pull_rest = 0;  // graphs past k_marksimp's / k_pull_lds's tiers (their global grids skipped at 0)
   double postV = 0, postE = 0;       // nodes / edges of the post graphs (k_proto's input)
   double bigV = 0, bigE = 0;         // nodes / edges of the graphs of >= NEMO_CSR_BIG nodes
@@ -603,6 +604,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "stage_aux")) {  // 0: the hand-over kernels on the context's stream
     c->stage_on_aux = value != 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "diff_aux")) {  // 0: the diff kernels on the context's stream, in call order
+    c->diff_on_aux = value != 0;
     return NEMO_OK;
   }
   if (!strcmp(name, "pull_aux")) {  // 0: pulls on the context's stream, after everything queued before them
@@ -1497,11 +1502,14 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   c->n_uniq = nu;
   // the diff kernels go on `aux` once `stream` has reached this point (the load /
   // rebuild of the graphs they read is queued there)
-  if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-  if ((rc = ensure_event(c, &c->ev_fork))) return rc;
-  HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-  hipStream_t s = c->aux;
+  hipStream_t s = c->stream;
+  if (c->diff_on_aux) {
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    if ((rc = ensure_event(c, &c->ev_fork))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    s = c->aux;
+  }
   nemo::launch_to_host(c->d_dsrc, src, 3 * n_failed * 4, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_dsrc, s));
   nemo::launch_zero(c->d_nmiss, 4, s);
