@@ -735,7 +735,6 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     // leaf candidates LC(x) = B(x) & ~OR B(children) of goals, then per rule the OR of its
     // children's LC (the longest-path workgroups' LP test: a D rule with an LC child), all
     // from LDS; the rules' words go to HBM (lw by position)
-    const uint64_t *rg = (const uint64_t *)ringp(0);
     // over the links of the whole-graph image (still in LDS: owner's slot << 16 | child's
     // slot, slots = reversed walk indices) with LDS atomics, then per index
     uint64_t *const rw = (uint64_t *)ringp(0);
