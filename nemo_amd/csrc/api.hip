@@ -1301,8 +1301,10 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   const uint64_t rw = (uint64_t)c->n_runs * c->W;
   if ((rc = ensure_event(c, &c->ev_protos))) return rc;
   if ((rc = hgrow(c, &c->h_tab, &c->h_tab_cap, 2 * rw + 1))) return rc;
-  nemo::launch_to_host(c->h_tab, c->dc.proto_bits, rw * 4, s);
-  nemo::launch_to_host(c->h_tab + rw, c->dc.graph_tables, rw * 4, s);
+  nemo::HostCopies hc;
+  hc.add(c->h_tab, c->dc.proto_bits, rw * 4);
+  hc.add(c->h_tab + rw, c->dc.graph_tables, rw * 4);
+  nemo::launch_to_host_multi(hc, s);
   HIPCHK(c, hipEventRecord(c->ev_protos, s));
   c->protos_done = true;
   return NEMO_OK;
@@ -1612,8 +1614,10 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   if ((rc = ensure_event(c, &c->ev_diff))) return rc;
   if ((rc = hgrow(c, &c->h_mask, &c->h_mask_cap, n_failed * V0))) return rc;
   if ((rc = hgrow(c, &c->h_nmiss, &c->h_nmiss_cap, (uint64_t)1))) return rc;
-  nemo::launch_to_host(c->h_mask, c->d_dmask, n_failed * V0, s);
-  nemo::launch_to_host(c->h_nmiss, c->d_nmiss, 4, s);
+  nemo::HostCopies hc;
+  hc.add(c->h_mask, c->d_dmask, n_failed * V0);
+  hc.add(c->h_nmiss, c->d_nmiss, 4);
+  nemo::launch_to_host_multi(hc, s);
   HIPCHK(c, hipEventRecord(c->ev_diff, s));
   c->aux_pending = true;
   c->n_entries = (uint32_t)n_failed;
@@ -1782,10 +1786,12 @@ int nemo_triggers(nemo_ctx *c) {
   if ((rc = hgrow(c, &c->h_tpre, &c->h_tpre_cap, 3 * c->tcap[0] + 3))) return rc;
   if ((rc = hgrow(c, &c->h_tpost, &c->h_tpost_cap, 2 * c->tcap[1] + 2))) return rc;
   if ((rc = hgrow(c, &c->h_tasync, &c->h_tasync_cap, c->tcap[2] + 1))) return rc;
-  nemo::launch_to_host(c->h_tcounts, c->d_tcounts, 12, s);
-  nemo::launch_to_host(c->h_tpre, c->d_tpre, 12 * c->tcap[0], s);
-  nemo::launch_to_host(c->h_tpost, c->d_tpost, 8 * c->tcap[1], s);
-  nemo::launch_to_host(c->h_tasync, c->d_tasync, 4 * c->tcap[2], s);
+  nemo::HostCopies hc;
+  hc.add(c->h_tcounts, c->d_tcounts, 12);
+  hc.add(c->h_tpre, c->d_tpre, 12 * c->tcap[0]);
+  hc.add(c->h_tpost, c->d_tpost, 8 * c->tcap[1]);
+  hc.add(c->h_tasync, c->d_tasync, 4 * c->tcap[2]);
+  nemo::launch_to_host_multi(hc, s);
   HIPCHK(c, hipEventRecord(c->ev_trig, s));
   c->trig_pending = true;
   return NEMO_OK;
@@ -2028,9 +2034,11 @@ static int pull_launch(nemo_ctx *c) {
   }
   int rc = timed_on(c, s, "k_pull", 4 * E + 13 * V, E, [&] { nemo::launch_pull(c->dc, a, slots, rest, s); });
   if (rc) return rc;
-  nemo::launch_to_host(c->h_poff, c->d_poff, slots * 8ull, s);
-  nemo::launch_to_host(c->h_pcnt, c->d_pcnt, slots * 4ull, s);
-  nemo::launch_to_host(c->h_pcur, c->d_pcur, sizeof(unsigned long long), s);
+  nemo::HostCopies hc;
+  hc.add(c->h_poff, c->d_poff, slots * 8ull);
+  hc.add(c->h_pcnt, c->d_pcnt, slots * 4ull);
+  hc.add(c->h_pcur, c->d_pcur, sizeof(unsigned long long));
+  nemo::launch_to_host_multi(hc, s);
   HIPCHK(c, hipEventRecord(c->ev_pull, s));
   if (on_aux) {
     if ((rc = ensure_event(c, &c->ev_auxpull))) return rc;

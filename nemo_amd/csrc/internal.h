@@ -179,6 +179,19 @@ void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipSt
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
 void launch_goal_labels(const DevCorpus &c, uint32_t g, uint32_t *out, hipStream_t s);
 void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 1024);
+struct HostCopy {
+  uint8_t *dst;
+  const uint8_t *src;
+  uint64_t n;
+};
+struct HostCopies {  // up to four copies by one k_to_host_multi launch
+  HostCopy seg[4];
+  uint32_t n = 0;
+  void add(void *d, const void *s, uint64_t bytes) {
+    if (bytes) seg[n++] = {(uint8_t *)d, (const uint8_t *)s, bytes};
+  }
+};
+void launch_to_host_multi(const HostCopies &h, hipStream_t s);
 void launch_zero(void *dst, uint64_t bytes, hipStream_t s);
 
 }  // namespace nemo

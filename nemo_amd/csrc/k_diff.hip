@@ -1116,6 +1116,32 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_to_host(uint8_t *__restrict__ ds
   }
 }
 
+// Several small copies in one launch (blockIdx.y = segment): each launch on the
+// analysis stream costs a dispatch and a wait of its own.
+__global__ __launch_bounds__(NEMO_BLOCK) void k_to_host_multi(HostCopies h) {
+  const HostCopy &g = h.seg[blockIdx.y];
+  uint8_t *__restrict__ dst = g.dst;
+  const uint8_t *__restrict__ src = g.src;
+  const uint64_t n = g.n, stride = (uint64_t)gridDim.x * NEMO_BLOCK;
+  const uint64_t t = (uint64_t)blockIdx.x * NEMO_BLOCK + threadIdx.x;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
+    const uint64_t n16 = n >> 4;
+    for (uint64_t i = t; i < n16; i += stride) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+    for (uint64_t i = (n16 << 4) + t; i < n; i += stride) dst[i] = src[i];
+  } else {
+    for (uint64_t i = t; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+void launch_to_host_multi(const HostCopies &h, hipStream_t s) {
+  uint64_t blocks = 1;
+  for (uint32_t k = 0; k < h.n; k++)
+    blocks = std::max<uint64_t>(blocks, (h.seg[k].n + 16ull * NEMO_BLOCK - 1) / (16ull * NEMO_BLOCK));
+  if (!h.n) return;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_to_host_multi, dim3((uint32_t)blocks, h.n), dim3(NEMO_BLOCK), 0, s, h);
+}
+
 void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks) {
   if (!bytes) return;
   uint64_t blocks = (bytes + 16ull * NEMO_BLOCK - 1) / (16ull * NEMO_BLOCK);
