@@ -57,17 +57,41 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t *q
   if (pred) q[base + mbcnt(m)] = val;
 }
 
-// Block-wide exclusive scan of one u32 per thread; `lds` holds B/64 u32.
-template <int B = NEMO_BLOCK>
-__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, uint32_t *lds) {
-  constexpr int NW = B / 64;
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+// Inclusive wave scan by DPP (six VALU adds, no LDS permutes): Hillis-Steele
+// within each 16-lane row (row_shr 1, 2, 4, 8; lanes shifted past the row's
+// start read 0), then row 0's total into row 1 and row 2's into row 3
+// (row_bcast:15), then rows 0-1's total into rows 2-3 (row_bcast:31).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  uint32_t v = x;
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// The same by LDS permutes (__shfl_up).  DPP is the faster form where measured
+// (k_build, k_pull_lds); k_chains measured 1.76 -> 2.0 ms with it, so the
+// default stays the permute form.
+__device__ __forceinline__ uint32_t wave_incl_scan_shfl(uint32_t x) {
+  const uint32_t lane = lane_id();
   uint32_t v = x;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t y = __shfl_up(v, d);
     if (lane >= (uint32_t)d) v += y;
   }
+  return v;
+}
+
+// Block-wide exclusive scan of one u32 per thread; `lds` holds B/64 u32.
+template <int B = NEMO_BLOCK, bool DPP = false>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, uint32_t *lds) {
+  constexpr int NW = B / 64;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  const uint32_t v = DPP ? wave_incl_scan(x) : wave_incl_scan_shfl(x);
   if (lane == 63) lds[w] = v;
   __syncthreads();
   uint32_t off = 0, tot = 0;
@@ -86,7 +110,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
 // Each round takes PER consecutive elements per thread: 4 for LDS arrays (few
 // bank conflicts), 16 for HBM arrays (16 independent loads in flight per
 // thread, so a long scan costs few latency-bound rounds).
-template <int B = NEMO_BLOCK, int PER = 4, typename T>
+template <int B = NEMO_BLOCK, int PER = 4, bool DPP = false, typename T>
 __device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_t *lds) {
   uint32_t carry = 0;
   for (uint32_t base = 0; base < n; base += B * PER) {
@@ -98,7 +122,7 @@ __device__ __forceinline__ uint32_t block_scan_inplace(T *a, uint32_t n, uint32_
       s += x[k];
     }
     uint32_t tot;
-    uint32_t ex = block_exscan<B>(s, &tot, lds) + carry;
+    uint32_t ex = block_exscan<B, DPP>(s, &tot, lds) + carry;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       if (i0 + k < n) a[i0 + k] = (T)ex;
@@ -122,14 +146,14 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <bool DPP = false>
 __device__ __forceinline__ uint32_t wave_exscan(uint32_t x, uint32_t *total) {
-  const uint32_t lane = lane_id();
-  uint32_t v = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(v, d);
-    if (lane >= (uint32_t)d) v += y;
+  if (DPP) {
+    const uint32_t v = wave_incl_scan(x);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return v - x;
   }
+  const uint32_t v = wave_incl_scan_shfl(x);
   *total = __shfl(v, 63);
   return v - x;
 }

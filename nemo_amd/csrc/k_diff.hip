@@ -963,7 +963,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
     if (u < V && ALIVE(u))
       for (uint32_t j = L.fp[u]; j < L.fp[u + 1]; j++) n += ALIVE(L.fc[j]);
     uint32_t tot;
-    const uint32_t ex = wave_exscan(n, &tot);
+    const uint32_t ex = wave_exscan<true>(n, &tot);
     if (lane == 0) s_pre[k * NW + w] = tot;
     if (k & 1) cp[k >> 1] |= ex << 16;
     else cp[k >> 1] = ex;
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
     const uint32_t nk = ((V + PULL_BLOCK - 1) / PULL_BLOCK) * NW, i0 = 2u * lane;
     const uint32_t x0 = i0 < nk ? s_pre[i0] : 0u, x1 = i0 + 1u < nk ? s_pre[i0 + 1u] : 0u;
     uint32_t nn;
-    const uint32_t ex = wave_exscan(x0 + x1, &nn);
+    const uint32_t ex = wave_exscan<true>(x0 + x1, &nn);
     if (i0 < nk) s_pre[i0] = ex;
     if (i0 + 1u < nk) s_pre[i0 + 1u] = ex + x0;
     if (lane == 0) {
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(PULL_BLOCK) void k_pull_lds(DevCorpus c, PullArgs a
       for (uint32_t j = L.fp[t]; j < L.fp[t + 1]; j++) n += ALIVE(L.fc[j]);
     }
     uint32_t tot;
-    uint64_t o = pos + block_exscan<PULL_BLOCK>(n, &tot, s_lds);
+    uint64_t o = pos + block_exscan<PULL_BLOCK, true>(n, &tot, s_lds);
     if (k < nch) {
       for (uint32_t j = gv.rp[h]; j < gv.rp[h + 1]; j++) {
         const uint32_t p = gv.rc[j];

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
       }
     }
     if (dir == 0) STAMP(2);
-    block_scan_inplace<B>(ptr, V + 1, s_lds);
+    block_scan_inplace<B, 4, true>(ptr, V + 1, s_lds);
     if (dir == 0) STAMP(3);
     lds16_to_hbm32<B>(optr, ptr, V + 1);
     __syncthreads();
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
 #pragma unroll
         for (int b = 0; b < 4; b++) n += w0 + k < nw4 && 4 * (w0 + k) + b < V && ((x[k] >> (8 * b)) & 0xFFu) == 0u;
       uint32_t tot;
-      uint32_t i = o + block_exscan<B>(n, &tot, s_lds);
+      uint32_t i = o + block_exscan<B, true>(n, &tot, s_lds);
 #pragma unroll
       for (int k = 0; k < SW; k++)
 #pragma unroll
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
       }
     }
     uint32_t tot;
-    uint32_t off = block_exscan<B>(sum, &tot, s_lds);
+    uint32_t off = block_exscan<B, true>(sum, &tot, s_lds);
     uint32_t *e2 = c.e2 + e0, *po = c.posoff + n0;
     for (uint32_t i = i0; i < i1; i += 4) {
       uint32_t u[4], a[4], n[4], y[4][4];
