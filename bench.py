@@ -393,143 +393,64 @@ def main():
 def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
     """C5 at its configured size (BASELINE.json configs[4]: 1k runs of 1M-node graphs), which does not fit
     one MI355X's 288 GB at once.  The rank's runs are generated up front (host memory) in batches of
-    --batch-runs, each a corpus of its own with run 0 replicated, not owned, after the first.  A pass loads
-    batch i+1 (nemo_load_corpus: H2D + CSR + Kahn levels) on one of two contexts, from a second host thread,
-    while batch i is analysed on the other: mark, diff (reference mode: failedRuns[0]'s label set, taken
-    from the batch holding it), simplify, protos partial, hand-over, pulls, every D2H.  The batches' proto
-    vectors are summed on the host (prototype.go:79-130).  value = runs of a pass / its wall time, uploads
-    included; generation is not timed (it stands in for reading Molly output)."""
-    import threading
-
-    from nemo_amd import engine as E
-    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE, NODE_RULE
+    --batch-runs, each a corpus of its own with run 0 replicated, not owned, after the first.  A pass is
+    nemo_amd/batched.py's BatchedPasses.run_pass (tests/test_gpu_batched.py checks the same code against the
+    oracle): batch i+1 loaded (H2D + CSR + Kahn levels) on one of two contexts from a second host thread while
+    batch i is analysed on the other, the batches' proto vectors summed on the host (prototype.go:79-130).
+    value = runs of a pass / its wall time, uploads included; generation and the one-time page-locking of the
+    batches are not timed (they stand in for reading Molly output; the pin time is reported)."""
+    from nemo_amd.batched import BatchedPasses, split_even
+    from nemo_amd.corpus import DIFF_PER_RUN, DIFF_REFERENCE
     from tools import synth
     mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
     R = args.runs_total // world
     base = rank * R
-    # batches of near-equal size (1000 runs at --batch-runs 160: seven of 143, not six of 160 and one of 40),
-    # so that each reload reuses the previous batch's device allocations (nemo_ctx::cache takes blocks at most
-    # 1/8 larger than asked; a 40-run batch between 160-run ones cost a 3.5 s re-allocation per pass)
-    nb = -(-R // max(1, min(args.batch_runs, R)))
-    B = -(-R // nb)
+    sizes = split_even(R, args.batch_runs)
     t0 = time.time()
-    batches = []
-    for a in range(0, R, B):
-        c, _ = synth.generate(min(B, R - a), run_base=base + a, prepend_run0=True, threads=threads, **gen)
+    batches, a = [], 0
+    for n in sizes:
+        c, _ = synth.generate(n, run_base=base + a, prepend_run0=True, threads=threads, **gen)
         batches.append(c)
+        a += n
     gen_s = time.time() - t0
-    succ_all, fail_all = [], []
-    for c in batches:
-        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
-        for it, st, o in zip(c.iteration, c.status, own):
-            if o:
-                (succ_all if st == "success" else fail_all).append(int(it))
-    success = [0] + [x for x in succ_all if x != 0]
-    f0_labels = None
-    if fail_all and mode == DIFF_REFERENCE:
-        f0 = min(fail_all) if world == 1 else None
-        for c in batches:
-            if f0 is not None and f0 in set(int(x) for x in c.iteration):
-                g = 2 * c.run_index(f0) + 1
-                a_, b_ = int(c.node_off[g]), int(c.node_off[g + 1])
-                f0_labels = c.label[a_:b_][(c.node_word[a_:b_] & NODE_RULE) == 0].copy()
-                break
-
-    def new_engine():
-        e = E.Engine(local)
-        for kv in args.set:
-            k, v = kv.split("=", 1)
-            e.set_option(k, int(v))
-        return e
-
-    engines = [new_engine(), new_engine()]
-    # every batch is uploaded once per pass: its arrays page-locked once, up front (not timed, like the
-    # generation), so each upload runs at the DMA rate instead of through the runtime's staging copies
-    pinned = [E.pin_corpus(c) for c in batches]
-    T = batches[0].n_tables
-
-    def analyse(eng, c):
-        own = c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)
-        its = [int(x) for x, o in zip(c.iteration, own) if o]
-        fset = set(fail_all)
-        bf = [it for it in its if it in fset]
-        eng.mark()
-        if bf:
-            if f0_labels is not None:
-                eng.diffprov_host_labels(bf, f0_labels)
-            else:
-                eng.diffprov(bf, DIFF_PER_RUN)
-        eng.simplify()
-        eng.protos_partial(success, 0)
-        eng.stage_simplified()
-        has0 = 0 in its
-        if has0:
-            eng.triggers()
-        eng.pull(1)
-        if bf:
-            eng.pull(2)
-        vec = eng.reduce_vector().astype(np.int64)
-        eng.run_tables(1)
-        if has0:
-            eng.trigger_rows()
-        if bf:
-            eng.diff_masks_view()
-        eng.missing()
-        eng.simplified_view()
-        return vec
-
-    phase = {"load_s": [], "analyse_s": [], "join_wait_s": []}
-
-    def timed_load(eng, c):
-        t = time.perf_counter()
-        eng.load(c)
-        eng.synchronize()
-        phase["load_s"].append(round(time.perf_counter() - t, 3))
-
-    def one_pass():
-        for v in phase.values():
-            v.clear()
-        vec = np.zeros(2 * T + 4, np.int64)
-        timed_load(engines[0], batches[0])
-        for i in range(len(batches)):
-            th = None
-            if i + 1 < len(batches):
-                nxt = engines[(i + 1) % 2]
-                th = threading.Thread(target=timed_load, args=(nxt, batches[i + 1]))
-                th.start()
-            t = time.perf_counter()
-            vec += analyse(engines[i % 2], batches[i])
-            phase["analyse_s"].append(round(time.perf_counter() - t, 3))
-            if th is not None:
-                t = time.perf_counter()
-                th.join()
-                phase["join_wait_s"].append(round(time.perf_counter() - t, 3))
+    opts = [tuple(kv.split("=", 1)) for kv in args.set]
+    bp = BatchedPasses(batches, mode=mode, device=local, options=[(k, int(v)) for k, v in opts])
+    phase = {}
+    try:
+        for _ in range(args.warmup):
+            bp.run_pass()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
-        return E.reduce_interpret(vec.astype(np.uint32), T, batches[0].table_post)
-
-    for _ in range(args.warmup):
-        one_pass()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        one_pass()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            phase = bp.run_pass().phases
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+    finally:
+        bp.close()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     runs = sum(int((c.owned if c.owned is not None else np.ones(c.n_runs, np.uint8)).sum()) for c in batches)
     total = runs * world
+    Vn = sum(int(c.node_off[-1]) for c in batches)
+    E_ = sum(int(c.edge_off[-1]) for c in batches)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg.get("cpu_runs"):
         cpu = cpu_baseline(args, cfg, gen, None, None, None, None, mode)  # its bounded sample of the same shape
-    Vn = sum(int(c.node_off[-1]) for c in batches)
-    E_ = sum(int(c.edge_off[-1]) for c in batches)
+        # the sample's graphs are ~20x smaller than this line's: state the baseline per node too, and scaled
+        # to this line's nodes per run (linear scaling: the oracle is superlinear in graph size, so the
+        # scaled figure overstates the CPU)
+        nodes_per_run = Vn / max(sum(c.n_runs for c in batches), 1)
+        cpu["value_nodes_per_s"] = round(cpu["value"] * cpu["sample_nodes_per_run"], 1)
+        cpu["value_scaled_to_line"] = round(cpu["value_nodes_per_s"] / nodes_per_run, 4)
+        cpu["scaling_note"] = (f"value is runs/s of the sample's {cpu['sample_nodes_per_run']:.0f}-node runs; "
+                               f"value_scaled_to_line = nodes/s / this line's {nodes_per_run:.0f} nodes per run "
+                               "(linear in nodes: an upper bound for the CPU)")
     out = {"metric": METRIC, "value": round(total * args.steps / elapsed, 2), "unit": "runs/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
@@ -537,26 +458,24 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
                                   "nodes / ~4 edges per node at EOT eot (BASELINE configs[4]); a step is one pass "
                                   "over every run, batches of batch_runs uploaded on one context while the previous "
                                   "batch is analysed on another, uploads included",
-                      "runs_total": total, "runs_per_gpu": runs, "batch_runs": B, "batches_per_gpu": len(batches),
+                      "runs_total": total, "runs_per_gpu": runs, "batch_runs": max(sizes), "batch_sizes": sizes,
+                      "batches_per_gpu": len(batches),
                       "nodes_per_graph": gen["target_nodes"], "eot": gen["eot"], "nodes_total_rank0": Vn,
                       "edges_total_rank0": E_, "edges_per_node": round(E_ / max(Vn, 1), 3),
-                      "failed_runs_rank0": len(fail_all), "diff_mode": args.diff_mode,
+                      "failed_runs_rank0": len(bp.failed), "diff_mode": args.diff_mode,
                       "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped); batches "
                                      f"page-locked once (nemo_host_register)",
                       "lib_options": args.set},
            "roofline": None, "cpu_baseline": cpu, "gen_seconds_rank0": round(gen_s, 2),
-           "pass_phases_rank0": dict(phase),
-           "note": "no per-kernel roofline on this line: the resident-batch line (--config c5) carries it"}
+           "pass_phases_rank0": dict(phase), "pin_s_rank0": round(bp.pin_s, 3), "pin_failed_arrays": bp.pin_failed,
+           "note": "no per-kernel roofline on this line: the resident-batch line (--config c5) carries it; the "
+                   "one-time page-locking (pin_s_rank0) is outside the timed passes"}
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as fh:
                 fh.write(line + "\n")
-    for e in engines:
-        e.close()
-    for p_ in pinned:
-        E.unpin_corpus(p_)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -771,6 +690,7 @@ def cpu_baseline(args, cfg, gen, corpus, success, failed, owned_runs, mode):
     fa1 = [x for x in s_fail if x in set(one.iteration.tolist())]
     v_one, reps1, t_one = leg(1, one, su1, fa1, int(own1.sum()))
     return {"value": round(v_all, 4), "unit": "runs/s", "cores": threads, "kind": "port",
+            "sample_nodes_per_run": round(int(sample.node_off[-1]) / max(sample.n_runs, 1), 1),
             "value_1core": round(v_one, 4), "nproc": info["nproc"], "usable_cores": info["usable_cores"],
             "cgroup_cpu_quota": info["cgroup_cpu_quota"], "omp_num_threads_env": info["omp_num_threads_env"],
             "cores_rule": "every usable core, or the cgroup cpu.max quota when one is set (OMP_NUM_THREADS "

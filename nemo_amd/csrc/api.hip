@@ -1492,7 +1492,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->d_dxw = nullptr;
     c->dx_nu_cap = c->dx_nch_cap = 0;
     if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
-    if ((rc = dalloc(c, &c->d_dxsval, ((size_t)nu * V0 + 1) / 2))) return rc;  // u16
+    if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu + nch))) return rc;  // maxima, then the chunks' walk flags
     if ((rc = dalloc(c, &c->d_dxw, 4 * (size_t)nch * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxfb, 8 * (size_t)nch * V0))) return rc;  // 32 bytes per position and chunk
@@ -1547,7 +1547,7 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     a.dw = a.bw + plane;
     a.lw = a.dw + plane;
     a.fb = reinterpret_cast<uint8_t *>(c->d_dxfb);
-    a.sval = reinterpret_cast<uint16_t *>(c->d_dxsval);
+    a.sval = c->d_dxsval;
     a.maxlen = c->d_dxlpl;
     a.wflag = c->d_dxlpl + c->dx_nu_cap;
     a.mask = c->d_dmask;
@@ -1725,10 +1725,10 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
   if (c->n_entries) {
     HIPCHK(c, hipEventSynchronize(c->ev_diff));
     nu_rows = *c->h_nmiss;
-    // k_dx keeps longest paths as u16 (k_dx.hip DX_VMAX): a longer one is flagged
-    if (c->dx_last && (nu_rows & 0x80000000u))
-      return fail(c, NEMO_ERR_INVALID, "diff graph of run 0: a path longer than 65533 steps (unsupported)");
-    nu_rows &= 0x7FFFFFFFu;
+    // the fused walks' bounded hand-off wait (k_dx.hip dx_publish) gave up: the rows are void
+    if (c->dx_last && (nu_rows & DX_ERR_HANDOFF))
+      return fail(c, NEMO_ERR_INVALID, "diff walks: a longest-path workgroup timed out waiting for its Bwd* hand-off");
+    nu_rows &= DX_ROWS;
   }
   // rows of the distinct computations (unique index, rule), then one copy per entry
   int rc;
@@ -1991,6 +1991,9 @@ int nemo_simplified_view(nemo_ctx *c, const uint8_t **state, const uint64_t **ch
   HIPCHK(c, hipEventSynchronize(c->ev_copied));
   const uint64_t n = c->h_choff[c->G];
   if (n > c->staged_cap) {  // the hint was short: stage again at the real count
+    // on the context's stream, behind everything queued since the first stage (work that
+    // rewrites flags may follow it there; `aux` was ordered only after the first stage)
+    c->stage_stream = c->stream;
     int rc = stage_enqueue(c, n);
     if (rc) return rc;
     HIPCHK(c, hipEventSynchronize(c->ev_copied));

@@ -76,6 +76,11 @@ struct DxImgScratch {
   uint32_t *tsum;            // scan tiles
 };
 
+// the diff call's row counter (DxArgs::n_missing): rows in the low bits, bit 30 raised when a
+// fused walk's hand-off wait gave up (k_dx.hip dx_publish)
+#define DX_ROWS 0x3FFFFFFFu
+#define DX_ERR_HANDOFF 0x40000000u
+
 // One multi-entry CreateNaiveDiffProv call (k_dx.hip): nu distinct label
 // sources in chunks of 64, one bit per source in every u64 word.
 struct DxArgs {
@@ -99,7 +104,7 @@ struct DxArgs {
   uint64_t *dw;              // [nch][V0] D = Fwd* & Bwd* by position (k_dx_lp; k_dx_mask reads fb & bw)
   uint64_t *lw;              // [nch][V0] leaf candidates: Bwd* goals without a Bwd* child, by position
   uint8_t *fb;               // [nch][64 / NE][V0] Fwd* bits of the NE sources of longest-path workgroup g
-  uint16_t *sval;            // [nu][V0] val = 1 + the longest path from Good (0 off Fwd*) by position
+  uint32_t *sval;            // [nu][V0] val = 1 + the longest path from Good (0 off Fwd*) by position
   uint32_t *maxlen;          // [nu] the longest LP val of each source (zeroed per call)
   uint32_t *wflag;           // [nch] Bwd* walk of the chunk done (whole-graph walks; zeroed per call)
   uint32_t ne;               // sources per longest-path workgroup of the walks launched (k_dx_mask)

@@ -509,13 +509,36 @@ __device__ __forceinline__ DxLds<T, NE> dx_carve(void *base, uint32_t R, uint32_
   L.st = (uint32_t *)p;
   return L;
 }
-#define DX_VMAX 0xFFFEu  // longest val kept (u16 per source and position); past it the call fails
+// (val <= the nodes on a path <= V0: u32 values never overflow)
 #define DXP_B 256        // k_dx_lp: threads per workgroup
 #define DXF_K 6          // positions per thread and round of the leaf-candidate and fused LP passes
 
 template <int NE, int NT>
 __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a, uint32_t chunk, uint32_t grp,
                                             const uint32_t *ring0, uint32_t rs, uint8_t *lpb);
+
+// The fused walks' hand-off from a chunk's Bwd* workgroup to its longest-path workgroups
+// (one writer, several readers, flag values 1 then 2 per call; k_dx_label zeroes the flags).
+//   writer: payload stores by every wave; each wave drains them (s_waitcnt vmcnt(0)); a
+//           workgroup barrier; then one lane stores the flag with an agent-scope RELEASE
+//           (buffer_wbl2 sc1 + s_waitcnt: every store of this workgroup that L2 acknowledged
+//           reaches memory before the flag does -- without the release, the write-through
+//           payload and the flag go out through different L2 channels and the flag can land
+//           first; that was round 5's r05aa D-mask mismatch, test_deep_shape, per-run mode).
+//   reader: one lane polls the flag (relaxed, agent scope), then an agent-scope ACQUIRE fence
+//           (buffer_inv sc1: the CU's L1 and this XCD's L2 drop stale lines), then a workgroup
+//           barrier; the other waves' payload loads are ordered after it by the barrier.
+// Forward progress: readers spin, so every writer must be dispatched while readers wait.  The
+// writers are blocks [0, nch) of the launch and the hardware dispatches a grid's workgroups in
+// blockIdx order, so a writer is resident before any reader of its chunk.  The spin is bounded
+// all the same (DX_SPIN_MAX polls, seconds): past it the reader gives up, raises DX_ERR_HANDOFF in
+// the call's row counter and the host fails the call (nemo_fetch_missing) instead of hanging.
+#define DX_SPIN_MAX (1u << 21)
+__device__ __forceinline__ void dx_publish(uint32_t *flag, uint32_t v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int MODE, int NE, bool WHOLE, int NT>
 __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, const DxImg &m0, const DxImg &m1,
@@ -539,7 +562,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   };
   auto ringp = [&](uint32_t e) -> T * { return L.ring0 + (size_t)e * L.rs; };
   uint64_t *const bwv = a.bw + (size_t)chunk * V;
-  auto sval = [&](uint32_t e) -> uint16_t * {
+  auto sval = [&](uint32_t e) -> uint32_t * {
     return a.sval + (size_t)min(64u * chunk + min(grp * NE + e, 63u), a.nu - 1u) * V;
   };
   // this workgroup's Fwd* byte plane (bit e: source 64 chunk + NE grp + e), MODE 2
@@ -607,7 +630,6 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
   // ---- finalize of window kw: values to HBM ----
   auto finalize = [&](uint32_t kw, uint32_t wt, uint32_t nwt) {
     const uint32_t w0 = m.wb[kw], n = m.wb[kw + 1] - w0;
-    bool over = false;
     for (uint32_t kk = wt; kk < n; kk += nwt) {
       const uint32_t i = w0 + kk, sl = slot(i);
       if (MODE == 0) {
@@ -618,14 +640,12 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
         for (int e = 0; e < NE; e++) {
           if (srcu(e) == NEMO_NONE) continue;
           const uint32_t v = (uint32_t)ringp(e)[sl];
-          over |= v > DX_VMAX;
-          if (!WHOLE || !a.fuse) sval(e)[i] = (uint16_t)min(v, (uint32_t)DX_VMAX);  // fused: values stay in LDS
+          if (!WHOLE || !a.fuse) sval(e)[i] = v;  // fused: values stay in LDS
           fbits |= (v ? 1u : 0u) << e;
         }
         fbp[i] = (uint8_t)fbits;
       }
     }
-    if (MODE == 2 && __any(over) && lane == 0) atomicOr(a.n_missing, 0x80000000u);
   };
   // ---- the walk of window kw by wave e ----
   auto walk = [&](uint32_t kw, uint32_t buf, uint32_t e) {
@@ -729,9 +749,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     // the masks meanwhile), then the rules' leaf-child words (flag 2)
     for (uint32_t i = tid; i < V; i += NT)
       __hip_atomic_store(bwv + i, (uint64_t)ringp(0)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dx_publish(a.wflag + chunk, 1u);
     // leaf candidates LC(x) = B(x) & ~OR B(children) of goals, then per rule the OR of its
     // children's LC (the longest-path workgroups' LP test: a D rule with an LC child), all
     // from LDS; the rules' words go to HBM (lw by position)
@@ -765,11 +783,7 @@ __device__ __forceinline__ void dx_walk(const DevCorpus &c, const DxArgs &a, con
     uint64_t *olw = a.lw + (size_t)chunk * V;
     for (uint32_t i = tid; i < V; i += NT)
       __hip_atomic_store(olw + (V - 1u - i), rw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // publish (write-through payload): every storing wave drains its stores, then one lane
-    // sets the flag with an agent-scope atomic store; the readers acquire
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.wflag + chunk, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dx_publish(a.wflag + chunk, 2u);
     STAMP(5);
     return;
   }
@@ -846,11 +860,18 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
     pinf[k] = a.p.info[p];
     ptp[k] = a.own_mask ? a.p.tpos[p] : 0u;
   }
-  // one lane polls the chunk's flag until it reaches `want`, then one acquire for the workgroup
+  // one lane polls the chunk's flag until it reaches `want` (bounded: dx_publish), then one
+  // acquire for the workgroup
   auto wait_flag = [&](uint32_t want) {
     if (tid == 0) {
-      while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+      uint32_t n = 0;
+      while (__hip_atomic_load(a.wflag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (++n == DX_SPIN_MAX) {
+          atomicOr(a.n_missing, DX_ERR_HANDOFF);
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
+      }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -866,7 +887,6 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   uint32_t mx[NE];
 #pragma unroll
   for (int e = 0; e < NE; e++) mx[e] = 0;
-  bool over = false;
   const uint64_t *bw = a.bw + (size_t)chunk * V, *lw = a.lw + (size_t)chunk * V;
   for (uint32_t base = 0; base < V; base += DXF_K * NT) {  // DXF_K positions per thread, loads together
     uint64_t b[DXF_K];
@@ -880,7 +900,6 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
 #pragma unroll
       for (int e = 0; e < NE; e++) {
         const uint32_t v = ring0[(size_t)e * rs + pos];
-        over |= v > DX_VMAX;
         f |= (v ? 1u : 0u) << e;
       }
       const uint32_t d = f & live & (uint32_t)(b[k] >> sh) & NM;
@@ -888,7 +907,6 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
       if (!own) dpl[pos] = (uint8_t)d;
     }
   }
-  if (__any(over) && lane_id() == 0) atomicOr(a.n_missing, 0x80000000u);
   __syncthreads();
   // one entry per source: the D masks by node, consecutive nodes per wave (coalesced bytes),
   // while the Bwd* workgroup computes the leaf candidates
@@ -943,7 +961,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   }
   __syncthreads();
   STAMP(5);
-  if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = min(s_max[tid], (uint32_t)DX_VMAX);
+  if (tid < (uint32_t)NE && ((live >> tid) & 1u)) a.maxlen[64u * chunk + sh + tid] = s_max[tid];
   // the rows: counted per thread, one block scan and one global atomic per workgroup
   __shared__ uint32_t s_scan[NT / 64], s_base;
   auto hits = [&](uint32_t pos) -> uint32_t {
@@ -960,7 +978,7 @@ __device__ __forceinline__ void dx_lp_fused(const DevCorpus &c, const DxArgs &a,
   for (uint32_t pos = tid; pos < V; pos += NT) cnt += (uint32_t)__popc(hits(pos));
   uint32_t tot;
   uint32_t q = block_exscan<NT>(cnt, &tot, s_scan);
-  if (tid == 0 && tot) s_base = atomicAdd(a.n_missing, tot) & 0x7FFFFFFFu;
+  if (tid == 0 && tot) s_base = atomicAdd(a.n_missing, tot) & DX_ROWS;
   if (!tot) return;  // workgroup-uniform
   __syncthreads();
   q += s_base;
@@ -1089,7 +1107,7 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_dx_emit(DxArgs a) {
   if (!tot) return;
   uint32_t base = 0;
   if (lane_id() == 0) base = atomicAdd(a.n_missing, tot);
-  uint32_t q = ((__builtin_amdgcn_readfirstlane(base) & 0x7FFFFFFFu) + ex);
+  uint32_t q = ((__builtin_amdgcn_readfirstlane(base) & DX_ROWS) + ex);
   const uint32_t node = hit ? a.p.pnode[pos] : 0u;
 #pragma unroll
   for (int k = 0; k < 8; k++) {

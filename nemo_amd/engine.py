@@ -121,12 +121,15 @@ def _p(a: Optional[np.ndarray]):
     return None if a is None or a.size == 0 else a.ctypes.data
 
 
+PIN_FIELDS = ("node_word", "label", "edge_src", "edge_dst", "id_rank")
+
+
 def pin_corpus(corpus: Corpus) -> list:
     """Page-lock a corpus' large host arrays (nemo_host_register) so that every nemo_load_corpus of it
     uploads by DMA; returns the registered arrays for unpin_corpus."""
     L = lib()
     pinned = []
-    for k in ("node_word", "label", "edge_src", "edge_dst", "id_rank"):
+    for k in PIN_FIELDS:
         a = getattr(corpus, k, None)
         if a is None or a.size == 0 or not a.flags["C_CONTIGUOUS"]:
             continue

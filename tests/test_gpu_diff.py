@@ -138,3 +138,28 @@ def test_failed_load_then_reshaped_reload(eng):
     deep, _ = synth.generate(8, target_nodes=30000, eot=30, body_extra=6, nval=3, nloc=4, p_fault=0.5,
                              prepend_run0=True, seed=7)
     _check_corpus(eng, deep, windows=(0, 1))
+
+
+@pytest.mark.parametrize("shape", ["c3_fused", "deep_windowed"])
+def test_repeated_calls_stable(eng, shape):
+    """Round 5 saw one red run of test_deep_shape (per-run mode, default window: 2 of 4 D masks wrong) that
+    did not come back.  The same calls repeated on one loaded corpus, each compared with the oracle: the fused
+    whole-graph walks (C3 shape: the Bwd* -> longest-path hand-off, k_dx.hip dx_publish) and the windowed
+    walks (E0 > 65535: k_dx_lp / k_dx_emit / k_dx_mask after the walks)."""
+    if shape == "c3_fused":
+        corpus, _ = synth.generate(60, p_fault=0.5, prepend_run0=True, **synth.CONFIGS["c3"])
+    else:
+        corpus, _ = synth.generate(10, target_nodes=40000, eot=40, body_extra=6, nval=3, nloc=4, p_fault=0.5,
+                                   prepend_run0=True)
+    f = corpus.failed_iters()
+    eng.load(corpus)
+    eng.mark()
+    orc = O.analyze(corpus, [0], f, diff_mode=DIFF_PER_RUN, threads=8, diff_only=True)
+    want_m, want_r = orc.diff_mask, _rows(orc.missing)
+    for it in range(40):
+        eng.diffprov(f, DIFF_PER_RUN)
+        m, r = eng.diff_masks(len(f)), _rows(eng.missing())
+        bad = np.nonzero((m != want_m).any(1))[0]
+        assert not len(bad), (f"call {it}: D masks of entries {bad.tolist()} differ at "
+                              f"{[int((m[e] != want_m[e]).sum()) for e in bad]} nodes")
+        assert np.array_equal(r, want_r), f"call {it}: missing rows differ"

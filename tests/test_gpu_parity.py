@@ -551,3 +551,42 @@ def test_pull_on_aux_stream(eng):
         _check(eng, corpus, mode=DIFF_PER_RUN)  # twice on one context: the second load joins the first pull
     finally:
         eng.set_option("pull_aux", 0)
+
+
+@pytest.mark.parametrize("stage_aux,diff_aux", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_stage_and_diff_streams(eng, stage_aux, diff_aux):
+    """Options stage_aux / diff_aux: the hand-over kernels and the diff kernels on the aux stream or on
+    the context's stream.  A small corpus is staged first, so the next corpus' stage runs at a short
+    pair-count hint and nemo_simplified_view re-stages (on the context's stream) -- every output still
+    equals the oracle's."""
+    from nemo_amd.corpus import F_DELETED, F_HOLDS, F_KEPT
+    from tools import synth
+    small, _ = synth.generate(4, target_nodes=300)
+    big, _ = synth.generate(30, target_nodes=2500, p_fault=0.4)
+    eng.set_option("stage_aux", stage_aux)
+    eng.set_option("diff_aux", diff_aux)
+    try:
+        for corpus in (small, big):
+            s, f = corpus.success_iters(), corpus.failed_iters()
+            orc = O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN, skip_pulls=True)
+            eng.load(corpus)
+            eng.mark()
+            eng.simplify()
+            eng.stage_simplified()
+            eng.prototypes(s)
+            eng.diffprov(f, DIFF_PER_RUN)
+            state, off, ht = eng.simplified_view()
+            alive, holds = E.Engine.unpack_state(state, len(orc.flags))
+            assert np.array_equal(alive, (orc.flags & (F_KEPT | F_DELETED)) == F_KEPT)
+            assert np.array_equal(holds, (orc.flags & F_HOLDS) != 0)
+            G = corpus.n_graphs
+            g = np.repeat(np.arange(G), np.diff(off.astype(np.int64)))
+            k = np.arange(len(ht)) - off[g].astype(np.int64)
+            got = np.stack([g, k, ht[:, 0].astype(np.int64), ht[:, 1].astype(np.int64)], 1)
+            assert np.array_equal(got, orc.chains[:, :4].astype(np.int64))
+            if f:
+                assert np.array_equal(eng.diff_masks(len(f)), orc.diff_mask)
+                assert np.array_equal(eng.missing(), orc.missing)
+    finally:
+        eng.set_option("stage_aux", 1)
+        eng.set_option("diff_aux", 1)
