@@ -237,17 +237,17 @@ def main():
         eng.stage_simplified()
         if world > 1:
             dist.all_reduce(d_red)
+        eng.protos_stage(d_red.data_ptr())  # the vector's D2H queued behind the all-reduce
         if has_run0:
             eng.triggers()
         eng.pull(1)
         eng.pull(2)
         protos = eng.protos_finalize(d_red.data_ptr())
         tabs = eng.run_tables(1)
-        inter = np.asarray(protos["inter"], np.int64)
-        uni = np.asarray(protos["union"], np.int64)
-        if len(fidx):  # missingFrom (prototype.go:141-206) for every failed run
-            _ = (tabs[fidx][:, inter >> 5] >> (inter & 31).astype(np.uint32)) & 1 if len(inter) else None
-            _ = (tabs[fidx][:, uni >> 5] >> (uni & 31).astype(np.uint32)) & 1 if len(uni) else None
+        if len(fidx):  # missingFrom (prototype.go:141-206) for every failed run: proto tables absent from its set
+            tf = tabs[fidx]
+            _ = table_mask(protos["inter"], tf.shape[1]) & ~tf
+            _ = table_mask(protos["union"], tf.shape[1]) & ~tf
         if has_run0:
             eng.trigger_rows()
         masks = eng.diff_masks_view() if failed else None
@@ -388,6 +388,14 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def table_mask(tables, words):
+    """u32 bitset of a table-id list (missingFrom's proto side, prototype.go:191-198)."""
+    m = np.zeros(words, np.uint32)
+    for t in tables:
+        m[t >> 5] |= np.uint32(1 << (t & 31))
+    return m
 
 
 def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):

@@ -210,6 +210,11 @@ int nemo_simplify(nemo_ctx *ctx);
 size_t nemo_reduce_len(const nemo_ctx *ctx);
 int nemo_protos_partial(nemo_ctx *ctx, const uint32_t *success_iters, size_t n_success,
                         uint32_t *d_reduce /* device, nemo_reduce_len() u32; NULL = the context's own */);
+/* Optional: queue the (reduced) vector's copy to pinned host memory on the
+ * context's stream now, behind the caller's all-reduce, so that
+ * nemo_protos_finalize on the same d_reduce only waits for it (no round trip
+ * of its own).  A node context reduces inside finalize: a no-op there.      */
+int nemo_protos_stage(nemo_ctx *ctx, const uint32_t *d_reduce);
 /* Interprets a (reduced) vector (d_reduce NULL = the context's own): inter/union
  * table ids, ascending, "post" excluded (prototype.go:106,120).  Returns counts through n_inter/n_union;
  * `inter`/`uni` may be NULL to query sizes (capacity n_tables is enough).   */

@@ -90,6 +90,7 @@ struct nemo_ctx {
   int32_t *d_ddepth = nullptr;
   uint32_t *d_dtopo = nullptr;       // g0 in Kahn order (DiffArgs::tpos ...)
   uint64_t miss_cap = 0;
+  uint64_t mrows_hint = 256, mrows_staged = 0;  // missing rows copied with the D masks (last call's count)
   // entries that share a label source share one computation: n_uniq distinct
   // sources, entry e's result is unique result dmap[e] (d_dmap on the device)
   uint32_t n_uniq = 0, *d_dmap = nullptr;
@@ -154,6 +155,16 @@ struct nemo_ctx {
   uint32_t *h_tpre = nullptr, *h_tpost = nullptr, *h_tasync = nullptr;
   uint64_t h_tpre_cap = 0, h_tpost_cap = 0, h_tasync_cap = 0;
   hipEvent_t ev_protos = nullptr, ev_red = nullptr, ev_diff = nullptr, ev_misc = nullptr;
+  const uint32_t *red_staged = nullptr;  // nemo_protos_stage's vector, copied into h_red behind ev_red
+  // The global tiers' worklist sizes [load (k_csr/k_topo), chains (k_chains_list/_big), protos
+  // (k_pg_*)] of the last full pass.  They are functions of the loaded corpus and the options
+  // alone (sizes, Kahn level counts, in-degree caps, chain counts: every pass recomputes the
+  // same), so once a pass's counts are known an empty tier is not launched at all (each of its
+  // ~10 empty launches cost ~6 us on the analysis stream).  Reset by a load and by any option.
+  uint32_t *h_tiers = nullptr;
+  hipEvent_t ev_tiers = nullptr;
+  bool tiers_pending = false, tiers_ok = false;
+  uint32_t tiers[3] = {0, 0, 0}, tiers_run = 0;
 
   // pinned upload staging (success flags, diff sources): reused once the
   // previous upload from the same buffer has landed (ev_up*)
@@ -343,6 +354,36 @@ static int ensure_event(nemo_ctx *c, hipEvent_t *e) {
   return NEMO_OK;
 }
 
+static void tiers_reset(nemo_ctx *c) {
+  c->tiers_ok = c->tiers_pending = false;
+  c->tiers_run = 0;
+}
+// tier k's worklist is known to be empty (no launch needed)
+static bool tier_empty(nemo_ctx *c, int k) {
+  if (!c->tiers_ok && c->tiers_pending && hipEventQuery(c->ev_tiers) == hipSuccess) {
+    for (int i = 0; i < 3; i++) c->tiers[i] = c->h_tiers[i];
+    c->tiers_ok = true;
+    c->tiers_pending = false;
+  }
+  return c->tiers_ok && c->tiers[k] == 0;
+}
+// after a pass that launched all three tiers: their list counts to pinned host memory
+static int tiers_capture(nemo_ctx *c, hipStream_t s) {
+  if (c->tiers_ok || c->tiers_pending || c->tiers_run != 7u || !c->G) return NEMO_OK;
+  if (!c->h_tiers) HIPCHK(c, hipHostMalloc((void **)&c->h_tiers, 16));
+  int rc;
+  if ((rc = ensure_event(c, &c->ev_tiers))) return rc;
+  const size_t L = (size_t)c->G + 1;
+  nemo::HostCopies hc;
+  hc.add(c->h_tiers + 0, c->dc.sel + 2 * L, 4);
+  hc.add(c->h_tiers + 1, c->dc.sel + L, 4);
+  hc.add(c->h_tiers + 2, c->dc.sel + 3 * L, 4);
+  nemo::launch_to_host_multi(hc, s);
+  HIPCHK(c, hipEventRecord(c->ev_tiers, s));
+  c->tiers_pending = true;
+  return NEMO_OK;
+}
+
 // `stream` waits for the diff kernels queued on `aux` (see nemo_ctx::aux)
 static int join_aux(nemo_ctx *c) {
   if (!c->aux_pending) return NEMO_OK;
@@ -449,6 +490,7 @@ int nemo_ctx_create(int device, nemo_ctx **out) {
 }
 
 static void release_corpus(nemo_ctx *c) {
+  tiers_reset(c);
   drop_cache(c);  // blocks no allocation took since the last load
   for (void *p : c->allocs) {  // kept for the next load
     auto b = c->alloc_bytes.find(p);
@@ -552,6 +594,8 @@ void nemo_ctx_destroy(nemo_ctx *c) {
     if (e) hipEventDestroy(e);
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
+  if (c->h_tiers) hipHostFree(c->h_tiers);
+  if (c->ev_tiers) hipEventDestroy(c->ev_tiers);
   if (c->aux) hipStreamDestroy(c->aux);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->own) hipStreamDestroy(c->own);
@@ -570,6 +614,7 @@ int nemo_set_stream(nemo_ctx *c, void *stream) {
 int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   DISPATCH(node_set_option(c, name, value));
   if (!c || !name) return NEMO_ERR_INVALID;
+  tiers_reset(c);  // any option may move graphs between tiers
   if (!strcmp(name, "chains_lds_max")) {
     c->hcap_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.hcap_limit = c->hcap_limit;
@@ -818,12 +863,16 @@ static int device_load(nemo_ctx *c) {
     return rc;
   // graphs past k_build: k_csr (one workgroup per graph) below NEMO_CSR_BIG nodes, k_csrb_* above
   const double Eg = std::max(0.0, E - c->bigE), Vg = std::max(0.0, V - c->bigV);
-  if ((rc = timed(c, "k_csr", 16 * Eg + 12 * Vg, Eg, [&] { nemo::launch_load(c->dc, c->stream); }))) return rc;
+  const bool load_tier = !tier_empty(c, 0);
+  if (load_tier && (rc = timed(c, "k_csr", 16 * Eg + 12 * Vg, Eg, [&] { nemo::launch_load(c->dc, c->stream); })))
+    return rc;
+  if (load_tier) c->tiers_run |= 1u;
   if (c->dc.n_big &&
       (rc = timed(c, "k_csrb", 16 * c->bigE + 12 * c->bigV, c->bigE,
                   [&] { nemo::launch_csr_big(c->dc, c->big_chunks, c->stream); })))
     return rc;
-  if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream); }))) return rc;
+  if ((rc = timed(c, "k_topo", 4 * E + 16 * V, E, [&] { nemo::launch_topo(c->dc, c->stream, load_tier); })))
+    return rc;
   // the multi-entry diff's relayout of run 0's post graph and its walk images
   // are built by the first diffprov after a load (nemo_rebuild re-derives the
   // same graph: a relayout built from an earlier Kahn order of it stays valid)
@@ -1253,8 +1302,11 @@ int nemo_simplify(nemo_ctx *c) {
   }
   const double V = (double)c->V, E = (double)c->E;
   // reads: flags 1 + Kahn level 4 + node word 4 (+ ID rank 4) per node, the edge list 8 per edge
-  rc = timed(c, "k_chains", (c->has_rank ? 13 : 9) * V + 8 * E, 0, [&] { nemo::launch_chains(c->dc, c->stream); });
+  const bool chain_tiers = !tier_empty(c, 1);
+  rc = timed(c, "k_chains", (c->has_rank ? 13 : 9) * V + 8 * E, 0,
+             [&] { nemo::launch_chains(c->dc, c->stream, chain_tiers); });
   if (rc) return rc;
+  if (chain_tiers) c->tiers_run |= 2u;
   if ((rc = ensure_event(c, &c->ev_simp))) return rc;
   HIPCHK(c, hipEventRecord(c->ev_simp, c->stream));  // a simplified pull on `aux` starts here
   c->simplified = true;
@@ -1270,6 +1322,10 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   if (!c->simplified) return fail(c, NEMO_ERR_STATE, "nemo_protos_partial before nemo_simplify");
   if (!d_red) d_red = c->d_red;  // single-process callers use the context's own vector
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->red_staged) {  // a staged copy of an older vector: wait for it, then forget it
+    HIPCHK(c, hipEventSynchronize(c->ev_red));
+    c->red_staged = nullptr;
+  }
   if (!c->ev_up_succ) HIPCHK(c, hipEventCreateWithFlags(&c->ev_up_succ, hipEventDisableTiming));
   else HIPCHK(c, hipEventSynchronize(c->ev_up_succ));  // the previous upload has landed
   int rg = hgrow(c, &c->h_succ, &c->h_succ_cap, std::max<uint64_t>(c->n_runs, 1));
@@ -1289,8 +1345,11 @@ int nemo_protos_partial(nemo_ctx *c, const uint32_t *success_iters, size_t n_suc
   // waits for the copy's blit to drain); the reduction's inputs follow it
   // post graphs only (HBM lower bound): edges in source Kahn order 4E, node word 4V, flags 1V
   const double V = c->postV, E = c->postE;
-  int rc = timed(c, "k_proto", 4 * E + 5 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s); });
+  const bool proto_tier = !tier_empty(c, 2);
+  int rc = timed(c, "k_proto", 4 * E + 5 * V, 2 * E, [&] { nemo::launch_proto(c->dc, s, proto_tier); });
   if (rc) return rc;
+  if (proto_tier) c->tiers_run |= 4u;
+  if ((rc = tiers_capture(c, s))) return rc;
   nemo::launch_to_host(c->d_is_success, succ, c->n_runs, s);  // pinned -> device by a copy kernel (no blit queue)
   HIPCHK(c, hipEventRecord(c->ev_up_succ, s));
   nemo::launch_zero(d_red, nemo_reduce_len(c) * 4, s);
@@ -1333,6 +1392,27 @@ int nemo_reduce_interpret(const uint32_t *red, uint32_t T, uint32_t table_post, 
   return NEMO_OK;
 }
 
+static int protos_stage(nemo_ctx *c, const uint32_t *d_red) {
+  int rc;
+  if ((rc = ensure_event(c, &c->ev_red))) return rc;
+  if (c->red_staged) HIPCHK(c, hipEventSynchronize(c->ev_red));  // h_red may be in flight
+  if ((rc = hgrow(c, &c->h_red, &c->h_red_cap, 2 * (uint64_t)c->T + 4))) return rc;
+  nemo::launch_to_host(c->h_red, d_red, (2 * (uint64_t)c->T + 4) * 4, c->stream);
+  HIPCHK(c, hipEventRecord(c->ev_red, c->stream));
+  c->red_staged = d_red;
+  return NEMO_OK;
+}
+
+int nemo_protos_stage(nemo_ctx *c, const uint32_t *d_red) {
+  if (!c) return NEMO_ERR_INVALID;
+  if (c->node) return NEMO_OK;  // the node context reduces inside nemo_protos_finalize
+  if (!d_red) d_red = c->d_red;
+  if (!d_red) return fail(c, NEMO_ERR_STATE, "nemo_protos_stage before nemo_load_corpus");
+  if (!c->protos_done) return fail(c, NEMO_ERR_STATE, "nemo_protos_stage before nemo_protos_partial");
+  HIPCHK(c, hipSetDevice(c->device));
+  return protos_stage(c, d_red);
+}
+
 int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved, uint32_t *inter,
                          uint32_t *n_inter, uint32_t *uni, uint32_t *n_union, uint64_t *pre_holds,
                          uint32_t *n_runs_total) {
@@ -1343,11 +1423,9 @@ int nemo_protos_finalize(nemo_ctx *c, const uint32_t *d_red, uint32_t *achieved,
   HIPCHK(c, hipSetDevice(c->device));
   const uint32_t T = c->T;
   int rc;
-  if ((rc = ensure_event(c, &c->ev_red))) return rc;
-  if ((rc = hgrow(c, &c->h_red, &c->h_red_cap, 2 * (uint64_t)T + 4))) return rc;
-  nemo::launch_to_host(c->h_red, d_red, (2 * (uint64_t)T + 4) * 4, c->stream);
-  HIPCHK(c, hipEventRecord(c->ev_red, c->stream));
+  if (c->red_staged != d_red && (rc = protos_stage(c, d_red))) return rc;
   HIPCHK(c, hipEventSynchronize(c->ev_red));
+  c->red_staged = nullptr;  // consumed: the next finalize copies again unless staged again
   const uint32_t *red = c->h_red;
   if (pre_holds) *pre_holds = red[2 * T + 2];
   if (n_runs_total) *n_runs_total = red[2 * T + 3];
@@ -1614,9 +1692,14 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   if ((rc = ensure_event(c, &c->ev_diff))) return rc;
   if ((rc = hgrow(c, &c->h_mask, &c->h_mask_cap, n_failed * V0))) return rc;
   if ((rc = hgrow(c, &c->h_nmiss, &c->h_nmiss_cap, (uint64_t)1))) return rc;
+  // the missing rows too, at the last call's count: nemo_fetch_missing then needs no round
+  // trip of its own unless this call found more (d_miss holds n_failed (V0 + 1) rows)
+  c->mrows_staged = std::min<uint64_t>(c->mrows_hint, (uint64_t)n_failed * (V0 + 1));
+  if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * c->mrows_staged + 2))) return rc;
   nemo::HostCopies hc;
   hc.add(c->h_mask, c->d_dmask, n_failed * V0);
   hc.add(c->h_nmiss, c->d_nmiss, 4);
+  hc.add(c->h_mrows, c->d_miss, 8 * c->mrows_staged);
   nemo::launch_to_host_multi(hc, s);
   HIPCHK(c, hipEventRecord(c->ev_diff, s));
   c->aux_pending = true;
@@ -1733,13 +1816,16 @@ int nemo_fetch_missing(nemo_ctx *c, nemo_missing *out, uint64_t cap, uint64_t *n
   // rows of the distinct computations (unique index, rule), then one copy per entry
   int rc;
   if ((rc = ensure_event(c, &c->ev_misc))) return rc;
-  if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * (uint64_t)nu_rows + 2))) return rc;
-  const uint32_t *rows = c->h_mrows;
-  if (nu_rows) {
+  if (nu_rows > c->mrows_staged) {  // more rows than diffprov copied with the masks
+    if ((rc = hgrow(c, &c->h_mrows, &c->h_mrows_cap, 2 * (uint64_t)nu_rows + 2))) return rc;
+    if ((rc = join_aux(c))) return rc;
     nemo::launch_to_host(c->h_mrows, c->d_miss, 8ull * nu_rows, c->stream);
     HIPCHK(c, hipEventRecord(c->ev_misc, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev_misc));
+    c->mrows_staged = nu_rows;
   }
+  c->mrows_hint = std::max<uint64_t>(256, nu_rows);
+  const uint32_t *rows = c->h_mrows;
   std::vector<std::vector<uint32_t>> per(c->n_uniq);
   for (uint32_t i = 0; i < nu_rows; i++) per[rows[2 * i]].push_back(rows[2 * i + 1]);
   uint64_t n = 0;
@@ -2097,10 +2183,15 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
-  if (!c->pull_synced) HIPCHK(c, hipEventSynchronize(c->ev_pull));  // pinned slot table still in flight
+  const uint32_t slots = which == 2 ? c->n_entries : c->G;
+  // the previous pull's slot table may still be in flight into the pinned tables: wait for it
+  // only when they are about to be reallocated (a pull queued behind another on the same
+  // stream overwrites the device tables in order; the host reads them in pull_sync after the
+  // last pull's event)
+  if (!c->pull_synced && (slots + 1 > c->pull_slot_cap || slots + 1 > c->h_pslot_cap))
+    HIPCHK(c, hipEventSynchronize(c->ev_pull));
   c->pull_synced = true;
   if (which == 2 && (rc = join_aux(c))) return rc;  // the D masks
-  const uint32_t slots = which == 2 ? c->n_entries : c->G;
   // diff entries sharing a label source have one D mask, hence one graph: it is
   // compacted once and their slots share its region (pull_sync expands the table)
   const bool share = which == 2 && c->n_uniq < c->n_entries;
@@ -2161,6 +2252,7 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
     a.maxck = (uint32_t)(2 * ((c->bigVmax + 4095) / 4096));
     const size_t need = (size_t)rows * a.maxck;
     if (need > c->pull_ck_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));  // a previous pull may still use the chunk table
       dfree(c, c->d_pck);
       c->d_pck = nullptr;
       c->pull_ck_cap = 0;

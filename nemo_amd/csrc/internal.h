@@ -149,17 +149,17 @@ struct TrigArgs {
 __host__ __device__ uint32_t build_tier_bytes(uint32_t v, uint32_t e);
 void launch_build(const DevCorpus &c, hipStream_t s);
 void launch_load(const DevCorpus &c, hipStream_t s);
-void launch_topo(const DevCorpus &c, hipStream_t s);
+void launch_topo(const DevCorpus &c, hipStream_t s, bool list = true);
 void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s);
 // per_graph false: no graph below NEMO_CSR_BIG is past the skipped tier (host count), so only the big-graph kernels run
 void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
 void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
 void launch_marksimp(const DevCorpus &c, hipStream_t s);
-void launch_chains(const DevCorpus &c, hipStream_t s);
+void launch_chains(const DevCorpus &c, hipStream_t s, bool tiers = true);
 void launch_chains_glob(const DevCorpus &c, hipStream_t s);
 uint64_t glob_words(uint64_t V, uint64_t E);  // k_chains_glob scratch of one graph (u32)
 uint32_t glob_team_words();                   // k_glob_prep's team scratch (u32)
-void launch_proto(const DevCorpus &c, hipStream_t s);
+void launch_proto(const DevCorpus &c, hipStream_t s, bool tiers = true);
 void launch_reduce(const DevCorpus &c, const uint8_t *is_success, const uint8_t *owned, uint32_t first_run,
                    uint32_t *red, hipStream_t s);
 void launch_diff(const DevCorpus &c, const DiffArgs &a, uint32_t n_entries, uint32_t V0, hipStream_t s);
@@ -183,7 +183,7 @@ void launch_pack_state(const uint8_t *flags, uint32_t *out, uint64_t V, hipStrea
 void launch_chain_gather(const DevCorpus &c, uint64_t *off, uint32_t *out, hipStream_t s);
 void launch_triggers(const DevCorpus &c, const TrigArgs &a, int phase, hipStream_t s);
 void launch_goal_labels(const DevCorpus &c, uint32_t g, uint32_t *out, hipStream_t s);
-void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 1024);
+void launch_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t s, uint32_t max_blocks = 64);
 struct HostCopy {
   uint8_t *dst;
   const uint8_t *src;

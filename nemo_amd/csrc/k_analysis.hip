@@ -1013,12 +1013,12 @@ void launch_marksimp(const DevCorpus &c, hipStream_t s) {
   hipFuncSetAttribute((const void *)k_marksimp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
   hipLaunchKernelGGL(k_marksimp, dim3(c.G), dim3(MS_BLOCK), b, s, c);
 }
-void launch_proto(const DevCorpus &c, hipStream_t s) {
+void launch_proto(const DevCorpus &c, hipStream_t s, bool tiers) {
   if (c.lds_bytes) {
     hipFuncSetAttribute((const void *)k_proto_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
     hipLaunchKernelGGL(k_proto_lds, dim3(c.n_runs), dim3(PROTO_BLOCK), c.lds_bytes, s, c);
   }
-  if (!c.n_runs) return;
+  if (!c.n_runs || !tiers) return;  // !tiers: the host knows the global tier's list is empty
   launch_zero(proto_list(c), sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_proto_sel, dim3((c.n_runs + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
   const dim3 grid(c.pg_chunks, std::min(c.n_runs, 256u));

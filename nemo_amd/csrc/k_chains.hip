@@ -1241,9 +1241,13 @@ __global__ __launch_bounds__(NEMO_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 }
 
 #define CHAINS_GRID 1024u
-void launch_chains(const DevCorpus &c, hipStream_t s) {
+void launch_chains(const DevCorpus &c, hipStream_t s, bool tiers) {
   if (!c.G) return;
   hipLaunchKernelGGL((k_chains<CH_HCAP, 120>), dim3(c.G), dim3(NEMO_BLOCK), 0, s, c);
+  if (!tiers) {  // the host knows the first tier hands nothing back (api.hip tiers_known)
+    launch_chains_glob(c, s);
+    return;
+  }
   launch_zero(c.sel + c.G + 1, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_chains_sel, dim3((c.G + NEMO_BLOCK - 1) / NEMO_BLOCK), dim3(NEMO_BLOCK), 0, s, c);
   hipLaunchKernelGGL((k_chains_list<2048, 512>), dim3(std::min(c.G, CHAINS_GRID)), dim3(NEMO_BLOCK), 0, s, c);

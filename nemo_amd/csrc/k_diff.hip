@@ -1133,12 +1133,17 @@ __global__ __launch_bounds__(NEMO_BLOCK) void k_to_host_multi(HostCopies h) {
   }
 }
 
+// PCIe-bound copies: a few dozen workgroups keep the link busy (each lane's 16-byte store to
+// host memory is microseconds in flight); a 1024-block grid of them held every CU's wave slots
+// for the ~100 us of the reference-mode D-mask copy, and the analysis stream's next kernel
+// (k_chains) could not start beside it
+#define TO_HOST_BLOCKS 64u
 void launch_to_host_multi(const HostCopies &h, hipStream_t s) {
   uint64_t blocks = 1;
   for (uint32_t k = 0; k < h.n; k++)
     blocks = std::max<uint64_t>(blocks, (h.seg[k].n + 16ull * NEMO_BLOCK - 1) / (16ull * NEMO_BLOCK));
   if (!h.n) return;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > TO_HOST_BLOCKS) blocks = TO_HOST_BLOCKS;
   hipLaunchKernelGGL(k_to_host_multi, dim3((uint32_t)blocks, h.n), dim3(NEMO_BLOCK), 0, s, h);
 }
 

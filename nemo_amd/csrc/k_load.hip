@@ -1310,10 +1310,11 @@ void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s) {
   hipLaunchKernelGGL(k_csrb_rows, grid, dim3(CSRB_BLOCK), 0, s, c);
   hipLaunchKernelGGL(k_csrb_fin, dim3((c.n_big + CSRB_BLOCK - 1) / CSRB_BLOCK), dim3(CSRB_BLOCK), 0, s, c);
 }
-void launch_topo(const DevCorpus &c, hipStream_t s) {  // after launch_load: its list
+void launch_topo(const DevCorpus &c, hipStream_t s, bool list) {  // after launch_load: its list
   if (!c.G) return;
   const uint32_t grid = std::min(c.G, LOAD_GRID);
-  if (c.gblock == 1024)
+  if (!list) {  // the host knows the list is empty (api.hip tiers_known)
+  } else if (c.gblock == 1024)
     hipLaunchKernelGGL(k_topo<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
     hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);

@@ -80,6 +80,7 @@ def lib():
             "nemo_simplify": ([vp], i32),
             "nemo_reduce_len": ([vp], sz),
             "nemo_protos_partial": ([vp, vp, sz, vp], i32),
+            "nemo_protos_stage": ([vp, vp], i32),
             "nemo_protos_finalize": ([vp, vp, P(u32), vp, P(u32), vp, P(u32), P(u64), P(u32)], i32),
             "nemo_fetch_reduce": ([vp, vp, u64], i32),
             "nemo_prototypes": ([vp, vp, sz, P(u32), vp, P(u32), vp, P(u32)], i32),
@@ -218,6 +219,10 @@ class Engine:
         out = np.zeros(n, np.uint32)
         self._chk(self.L.nemo_fetch_reduce(self.h, _p(out), n))
         return out
+
+    def protos_stage(self, d_reduce_ptr: int) -> None:
+        """nemo_protos_stage: queue the (reduced) vector's D2H now; protos_finalize then only waits."""
+        self._chk(self.L.nemo_protos_stage(self.h, ctypes.c_void_p(d_reduce_ptr)))
 
     def protos_finalize(self, d_reduce_ptr: int):
         T = self.corpus.n_tables

@@ -590,3 +590,48 @@ def test_stage_and_diff_streams(eng, stage_aux, diff_aux):
     finally:
         eng.set_option("stage_aux", 1)
         eng.set_option("diff_aux", 1)
+
+
+@pytest.mark.parametrize("knobs", [(), (("chains_lds_max", 12), ("chains_comp_max", 5), ("graph_lds_max", 30),
+                                        ("build_lds_max", 30))])
+def test_repeated_passes_tier_cache(eng, knobs):
+    """The global tiers' list sizes are captured after the first full pass and an empty tier is not launched
+    afterwards (api.hip tier_empty).  Several passes (rebuild, mark, simplify, protos, diff, triggers, pulls) over
+    one loaded corpus, with every tier empty (library defaults) and with every tier taking graphs (small LDS caps),
+    each pass equal to the oracle; then an option change (which resets the cache) and one more pass."""
+    import random
+    from tests.small import random_prov
+    from tools import synth
+    rng = random.Random(3)
+    graphs = [(it, "success" if it == 0 or rng.random() < 0.7 else "failure",
+               random_prov(rng, "pre", 40, p_edge=0.2, p_next=0.9), random_prov(rng, "post", 40, p_edge=0.2, p_next=0.9))
+              for it in range(30)]
+    corpus = corpus_from_graphs(graphs) if knobs else synth.generate(30, target_nodes=2000, p_fault=0.4)[0]
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, diff_mode=DIFF_PER_RUN)
+    for k, v in knobs:
+        eng.set_option(k, v)
+    try:
+        eng.load(corpus)
+        for p in range(4):
+            if p == 3:
+                eng.set_option("global_block", 256)  # resets the cache: the tiers run again
+            eng.rebuild()
+            eng.mark()
+            eng.simplify()
+            achieved, inter, uni = eng.prototypes(s)
+            eng.diffprov(f, DIFF_PER_RUN)
+            eng.triggers()
+            eng.pull(1)
+            off, cnt, src, dst = eng.pulled_all(corpus.n_graphs)
+            pulled = [(src[int(a):int(a) + int(n)], dst[int(a):int(a) + int(n)]) for a, n in zip(off, cnt)]
+            pre, post, asy = eng.trigger_rows()
+            res = E.EngineResult(flags=eng.flags(), chains=eng.chains(), proto_bits=eng.run_tables(0),
+                                 graph_tables=eng.run_tables(1), achieved=achieved, inter=inter, union=uni,
+                                 diff_mask=eng.diff_masks(len(f)), missing=eng.missing(), pre_rows=pre,
+                                 post_rows=post, async_rules=asy, pulled=pulled)
+            assert_same(corpus, res, orc, len(f))
+    finally:
+        for k, _ in knobs:
+            eng.set_option(k, -1)
+        eng.set_option("global_block", -1)

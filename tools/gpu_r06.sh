@@ -18,3 +18,29 @@ bench)
   python -c "import json;d=json.load(open('gpurun_out/${tag}_bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'])" ;;
 esac
 echo part $1 done
+case "$1" in
+perrun)
+  timeout -k 10 400 python -u bench.py --diff-mode per_run --no-cpu-baseline --e2e-runs 0 > gpurun_out/${tag}_perrun.json 2> gpurun_out/${tag}_perrun.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_perrun.json'));r=d['roofline_diff'];print(d['value'],d['ms_per_step'],r['avg_launch_ms'],r['frac'])" ;;
+c5)
+  timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5.json 2> gpurun_out/${tag}_c5.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5.json'));print(d['value'],d['ms_per_step'],d['roofline_diff']['avg_launch_ms']);[print(k,v) for k,v in d['kernels'].items()]" ;;
+esac
+case "$1" in
+host)
+  timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_host.txt 2>&1 || exit 1
+  cat gpurun_out/${tag}_host.txt ;;
+trace)
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o kt --output-format csv -- python3 bench.py --no-cpu-baseline --e2e-runs 0 --steps 4 --diff-reps 0 > gpurun_out/${tag}_trace.log 2>&1 || exit 1
+  python tools/timeline.py $(find gpurun_out/${tag}_trace -name "kt_kernel_trace.csv" | head -1) > gpurun_out/${tag}_timeline.txt || exit 1
+  tail -3 gpurun_out/${tag}_timeline.txt ;;
+esac
+case "$1" in
+hostab)
+  timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostA.txt 2>&1 || exit 1
+  STAGE_FIRST=1 timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostB.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostA2.txt 2>&1 || exit 1
+  STAGE_FIRST=1 timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostB2.txt 2>&1 || exit 1
+  grep "ms per step" gpurun_out/${tag}_host*.txt ;;
+esac
