@@ -62,6 +62,8 @@ struct nemo_ctx {
   uint32_t gblock_force = 0;         // global_block option (0 = by corpus shape)
   uint32_t glob_block_force = 0;     // chains_glob_block option (0 = by the number of deep graphs)
   bool glob_prep_off = false;        // chains_glob_prep option 0: k_chains_glob builds its own H* order (test knob)
+  bool topo_ell_off = true;          // topo_ell option 1: deep graphs' Kahn levels by k_topo_ell (measured slower
+                                     // at C5: 103 vs 84 ms per launch with its records; kept as an option, tested)
   double tierV = 0, tierE = 0;       // nodes / edges of the graphs within the tier's V/E caps
   bool diff_on_aux = true;           // diff kernels on `aux` beside the simplification (option diff_aux)
   uint32_t ms_rest = 0, pull_rest = 0;  // graphs past k_marksimp's / k_pull_lds's tiers (their global grids skipped at 0)
@@ -188,6 +190,11 @@ struct nemo_ctx {
   // beside the protos and hand-over kernels of `stream`; anything that rewrites its inputs
   // first waits for ev_auxpull
   hipEvent_t ev_simp = nullptr, ev_auxpull = nullptr;
+  // recorded by nemo_simplify once the node flags are final (after the mark / clean / delete-set
+  // kernels, before the chain cover, which only reads them): the staged 2-bit node state is
+  // packed and copied from there on, beside the chain cover (nemo_stage_simplified)
+  hipEvent_t ev_flags = nullptr, ev_state = nullptr;
+  bool flags_final = false;  // ev_flags marks the current flags (no flag-rewriting call since)
   // the hand-over kernels of nemo_stage_simplified on `aux` (option stage_aux, default on):
   // behind everything `stream` has queued so far, beside the triggers and pulls queued after
   hipEvent_t ev_stage = nullptr;
@@ -303,6 +310,7 @@ static hipEvent_t get_event(nemo_ctx *c) {
 
 // Kernels that rewrite node flags must not overtake a staged copy still in flight.
 static int guard_staged(nemo_ctx *c) {
+  c->flags_final = false;  // the caller is about to rewrite node flags
   if (c->staged) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));
   if (c->pull_aux_pending) {  // a pull on `aux` still reads the graphs, flags and chains
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_auxpull, 0));
@@ -491,6 +499,7 @@ int nemo_ctx_create(int device, nemo_ctx **out) {
 
 static void release_corpus(nemo_ctx *c) {
   tiers_reset(c);
+  c->flags_final = false;
   drop_cache(c);  // blocks no allocation took since the last load
   for (void *p : c->allocs) {  // kept for the next load
     auto b = c->alloc_bytes.find(p);
@@ -590,7 +599,8 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   for (void *h : {(void *)c->h_red, (void *)c->h_tab, (void *)c->h_nmiss, (void *)c->h_mrows, (void *)c->h_mask,
                   (void *)c->h_tpre, (void *)c->h_tpost, (void *)c->h_tasync})
     if (h) hipHostFree(h);
-  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc, c->ev_simp, c->ev_auxpull, c->ev_stage})
+  for (hipEvent_t e : {c->ev_protos, c->ev_red, c->ev_diff, c->ev_misc, c->ev_simp, c->ev_auxpull, c->ev_stage,
+                       c->ev_flags, c->ev_state})
     if (e) hipEventDestroy(e);
   if (c->h_dsrc) hipHostFree(c->h_dsrc);
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
@@ -678,6 +688,11 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "diff_fuse")) {  // test knob: 0 runs k_dx_lp / k_dx_emit after whole-graph walks too
     c->diff_unfused = value == 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "topo_ell")) {  // 1: k_topo_ell for the deep graphs (child records); 0 / -1: k_topo_deep
+    c->topo_ell_off = value <= 0;
+    c->dc.topo_ell = c->topo_ell_off ? 0u : 1u;
     return NEMO_OK;
   }
   if (!strcmp(name, "chains_glob_prep")) {  // 0: no k_glob_prep (the per-graph front phases); takes effect at the next load
@@ -998,6 +1013,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     d.glob_list = dgl;
     d.n_glob = (uint32_t)gl.size();
     d.glob_prep = !gl.empty() && !c->has_rank && !c->glob_prep_off;
+    d.topo_ell = c->topo_ell_off ? 0u : 1u;
     d.team = nullptr;
     A(d.team, nemo::glob_team_words());
     int ncu = 0;
@@ -1300,6 +1316,9 @@ int nemo_simplify(nemo_ctx *c) {
     rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, false, c->stream); });
     if (rc) return rc;
   }
+  if ((rc = ensure_event(c, &c->ev_flags))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev_flags, c->stream));  // the flags are final (the chain cover reads them)
+  c->flags_final = true;
   const double V = (double)c->V, E = (double)c->E;
   // reads: flags 1 + Kahn level 4 + node word 4 (+ ID rank 4) per node, the edge list 8 per edge
   const bool chain_tiers = !tier_empty(c, 1);
@@ -1968,8 +1987,40 @@ int nemo_fetch_chains(nemo_ctx *c, nemo_chain *out, uint64_t cap, uint64_t *n_ou
   return NEMO_OK;
 }
 
-// Enqueue the chain pairs at a capacity of `cap` pairs and the two bulk copies
-// (node flags, pairs) on the copy stream.
+// bulk D2H on the copy stream: the runtime's copies (SDMA if asked, else its blit kernel on the
+// copy stream's CUs) or a k_to_host grid of stage_blocks workgroups
+static hipError_t stage_copy(nemo_ctx *c, void *dst, const void *src, size_t n) {
+  if (!n) return hipSuccess;
+  if (c->stage_blocks) {
+    nemo::launch_to_host(dst, src, n, c->copy, c->stage_blocks);
+    return hipGetLastError();
+  }
+  if (c->stage_sdma) {
+    if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->copy) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    c->stage_sdma = false;
+  }
+  return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->copy);
+}
+
+// The 2-bit node state on stream s and its copy; s has reached the point where the flags are final.
+static int stage_state(nemo_ctx *c, hipStream_t s) {
+  int rc;
+  const uint64_t sbytes = 4 * ((c->V + 15) / 16);  // 2-bit node state
+  if (!c->d_state && (rc = dalloc(c, &c->d_state, sbytes / 4 + 1))) return rc;
+  rc = timed_on(c, s, "k_pack_state", (double)c->V + (double)sbytes, 0,
+                [&] { nemo::launch_pack_state(c->dc.flags, c->d_state, c->V, s); });
+  if (rc) return rc;
+  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, sbytes + 16))) return rc;
+  if ((rc = ensure_event(c, &c->ev_state))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev_state, s));
+  HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_state, 0));
+  HIPCHK(c, stage_copy(c, c->h_flags, c->d_state, sbytes));
+  return NEMO_OK;
+}
+
+// Enqueue the chain pairs at a capacity of `cap` pairs and their bulk copy on the copy stream
+// (behind the node state's, which stage_state queued first).
 static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
   int rc;
   hipStream_t s = c->stage_stream ? c->stage_stream : c->stream;
@@ -1982,35 +2033,14 @@ static int stage_enqueue(nemo_ctx *c, uint64_t cap) {
     if ((rc = dalloc(c, &c->d_chht, pw * cap + 2))) return rc;
     c->d_chht_cap = pw * cap + 2;
   }
-  const uint64_t sbytes = 4 * ((c->V + 15) / 16);  // 2-bit node state
-  if (!c->d_state && (rc = dalloc(c, &c->d_state, sbytes / 4 + 1))) return rc;
   rc = timed_on(c, s, "k_chain_pairs", 4.0 * pw * (double)cap + 20.0 * c->G, 0,
                 [&] { nemo::launch_chain_pairs(c->dc, c->d_choff, c->d_chht, cap, c->pairs_wide ? 1 : 0, s); });
   if (rc) return rc;
-  rc = timed_on(c, s, "k_pack_state", (double)c->V + (double)sbytes, 0,
-                [&] { nemo::launch_pack_state(c->dc.flags, c->d_state, c->V, s); });
-  if (rc) return rc;
-  if ((rc = hgrow(c, &c->h_flags, &c->h_flags_cap, sbytes + 16))) return rc;
   if ((rc = hgrow(c, &c->h_chht, &c->h_chht_cap, pw * cap + 2))) return rc;
   nemo::launch_to_host(c->h_choff, c->d_choff, ((size_t)c->G + 1) * 8, s);
   HIPCHK(c, hipEventRecord(c->ev_ready, s));
   HIPCHK(c, hipStreamWaitEvent(c->copy, c->ev_ready, 0));
-  if (c->stage_blocks) {  // CU stores into pinned memory from a small grid beside the analysis
-    nemo::launch_to_host(c->h_flags, c->d_state, sbytes, c->copy, c->stage_blocks);
-    nemo::launch_to_host(c->h_chht, c->d_chht, pw * cap * 4, c->copy, c->stage_blocks);
-  } else {  // runtime copies: SDMA (the pinned buffers are device-addressable), else the runtime's blit kernel
-    auto copy = [&](void *dst, const void *src, size_t n) -> hipError_t {
-      if (!n) return hipSuccess;
-      if (c->stage_sdma) {
-        if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->copy) == hipSuccess) return hipSuccess;
-        (void)hipGetLastError();
-        c->stage_sdma = false;
-      }
-      return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->copy);
-    };
-    HIPCHK(c, copy(c->h_flags, c->d_state, sbytes));
-    HIPCHK(c, copy(c->h_chht, c->d_chht, pw * cap * 4));
-  }
+  HIPCHK(c, stage_copy(c, c->h_chht, c->d_chht, pw * cap * 4));
   HIPCHK(c, hipEventRecord(c->ev_copied, c->copy));
   c->staged_cap = cap;
   return NEMO_OK;
@@ -2045,10 +2075,20 @@ int nemo_stage_simplified(nemo_ctx *c) {
   if ((rc = hgrow(c, &c->h_choff, &c->h_choff_cap, (uint64_t)c->G + 1))) return rc;
   if (c->stage_on_aux) {  // read-only on the analysis: `stream` goes on to the triggers and pulls
     if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    // the node state from where nemo_simplify's flags were final (beside the chain cover), then
+    // the chain pairs from here (the chain cover and whatever the caller queued since)
+    if (!c->flags_final) {  // flags rewritten since nemo_simplify: pack them where `stream` is now
+      if ((rc = ensure_event(c, &c->ev_flags))) return rc;
+      HIPCHK(c, hipEventRecord(c->ev_flags, c->stream));
+    }
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_flags, 0));
+    if ((rc = stage_state(c, c->aux))) return rc;
     if ((rc = ensure_event(c, &c->ev_stage))) return rc;
     HIPCHK(c, hipEventRecord(c->ev_stage, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_stage, 0));
     s = c->aux;
+  } else if ((rc = stage_state(c, s))) {
+    return rc;
   }
   c->stage_stream = s;
   rc = timed_on(c, s, "k_chain_gather", 0, 0, [&] { nemo::launch_chain_gather(c->dc, c->d_choff, nullptr, s); });
@@ -2337,7 +2377,11 @@ int nemo_debug_copy(nemo_ctx *c, const char *name, void *out, uint64_t offset, u
   else if (n == "r0idx") base = c->d_r0idx;
   else if (n == "stamps") base = c->dc.stamps;
   else if (n == "sel") base = c->dc.sel;
-  else if (n == "redo") base = c->dc.redo;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
+  else if (n == "redo") base = c->dc.redo;
+  else if (n == "s_a") base = c->dc.s_a;
+  else if (n == "gscratch") base = c->dc.gscratch;
+  else if (n == "gs_off") base = c->dc.gs_off;
+  else if (n == "err") base = c->dc.err;  // worklists: [4][G+1] u32, count first (pulls, chains, load, protos)
   if (!base) return fail(c, NEMO_ERR_INVALID, "unknown array %s", name);
   HIPCHK(c, hipSetDevice(c->device));
   int rc = join_aux(c);  // the diff kernels on `aux` write dbits, dmask and the Kahn relayout

@@ -1631,9 +1631,20 @@ void launch_chains_glob(const DevCorpus &c, hipStream_t s) {
   if (!c.gscratch) return;
   if (c.glob_prep) {
     launch_zero(c.team, PT_TEAMS * PT_WORDS * sizeof(uint32_t), s);
-    // every member of a team must be resident at once (team barriers): one
-    // 1024-thread workgroup per CU, at most the device's CUs
-    const uint32_t m = std::max(1u, std::min<uint32_t>(PT_M, c.n_cu / PT_TEAMS));
+    // every member of a team must be resident at once (team barriers spin): the whole grid of
+    // PT_B-thread workgroups must fit the device's CUs at the kernel's occupancy, which the
+    // runtime reports; the grid never asks for more workgroups than that
+    static int occ = -1;
+    if (occ < 0) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_glob_prep, PT_B, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        n = 1;
+      }
+      occ = std::max(1, n);
+    }
+    const uint32_t fit = (uint32_t)occ * c.n_cu / PT_TEAMS;  // members per team the device holds at once
+    const uint32_t m = std::max(1u, std::min<uint32_t>({PT_M, c.n_cu / PT_TEAMS, fit}));
     hipLaunchKernelGGL(k_glob_prep, dim3(PT_TEAMS * m), dim3(PT_B), 0, s, c);
   }
   if (c.glob_block == 512)

@@ -845,6 +845,9 @@ __global__ __launch_bounds__(B) void k_topo(DevCorpus c) {
 // every child, ready or not), so a level starts from LDS instead of waiting on
 // an HBM round trip for its rows.  Frontier entries past TD_Q are read back
 // from topo[] and their rows loaded.
+__device__ __forceinline__ bool topo_ell_takes(const DevCorpus &c, uint32_t g) {
+  return c.topo_ell && c.gscratch && c.gs_off[g] != ~0ull;
+}
 __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   __shared__ uint2 s_q[2][TD_Q];
   // appends of level L go to s_n[(L + 1) % 3]: read after the level's barrier,
@@ -852,7 +855,7 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   __shared__ uint32_t s_n[3];
   __shared__ uint32_t s_eo[TD_B], s_j0[TD_B], s_red[TD_B / 64];
   const uint32_t g = c.big[blockIdx.x];
-  if (c.err[g]) return;
+  if (c.err[g] || topo_ell_takes(c, g)) return;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
   if ((build_fits(c, V, E) && !c.redo[g]) || V < CSR_LDS) return;
@@ -972,6 +975,172 @@ __global__ __launch_bounds__(TD_B) void k_topo_deep(DevCorpus c) {
   }
 }
 
+// Kahn levels of the deep graphs, one HBM round trip per level (round 6).  k_topo_deep's level is
+// two dependent round trips: the frontier's children (fc[] at the row starts it holds) and then
+// their in-degree atomics.  Here every node has a child record of TE_K u32 in its graph's
+// gscratch region (free at load time; k_chains_glob's until the next rebuild): its children
+// (NEMO_NONE padded), or for a longer row TE_OVF, its row start and degree.  The frontier holds
+// each node's record in LDS, so a level is: the frontier's children from the LDS records into an
+// LDS edge list (a round trip to fc[] only for a level holding a row past TE_K) -> one edge per
+// thread: its child's in-degree atomic and, in the same round trip, the child's record -> the
+// ready children appended with their records.  Edge-parallel as k_topo_deep: a long row is
+// spread over the lanes, not walked by one.
+#define TE_K 16
+#define TE_Q 256u    // LDS frontier records per buffer (2 x 256 x 64 B)
+#define TE_EL 4096u  // LDS edge list of a chunk of TD_B frontier nodes (longer: several passes)
+#define TE_OVF 0xFFFFFFFEu
+__global__ __launch_bounds__(NEMO_BLOCK) void k_topo_ellprep(DevCorpus c) {
+  const uint32_t g = c.big[blockIdx.y];
+  if (c.err[g] || !topo_ell_takes(c, g)) return;
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  if ((build_fits(c, V, E) && !c.redo[g]) || V < CSR_LDS) return;
+  const uint32_t *fp = c.fp + n0 + g, *fc = c.fc + e0;
+  uint4 *ell = reinterpret_cast<uint4 *>(c.gscratch + c.gs_off[g]);
+  for (uint32_t v = blockIdx.x * NEMO_BLOCK + threadIdx.x; v < V; v += gridDim.x * NEMO_BLOCK) {
+    const uint32_t a = fp[v], d = fp[v + 1] - a;
+    uint32_t r[TE_K];
+    if (d <= TE_K) {
+#pragma unroll
+      for (int k = 0; k < TE_K; k++) r[k] = (uint32_t)k < d ? fc[a + k] : NEMO_NONE;
+    } else {
+      r[0] = TE_OVF;
+      r[1] = a;
+      r[2] = d;
+#pragma unroll
+      for (int k = 3; k < TE_K; k++) r[k] = NEMO_NONE;
+    }
+#pragma unroll
+    for (int q = 0; q < TE_K / 4; q++)
+      ell[(TE_K / 4) * (size_t)v + q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+  }
+}
+
+__global__ __launch_bounds__(NEMO_BLOCK) void k_topo_ell(DevCorpus c) {
+  constexpr uint32_t RQ = TE_K / 4;  // uint4 per record
+  __shared__ uint4 s_q[2][TE_Q][RQ];
+  __shared__ uint32_t s_el[TE_EL];  // the chunk's children, by the exclusive degree offsets
+  // appends of level L go to s_n[(L + 1) % 3]: read after the level's barrier, reset during
+  // level L + 2, so one barrier per level orders everything (as k_topo_deep)
+  __shared__ uint32_t s_n[3], s_red[NEMO_BLOCK / 64];
+  const uint32_t g = c.big[blockIdx.x];
+  if (c.err[g] || !topo_ell_takes(c, g)) return;
+  const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
+  const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
+  if ((build_fits(c, V, E) && !c.redo[g]) || V < CSR_LDS) return;
+  const uint32_t *rp = c.rp + n0 + g, *fc = c.fc + e0;
+  const uint4 *ell = reinterpret_cast<const uint4 *>(c.gscratch + c.gs_off[g]);
+  uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g, *cnt = c.s_a + n0 + g, *nlv = c.nlv + n0;
+  const uint32_t tid = threadIdx.x;
+  if (tid < 3) s_n[tid] = 0;
+  if (tid == 0) lvl[0] = 0;
+  __syncthreads();
+  // level 0: the sources, with their records
+  for (uint32_t b = 0; b < V; b += NEMO_BLOCK) {
+    const uint32_t v = b + tid;
+    const uint32_t d = v < V ? rp[v + 1] - rp[v] : 1u;
+    if (v < V) cnt[v] = d;
+    const bool p = d == 0u;
+    const uint64_t m = __ballot(p);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&s_n[1], (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, 0);
+    if (p) {
+      const uint32_t i = base + mbcnt(m);
+      topo[i] = v;
+      nlv[v] = 0;
+      if (i < TE_Q)
+#pragma unroll
+        for (uint32_t q = 0; q < RQ; q++) s_q[0][i][q] = ell[RQ * (size_t)v + q];
+    }
+  }
+  __syncthreads();
+  uint32_t lo = 0, hi = s_n[1], nl = 0, cur = 0, k3 = 1;  // k3 = (nl + 1) % 3
+  while (lo < hi) {
+    const uint32_t n = hi - lo, kn = k3 == 2 ? 0u : k3 + 1u;  // this level's append counter
+    if (tid == 0) s_n[kn == 2 ? 0u : kn + 1u] = 0;            // = (nl + 3) % 3: free since level nl - 1
+    for (uint32_t b = 0; b < n; b += NEMO_BLOCK) {
+      const uint32_t i = b + tid;
+      uint32_t r[TE_K];
+#pragma unroll
+      for (int k = 0; k < TE_K; k++) r[k] = NEMO_NONE;
+      if (i < n) {  // (no arrays of uint4: they were kept in scratch)
+        const uint4 *src = i < TE_Q ? &s_q[cur][i][0] : nullptr;
+        const uint32_t u = i < TE_Q ? 0u : topo[lo + i];  // past the LDS frontier: the record from HBM
+#pragma unroll
+        for (uint32_t t = 0; t < RQ; t++) {
+          const uint4 x = src ? src[t] : ell[RQ * (size_t)u + t];
+          r[4 * t] = x.x, r[4 * t + 1] = x.y, r[4 * t + 2] = x.z, r[4 * t + 3] = x.w;
+        }
+      }
+      const bool ovf = r[0] == TE_OVF;
+      uint32_t d = 0;
+      if (!ovf) {
+#pragma unroll
+        for (int k = 0; k < TE_K; k++) d += r[k] != NEMO_NONE ? 1u : 0u;
+      } else {
+        d = r[2];
+      }
+      uint32_t tot;
+      const uint32_t eo = block_exscan<NEMO_BLOCK>(d, &tot, s_red);
+      // the chunk's children into the LDS edge list, TE_EL at a time (rows in order of eo)
+      for (uint32_t p0 = 0; p0 < tot; p0 += TE_EL) {
+        if (ovf) {  // a long row: its children from fc[] (every lane's loads in flight together)
+          const uint32_t a = max(eo, p0), z = min(eo + d, p0 + TE_EL);
+          for (uint32_t x = a; x < z; x += 8) {  // eight loads in flight, then their stores
+            uint32_t y[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) y[k] = x + k < z ? fc[r[1] + (x + k - eo)] : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+              if (x + k < z) s_el[x + k - p0] = y[k];
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < TE_K; k++) {
+            const uint32_t x = eo + k;
+            if ((uint32_t)k < d && x >= p0 && x < p0 + TE_EL) s_el[x - p0] = r[k];
+          }
+        }
+        __syncthreads();
+        const uint32_t ne = min(tot - p0, TE_EL);
+        // one edge per thread and round: the child's in-degree atomic and its record
+        for (uint32_t e = tid; e < ne; e += NEMO_BLOCK) {
+          const uint32_t ch = s_el[e];
+          const uint32_t old = atomicSub(&cnt[ch], 1u);
+          const uint4 c0 = ell[RQ * (size_t)ch], c1 = ell[RQ * (size_t)ch + 1];
+          const uint4 c2 = ell[RQ * (size_t)ch + 2], c3 = ell[RQ * (size_t)ch + 3];
+          static_assert(RQ == 4, "four uint4 per record");
+          if (old == 1u) {  // ready: a slot by one LDS atomic (a level has a few dozen)
+            const uint32_t at = atomicAdd(&s_n[kn], 1u);
+            topo[hi + at] = ch;
+            nlv[ch] = nl + 1;
+            if (at < TE_Q) {
+              s_q[cur ^ 1][at][0] = c0;
+              s_q[cur ^ 1][at][1] = c1;
+              s_q[cur ^ 1][at][2] = c2;
+              s_q[cur ^ 1][at][3] = c3;
+            }
+          }
+        }
+        __syncthreads();  // s_el is rewritten by the next pass / chunk
+      }
+    }
+    __syncthreads();
+    const uint32_t m = s_n[kn];
+    nl++;
+    lo = hi;
+    hi += m;
+    cur ^= 1;
+    k3 = kn;
+    if (tid == 0) lvl[nl] = lo;
+  }
+  if (tid == 0) {
+    c.nlev[g] = nl;
+    if (hi != V) c.err[g] = NEMO_ERR_CYCLE;
+  }
+}
 
 #define LOAD_GRID 2048u
 
@@ -1318,7 +1487,12 @@ void launch_topo(const DevCorpus &c, hipStream_t s, bool list) {  // after launc
     hipLaunchKernelGGL(k_topo<1024>, dim3(grid), dim3(1024), 0, s, c);
   else
     hipLaunchKernelGGL(k_topo<NEMO_BLOCK>, dim3(grid), dim3(NEMO_BLOCK), 0, s, c);
-  if (c.n_big) hipLaunchKernelGGL(k_topo_deep, dim3(c.n_big), dim3(TD_B), 0, s, c);
+  if (!c.n_big) return;
+  hipLaunchKernelGGL(k_topo_deep, dim3(c.n_big), dim3(TD_B), 0, s, c);  // graphs without child records
+  if (c.topo_ell && c.gscratch) {
+    hipLaunchKernelGGL(k_topo_ellprep, dim3(256, c.n_big), dim3(NEMO_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(k_topo_ell, dim3(c.n_big), dim3(NEMO_BLOCK), 0, s, c);
+  }
 }
 
 }  // namespace nemo

@@ -72,7 +72,20 @@ def wide_prov(cond: str, width: int, seed: int, hub: int = 0, cycle: bool = Fals
     return {"goals": goals, "rules": rules, "edges": edges}
 
 
-def test_wide_level_past_lds_frontier(eng):
+@pytest.fixture(params=["topo_deep", "topo_ell"])
+def kahn(request, eng):
+    """The big graphs' Kahn levels by k_topo_deep, or by k_topo_ell (child records in the deep-graph
+    scratch: every big graph gets one at chains_glob_min_v 0; records of 8 children, longer rows read
+    from fc[])."""
+    ell = request.param == "topo_ell"
+    eng.set_option("topo_ell", 1 if ell else 0)
+    eng.set_option("chains_glob_min_v", 0 if ell else 65536)
+    yield request.param
+    eng.set_option("topo_ell", -1)
+    eng.set_option("chains_glob_min_v", 65536)
+
+
+def test_wide_level_past_lds_frontier(eng, kahn):
     graphs = [(it, "success" if it != 2 else "failure", wide_prov("pre", 5000, it), wide_prov("post", 5000, 10 + it))
               for it in range(3)]
     corpus = corpus_from_graphs(graphs)
@@ -81,7 +94,7 @@ def test_wide_level_past_lds_frontier(eng):
     _check(eng, corpus, mode=DIFF_PER_RUN)
 
 
-def test_hub_out_degree(eng):
+def test_hub_out_degree(eng, kahn):
     graphs = [(it, "success" if it != 1 else "failure", wide_prov("pre", 2000, it, hub=300),
                wide_prov("post", 2000, 20 + it, hub=37)) for it in range(2)]
     corpus = corpus_from_graphs(graphs)
@@ -89,13 +102,39 @@ def test_hub_out_degree(eng):
     _check(eng, corpus)
 
 
-def test_cycle_in_big_graph_refused(eng):
+def test_cycle_in_big_graph_refused(eng, kahn):
     graphs = [(0, "success", wide_prov("pre", 3000, 1), wide_prov("post", 3000, 2, cycle=True))]
     corpus = corpus_from_graphs(graphs)
     assert corpus.graph_size(1) >= 8192
     with pytest.raises(E.NemoError) as ei:
         eng.load(corpus)
     assert ei.value.code == 4
+
+
+def test_topo_ell_same_levels_as_topo_deep(eng):
+    """k_topo_ell and k_topo_deep give the same Kahn level offsets and per-level node sets (the order within
+    a level depends on timing) on the C5 generator's shape (~4 children per rule, rows past 8 children)."""
+    import numpy as np
+    from tools import synth
+    corpus, _ = synth.generate(3, target_nodes=70000, eot=60, body_extra=6, nval=3, nloc=4, p_fault=0.5)
+    V, G = int(corpus.node_off[-1]), corpus.n_graphs
+    got = {}
+    for ell in (0, 1):
+        eng.set_option("topo_ell", ell)
+        try:
+            eng.load(corpus)
+            got[ell] = {k: eng.debug_copy(k, 0, n).view(np.uint32)
+                        for k, n in (("topo", 4 * V), ("lvl", 4 * (V + G)), ("nlev", 4 * G), ("nlv", 4 * V))}
+        finally:
+            eng.set_option("topo_ell", -1)
+    a, b = got[0], got[1]
+    assert np.array_equal(a["nlev"], b["nlev"]) and np.array_equal(a["lvl"], b["lvl"])
+    assert np.array_equal(a["nlv"], b["nlv"])
+    for g in range(G):
+        n0 = int(corpus.node_off[g])
+        off = a["lvl"][n0 + g: n0 + g + int(a["nlev"][g]) + 1]
+        for l0, l1 in zip(off[:-1], off[1:]):
+            assert sorted(a["topo"][n0 + l0:n0 + l1]) == sorted(b["topo"][n0 + l0:n0 + l1])
 
 
 def _inject(corpus, g, extra):

@@ -44,3 +44,17 @@ hostab)
   STAGE_FIRST=1 timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostB2.txt 2>&1 || exit 1
   grep "ms per step" gpurun_out/${tag}_host*.txt ;;
 esac
+case "$1" in
+hostab2)
+  timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostA.txt 2>&1 || exit 1
+  STAGE_FIRST=1 timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostB.txt 2>&1 || exit 1
+  NEMO_STAGE_SDMA=1 timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostC.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/step_host.py > gpurun_out/${tag}_hostA2.txt 2>&1 || exit 1
+  grep "ms per step" gpurun_out/${tag}_host*.txt ;;
+esac
+case "$1" in
+c5ab)
+  timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --diff-reps 2 > gpurun_out/${tag}_c5.json 2> gpurun_out/${tag}_c5.err || exit 1
+  timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --diff-reps 2 --set topo_ell=0 > gpurun_out/${tag}_c5_old.json 2> gpurun_out/${tag}_c5_old.err || exit 1
+  for f in gpurun_out/${tag}_c5.json gpurun_out/${tag}_c5_old.json; do python -c "import json,sys;d=json.load(open('$f'));print('$f',d['value'],d['ms_per_step'],{k:v['ms_total'] for k,v in d['kernels'].items() if k in ('k_topo','k_csrb','k_chains','k_proto')})"; done ;;
+esac

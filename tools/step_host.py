@@ -23,6 +23,8 @@ if success[0] != 0:
     success = [0] + [s for s in success if s != 0]
 eng = Engine(0)
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
+if os.environ.get("NEMO_STAGE_SDMA") == "1":
+    eng.set_option("stage_sdma", 1)
 eng.load(corpus)
 d_red = torch.zeros(eng.reduce_len(), dtype=torch.int32, device="cuda")
 fidx = np.array([corpus.run_index(f) for f in failed], np.int64)
