@@ -27,6 +27,7 @@ Launched as `python bench.py` (N=1) or under torch.distributed.run for N>1
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -63,8 +64,11 @@ def parse():
                     help="end-to-end leg (rank 0, N=1): runs of the same shape written as a Molly directory, then "
                          "streaming native ingest -> H2D -> analysis -> host results, pipelined by chunk (0: off)")
     ap.add_argument("--e2e-chunk", type=int, default=500)
-    ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
-                    help="off: the timed steps run without per-launch HIP events (two extra steps collect them)")
+    ap.add_argument("--kernel-timing", choices=["dominant", "on", "off"], default="dominant",
+                    help="dominant: every kernel group is timed with HIP events during the warmup steps, and the "
+                         "timed steps time only the dominant group (the roofline's kernel; an event pair costs the "
+                         "stream a few us per launch); on: every group in the timed steps too; off: the timed steps "
+                         "run without events (two extra steps collect them)")
     ap.add_argument("--stage-blocks", type=int, default=0, help="bulk D2H staging by a k_to_host grid of this size (0: runtime copies)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="N=1 only: the corpus run-sharded over this many libnemohip contexts on the one GPU, each "
@@ -257,36 +261,66 @@ def main():
 
     if lanes_n > 1:
         step = lambda: step_lanes(lanes, corpus, mode)  # noqa: E731
+
+    def gather_timings():
+        out = {}
+        for e in engines:  # per-launch figures of every lane (a lane's launch overlaps the others')
+            for k, v in e.timings().items():
+                a = out.setdefault(k, {"launches": 0, "ms": 0.0, "bytes": 0.0, "edges": 0.0})
+                for f in a:
+                    a[f] += v[f]
+        return out
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     hbm_used = free0 - torch.cuda.mem_get_info()[0]  # the resident corpus + every buffer a step grew
+    warm = None
+    if args.kernel_timing == "dominant" and args.warmup > 0:
+        # one more untimed step, every group timed: picks the dominant group and gives the per-group
+        # table (the first warmup step runs cold, so it is not the one measured)
+        for e in engines:
+            e.set_timing(True)
+            e.reset_timings()
+        step()
+        torch.cuda.synchronize()
+        warm = gather_timings()
+    dom_group = max(warm.items(), key=lambda kv: kv[1]["ms"])[0] if warm else None
     for e in engines:
-        e.set_timing(args.kernel_timing == "on")
+        e.set_timing(args.kernel_timing != "off")
+        e.set_timing_groups([dom_group] if dom_group else [])
         e.reset_timings()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # the host's cyclic garbage collector runs outside the timed steps (a full collection of the
+    # corpus' Python objects landed in a timed step and cost it ~15 ms)
+    gc.collect()
+    gc.disable()
     t_start = time.perf_counter()
+    step_ends = []
     for _ in range(args.steps):
         step()
+        step_ends.append(time.perf_counter())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    gc.enable()
+    step_ms = [round((b - a) * 1e3, 3) for a, b in zip([t_start] + step_ends[:-1], step_ends)]
     if args.kernel_timing == "off":
         for e in engines:
             e.set_timing(True)
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-    tim = {}
-    for e in engines:  # per-launch figures of every lane (a lane's launch overlaps the others')
-        for k, v in e.timings().items():
-            a = tim.setdefault(k, {"launches": 0, "ms": 0.0, "bytes": 0.0, "edges": 0.0})
-            for f in a:
-                a[f] += v[f]
+    tim = gather_timings()
+    for e in engines:
         e.set_timing(False)
+        e.set_timing_groups([])
+    # the per-group table and the traversed edges (algorithmic counts) come from the warmup steps when
+    # the timed steps timed only the dominant group; the roofline from the timed steps' own events
+    table, table_steps = (warm, 1) if dom_group else (tim, args.steps if args.kernel_timing != "off" else 2)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -298,15 +332,15 @@ def main():
         dist.all_reduce(t)
         total_runs = int(t.item())
     runs_per_s = total_runs * args.steps / elapsed
-    edges = sum(v["edges"] for v in tim.values())
+    edges = sum(v["edges"] for v in table.values()) * args.steps / max(table_steps, 1)
     if world > 1:
         t = torch.tensor([edges], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
         edges = float(t.item())
     # edges/s: edges examined by all traversal kernels of all ranks over the wall time
     edges_per_s = edges / elapsed
-    dom = max(tim.items(), key=lambda kv: kv[1]["ms"])
-    dname, d = dom
+    dname = dom_group or max(tim.items(), key=lambda kv: kv[1]["ms"])[0]
+    d = tim[dname]
     per_launch_bytes = d["bytes"] / d["launches"]
     avg_ms = d["ms"] / d["launches"]
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
@@ -364,7 +398,10 @@ def main():
         "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
                         "gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
-                    for k, v in sorted(tim.items(), key=lambda kv: -kv[1]["ms"])},
+                    for k, v in sorted(table.items(), key=lambda kv: -kv[1]["ms"])},
+        "kernel_timing": {"mode": args.kernel_timing, "timed_steps_groups": [dom_group] if dom_group else "all",
+                          "kernels_table_from": "one untimed step after the warmup" if dom_group else "the timed steps"},
+        "step_host_ms_rank0": step_ms,
         "gen_seconds_rank0": round(gen_s, 2),
         "hbm_used_gb_rank0": round(hbm_used / 1e9, 2),
         "diff_dedupe": "entries sharing a label source share one computation (reference mode: failedRuns[0] "
@@ -373,8 +410,8 @@ def main():
     if e2e is not None:
         out["e2e_runs_per_s"] = e2e["runs_per_s"]
         out["e2e"] = e2e
-    if "k_diff" in tim:  # all entries of a diffprov call run concurrently: the launch time is each entry's latency
-        out["k_diff_entry_latency_ms"] = round(tim["k_diff"]["ms"] / tim["k_diff"]["launches"], 4)
+    if "k_diff" in table:  # all entries of a diffprov call run concurrently: the launch time is each entry's latency
+        out["k_diff_entry_latency_ms"] = round(table["k_diff"]["ms"] / table["k_diff"]["launches"], 4)
     if rdiff is not None:
         out["roofline_diff"] = rdiff
     if rank == 0:

@@ -172,6 +172,11 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);
+/* Restrict the timing to these groups (comma-separated names as nemo_timings
+ * reports them, e.g. "k_build"); NULL or "" = every group.  An event pair
+ * costs the stream a few microseconds: a benchmark times only the kernel it
+ * prices against the roofline.                                              */
+int nemo_set_timing_groups(nemo_ctx *ctx, const char *groups);
 
 /* ---- load (loadProv, graphing/pre-post-prov.go:25-213) ---------------------
  * Copies the corpus to HBM, builds forward + reverse CSR and the topological

@@ -41,6 +41,7 @@ struct nemo_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   std::string err;
+  std::vector<std::string> tgroups;  // nemo_set_timing_groups: the timed groups (empty: all)
   bool timing = false;
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;
@@ -322,7 +323,9 @@ static int guard_staged(nemo_ctx *c) {
 template <class F>
 static int timed_on(nemo_ctx *c, hipStream_t st, const char *name, double bytes, double edges, F &&f) {
   hipEvent_t a = nullptr, b = nullptr;
-  if (c->timing) {
+  const bool timed = c->timing && (c->tgroups.empty() ||
+                                   std::find(c->tgroups.begin(), c->tgroups.end(), name) != c->tgroups.end());
+  if (timed) {
     a = get_event(c);
     b = get_event(c);
     hipEventRecord(a, st);
@@ -330,7 +333,7 @@ static int timed_on(nemo_ctx *c, hipStream_t st, const char *name, double bytes,
   f();
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(c, NEMO_ERR_HIP, "launch %s: %s", name, hipGetErrorString(e));
-  if (c->timing) {
+  if (timed) {
     hipEventRecord(b, st);
     c->pending.push_back({name, a, b, bytes, edges});
     if (c->pending.size() > 4096) {  // bound outstanding events (they may be on two streams)
@@ -721,6 +724,19 @@ int nemo_set_timing(nemo_ctx *c, int enable) {
   DISPATCH(node_set_timing(c, enable));
   if (!c) return NEMO_ERR_INVALID;
   c->timing = enable != 0;
+  return NEMO_OK;
+}
+
+int nemo_set_timing_groups(nemo_ctx *c, const char *groups) {
+  DISPATCH(node_set_timing_groups(c, groups));
+  if (!c) return NEMO_ERR_INVALID;
+  c->tgroups.clear();
+  for (const char *p = groups; p && *p;) {
+    const char *q = strchr(p, ',');
+    const size_t n = q ? (size_t)(q - p) : strlen(p);
+    if (n) c->tgroups.emplace_back(p, n);
+    p = q ? q + 1 : p + n;
+  }
   return NEMO_OK;
 }
 

@@ -22,6 +22,7 @@ void node_destroy(Node *n);
 int node_set_stream(nemo_ctx *c, void *stream);
 int node_set_option(nemo_ctx *c, const char *name, int64_t value);
 int node_set_timing(nemo_ctx *c, int enable);
+int node_set_timing_groups(nemo_ctx *c, const char *groups);
 uint64_t node_num_nodes(const nemo_ctx *c);
 uint64_t node_num_edges(const nemo_ctx *c);
 int node_load_corpus(nemo_ctx *c, const nemo_corpus *in);

@@ -292,6 +292,10 @@ int node_set_timing(nemo_ctx *c, int enable) {
   for (auto &s : N(c)->sh) SCHK(c, s, nemo_set_timing(s.ctx, enable));
   return NEMO_OK;
 }
+int node_set_timing_groups(nemo_ctx *c, const char *groups) {
+  for (auto &s : N(c)->sh) SCHK(c, s, nemo_set_timing_groups(s.ctx, groups));
+  return NEMO_OK;
+}
 uint64_t node_num_nodes(const nemo_ctx *c) { return N(c)->V; }
 uint64_t node_num_edges(const nemo_ctx *c) { return N(c)->E; }
 size_t node_reduce_len(const nemo_ctx *c) { return 2 * (size_t)N(c)->T + 4; }

@@ -69,6 +69,7 @@ def lib():
             "nemo_last_error": ([vp], ctypes.c_char_p),
             "nemo_set_stream": ([vp, vp], i32),
             "nemo_set_timing": ([vp, i32], i32),
+            "nemo_set_timing_groups": ([vp, ctypes.c_char_p], i32),
             "nemo_set_option": ([vp, ctypes.c_char_p, ctypes.c_int64], i32),
             "nemo_load_corpus": ([vp, vp], i32),
             "nemo_host_register": ([vp, u64], i32),
@@ -191,6 +192,10 @@ class Engine:
 
     def set_timing(self, on: bool = True) -> None:
         self._chk(self.L.nemo_set_timing(self.h, int(on)))
+
+    def set_timing_groups(self, groups: Sequence[str] = ()) -> None:
+        """Time only these groups (empty: every group)."""
+        self._chk(self.L.nemo_set_timing_groups(self.h, ",".join(groups).encode()))
 
     def load(self, corpus: Corpus) -> None:
         cs = corpus.c_struct()

@@ -184,3 +184,15 @@ def test_load_error_counts_in_big_graph(eng, case):
         eng.load(corpus)
     assert f"inserted number of edges ({want}) does not equal number of antecedent provenance edges ({E_})" \
         in str(ei.value)
+
+
+def test_diff_fallback_past_walk_window(eng):
+    """A run-0 post graph with a row of more links than one walk window holds (dx_max_row = 8192): the
+    multi-entry diff (k_dx) cannot stage it, and CreateNaiveDiffProv runs on the one-workgroup-per-entry
+    kernels of k_diff.hip, the library's fallback tier; both diff modes against the oracle."""
+    graphs = [(0, "success", wide_prov("pre", 2500, 1), wide_prov("post", 2500, 2, hub=9000)),
+              (1, "failure", wide_prov("pre", 2500, 3), wide_prov("post", 2500, 4)),
+              (2, "failure", wide_prov("pre", 2500, 5), wide_prov("post", 2400, 6))]
+    corpus = corpus_from_graphs(graphs)
+    _check(eng, corpus)
+    _check(eng, corpus, mode=DIFF_PER_RUN)

@@ -58,3 +58,82 @@ c5ab)
   timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --diff-reps 2 --set topo_ell=0 > gpurun_out/${tag}_c5_old.json 2> gpurun_out/${tag}_c5_old.err || exit 1
   for f in gpurun_out/${tag}_c5.json gpurun_out/${tag}_c5_old.json; do python -c "import json,sys;d=json.load(open('$f'));print('$f',d['value'],d['ms_per_step'],{k:v['ms_total'] for k,v in d['kernels'].items() if k in ('k_topo','k_csrb','k_chains','k_proto')})"; done ;;
 esac
+case "$1" in
+timingab)
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_on.json 2>/dev/null || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing off > gpurun_out/${tag}_off.json 2>/dev/null || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_on2.json 2>/dev/null || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing off > gpurun_out/${tag}_off2.json 2>/dev/null || exit 1
+  for f in on off on2 off2; do python -c "import json;d=json.load(open('gpurun_out/${tag}_$f.json'));print('$f',d['value'],d['ms_per_step'])"; done ;;
+esac
+case "$1" in
+timingab2)
+  for m in dominant on dominant off; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing $m > gpurun_out/${tag}_$m.json 2>/dev/null || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_$m.json'));print('$m',d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['avg_launch_ms'])"
+  done ;;
+esac
+case "$1" in
+benchprev)
+  for b in bench_prev.py bench.py bench_prev.py bench.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_x.json 2>/dev/null || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'])"
+  done ;;
+esac
+case "$1" in
+benchprev2)
+  for b in bench_prev.py bench.py bench_prev.py bench.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing off > gpurun_out/${tag}_x.json 2>/dev/null || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d.get('step_host_ms_rank0'))"
+  done ;;
+esac
+case "$1" in
+benchprev3)
+  for b in bench_prev.py bench.py bench_v2.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing off > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d.get('step_host_ms_rank0'))"; grep STEPS gpurun_out/${tag}_x.err || true
+  done ;;
+esac
+case "$1" in
+benchprev4)
+  for b in bench_v3.py bench_v2.py bench_v3.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --kernel-timing off > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d.get('step_host_ms_rank0'))"
+  done ;;
+esac
+case "$1" in
+benchgc)
+  for b in bench.py bench_prev.py bench.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],d.get('step_host_ms_rank0'))"; grep STEPS gpurun_out/${tag}_x.err || true
+  done ;;
+esac
+case "$1" in
+bisect)
+  for b in bench_prev.py bench_va.py bench_vb.py bench_vc.py bench.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'])"; grep STEPS gpurun_out/${tag}_x.err || true
+  done ;;
+esac
+case "$1" in
+bisect2)
+  for b in bench_vb.py bench_p1.py bench_p2.py bench_p3.py bench_prev.py bench_vb.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'])"; grep STEPS gpurun_out/${tag}_x.err | cut -c1-40 || true
+  done ;;
+esac
+case "$1" in
+e2eab)  # the e2e leg of round 4's tree and of this one, alternately, on one box
+  for t in r04 now r04 now; do
+    if [ $t = r04 ]; then d=var/r04tree; else d=.; fi
+    (cd $d && timeout -k 10 400 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --diff-reps 0) > gpurun_out/${tag}_e2e_$t.json 2>/dev/null || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_e2e_$t.json'));e=d['e2e'];print('$t',e['runs_per_s'],e['total_s'],e['ingest_only_s'],e['ingest_gb_per_s'],e['device_and_handover_s'])"
+  done ;;
+esac
+case "$1" in
+bisect3)
+  for b in bench.py bench_prev.py bench.py; do
+    timeout -k 10 300 python -u $b --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_x.json 2>gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],str(d.get('step_host_ms_rank0'))[:40])"
+  done ;;
+esac
