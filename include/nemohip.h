@@ -168,7 +168,15 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *                       nemo_simplify (1) or on the context's stream (0, default)
  *   "diff_fuse"         whole-graph diff walks finish LP rules, missing rows and
  *                       one-entry masks themselves (1, default) or hand them to
- *                       separate kernels (0; test knob) */
+ *                       separate kernels (0; test knob)
+ *   "build_marksimp"    k_build's graphs get their deferred mark + simplification
+ *                       at the end of k_build, from the edges it holds (1), or
+ *                       from k_marksimp in nemo_simplify (0, default)
+ *   "load_parts"        corpora of big graphs only: uploads in this many parts,
+ *                       each part's CSR build behind its own upload (default 4;
+ *                       1 = one upload, then the build)
+ *   "topo_ell"          deep graphs' Kahn levels by the edge-parallel k_topo_ell
+ *                       (1) or one workgroup per graph, k_topo_deep (0, default) */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
 /* Record a hipEvent pair around every launch (per-kernel timing, see nemo_timings). */
 int nemo_set_timing(nemo_ctx *ctx, int enable);

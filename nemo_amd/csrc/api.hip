@@ -40,6 +40,11 @@ struct nemo_ctx {
   Node *node = nullptr;  // node context: every entry point dispatches to node.hip
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
+  // uploads of a corpus of big graphs, in parts, so that the CSR build of part k overlaps the
+  // upload of part k + 1 (nemo_load_corpus; option load_parts)
+  hipStream_t up = nullptr;
+  std::vector<hipEvent_t> ev_up;
+  uint32_t load_parts = 4;
   std::string err;
   std::vector<std::string> tgroups;  // nemo_set_timing_groups: the timed groups (empty: all)
   bool timing = false;
@@ -73,6 +78,11 @@ struct nemo_ctx {
   uint64_t bigVmax = 0;              // the largest of them
   uint32_t big_chunks = 1;           // k_csrb_* workgroups per big graph
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
+  bool ms_fuse_off = true;           // option build_marksimp 1: k_build's marksimp tail (measured slower at C3:
+                                     // k_build 3.00 -> 3.86 ms against k_marksimp's 0.80 ms; four workgroups
+                                     // per CU by k_build's LDS image where k_marksimp runs eight waves per SIMD)
+  bool ms_fused = false;             // k_build's tail wrote its graphs' final flags at the last load / rebuild,
+                                     // not yet consumed by nemo_simplify (k_marksimp skips those graphs)
 
   DevCorpus dc{};
   uint8_t *d_owned = nullptr, *d_is_success = nullptr;
@@ -560,6 +570,7 @@ static void release_corpus(nemo_ctx *c) {
   c->staged = false;
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
   c->mark_pending = false;
+  c->ms_fused = false;
 }
 
 void nemo_ctx_destroy(nemo_ctx *c) {
@@ -609,6 +620,11 @@ void nemo_ctx_destroy(nemo_ctx *c) {
   if (c->h_tcounts) hipHostFree(c->h_tcounts);
   if (c->h_tiers) hipHostFree(c->h_tiers);
   if (c->ev_tiers) hipEventDestroy(c->ev_tiers);
+  for (hipEvent_t e : c->ev_up) hipEventDestroy(e);
+  if (c->up) {
+    hipStreamSynchronize(c->up);
+    hipStreamDestroy(c->up);
+  }
   if (c->aux) hipStreamDestroy(c->aux);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->own) hipStreamDestroy(c->own);
@@ -628,6 +644,7 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   DISPATCH(node_set_option(c, name, value));
   if (!c || !name) return NEMO_ERR_INVALID;
   tiers_reset(c);  // any option may move graphs between tiers
+  c->ms_fused = false;  // ... and the fused tail's graphs were chosen under the old caps
   if (!strcmp(name, "chains_lds_max")) {
     c->hcap_limit = value < 0 ? 0xFFFFFFFFu : (uint32_t)value;
     c->dc.hcap_limit = c->hcap_limit;
@@ -691,6 +708,14 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "diff_fuse")) {  // test knob: 0 runs k_dx_lp / k_dx_emit after whole-graph walks too
     c->diff_unfused = value == 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "build_marksimp")) {  // 1: k_build's tail; 0 / -1: k_marksimp takes every tier graph
+    c->ms_fuse_off = value <= 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "load_parts")) {  // big-graph corpora: uploads in this many parts (1: one upload, then the build)
+    c->load_parts = value < 1 ? 4u : (uint32_t)std::min<int64_t>(value, 64);
     return NEMO_OK;
   }
   if (!strcmp(name, "topo_ell")) {  // 1: k_topo_ell for the deep graphs (child records); 0 / -1: k_topo_deep
@@ -868,9 +893,31 @@ static int check_graph_errors(nemo_ctx *c) {
   return NEMO_OK;
 }
 
-static int device_load(nemo_ctx *c) {
+// parts: upload parts of a big-graph corpus (nemo_load_corpus): part k's edges land behind
+// ev_up[k] on the upload stream, and its graphs' bucketed CSR build waits for that event only
+// (the CSR build of part k overlaps the upload of part k + 1); the rest of the load runs behind
+// the last part
+static int device_load(nemo_ctx *c, const std::vector<uint32_t> *parts = nullptr) {
   int rc;
+  const bool split = c->dc.n_big && parts && parts->size() > 2;
   nemo::launch_zero(c->dc.err, c->G * sizeof(uint32_t), c->stream);
+  if (split) {
+    // part k = big-list entries [parts[k], parts[k + 1]) (every graph big: the list is every graph
+    // in order, so a part's edges are one contiguous range)
+    for (size_t k = 0; k + 1 < parts->size(); k++) {
+      DevCorpus sc = c->dc;
+      const uint32_t b0 = (*parts)[k], b1 = (*parts)[k + 1];
+      sc.big = c->dc.big + b0;
+      sc.cb_hoff = c->dc.cb_hoff + b0;
+      sc.n_big = b1 - b0;
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_up[k], 0));
+      const double f = (double)sc.n_big / (double)c->dc.n_big;
+      if ((rc = timed(c, "k_csrb", f * (16 * c->bigE + 12 * c->bigV), f * c->bigE,
+                      [&] { nemo::launch_csr_big(sc, c->big_chunks, c->stream); })))
+        return rc;
+    }
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_up.back(), 0));
+  }
   // graphs within k_build's LDS caps vs the global tier
   double Vb = 0, Eb = 0, Vp = 0, Ep = 0;
   for (uint32_t g = 0; g < c->G && c->dc.bld_bytes; g++) {
@@ -885,20 +932,26 @@ static int device_load(nemo_ctx *c) {
     }
   }
   const double V = (double)c->V - Vb, E = (double)c->E - Eb;
+  // k_build's tail runs the deferred mark + simplification (k_marksimp's work) on the edges still
+  // in its registers when every k_build graph fits the tail's LDS image
+  c->dc.ms_fuse = !c->ms_fuse_off && c->dc.t_ms.bytes && c->dc.bld_bytes &&
+                  marksimp_bytes(c->dc.bld_v, c->dc.words) <= c->dc.bld_bytes;
   // k_build, HBM lower bound: read the edge list (8E) and node words (4V);
   // write both column arrays (8E), both row-pointer arrays (8V), the Kahn
   // order (4V) and per-node level (4V); the level offsets are per level; post
-  // graphs also their edges in source Kahn order (4E) and position offsets (4V)
-  if ((rc = timed(c, "k_build", 16 * Eb + 20 * Vb + 4 * Ep + 4 * Vp, 2 * Eb,
+  // graphs also their edges in source Kahn order (4E) and position offsets (4V);
+  // with the tail, the node flags (1V)
+  if ((rc = timed(c, "k_build", 16 * Eb + (c->dc.ms_fuse ? 21 : 20) * Vb + 4 * Ep + 4 * Vp, 2 * Eb,
                   [&] { nemo::launch_build(c->dc, c->stream); })))
     return rc;
+  c->ms_fused = c->dc.ms_fuse != 0;
   // graphs past k_build: k_csr (one workgroup per graph) below NEMO_CSR_BIG nodes, k_csrb_* above
   const double Eg = std::max(0.0, E - c->bigE), Vg = std::max(0.0, V - c->bigV);
   const bool load_tier = !tier_empty(c, 0);
   if (load_tier && (rc = timed(c, "k_csr", 16 * Eg + 12 * Vg, Eg, [&] { nemo::launch_load(c->dc, c->stream); })))
     return rc;
   if (load_tier) c->tiers_run |= 1u;
-  if (c->dc.n_big &&
+  if (c->dc.n_big && !split &&
       (rc = timed(c, "k_csrb", 16 * c->bigE + 12 * c->bigV, c->bigE,
                   [&] { nemo::launch_csr_big(c->dc, c->big_chunks, c->stream); })))
     return rc;
@@ -917,6 +970,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->copy) HIPCHK(c, hipStreamSynchronize(c->copy));
   if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
+  if (c->up) HIPCHK(c, hipStreamSynchronize(c->up));
   release_corpus(c);
   if (in->n_tables > NEMO_MAX_TABLES)
     return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
@@ -1127,7 +1181,33 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     HIPCHK(c, hipMemcpyAsync(label, in->label, V * 4, hipMemcpyHostToDevice, s));
     if (rank) HIPCHK(c, hipMemcpyAsync(rank, in->id_rank, V * 4, hipMemcpyHostToDevice, s));
   }
-  if (E) {
+  // a corpus of big graphs only (the deep configs) uploads its edges in parts on a stream of
+  // their own, so that the bucketed CSR build of part k runs while part k + 1 is in flight
+  std::vector<uint32_t> parts;
+  if (getenv("NEMO_LOAD_DEBUG"))
+    fprintf(stderr, "nemo_load_corpus: E %zu n_big %u G %zu cb_hist %d load_parts %u\n", E, d.n_big, G,
+            d.cb_hist != nullptr, c->load_parts);
+  if (E && d.n_big == G && d.cb_hist && c->load_parts > 1 && G >= 2 * c->load_parts) {
+    for (uint32_t k = 0; k <= c->load_parts; k++) parts.push_back((uint32_t)((uint64_t)G * k / c->load_parts));
+    if (!c->up) HIPCHK(c, hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+    while (c->ev_up.size() < parts.size() - 1) {
+      hipEvent_t e = nullptr;
+      HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_up.push_back(e);
+    }
+    // the node arrays and offsets queued on `s` first: the upload stream starts behind them
+    if ((rc = ensure_event(c, &c->ev_misc))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_misc, s));
+    HIPCHK(c, hipStreamWaitEvent(c->up, c->ev_misc, 0));
+    for (size_t k = 0; k + 1 < parts.size(); k++) {
+      const uint64_t a = c->edge_off[parts[k]], n = c->edge_off[parts[k + 1]] - a;  // big list = every graph
+      if (n) {
+        HIPCHK(c, hipMemcpyAsync(es + a, in->edge_src + a, n * 4, hipMemcpyHostToDevice, c->up));
+        HIPCHK(c, hipMemcpyAsync(ed + a, in->edge_dst + a, n * 4, hipMemcpyHostToDevice, c->up));
+      }
+      HIPCHK(c, hipEventRecord(c->ev_up[k], c->up));
+    }
+  } else if (E) {
     HIPCHK(c, hipMemcpyAsync(es, in->edge_src, E * 4, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(ed, in->edge_dst, E * 4, hipMemcpyHostToDevice, s));
   }
@@ -1261,7 +1341,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     if ((rc = dalloc(c, &c->d_tpost, 2 * c->tcap[1] + 2))) return rc;
     if ((rc = dalloc(c, &c->d_tasync, c->tcap[2] + 1))) return rc;
   }
-  if ((rc = device_load(c))) return rc;
+  if ((rc = device_load(c, &parts))) return rc;
   if ((rc = check_graph_errors(c))) return rc;
   c->loaded = true;
   return NEMO_OK;
@@ -1291,6 +1371,7 @@ static int ensure_marked(nemo_ctx *c) {
   int rc = timed(c, "k_mark", 8 * E + 13 * V, 2 * E, [&] { nemo::launch_mark(c->dc, false, c->stream); });
   if (rc) return rc;
   c->mark_pending = false;
+  c->ms_fused = false;  // k_mark rewrote every graph's flags (holds only)
   return NEMO_OK;
 }
 
@@ -1321,8 +1402,13 @@ int nemo_simplify(nemo_ctx *c) {
   if (rc) return rc;
   if (c->mark_pending) {
     const double V = c->tierV, E = c->tierE, Vg = (double)c->V - V, Eg = (double)c->E - E;
-    rc = timed(c, "k_marksimp", 8 * E + 5 * V, 5 * E, [&] { nemo::launch_marksimp(c->dc, c->stream); });
-    if (rc) return rc;
+    // k_build's tail did its graphs (ms_fused); an empty load tier means it took every graph
+    // (none past its caps or handed back), so nothing is left for k_marksimp
+    const bool skip_built = c->ms_fused;
+    if (!(skip_built && tier_empty(c, 0)) &&
+        (rc = timed(c, "k_marksimp", 8 * E + 5 * V, 5 * E,
+                    [&] { nemo::launch_marksimp(c->dc, c->stream, skip_built); })))
+      return rc;
     rc = timed(c, "k_simplify", 8 * Eg + 14 * Vg, 2 * Eg,
                [&] { nemo::launch_simplify(c->dc, true, c->stream, c->ms_rest != 0); });
     if (rc) return rc;
@@ -1332,6 +1418,7 @@ int nemo_simplify(nemo_ctx *c) {
     rc = timed(c, "k_simplify", 8 * E + 14 * V, 2 * E, [&] { nemo::launch_simplify(c->dc, false, c->stream); });
     if (rc) return rc;
   }
+  c->ms_fused = false;  // consumed: the chain cover marks the flags, a later simplification recomputes them
   if ((rc = ensure_event(c, &c->ev_flags))) return rc;
   HIPCHK(c, hipEventRecord(c->ev_flags, c->stream));  // the flags are final (the chain cover reads them)
   c->flags_final = true;

@@ -204,6 +204,7 @@ struct DevCorpus {
   uint32_t glob_stop;                    // diagnostic (stamps build): k_chains_glob returns after phase k (0: none)
   uint32_t glob_prep;                    // 1: k_glob_prep builds the deep graphs' H* order and adjacency (identity ranks)
   uint32_t topo_ell;                     // 1: deep graphs' Kahn levels by k_topo_ell (child records in gscratch)
+  uint32_t ms_fuse;                      // 1: k_build's tail runs marksimp_graph on its graphs (marksimp.h)
   uint32_t n_glob;                       // deep graphs (gs_off != ~0)
   const uint32_t *glob_list;             // [n_glob] their graph ids
   uint32_t *team;                        // k_glob_prep's team scratch (barrier counters, phase sums)

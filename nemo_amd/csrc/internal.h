@@ -154,7 +154,7 @@ void launch_csr_big(const DevCorpus &c, uint32_t chunks, hipStream_t s);
 // per_graph false: no graph below NEMO_CSR_BIG is past the skipped tier (host count), so only the big-graph kernels run
 void launch_mark(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
 void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per_graph = true);
-void launch_marksimp(const DevCorpus &c, hipStream_t s);
+void launch_marksimp(const DevCorpus &c, hipStream_t s, bool skip_built);
 void launch_chains(const DevCorpus &c, hipStream_t s, bool tiers = true);
 void launch_chains_glob(const DevCorpus &c, hipStream_t s);
 uint64_t glob_words(uint64_t V, uint64_t E);  // k_chains_glob scratch of one graph (u32)

@@ -4,6 +4,7 @@
 
 #include "device.h"
 #include "internal.h"
+#include "marksimp.h"
 
 namespace nemo {
 
@@ -281,10 +282,6 @@ __global__ __launch_bounds__(MW_BLOCK) void k_mw_simplify_4(DevCorpus c, int ski
 #define PG_BLOCK 256
 #define PG_SWEEP 64  // one wave per graph: a level has a few dozen nodes
 #define SB_NR 0x20u      // goal has a REG or TAIL parent (not a root)
-// byte v of a 4-aligned byte array (LDS, or a corpus-wide array with v the global index)
-__device__ __forceinline__ void or8(uint8_t *b, uint64_t v, uint32_t bits) {
-  atomicOr((uint32_t *)b + (v >> 2), bits << (8u * (uint32_t)(v & 3u)));
-}
 
 // k_proto_lds takes the graphs within its LDS tier (and its chain cap) that
 // k_build built: their edges in source Kahn order are in c.e2 / c.posoff
@@ -760,179 +757,33 @@ __global__ __launch_bounds__(PROTO_BLOCK) void k_proto_lds(DevCorpus c) {
 
 
 // markConditionHolds + cleanCopyProv + the local part of collapseNextChains
-// fused for the LDS-tier graphs, straight from the input edge list.  Every
-// rule of k_mark / k_simplify_flags is a predicate over a node's in- or
-// out-edges, so each phase is one pass over the graph's edges (held in
-// registers, MS_EPT per thread) that ORs bits into per-node LDS bytes; no CSR
-// is staged.  LDS holds ~4 B per node (u16 node word, flags, one aux byte),
+// fused for the LDS-tier graphs, straight from the input edge list
+// (marksimp.h).  LDS holds ~4 B per node (u16 node word, flags, one aux byte),
 // so the CU is filled by waves, not capped by LDS.  Same outputs as the
 // CSR-walking kernels (pre-post-prov.go:218-244, preprocessing.go:13-348).
-#define MS_BLOCK 256
-#define MS_EPT 32
-#define A_IN 0x01u   // in-degree > 0
-#define A_OUT 0x02u  // out-degree > 0
-#define A_PC 0x04u   // node of table C with a parent of table C (pos source)
-#define A_NC 0x08u   // ... one of which has a parent itself (neg source)
-#define A_POS 0x10u  // child of an A_PC node
-#define A_NEG 0x20u  // child of an A_NC node
-#define A_GP 0x40u   // kept next rule: a parent goal has a kept next-rule parent
-#define A_GC 0x80u   // kept next rule: a child goal has a kept next-rule child
-
-
-
-__global__ __launch_bounds__(MS_BLOCK) void k_marksimp(DevCorpus c) {
+// skip_built: the graphs k_build's fused tail already did (ms_built_by_build).
+__global__ __launch_bounds__(MS_BLOCK) void k_marksimp(DevCorpus c, int skip_built) {
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ uint32_t s_any, s_pre, s_hold;
+  __shared__ uint32_t s_misc[3];
   const uint32_t g = blockIdx.x;
   if (c.err[g]) return;
   const GraphView gv = c.view(g);
   if (!tier_fits(c.t_ms, gv.V, gv.E, gv.nlev)) return;
-  const uint32_t V = gv.V, E = gv.E, W = c.words, tid = threadIdx.x;
-  uint8_t *p = dyn;
-  uint32_t *tq = (uint32_t *)p;
-  p += lds_align(8u * W);
-  uint16_t *nw = (uint16_t *)p;
-  p += lds_align(2u * V);
-  uint8_t *fl = p;
-  p += lds_align(V);
-  uint8_t *ax = p;
+  if (skip_built && ms_built_by_build(c, g, gv.V, gv.E)) return;
+  const uint32_t E = gv.E, tid = threadIdx.x;
   const uint32_t *es = c.esrc + gv.e0, *ed = c.edst + gv.e0;
   // every input load issued back to back: the edges (src << 16 | dst) of the
-  // first MS_EPT x block, then the node words
-  const bool one = E <= MS_EPT * MS_BLOCK;
+  // first MS_EPT x block, then the node words (inside marksimp_graph)
   uint32_t sd[MS_EPT];
+  auto load = [&](uint32_t base) {
 #pragma unroll
-  for (int q = 0; q < MS_EPT; q++) {
-    const uint32_t e = tid + q * MS_BLOCK;
-    sd[q] = e < E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
-  }
-  for (uint32_t base = 0; base < V; base += 8 * MS_BLOCK) {
-    uint32_t w[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + q * MS_BLOCK + tid;
-      w[q] = v < V ? gv.word[v] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t v = base + q * MS_BLOCK + tid;
-      if (v < V) nw[v] = nw_of(w[q]);
-    }
-  }
-  for (uint32_t i = tid; i < W; i += MS_BLOCK) tq[i] = 0;
-  for (uint32_t i = tid; i < (V + 3) / 4; i += MS_BLOCK) ((uint32_t *)ax)[i] = 0;
-  if (tid == 0) {
-    s_any = 0;
-    s_pre = 0;
-    s_hold = 0;
-  }
-  __syncthreads();
-  // one pass over the edges: fn(src, dst) for every edge of the graph
-  auto edges = [&](auto fn) {
-    for (uint32_t base = 0; base < E; base += MS_EPT * MS_BLOCK) {
-      if (!one) {
-#pragma unroll
-        for (int q = 0; q < MS_EPT; q++) {
-          const uint32_t e = base + tid + q * MS_BLOCK;
-          sd[q] = e < E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < MS_EPT; q++)
-        if (sd[q] != 0xFFFFFFFFu) fn(sd[q] >> 16, sd[q] & 0xFFFFu);
+    for (int q = 0; q < MS_EPT; q++) {
+      const uint32_t e = base + tid + q * MS_BLOCK;
+      sd[q] = e < E ? (es[e] << 16) | ed[e] : 0xFFFFFFFFu;
     }
   };
-  const uint32_t C = (g & 1) ? c.table_post : c.table_pre;
-#define NTAB(v) (nw[v] & NW_TABLE)
-#define NRULE(v) ((nw[v] & NW_RULE) != 0)
-  // degrees, and the (T:C)->(Rc:C) edges of markConditionHolds' pattern
-  edges([&](uint32_t s, uint32_t d) {
-    or8(ax, s, A_OUT);
-    or8(ax, d, A_IN);
-    if (NTAB(s) == C && NTAB(d) == C) or8(ax, d, A_PC);
-  });
-  __syncthreads();
-  // negative pattern: X->(T':C)->(R':C); then pos/neg onto the goals below Rc
-  edges([&](uint32_t s, uint32_t d) {
-    if ((ax[s] & A_IN) && NTAB(s) == C && NTAB(d) == C) or8(ax, d, A_NC);
-  });
-  __syncthreads();
-  edges([&](uint32_t s, uint32_t d) {
-    const uint32_t a = ax[s];
-    if (a & (A_PC | A_NC)) or8(ax, d, ((a & A_PC) ? A_POS : 0u) | ((a & A_NC) ? A_NEG : 0u));
-  });
-  __syncthreads();
-  // qualifying tables Tq: goals with a rule child, the positive and not the negative pattern
-  bool any = false;
-  for (uint32_t x = tid; x < V; x += MS_BLOCK) {
-    const uint32_t a = ax[x];
-    if (NRULE(x) || !(a & A_OUT) || (a & (A_POS | A_NEG)) != A_POS) continue;
-    atomicOr(&tq[NTAB(x) >> 5], 1u << (NTAB(x) & 31));
-    any = true;
-  }
-  if (__any(any) && lane_id() == 0) s_any = 1;
-  __syncthreads();
-  // holds + cleanCopyProv's KEPT (preprocessing.go:13-63)
-  const bool anyq = s_any != 0;
-  uint32_t pre = 0;
-  for (uint32_t x4 = tid; x4 < (V + 3) / 4; x4 += MS_BLOCK) {
-    uint32_t packed = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t x = 4 * x4 + b;
-      if (x >= V) break;
-      const uint32_t t = NTAB(x), a = ax[x];
-      const bool rule = NRULE(x);
-      const bool h = anyq && !rule && (t == C || ((tq[t >> 5] >> (t & 31)) & 1u));
-      uint32_t f = h ? NEMO_F_HOLDS : 0u;
-      if (!rule || (a & (A_IN | A_OUT)) == (A_IN | A_OUT)) f |= NEMO_F_KEPT;
-      packed |= f << (8 * b);
-      pre += (h && t == c.table_pre) ? 1u : 0u;
-    }
-    ((uint32_t *)fl)[x4] = packed;
-  }
-  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);
-  if (lane_id() == 0 && pre) atomicAdd(&s_pre, pre);
-  __syncthreads();
-  // collapseNextChains' local rules (preprocessing.go:66-348): goals with a
-  // kept next-rule parent / child ...
-#define ISNEXT(v) ((nw[v] & NW_NEXT) && (fl[v] & NEMO_F_KEPT))
-  edges([&](uint32_t s, uint32_t d) {
-    if (ISNEXT(s) && !NRULE(d)) or8(fl, d, FT_NP);
-    if (ISNEXT(d) && !NRULE(s)) or8(fl, s, FT_NC);
-  });
-  __syncthreads();
-  // ... and next rules with a next grandparent / grandchild
-  edges([&](uint32_t s, uint32_t d) {
-    if (ISNEXT(d) && (fl[s] & FT_NP)) or8(ax, d, A_GP);
-    if (ISNEXT(s) && (fl[d] & FT_NC)) or8(ax, s, A_GC);
-  });
-  __syncthreads();
-  bool hold = false;
-  uint8_t *out = gv.flags;
-  for (uint32_t x = tid; x < V; x += MS_BLOCK) {
-    uint32_t f = fl[x];
-    if (ISNEXT(x)) {
-      const bool gp = (ax[x] & A_GP) != 0, gc = (ax[x] & A_GC) != 0;
-      if (gp || gc) f |= NEMO_F_DELETED;
-      if (!gp && gc) f |= NEMO_F_HEAD;
-      if (gp && !gc) f |= NEMO_F_TAIL;
-    } else if (!NRULE(x)) {
-      if ((f & FT_NP) && (f & FT_NC)) f |= NEMO_F_DELETED;
-      f &= ~(FT_NP | FT_NC);
-      hold |= (f & (NEMO_F_HOLDS | NEMO_F_DELETED)) == NEMO_F_HOLDS;
-    }
-    out[x] = (uint8_t)f;
-  }
-#undef ISNEXT
-#undef NTAB
-#undef NRULE
-  if (__any(hold) && lane_id() == 0) s_hold = 1;
-  __syncthreads();
-  if (tid == 0) {
-    c.prehold[g] = s_pre;
-    c.holdany[g] = s_hold;
-  }
+  load(0);
+  marksimp_graph<MS_BLOCK, MS_EPT, false>(c, g, gv.V, E, gv.word, gv.flags, sd, E <= MS_EPT * MS_BLOCK, load, dyn, s_misc);
 }
 
 // Cross-run reduction vector (nemo_reduce_len): per-table counts over owned
@@ -1007,11 +858,11 @@ void launch_simplify(const DevCorpus &c, bool skip_tier, hipStream_t s, bool per
   hipLaunchKernelGGL(k_mw_simplify_3, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
   hipLaunchKernelGGL(k_mw_simplify_4, mw_grid(c), dim3(MW_BLOCK), 0, s, c, sk);
 }
-void launch_marksimp(const DevCorpus &c, hipStream_t s) {
+void launch_marksimp(const DevCorpus &c, hipStream_t s, bool skip_built) {
   if (!c.t_ms.bytes) return;
   const uint32_t b = c.t_ms.bytes;
   hipFuncSetAttribute((const void *)k_marksimp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
-  hipLaunchKernelGGL(k_marksimp, dim3(c.G), dim3(MS_BLOCK), b, s, c);
+  hipLaunchKernelGGL(k_marksimp, dim3(c.G), dim3(MS_BLOCK), b, s, c, skip_built ? 1 : 0);
 }
 void launch_proto(const DevCorpus &c, hipStream_t s, bool tiers) {
   if (c.lds_bytes) {

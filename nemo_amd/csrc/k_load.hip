@@ -4,6 +4,7 @@
 
 #include "device.h"
 #include "internal.h"
+#include "marksimp.h"
 
 namespace nemo {
 
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
   __shared__ uint32_t s_lds[B / 64];
   __shared__ uint32_t s_bad, s_created, s_tail, s_cnt[3];
   __shared__ uint32_t s_sink[64];  // per-lane no-op atomic targets (one bank each: no same-address serialisation)
+  __shared__ uint32_t s_ms[3];
   const uint32_t g = blockIdx.x, tid = threadIdx.x;
   const uint64_t n0 = c.node_off[g], e0 = c.edge_off[g];
   const uint32_t V = (uint32_t)(c.node_off[g + 1] - n0), E = (uint32_t)(c.edge_off[g + 1] - e0);
@@ -515,12 +517,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     }
   }
   STAMP(15);
+  uint32_t err = s_created == E ? 0u : (uint32_t)NEMO_ERR_LOAD;
+  if (!err && hi != V) err = NEMO_ERR_CYCLE;
   if (tid == 0) {
     c.created[g] = s_created;
     c.nlev[g] = nl;
-    uint32_t err = s_created == E ? 0u : (uint32_t)NEMO_ERR_LOAD;
-    if (!err && hi != V) err = NEMO_ERR_CYCLE;
     c.err[g] = err;
+  }
+  // the deferred markConditionHolds + simplification of a well-formed graph
+  // (k_marksimp's work, nemo_simplify then skips the graph): its edges are
+  // still in sd, and the LDS image is free once the copies above have read it
+  if (c.ms_fuse && !err && tier_fits(c.t_ms, V, E, nl)) {
+    __syncthreads();
+    marksimp_graph<B, EPT, true>(c, g, V, E, word, c.flags + n0, sd, true, [](uint32_t) {}, dyn, s_ms);
   }
 }
 

@@ -635,3 +635,41 @@ def test_repeated_passes_tier_cache(eng, knobs):
         for k, _ in knobs:
             eng.set_option(k, -1)
         eng.set_option("global_block", -1)
+
+
+@pytest.mark.parametrize("seq", ["plain", "off", "twice", "option_between", "holds_first", "build_caps"])
+def test_build_marksimp_tail(eng, seq):
+    """k_build's tail runs the deferred mark + simplification (marksimp.h) of its graphs at load / rebuild and
+    nemo_simplify skips them in k_marksimp (api.hip ms_fused).  The result must not depend on the call sequence:
+    the tail off (option build_marksimp 0, the default); mark + simplify twice after one rebuild (the second pass recomputes:
+    the chain cover has marked the flags); an option change between rebuild and mark (tiers may move); the holds
+    flags read before the simplification (k_mark rewrites them); k_build's caps below some graphs (k_marksimp takes
+    those beside the tail's).  Flags, chains and protos against the oracle each time."""
+    from tools import synth
+    from nemo_amd.corpus import F_HOLDS
+    corpus, _ = synth.generate(24, target_nodes=1500, p_fault=0.4)
+    s, f = corpus.success_iters(), corpus.failed_iters()
+    orc = O.analyze(corpus, s, f, skip_pulls=True)
+    opts = [("build_marksimp", 0 if seq == "off" else 1)] + ([("build_lds_max", 1200)] if seq == "build_caps" else [])
+    for k, v in opts:
+        eng.set_option(k, v)
+    try:
+        eng.load(corpus)
+        for p in range(2):
+            eng.rebuild()
+            if seq == "option_between":
+                eng.set_option("chains_lds_max", -1)
+            eng.mark()
+            if seq == "holds_first":
+                assert np.array_equal(eng.flags(), orc.flags & F_HOLDS)
+            eng.simplify()
+            if seq == "twice":
+                eng.mark()
+                eng.simplify()
+            assert np.array_equal(eng.flags(), orc.flags), (seq, p)
+            assert np.array_equal(eng.chains(), orc.chains), (seq, p)
+            achieved, inter, uni = eng.prototypes(s)
+            assert achieved == orc.achieved and np.array_equal(inter, orc.inter) and np.array_equal(uni, orc.union)
+    finally:
+        for k, _ in opts:
+            eng.set_option(k, -1)

@@ -137,3 +137,27 @@ bisect3)
     python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$b',d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],str(d.get('step_host_ms_rank0'))[:40])"
   done ;;
 esac
+case "$1" in
+c5k)
+  timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5k.json 2> gpurun_out/${tag}_c5k.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k.json'));print('parts4',d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
+  timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --set load_parts=1 > gpurun_out/${tag}_c5k1.json 2> gpurun_out/${tag}_c5k1.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k1.json'));print('parts1',d['value'],d['ms_per_step'],d['pass_phases_rank0'])" ;;
+esac
+case "$1" in
+fuse)  # k_build's marksimp tail: its tests, then the C3 line with the tail on / off / on
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "build_marksimp or holds_before or build_tiers or heavy_indegree or repeated_passes or synthetic_corpus" > gpurun_out/${tag}_fuse_t.log 2>&1
+  rc=$?; tail -2 gpurun_out/${tag}_fuse_t.log; [ $rc -eq 0 ] || exit $rc
+  for v in 1 0 1; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --set build_marksimp=$v > gpurun_out/${tag}_fuse$v.json 2> gpurun_out/${tag}_fuse$v.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_fuse$v.json'));print('ms_fuse $v',d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],d['roofline'].get('avg_launch_ms'))"
+  done ;;
+esac
+case "$1" in
+loadab)  # one C5 batch's load: upload parts 4 vs 1, then a kernel + copy trace of parts 4
+  timeout -k 10 300 python -u tools/load_probe.py 143 load_parts=4 > gpurun_out/${tag}_lp4.log 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/load_probe.py 143 load_parts=1 > gpurun_out/${tag}_lp1.log 2>&1 || exit 1
+  tail -2 gpurun_out/${tag}_lp4.log; tail -2 gpurun_out/${tag}_lp1.log
+  cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace -o lp -- python3 $GRAFT_REPO_ROOT/tools/load_probe.py 143 load_parts=4 > $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace.log 2>&1 || exit 1
+  tail -2 $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace.log ;;
+esac
