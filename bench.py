@@ -76,6 +76,8 @@ def parse():
                          "sweeps overlap another's bandwidth-bound passes (default: the config's)")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="--runs-total passes: no load of the next pass's first batch beside the last analysis")
     ap.add_argument("--runs-total", type=int, default=None,
                     help="C5 at its configured size (BASELINE configs[4]: 1k runs): the runs in batches of "
                          "--batch-runs, each uploaded (H2D + CSR) on one of two contexts while the previous batch is "
@@ -442,6 +444,9 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
     nemo_amd/batched.py's BatchedPasses.run_pass (tests/test_gpu_batched.py checks the same code against the
     oracle): batch i+1 loaded (H2D + CSR + Kahn levels) on one of two contexts from a second host thread while
     batch i is analysed on the other, the batches' proto vectors summed on the host (prototype.go:79-130).
+    The last batch's analysis overlaps the load of the next pass's first batch (BatchedPasses prefetch;
+    --no-prefetch: each pass starts with its own first load): every timed pass does one load and one analysis
+    per batch, and the clock stops only after the load the last pass started is done.
     value = runs of a pass / its wall time, uploads included; generation and the one-time page-locking of the
     batches are not timed (they stand in for reading Molly output; the pin time is reported)."""
     from nemo_amd.batched import BatchedPasses, split_even
@@ -459,7 +464,8 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
         a += n
     gen_s = time.time() - t0
     opts = [tuple(kv.split("=", 1)) for kv in args.set]
-    bp = BatchedPasses(batches, mode=mode, device=local, options=[(k, int(v)) for k, v in opts])
+    bp = BatchedPasses(batches, mode=mode, device=local, options=[(k, int(v)) for k, v in opts],
+                       prefetch=not args.no_prefetch)
     phase = {}
     try:
         for _ in range(args.warmup):
@@ -470,6 +476,7 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
         t_start = time.perf_counter()
         for _ in range(args.steps):
             phase = bp.run_pass().phases
+        bp.drain()  # the next pass's first load, started inside the timed passes, is timed too
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -508,8 +515,9 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
                       "nodes_per_graph": gen["target_nodes"], "eot": gen["eot"], "nodes_total_rank0": Vn,
                       "edges_total_rank0": E_, "edges_per_node": round(E_ / max(Vn, 1), 3),
                       "failed_runs_rank0": len(bp.failed), "diff_mode": args.diff_mode,
-                      "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped); batches "
-                                     f"page-locked once (nemo_host_register)",
+                      "parallelism": f"run-sharded x{world}; two contexts per GPU (upload / analysis overlapped"
+                                     f"{'' if args.no_prefetch else ', the next pass first batch loaded beside the last analysis'}"
+                                     f"); batches page-locked once (nemo_host_register)",
                       "lib_options": args.set},
            "roofline": None, "cpu_baseline": cpu, "gen_seconds_rank0": round(gen_s, 2),
            "pass_phases_rank0": dict(phase), "pin_s_rank0": round(bp.pin_s, 3), "pin_failed_arrays": bp.pin_failed,

@@ -10,6 +10,10 @@ a sum of per-run count vectors here) and failedRuns[0]'s label set of the refere
 A pass loads batch i+1 (nemo_load_corpus: H2D + CSR + Kahn levels) on one context, from a second host
 thread, while batch i is analysed on the other: mark, diff, simplify, protos partial, hand-over, pulls,
 every D2H.  Batches are page-locked once (nemo_host_register), so each upload runs at the DMA rate.
+With prefetch=True the last batch's analysis also overlaps the load of the next pass's first batch (the
+batch ordinals run on across passes, so that load goes to the context the last batch is not on); every
+pass then does one load per batch inside it (its own batches 1.. and the next pass's batch 0), and
+close() waits for a load no pass used.
 bench.py's C5 1k-run line (`--runs-total`) and tests/test_gpu_batched.py run this same code.
 """
 from __future__ import annotations
@@ -69,9 +73,12 @@ class BatchedPasses:
     """Two contexts on one device; pass() analyses every batch once, uploads included."""
 
     def __init__(self, batches: Sequence[Corpus], mode: int = DIFF_REFERENCE, device: int = 0,
-                 options: Sequence[tuple] = (), pin: bool = True):
+                 options: Sequence[tuple] = (), pin: bool = True, prefetch: bool = False):
         self.batches = list(batches)
         self.mode = mode
+        self.prefetch = prefetch
+        self._ord = 0                      # batch ordinal across passes: batch k of the pass is on engine (_ord + k) % 2
+        self._pending = None               # (thread, errors, times) of a started load of the next pass's batch 0
         succ, fail = [], []
         for c in self.batches:
             for it, st, o in zip(c.iteration, c.status, _owned(c)):
@@ -111,7 +118,15 @@ class BatchedPasses:
                 self.pinned.append(p)
             self.pin_s = time.perf_counter() - t
 
+    def drain(self) -> None:
+        """Wait for a started load of the next pass's batch 0 (the next pass still uses it)."""
+        if self._pending is not None:
+            self._pending[0].join()
+
     def close(self) -> None:
+        if self._pending is not None:
+            self._pending[0].join()
+            self._pending = None
         for e in self.engines:
             e.close()
         self.engines = []
@@ -166,17 +181,45 @@ class BatchedPasses:
 
         vec = np.zeros(2 * self.T + 4, np.int64)
         out = [] if collect else None
-        timed_load(self.engines[0], self.batches[0])
-        if errs:
-            raise errs[0]
+        nb, o = len(self.batches), self._ord
+        eng = lambda k: self.engines[(o + k) % 2]  # noqa: E731
+        if self._pending is not None:  # batch 0's load, started beside the previous pass's last analysis
+            th0, errs0, times0 = self._pending
+            self._pending = None
+            tj = time.perf_counter()
+            th0.join()
+            phases["join_wait_s"].append(round(time.perf_counter() - tj, 3))
+            phases["load_s"] += times0
+            if errs0:
+                raise errs0[0]
+        else:
+            timed_load(eng(0), self.batches[0])
+            if errs:
+                raise errs[0]
         for i, c in enumerate(self.batches):
             th = None
-            if i + 1 < len(self.batches):
-                th = threading.Thread(target=timed_load, args=(self.engines[(i + 1) % 2], self.batches[i + 1]))
+            if i + 1 < nb:
+                th = threading.Thread(target=timed_load, args=(eng(i + 1), self.batches[i + 1]))
                 th.start()
+            elif self.prefetch:  # the next pass's batch 0, on the other engine
+                errs1: List[BaseException] = []
+                times1: List[float] = []
+
+                def load_next(e=eng(nb), c0=self.batches[0]):
+                    try:
+                        t1 = time.perf_counter()
+                        e.load(c0)
+                        e.synchronize()
+                        times1.append(round(time.perf_counter() - t1, 3))
+                    except BaseException as ex:  # re-raised by the pass that uses it
+                        errs1.append(ex)
+
+                th1 = threading.Thread(target=load_next)
+                th1.start()
+                self._pending = (th1, errs1, times1)
             t = time.perf_counter()
             try:
-                v, res = self._analyse(self.engines[i % 2], c, collect)
+                v, res = self._analyse(eng(i), c, collect)
                 phases["analyse_s"].append(round(time.perf_counter() - t, 3))
             finally:
                 if th is not None:
@@ -188,6 +231,7 @@ class BatchedPasses:
             vec += v
             if collect:
                 out.append(res)
+        self._ord = (o + nb) % 2
         for e in self.engines:
             e.synchronize()
         a, inter, uni = E.reduce_interpret(vec.astype(np.uint32), self.T, self.table_post)

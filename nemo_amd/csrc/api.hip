@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -45,6 +46,7 @@ struct nemo_ctx {
   hipStream_t up = nullptr;
   std::vector<hipEvent_t> ev_up;
   uint32_t load_parts = 4;
+  std::vector<uint32_t> big_host;  // the big-graph list (DevCorpus::big) on the host
   std::string err;
   std::vector<std::string> tgroups;  // nemo_set_timing_groups: the timed groups (empty: all)
   bool timing = false;
@@ -270,9 +272,16 @@ static int dalloc(nemo_ctx *c, T **p, size_t n) {
     q = it->second;
     c->cache.erase(it);
   } else {
-    // large blocks get a little headroom, so that the next corpus of about the same shape reuses them
-    const size_t want = bytes >= (64u << 20) ? ((bytes + bytes / 32) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1) : bytes;
+    // large blocks get headroom, so that the next corpus of about the same shape reuses them: 1/16
+    // (C5's 143-run batches differ by up to 3.3 % in edges; at 1/32 a load found some block too small
+    // about every other time, allocated anew (~28 ms) and the next load's drop_cache freed the unused
+    // block: hipFree waits for the whole device, ~220 ms behind the other context's analysis)
+    const size_t want = bytes >= (64u << 20) ? ((bytes + bytes / 16) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1) : bytes;
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&q, want);
+    if (getenv("NEMO_LOAD_DEBUG") && want >= (64u << 20))
+      fprintf(stderr, "dalloc: new block %zu MB (%s) %.1f ms, %zu cached\n", want >> 20, e == hipSuccess ? "ok" : "failed",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), c->cache.size());
     if (e != hipSuccess) {
       (void)hipGetLastError();
       drop_cache(c);  // no room: the cached blocks go first, then the headroom
@@ -893,30 +902,49 @@ static int check_graph_errors(nemo_ctx *c) {
   return NEMO_OK;
 }
 
-// parts: upload parts of a big-graph corpus (nemo_load_corpus): part k's edges land behind
-// ev_up[k] on the upload stream, and its graphs' bucketed CSR build waits for that event only
-// (the CSR build of part k overlaps the upload of part k + 1); the rest of the load runs behind
-// the last part
-static int device_load(nemo_ctx *c, const std::vector<uint32_t> *parts = nullptr) {
+// Upload parts of a corpus whose edges are mostly big graphs (nemo_load_corpus, option load_parts):
+// part k = the big-list entries [b0, b1) and the edge range [e0, e1) of the graphs from big[b0] up
+// to the next part's first big graph (every edge in exactly one part).
+struct LoadPart {
+  uint32_t b0, b1;
+  uint64_t e0, e1;
+};
+struct LoadParts {
+  std::vector<LoadPart> part;
+  const uint32_t *src = nullptr, *dst = nullptr;  // the caller's edge arrays (host)
+  uint32_t *es = nullptr, *ed = nullptr;          // their device copies
+};
+
+// With parts, part k's edges are copied on the upload stream and its big graphs' CSR build
+// (k_csrb) is queued behind that copy alone; the host issues part k + 1's copy after queueing part
+// k's kernels.  A copy from page-locked memory holds the issuing thread until it is done (~200 ms
+// for a C5 batch's edges, measured), so issuing every copy first left no kernel to overlap them
+// with.  The rest of the load (k_build, k_csr, the Kahn levels) runs behind the last part: the
+// deep graphs' k_topo_deep is per-graph latency (~74 ms for any number of graphs), so one launch
+// per part took 4 x 70 ms.
+static int device_load(nemo_ctx *c, const LoadParts *lp = nullptr) {
   int rc;
-  const bool split = c->dc.n_big && parts && parts->size() > 2;
+  const bool split = c->dc.n_big && lp && lp->part.size() > 1;
   nemo::launch_zero(c->dc.err, c->G * sizeof(uint32_t), c->stream);
   if (split) {
-    // part k = big-list entries [parts[k], parts[k + 1]) (every graph big: the list is every graph
-    // in order, so a part's edges are one contiguous range)
-    for (size_t k = 0; k + 1 < parts->size(); k++) {
-      DevCorpus sc = c->dc;
-      const uint32_t b0 = (*parts)[k], b1 = (*parts)[k + 1];
-      sc.big = c->dc.big + b0;
-      sc.cb_hoff = c->dc.cb_hoff + b0;
-      sc.n_big = b1 - b0;
+    for (size_t k = 0; k < lp->part.size(); k++) {
+      const LoadPart &q = lp->part[k];
+      if (q.e1 > q.e0) {
+        HIPCHK(c, hipMemcpyAsync(lp->es + q.e0, lp->src + q.e0, (q.e1 - q.e0) * 4, hipMemcpyHostToDevice, c->up));
+        HIPCHK(c, hipMemcpyAsync(lp->ed + q.e0, lp->dst + q.e0, (q.e1 - q.e0) * 4, hipMemcpyHostToDevice, c->up));
+      }
+      HIPCHK(c, hipEventRecord(c->ev_up[k], c->up));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_up[k], 0));
+      if (q.b1 == q.b0) continue;
+      DevCorpus sc = c->dc;
+      sc.big = c->dc.big + q.b0;
+      sc.cb_hoff = c->dc.cb_hoff + q.b0;
+      sc.n_big = q.b1 - q.b0;
       const double f = (double)sc.n_big / (double)c->dc.n_big;
       if ((rc = timed(c, "k_csrb", f * (16 * c->bigE + 12 * c->bigV), f * c->bigE,
                       [&] { nemo::launch_csr_big(sc, c->big_chunks, c->stream); })))
         return rc;
     }
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_up.back(), 0));
   }
   // graphs within k_build's LDS caps vs the global tier
   double Vb = 0, Eb = 0, Vp = 0, Ep = 0;
@@ -966,12 +994,16 @@ static int device_load(nemo_ctx *c, const std::vector<uint32_t> *parts = nullptr
 int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   DISPATCH(node_load_corpus(c, in));
   if (!c || !in) return NEMO_ERR_INVALID;
+  const bool dbg = getenv("NEMO_LOAD_DEBUG") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms_since = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->copy) HIPCHK(c, hipStreamSynchronize(c->copy));
   if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
   if (c->up) HIPCHK(c, hipStreamSynchronize(c->up));
   release_corpus(c);
+  const double t_rel = ms_since();
   if (in->n_tables > NEMO_MAX_TABLES)
     return fail(c, NEMO_ERR_LIMIT, "%u tables exceed NEMO_MAX_TABLES (%u)", in->n_tables, NEMO_MAX_TABLES);
   if (!in->iteration || !in->node_off || !in->edge_off || (!in->node_word && in->n_runs))
@@ -1129,6 +1161,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     if (!big.empty()) HIPCHK(c, hipMemcpy(db, big.data(), big.size() * 4, hipMemcpyHostToDevice));
     d.big = db;
     d.n_big = (uint32_t)big.size();
+    c->big_host = big;
     // the bucketed build's (bucket, chunk) count tables and (key, value) edge scratch
     d.cb_hist = d.cb_key = d.cb_val = nullptr;
     d.cb_hoff = nullptr;
@@ -1181,42 +1214,51 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     HIPCHK(c, hipMemcpyAsync(label, in->label, V * 4, hipMemcpyHostToDevice, s));
     if (rank) HIPCHK(c, hipMemcpyAsync(rank, in->id_rank, V * 4, hipMemcpyHostToDevice, s));
   }
-  // a corpus of big graphs only (the deep configs) uploads its edges in parts on a stream of
-  // their own, so that the bucketed CSR build of part k runs while part k + 1 is in flight
-  std::vector<uint32_t> parts;
-  if (getenv("NEMO_LOAD_DEBUG"))
-    fprintf(stderr, "nemo_load_corpus: E %zu n_big %u G %zu cb_hist %d load_parts %u\n", E, d.n_big, G,
-            d.cb_hist != nullptr, c->load_parts);
-  if (E && d.n_big == G && d.cb_hist && c->load_parts > 1 && G >= 2 * c->load_parts) {
-    for (uint32_t k = 0; k <= c->load_parts; k++) parts.push_back((uint32_t)((uint64_t)G * k / c->load_parts));
-    if (!c->up) HIPCHK(c, hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
-    while (c->ev_up.size() < parts.size() - 1) {
-      hipEvent_t e = nullptr;
-      HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->ev_up.push_back(e);
+  // a corpus whose edges are mostly in big graphs outside k_build's caps (the deep configs) uploads
+  // them in parts from device_load, each part's CSR build and Kahn levels behind its own copy
+  d.G = c->G;
+  set_build_tier(c);
+  LoadParts lp;
+  {
+    const uint32_t P = c->load_parts;
+    bool ok = E && d.cb_hist && P > 1 && d.n_big >= 2 * P && c->topo_ell_off && c->bigE >= 0.5 * (double)E;
+    for (uint32_t b = 0; b < d.n_big && ok; b++) {  // no big graph of k_build's (its redo flag comes later)
+      const uint32_t g = c->big_host[b];
+      const uint64_t v = c->node_off[g + 1] - c->node_off[g], e = c->edge_off[g + 1] - c->edge_off[g];
+      ok = !(d.bld_bytes && v <= d.bld_v && e <= d.bld_e);
     }
-    // the node arrays and offsets queued on `s` first: the upload stream starts behind them
-    if ((rc = ensure_event(c, &c->ev_misc))) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_misc, s));
-    HIPCHK(c, hipStreamWaitEvent(c->up, c->ev_misc, 0));
-    for (size_t k = 0; k + 1 < parts.size(); k++) {
-      const uint64_t a = c->edge_off[parts[k]], n = c->edge_off[parts[k + 1]] - a;  // big list = every graph
-      if (n) {
-        HIPCHK(c, hipMemcpyAsync(es + a, in->edge_src + a, n * 4, hipMemcpyHostToDevice, c->up));
-        HIPCHK(c, hipMemcpyAsync(ed + a, in->edge_dst + a, n * 4, hipMemcpyHostToDevice, c->up));
+    if (ok) {
+      if (!c->up) HIPCHK(c, hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+      while (c->ev_up.size() < P) {
+        hipEvent_t e = nullptr;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->ev_up.push_back(e);
       }
-      HIPCHK(c, hipEventRecord(c->ev_up[k], c->up));
+      for (uint32_t k = 0; k < P; k++) {
+        LoadPart q;
+        q.b0 = (uint32_t)((uint64_t)d.n_big * k / P);
+        q.b1 = (uint32_t)((uint64_t)d.n_big * (k + 1) / P);
+        q.e0 = k ? c->edge_off[c->big_host[q.b0]] : 0;
+        q.e1 = k + 1 < P ? c->edge_off[c->big_host[q.b1]] : E;
+        lp.part.push_back(q);
+      }
+      lp.src = in->edge_src;
+      lp.dst = in->edge_dst;
+      lp.es = es;
+      lp.ed = ed;
     }
-  } else if (E) {
+  }
+  if (lp.part.empty() && E) {
     HIPCHK(c, hipMemcpyAsync(es, in->edge_src, E * 4, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(ed, in->edge_dst, E * 4, hipMemcpyHostToDevice, s));
   }
+  if (dbg)
+    fprintf(stderr, "nemo_load_corpus: E %zu n_big %u G %zu cb_hist %d load_parts %u -> %zu parts; sync+release %.1f ms, +alloc %.1f ms\n",
+            E, d.n_big, G, d.cb_hist != nullptr, c->load_parts, lp.part.size(), t_rel, ms_since());
   HIPCHK(c, hipMemcpyAsync(c->d_owned, c->owned.data(), R, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemsetAsync(d.nch, 0, G * 4, s));
   HIPCHK(c, hipMemsetAsync(d.prehold, 0, G * 4, s));
-  d.G = c->G;
   d.hcap_limit = c->hcap_limit;
-  set_build_tier(c);
   d.comp_limit = c->comp_limit;
   set_lds_tier(c);
   set_global_block(c);
@@ -1341,8 +1383,10 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     if ((rc = dalloc(c, &c->d_tpost, 2 * c->tcap[1] + 2))) return rc;
     if ((rc = dalloc(c, &c->d_tasync, c->tcap[2] + 1))) return rc;
   }
-  if ((rc = device_load(c, &parts))) return rc;
+  if (dbg) fprintf(stderr, "nemo_load_corpus: host part done %.1f ms\n", ms_since());
+  if ((rc = device_load(c, lp.part.empty() ? nullptr : &lp))) return rc;
   if ((rc = check_graph_errors(c))) return rc;
+  if (dbg) fprintf(stderr, "nemo_load_corpus: done %.1f ms\n", ms_since());
   c->loaded = true;
   return NEMO_OK;
 }
@@ -1660,6 +1704,10 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
   const uint64_t E0 = c->edge_off[g0 + 1] - c->edge_off[g0];
   const bool dx = c->dx_ok && !c->diff_legacy && (c->diff_window != 2 || c->g0_maxdeg <= nemo::dx_max_row_tiny());
   int rc;
+  // capacities in whole 64-entry chunks: the per-entry buffers of corpora (batches) with a few more
+  // or fewer failed runs are the same size, so the allocation cache hands the same blocks back (a
+  // block no load takes is freed at the next load, and hipFree waits for the whole device)
+  const uint64_t nf_cap = (n_failed + 63) & ~(uint64_t)63;
   if (n_failed > c->diff_cap) {
     for (void *q : {(void *)c->d_dsrc, (void *)c->d_dmask, (void *)c->d_miss, (void *)c->d_dbits, (void *)c->d_dumask,
                     (void *)c->d_ddepth, (void *)c->d_dtopo})
@@ -1668,35 +1716,35 @@ static int diffprov_impl(nemo_ctx *c, const uint32_t *failed_iters, size_t n_fai
     c->d_ddepth = nullptr;
     c->d_dtopo = nullptr;
     c->legacy_cap = 0;
-    if ((rc = dalloc(c, &c->d_dsrc, 3 * n_failed))) return rc;
-    if ((rc = dalloc(c, &c->d_dmask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_miss, 2 * n_failed * (V0 + 1)))) return rc;
-    c->diff_cap = (uint32_t)n_failed;
+    if ((rc = dalloc(c, &c->d_dsrc, 3 * nf_cap))) return rc;
+    if ((rc = dalloc(c, &c->d_dmask, nf_cap * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_miss, 2 * nf_cap * (V0 + 1)))) return rc;
+    c->diff_cap = (uint32_t)nf_cap;
   }
   if (!dx && n_failed > c->legacy_cap) {  // the one-workgroup-per-entry kernels' scratch
     for (void *q : {(void *)c->d_dbits, (void *)c->d_dumask, (void *)c->d_ddepth, (void *)c->d_dtopo}) dfree(c, q);
     c->d_dbits = c->d_dumask = nullptr;
     c->d_ddepth = nullptr;
     c->d_dtopo = nullptr;
-    if ((rc = dalloc(c, &c->d_dbits, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dumask, n_failed * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_ddepth, n_failed * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dbits, nf_cap * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dumask, nf_cap * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_ddepth, nf_cap * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dtopo, 4 * V0 + 2 * E0 + 2 + c->n_r0lab))) return rc;
-    c->legacy_cap = (uint32_t)n_failed;
+    c->legacy_cap = (uint32_t)nf_cap;
   }
-  const uint32_t nch = (nu + 63) / 64, w32 = (uint32_t)((V0 + 31) / 32);
+  const uint32_t nch = (nu + 63) / 64, w32 = (uint32_t)((V0 + 31) / 32), nu_cap = 64 * nch;
   if (dx && (nu > c->dx_nu_cap || nch > c->dx_nch_cap)) {
     for (void *q : {(void *)c->d_dxpb, (void *)c->d_dxsval, (void *)c->d_dxlpl, (void *)c->d_dxw, (void *)c->d_dxfb})
       dfree(c, q);
     c->d_dxpb = c->d_dxsval = c->d_dxlpl = c->d_dxfb = nullptr;
     c->d_dxw = nullptr;
     c->dx_nu_cap = c->dx_nch_cap = 0;
-    if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu * w32))) return rc;
-    if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu * V0))) return rc;
-    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu + nch))) return rc;  // maxima, then the chunks' walk flags
+    if ((rc = dalloc(c, &c->d_dxpb, (size_t)nu_cap * w32))) return rc;
+    if ((rc = dalloc(c, &c->d_dxsval, (size_t)nu_cap * V0))) return rc;
+    if ((rc = dalloc(c, &c->d_dxlpl, (size_t)nu_cap + nch))) return rc;  // maxima, then the chunks' walk flags
     if ((rc = dalloc(c, &c->d_dxw, 4 * (size_t)nch * V0))) return rc;
     if ((rc = dalloc(c, &c->d_dxfb, 8 * (size_t)nch * V0))) return rc;  // 32 bytes per position and chunk
-    c->dx_nu_cap = nu;
+    c->dx_nu_cap = nu_cap;
     c->dx_nch_cap = nch;
   }
   if (!c->d_nmiss && (rc = dalloc(c, &c->d_nmiss, 1))) return rc;

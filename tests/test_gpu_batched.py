@@ -42,10 +42,7 @@ def _rows(m):
     return m[np.lexsort((m[:, 1], m[:, 0]))]
 
 
-@pytest.mark.parametrize("tiers", ["deep", "default"])
-@pytest.mark.parametrize("mode", [DIFF_PER_RUN, DIFF_REFERENCE])
-def test_batched_passes_match_oracle(tiers, mode):
-    sizes = [9, 4, 7, 9]  # unequal: the second load shrinks, the third and fourth grow again
+def _check_passes(sizes, mode, options=(), prefetch=False, passes=2):
     batches, whole = _batches(sizes, **SHAPE)
     s_all, f_all = whole.success_iters(), whole.failed_iters()
     assert f_all and len(batches) >= 3
@@ -55,11 +52,11 @@ def test_batched_passes_match_oracle(tiers, mode):
         g = 2 * whole.run_index(min(f_all)) + 1
         a, b = int(whole.node_off[g]), int(whole.node_off[g + 1])
         f0_labels = whole.label[a:b][(whole.node_word[a:b] & NODE_RULE) == 0]
-    bp = BatchedPasses(batches, mode=mode, options=DEEP if tiers == "deep" else ())
+    bp = BatchedPasses(batches, mode=mode, options=options, prefetch=prefetch)
     try:
         assert bp.pin_failed == 0
         assert bp.success[0] == 0 and sorted(bp.success) == sorted(s_all) and sorted(bp.failed) == sorted(f_all)
-        for p in range(2):  # a second pass reloads every batch into the other context's cached blocks
+        for p in range(passes):  # a later pass reloads every batch into the other context's cached blocks
             res = bp.run_pass(collect=True)
             assert np.array_equal(res.vec.astype(np.uint32), orc_all.reduce), f"pass {p}: reduction vectors differ"
             assert res.achieved == orc_all.achieved
@@ -83,3 +80,18 @@ def test_batched_passes_match_oracle(tiers, mode):
                     assert np.array_equal(_rows(r.missing), _rows(orc.missing)), "missing rows differ"
     finally:
         bp.close()
+
+
+@pytest.mark.parametrize("tiers", ["deep", "default"])
+@pytest.mark.parametrize("mode", [DIFF_PER_RUN, DIFF_REFERENCE])
+def test_batched_passes_match_oracle(tiers, mode):
+    # unequal: the second load shrinks, the third and fourth grow again
+    _check_passes([9, 4, 7, 9], mode, options=DEEP if tiers == "deep" else ())
+
+
+@pytest.mark.parametrize("parts", [4, 1])
+def test_batched_passes_prefetch(parts):
+    """bench.py's C5 1k line: the next pass's first batch loaded beside the last analysis (three batches, so the
+    batch ordinals alternate the contexts across passes), edge uploads in parts with each part's CSR build
+    behind its own copy (option load_parts) and in one piece; three passes against the oracle."""
+    _check_passes([9, 4, 7], DIFF_PER_RUN, options=(("load_parts", parts),), prefetch=True, passes=3)

@@ -161,3 +161,38 @@ loadab)  # one C5 batch's load: upload parts 4 vs 1, then a kernel + copy trace 
   cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace -o lp -- python3 $GRAFT_REPO_ROOT/tools/load_probe.py 143 load_parts=4 > $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace.log 2>&1 || exit 1
   tail -2 $GRAFT_REPO_ROOT/gpurun_out/${tag}_lptrace.log ;;
 esac
+case "$1" in
+loaddbg)  # load phases of one C5 batch and of the 1k-run batched pass (NEMO_LOAD_DEBUG)
+  NEMO_LOAD_DEBUG=1 timeout -k 10 300 python -u tools/load_probe.py 143 load_parts=4 > gpurun_out/${tag}_lpdbg.log 2>&1 || exit 1
+  tail -8 gpurun_out/${tag}_lpdbg.log
+  NEMO_LOAD_DEBUG=1 timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5kdbg.json 2> gpurun_out/${tag}_c5kdbg.err || exit 1
+  grep nemo_load gpurun_out/${tag}_c5kdbg.err | tail -14
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5kdbg.json'));print(d['value'],d['ms_per_step'],d['pass_phases_rank0'])" ;;
+esac
+case "$1" in
+parts)  # interleaved part uploads: the big-graph tests, then the C5 1k line with parts 4 / 1
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_batched.py tests/test_gpu_c5_shape.py tests/test_gpu_deep.py tests/test_gpu_scale.py > gpurun_out/${tag}_t.log 2>&1
+  rc=$?; tail -2 gpurun_out/${tag}_t.log; [ $rc -eq 0 ] || exit $rc
+  NEMO_LOAD_DEBUG=1 timeout -k 10 300 python -u tools/load_probe.py 143 > gpurun_out/${tag}_lpdbg.log 2>&1 || exit 1
+  tail -4 gpurun_out/${tag}_lpdbg.log
+  for v in 4 1; do
+    NEMO_LOAD_DEBUG=1 timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --set load_parts=$v > gpurun_out/${tag}_c5k$v.json 2> gpurun_out/${tag}_c5k$v.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k$v.json'));print('parts $v',d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
+  done ;;
+esac
+case "$1" in
+c5kdbg)
+  NEMO_LOAD_DEBUG=1 timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5k.json 2> gpurun_out/${tag}_c5k.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k.json'));print(d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
+  grep -E "dalloc|release" gpurun_out/${tag}_c5k.err | tail -40 ;;
+esac
+case "$1" in
+prefetch)  # batched passes with prefetch + parts: tests, then the C5 1k line and the C3 line
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_batched.py tests/test_gpu_c5_shape.py tests/test_gpu_diff.py > gpurun_out/${tag}_t.log 2>&1
+  rc=$?; tail -2 gpurun_out/${tag}_t.log; [ $rc -eq 0 ] || exit $rc
+  NEMO_LOAD_DEBUG=1 timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5k.json 2> gpurun_out/${tag}_c5k.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k.json'));print(d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
+  grep -E "dalloc" gpurun_out/${tag}_c5k.err | tail -8
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_c3.json 2> gpurun_out/${tag}_c3.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c3.json'));print('c3',d['value'],d['ms_per_step'],d['roofline']['frac'])" ;;
+esac
