@@ -172,9 +172,14 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *   "build_marksimp"    k_build's graphs get their deferred mark + simplification
  *                       at the end of k_build, from the edges it holds (1), or
  *                       from k_marksimp in nemo_simplify (0, default)
- *   "load_parts"        corpora of big graphs only: uploads in this many parts,
- *                       each part's CSR build behind its own upload (default 4;
- *                       1 = one upload, then the build)
+ *   "load_parts"        corpora mostly of big graphs: edge uploads in this many
+ *                       parts, each part's CSR build behind its own upload
+ *                       (default 4; 1 = one upload, then the build)
+ *   "load_async"        1: nemo_load_corpus returns once its work is queued; its
+ *                       graph checks (validations, acyclicity) are reported by
+ *                       the next nemo_rebuild / nemo_mark_holds / nemo_goal_labels /
+ *                       nemo_pull_edges, which then leaves no corpus loaded
+ *                       (0, default: nemo_load_corpus waits and reports them)
  *   "topo_ell"          deep graphs' Kahn levels by the edge-parallel k_topo_ell
  *                       (1) or one workgroup per graph, k_topo_deep (0, default) */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);

@@ -13,7 +13,10 @@ every D2H.  Batches are page-locked once (nemo_host_register), so each upload ru
 With prefetch=True the last batch's analysis also overlaps the load of the next pass's first batch (the
 batch ordinals run on across passes, so that load goes to the context the last batch is not on); every
 pass then does one load per batch inside it (its own batches 1.. and the next pass's batch 0), and
-close() waits for a load no pass used.
+close() waits for a load no pass used.  With load_async a load returns once its work is queued: the deep
+graphs' Kahn levels (~74 ms of per-graph latency at C5) finish behind the host, and the batch's mark
+reports the load's checks (nemo_set_option "load_async"; at C5 1k no faster, 418.6 vs 427.3 runs/s: the
+pass is then bound by the analyses, slowed from 0.25 to 0.30 s by the loads' kernels beside them).
 bench.py's C5 1k-run line (`--runs-total`) and tests/test_gpu_batched.py run this same code.
 """
 from __future__ import annotations
@@ -73,10 +76,14 @@ class BatchedPasses:
     """Two contexts on one device; pass() analyses every batch once, uploads included."""
 
     def __init__(self, batches: Sequence[Corpus], mode: int = DIFF_REFERENCE, device: int = 0,
-                 options: Sequence[tuple] = (), pin: bool = True, prefetch: bool = False):
+                 options: Sequence[tuple] = (), pin: bool = True, prefetch: bool = False,
+                 load_async: bool = False):
         self.batches = list(batches)
         self.mode = mode
         self.prefetch = prefetch
+        # option load_async: a load returns once queued (its Kahn levels still running); the batch's
+        # analysis (mark) then reports the load's checks
+        self.load_async = load_async
         self._ord = 0                      # batch ordinal across passes: batch k of the pass is on engine (_ord + k) % 2
         self._pending = None               # (thread, errors, times) of a started load of the next pass's batch 0
         succ, fail = [], []
@@ -102,6 +109,8 @@ class BatchedPasses:
             e = E.Engine(device)
             for k, v in options:
                 e.set_option(k, int(v))
+            if self.load_async:
+                e.set_option("load_async", 1)
             self.engines.append(e)
         self.T = self.batches[0].n_tables
         self.table_post = self.batches[0].table_post
@@ -174,7 +183,8 @@ class BatchedPasses:
             try:
                 t = time.perf_counter()
                 eng.load(c)
-                eng.synchronize()
+                if not self.load_async:
+                    eng.synchronize()
                 phases["load_s"].append(round(time.perf_counter() - t, 3))
             except BaseException as ex:  # re-raised on the calling thread
                 errs.append(ex)
@@ -209,7 +219,8 @@ class BatchedPasses:
                     try:
                         t1 = time.perf_counter()
                         e.load(c0)
-                        e.synchronize()
+                        if not self.load_async:
+                            e.synchronize()
                         times1.append(round(time.perf_counter() - t1, 3))
                     except BaseException as ex:  # re-raised by the pass that uses it
                         errs1.append(ex)

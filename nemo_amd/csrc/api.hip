@@ -46,6 +46,8 @@ struct nemo_ctx {
   hipStream_t up = nullptr;
   std::vector<hipEvent_t> ev_up;
   uint32_t load_parts = 4;
+  bool load_async = false;          // option load_async: nemo_load_corpus returns once its work is queued
+  bool load_check_pending = false;  // ... and the graph checks wait for the next call that reads the graphs
   std::vector<uint32_t> big_host;  // the big-graph list (DevCorpus::big) on the host
   std::string err;
   std::vector<std::string> tgroups;  // nemo_set_timing_groups: the timed groups (empty: all)
@@ -580,6 +582,7 @@ static void release_corpus(nemo_ctx *c) {
   c->loaded = c->marked = c->simplified = c->protos_done = c->trig_done = false;
   c->mark_pending = false;
   c->ms_fused = false;
+  c->load_check_pending = false;
 }
 
 void nemo_ctx_destroy(nemo_ctx *c) {
@@ -721,6 +724,10 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
   }
   if (!strcmp(name, "build_marksimp")) {  // 1: k_build's tail; 0 / -1: k_marksimp takes every tier graph
     c->ms_fuse_off = value <= 0;
+    return NEMO_OK;
+  }
+  if (!strcmp(name, "load_async")) {  // 1: nemo_load_corpus does not wait for its kernels (checks deferred)
+    c->load_async = value > 0;
     return NEMO_OK;
   }
   if (!strcmp(name, "load_parts")) {  // big-graph corpora: uploads in this many parts (1: one upload, then the build)
@@ -900,6 +907,16 @@ static int check_graph_errors(nemo_ctx *c) {
     return fail(c, (int)err[g], "Run %u: edge references a node index out of range", it);
   }
   return NEMO_OK;
+}
+
+// Option load_async: the last load's graph checks (validations, acyclicity), before the first call
+// that reads its graphs; a failed check leaves no corpus loaded, as a failed nemo_load_corpus does.
+static int ensure_load_checked(nemo_ctx *c) {
+  if (!c->load_check_pending) return NEMO_OK;
+  c->load_check_pending = false;
+  const int rc = check_graph_errors(c);
+  if (rc) c->loaded = false;
+  return rc;
 }
 
 // Upload parts of a corpus whose edges are mostly big graphs (nemo_load_corpus, option load_parts):
@@ -1385,7 +1402,11 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
   }
   if (dbg) fprintf(stderr, "nemo_load_corpus: host part done %.1f ms\n", ms_since());
   if ((rc = device_load(c, lp.part.empty() ? nullptr : &lp))) return rc;
-  if ((rc = check_graph_errors(c))) return rc;
+  if (c->load_async) {
+    c->load_check_pending = true;  // the checks wait on `stream` at the next call that reads the graphs
+  } else if ((rc = check_graph_errors(c))) {
+    return rc;
+  }
   if (dbg) fprintf(stderr, "nemo_load_corpus: done %.1f ms\n", ms_since());
   c->loaded = true;
   return NEMO_OK;
@@ -1396,7 +1417,9 @@ int nemo_rebuild(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   HIPCHK(c, hipSetDevice(c->device));
-  int rc = guard_staged(c);
+  int rc = ensure_load_checked(c);
+  if (rc) return rc;
+  rc = guard_staged(c);
   if (rc) return rc;
   if ((rc = join_aux(c))) return rc;  // the diff kernels read the graphs rebuilt here
   rc = device_load(c);
@@ -1424,6 +1447,7 @@ int nemo_mark_holds(nemo_ctx *c) {
   if (!c) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "nemo_mark_holds before nemo_load_corpus");
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rl = ensure_load_checked(c)) return rl;
   const double V = (double)c->V - c->tierV, E = (double)c->E - c->tierE;
   int rc = guard_staged(c);
   if (rc) return rc;
@@ -1918,6 +1942,8 @@ int nemo_goal_labels(nemo_ctx *c, uint32_t iteration, int cond, uint32_t *d_out,
   DISPATCH(node_goal_labels(c, iteration, cond, d_out, cap));
   if (!c || !d_out || (cond != 0 && cond != 1)) return NEMO_ERR_INVALID;
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rl = ensure_load_checked(c)) return rl;
   uint32_t r;
   int rc = run_index(c, iteration, &r);
   if (rc) return rc;
@@ -2373,7 +2399,8 @@ int nemo_pull_edges(nemo_ctx *c, int which) {
   if (!c->loaded) return fail(c, NEMO_ERR_STATE, "no corpus loaded");
   if (which == 1 && !c->simplified) return fail(c, NEMO_ERR_STATE, "simplified pull before nemo_simplify");
   HIPCHK(c, hipSetDevice(c->device));
-  int rc;
+  int rc = ensure_load_checked(c);
+  if (rc) return rc;
   const uint32_t slots = which == 2 ? c->n_entries : c->G;
   // the previous pull's slot table may still be in flight into the pinned tables: wait for it
   // only when they are about to be reallocated (a pull queued behind another on the same

@@ -42,7 +42,7 @@ def _rows(m):
     return m[np.lexsort((m[:, 1], m[:, 0]))]
 
 
-def _check_passes(sizes, mode, options=(), prefetch=False, passes=2):
+def _check_passes(sizes, mode, options=(), prefetch=False, passes=2, load_async=None):
     batches, whole = _batches(sizes, **SHAPE)
     s_all, f_all = whole.success_iters(), whole.failed_iters()
     assert f_all and len(batches) >= 3
@@ -52,7 +52,7 @@ def _check_passes(sizes, mode, options=(), prefetch=False, passes=2):
         g = 2 * whole.run_index(min(f_all)) + 1
         a, b = int(whole.node_off[g]), int(whole.node_off[g + 1])
         f0_labels = whole.label[a:b][(whole.node_word[a:b] & NODE_RULE) == 0]
-    bp = BatchedPasses(batches, mode=mode, options=options, prefetch=prefetch)
+    bp = BatchedPasses(batches, mode=mode, options=options, prefetch=prefetch, load_async=load_async)
     try:
         assert bp.pin_failed == 0
         assert bp.success[0] == 0 and sorted(bp.success) == sorted(s_all) and sorted(bp.failed) == sorted(f_all)
@@ -89,9 +89,11 @@ def test_batched_passes_match_oracle(tiers, mode):
     _check_passes([9, 4, 7, 9], mode, options=DEEP if tiers == "deep" else ())
 
 
-@pytest.mark.parametrize("parts", [4, 1])
-def test_batched_passes_prefetch(parts):
+@pytest.mark.parametrize("parts,load_async", [(4, True), (1, True), (4, False)])
+def test_batched_passes_prefetch(parts, load_async):
     """bench.py's C5 1k line: the next pass's first batch loaded beside the last analysis (three batches, so the
     batch ordinals alternate the contexts across passes), edge uploads in parts with each part's CSR build
-    behind its own copy (option load_parts) and in one piece; three passes against the oracle."""
-    _check_passes([9, 4, 7], DIFF_PER_RUN, options=(("load_parts", parts),), prefetch=True, passes=3)
+    behind its own copy (option load_parts) and in one piece, loads that return before their kernels finish
+    (option load_async) and loads that wait; three passes against the oracle."""
+    _check_passes([9, 4, 7], DIFF_PER_RUN, options=(("load_parts", parts),), prefetch=True, passes=3,
+                  load_async=load_async)

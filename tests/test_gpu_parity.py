@@ -85,6 +85,28 @@ def test_cycle_refused(eng):
     assert ei.value.code == 4
 
 
+def test_load_async_reports_at_mark(eng):
+    """Option load_async: nemo_load_corpus returns once its work is queued; the graph checks come from the next
+    call that reads the graphs (here nemo_mark_holds), which then leaves no corpus loaded, as a failed load
+    does.  A good corpus loaded the same way analyses as the oracle does."""
+    g = {"goals": [{"id": "goal0", "label": "a(1)", "table": "a", "time": "1"}],
+         "rules": [{"id": "rule0", "label": "a", "table": "a", "type": "next"}],
+         "edges": [{"from": "goal0", "to": "rule0"}, {"from": "rule0", "to": "goal0"}]}
+    eng.set_option("load_async", 1)
+    try:
+        eng.load(corpus_from_graphs([(0, "success", g, g)]))
+        with pytest.raises(E.NemoError) as ei:
+            eng.mark()
+        assert ei.value.code == 4 and "not acyclic" in str(ei.value)
+        with pytest.raises(E.NemoError) as ei:
+            eng.mark()
+        assert ei.value.code == 5
+        corpus, _ = random_corpus(77, n_runs=6, max_nodes=16)
+        _check(eng, corpus)
+    finally:
+        eng.set_option("load_async", 0)
+
+
 def test_diff_edge_pulls(eng):
     corpus, _ = random_corpus(4242, n_runs=5, max_nodes=20)
     f = corpus.failed_iters()

@@ -196,3 +196,10 @@ prefetch)  # batched passes with prefetch + parts: tests, then the C5 1k line an
   timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 > gpurun_out/${tag}_c3.json 2> gpurun_out/${tag}_c3.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/${tag}_c3.json'));print('c3',d['value'],d['ms_per_step'],d['roofline']['frac'])" ;;
 esac
+case "$1" in
+async)  # load_async: its tests, then the C5 1k line
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_batched.py tests/test_gpu_c5_shape.py "tests/test_gpu_parity.py::test_load_async_reports_at_mark" "tests/test_gpu_parity.py::test_cycle_refused" > gpurun_out/${tag}_t.log 2>&1
+  rc=$?; tail -2 gpurun_out/${tag}_t.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5k.json 2> gpurun_out/${tag}_c5k.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k.json'));print(d['value'],d['ms_per_step'],d['pass_phases_rank0'])" ;;
+esac
