@@ -179,7 +179,9 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *                       graph checks (validations, acyclicity) are reported by
  *                       the next nemo_rebuild / nemo_mark_holds / nemo_goal_labels /
  *                       nemo_pull_edges, which then leaves no corpus loaded
- *                       (0, default: nemo_load_corpus waits and reports them)
+ *                       (0, default: nemo_load_corpus waits and reports them).
+ *                       The corpus' arrays must stay valid until that call: the
+ *                       uploads from page-locked memory may still be in flight
  *   "topo_ell"          deep graphs' Kahn levels by the edge-parallel k_topo_ell
  *                       (1) or one workgroup per graph, k_topo_deep (0, default) */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);
