@@ -182,6 +182,9 @@ int nemo_set_stream(nemo_ctx *ctx, void *stream);
  *                       (0, default: nemo_load_corpus waits and reports them).
  *                       The corpus' arrays must stay valid until that call: the
  *                       uploads from page-locked memory may still be in flight
+ *   "build_relax"       k_build's Kahn levels by relaxation sweeps over the edges
+ *                       in registers, peeling if they give up (1), or by peeling
+ *                       (0, default)
  *   "topo_ell"          deep graphs' Kahn levels by the edge-parallel k_topo_ell
  *                       (1) or one workgroup per graph, k_topo_deep (0, default) */
 int nemo_set_option(nemo_ctx *ctx, const char *name, int64_t value);

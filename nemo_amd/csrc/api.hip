@@ -82,6 +82,8 @@ struct nemo_ctx {
   uint64_t bigVmax = 0;              // the largest of them
   uint32_t big_chunks = 1;           // k_csrb_* workgroups per big graph
   bool mark_pending = false;         // holds flags of the tier graphs not yet computed
+  bool relax_off = true;             // option build_relax 1: k_build's Kahn levels by relaxation sweeps first
+                                     // (measured slower at C3: k_build 2.96 -> 3.20 ms; kept as an option, tested)
   bool ms_fuse_off = true;           // option build_marksimp 1: k_build's marksimp tail (measured slower at C3:
                                      // k_build 3.00 -> 3.86 ms against k_marksimp's 0.80 ms; four workgroups
                                      // per CU by k_build's LDS image where k_marksimp runs eight waves per SIMD)
@@ -722,6 +724,11 @@ int nemo_set_option(nemo_ctx *c, const char *name, int64_t value) {
     c->diff_unfused = value == 0;
     return NEMO_OK;
   }
+  if (!strcmp(name, "build_relax")) {  // 1: k_build's Kahn levels by relaxation sweeps first; 0 / -1: peeling
+    c->relax_off = value <= 0;
+    c->dc.bld_relax = c->relax_off ? 0u : 1u;
+    return NEMO_OK;
+  }
   if (!strcmp(name, "build_marksimp")) {  // 1: k_build's tail; 0 / -1: k_marksimp takes every tier graph
     c->ms_fuse_off = value <= 0;
     return NEMO_OK;
@@ -1133,6 +1140,7 @@ int nemo_load_corpus(nemo_ctx *c, const nemo_corpus *in) {
     d.n_glob = (uint32_t)gl.size();
     d.glob_prep = !gl.empty() && !c->has_rank && !c->glob_prep_off;
     d.topo_ell = c->topo_ell_off ? 0u : 1u;
+    d.bld_relax = c->relax_off ? 0u : 1u;
     d.team = nullptr;
     A(d.team, nemo::glob_team_words());
     int ncu = 0;

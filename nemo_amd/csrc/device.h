@@ -205,6 +205,7 @@ struct DevCorpus {
   uint32_t glob_prep;                    // 1: k_glob_prep builds the deep graphs' H* order and adjacency (identity ranks)
   uint32_t topo_ell;                     // 1: deep graphs' Kahn levels by k_topo_ell (child records in gscratch)
   uint32_t ms_fuse;                      // 1: k_build's tail runs marksimp_graph on its graphs (marksimp.h)
+  uint32_t bld_relax;                    // 1: k_build's Kahn levels by relaxation sweeps (peeling if they give up)
   uint32_t n_glob;                       // deep graphs (gs_off != ~0)
   const uint32_t *glob_list;             // [n_glob] their graph ids
   uint32_t *team;                        // k_glob_prep's team scratch (barrier counters, phase sums)

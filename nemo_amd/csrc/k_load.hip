@@ -372,12 +372,94 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
     STAMP(12 + dir);
   }
   atomicAdd(&s_created, created);
-  // Kahn levels over the forward rows still in LDS (ptr[v] = end of row v)
   uint32_t *nlv = c.nlv + n0;
-  // the sources in node order: each thread counts those of a contiguous run
+  uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g;
+  uint32_t hi = 0, nl = 0;
+  // (round 6) Kahn levels by relaxation: lv(v) = max over v's parents of lv(u) + 1, swept over the
+  // edges still in registers until a sweep changes nothing.  That is the longest path from a
+  // source, the level Kahn's peeling gives; a sweep has no dependent chain (every edge's two LDS
+  // reads are independent), where a peeled level is a chain of LDS round trips and a barrier.
+  // Levels are u8 in cnt8's bytes (the in-degrees are recounted for the peeling below if the
+  // sweeps give up), their histogram packed u16 in s_rule's bytes (the rule bitmap is done with):
+  // a graph with more levels than either holds, or sweeps still changing after that many rounds
+  // (a cycle, or lost updates: two lanes writing one node's byte), takes the peeling path.
+  bool relaxed = false;
+  if (c.bld_relax) {
+    const uint32_t lcap = min(254u, lds_align(4u * ((V + 31u) / 32u)) / 2u - 1u);  // levels the histogram holds
+    for (uint32_t w = tid; w < (V + 3) / 4; w += B) cnt32[w] = 0;
+    if (tid < 3) s_cnt[tid] = 0;  // sweep r's "changed" flag is s_cnt[r % 3] (cleared two sweeps ahead)
+    if (tid == 0) s_tail = 0;
+    __syncthreads();
+    bool gave_up = false;
+    for (uint32_t r = 0;; r++) {
+      if (tid == 0) s_cnt[(r + 1) % 3] = 0;  // its last readers passed the barrier of sweep r - 1
+      bool ch = false;
+#pragma unroll
+      for (int q = 0; q < EPT; q++) {
+        if (sd[q] != ~0u) {
+          const uint32_t u = sd[q] >> 16, v = sd[q] & 0xFFFFu;
+          const uint32_t lu = cnt8[u] + 1u;
+          if (lu > cnt8[v]) {
+            cnt8[v] = (uint8_t)min(lu, 255u);
+            ch = true;
+          }
+        }
+        if ((q & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // eight edges' reads in flight at a time
+      }
+      if (__any(ch) && lane_id() == 0) s_cnt[r % 3] = 1;  // (not __syncthreads_or: its hidden LDS word
+      __syncthreads();                                    // cost k_build a workgroup per CU)
+      if (!s_cnt[r % 3]) break;
+      if (r + 1 >= lcap) {  // uniform: every thread read the same flag
+        gave_up = true;
+        break;
+      }
+    }
+    if (!gave_up) {  // a sweep can carry a level far along (edges in order): the levels are bounded, not the sweeps
+      uint32_t mx = 0;
+      for (uint32_t v = tid; v < V; v += B) mx = max(mx, (uint32_t)cnt8[v]);
+      for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+      if (lane_id() == 0) atomicMax(&s_tail, mx);
+      __syncthreads();
+      gave_up = s_tail >= lcap;  // (a saturated byte, 255, is past lcap too)
+    }
+    if (!gave_up) {
+      uint32_t *hist32 = s_rule;
+      uint16_t *hist = (uint16_t *)s_rule;
+      for (uint32_t i = tid; i < (lcap + 2) / 2; i += B) hist32[i] = 0;
+      nl = V ? s_tail + 1u : 0u;
+      __syncthreads();
+      for (uint32_t v = tid; v < V; v += B) {  // coalesced
+        const uint32_t l = cnt8[v];
+        atomicAdd(&hist32[l >> 1], 1u << (16 * (l & 1)));
+        nlv[v] = l;
+      }
+      __syncthreads();
+      block_scan_inplace<B, 4, true>(hist, nl + 1, s_lds);  // level starts; hist[nl] = V
+      for (uint32_t i = tid; i <= nl; i += B) lvl[i] = hist[i];
+      for (uint32_t v = tid; v < V; v += B) {
+        const uint32_t l = cnt8[v], sh = 16 * (l & 1);
+        q16[(atomicAdd(&hist32[l >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)v;
+      }
+      hi = V;
+      relaxed = true;
+    } else {  // back to in-degree counters (and the append counters the flags used) for the peeling
+      for (uint32_t w = tid; w < (V + 3) / 4; w += B) cnt32[w] = 0;
+      if (tid < 3) s_cnt[tid] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < EPT; q++)
+        if (sd[q] != ~0u) {
+          const uint32_t v = sd[q] & 0xFFFFu;
+          atomicAdd(&cnt32[v >> 2], 1u << (8 * (v & 3)));
+        }
+    }
+    __syncthreads();
+  }
+  // Kahn levels by peeling, over the forward rows still in LDS (ptr[v] = end of row v).
+  // The sources in node order: each thread counts those of a contiguous run
   // of counter words (all its reads in flight together), one block scan
   // places them (no per-wave append chain)
-  {
+  if (!relaxed) {
     constexpr int SW = 4;  // counter words (4 nodes each) per thread per round
     const uint32_t nw4 = (V + 3) / 4;
     uint32_t o = 0;
@@ -407,13 +489,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BLD_OCC(B))))
   }
   __syncthreads();
   STAMP(14);
-  uint32_t *topo = c.topo + n0, *lvl = c.lvl + n0 + g;
   // one barrier per level: level k appends behind the frontier through its
   // own counter s_cnt[k % 3]; the counter of level k + 1 is cleared during
   // level k (its last readers passed the barrier of level k - 1)
-  uint32_t lo = 0, hi = s_tail, nl = 0;
-  if (tid == 0) lvl[0] = 0;
-  while (lo < hi) {
+  uint32_t lo = 0;
+  if (!relaxed) {
+    hi = s_tail;
+    if (tid == 0) lvl[0] = 0;
+  }
+  while (!relaxed && lo < hi) {
     uint32_t *cur = &s_cnt[nl % 3];
     if (tid == 0) s_cnt[(nl + 1) % 3] = 0;
     for (uint32_t base = lo; base < hi; base += B) {

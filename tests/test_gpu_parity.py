@@ -239,26 +239,32 @@ def test_build_tiers_identical_device_arrays(eng, shape):
     sizes = {"topo": 4 * V, "lvl": 4 * (V + G), "nlev": 4 * G, "fp": 4 * (V + G), "fc": 4 * E,
              "rp": 4 * (V + G), "rc": 4 * E}
     got = {}
-    for build_max in (-1, 0):
+    # k_build with its relaxation sweeps (build_relax 1), the global tier, k_build peeling (the default)
+    for key, build_max, relax in (("relax", -1, 1), ("global", 0, 0), ("peel", -1, 0)):
         eng.set_option("build_lds_max", build_max)
+        eng.set_option("build_relax", relax)
         try:
             eng.load(corpus)
-            got[build_max] = {k: eng.debug_copy(k, 0, n).view(np.uint32) for k, n in sizes.items()}
+            got[key] = {k: eng.debug_copy(k, 0, n).view(np.uint32) for k, n in sizes.items()}
+            got[key]["nlv"] = eng.debug_copy("nlv", 0, 4 * V).view(np.uint32)
         finally:
             eng.set_option("build_lds_max", -1)
-    for k in ("nlev", "fp", "fc", "rp", "rc"):
-        assert np.array_equal(got[-1][k], got[0][k]), k
+            eng.set_option("build_relax", -1)
+    for other in ("global", "peel"):
+        for k in ("nlev", "fp", "fc", "rp", "rc"):
+            assert np.array_equal(got["relax"][k], got[other][k]), (other, k)
+        # Kahn order inside a level depends on wave timing: compare level sets
+        a, b, lv = got["relax"]["topo"], got[other]["topo"], got["relax"]["lvl"]
+        for g in range(G):
+            n0, n1 = int(corpus.node_off[g]), int(corpus.node_off[g + 1])
+            off = lv[n0 + g: n0 + g + int(got["relax"]["nlev"][g]) + 1]
+            assert np.array_equal(off, got[other]["lvl"][n0 + g: n0 + g + len(off)]), (other, g)
+            for l0, l1 in zip(off[:-1], off[1:]):
+                assert sorted(a[n0 + l0:n0 + l1]) == sorted(b[n0 + l0:n0 + l1])
+            assert int(off[-1]) == n1 - n0
+    assert np.array_equal(got["relax"]["nlv"], got["peel"]["nlv"])
     if shape == "long":
-        assert int(got[-1]["nlev"].max()) > 256
-    # Kahn order inside a level depends on wave timing: compare level sets
-    a, b, lv = got[-1]["topo"], got[0]["topo"], got[-1]["lvl"]
-    for g in range(G):
-        n0, n1 = int(corpus.node_off[g]), int(corpus.node_off[g + 1])
-        off = lv[n0 + g: n0 + g + int(got[-1]["nlev"][g]) + 1]
-        assert np.array_equal(off, got[0]["lvl"][n0 + g: n0 + g + len(off)])
-        for l0, l1 in zip(off[:-1], off[1:]):
-            assert sorted(a[n0 + l0:n0 + l1]) == sorted(b[n0 + l0:n0 + l1])
-        assert int(off[-1]) == n1 - n0
+        assert int(got["relax"]["nlev"].max()) > 256
 
 
 @pytest.mark.parametrize("lds_max", [0, 1500, 2600])

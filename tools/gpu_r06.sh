@@ -203,3 +203,12 @@ async)  # load_async: its tests, then the C5 1k line
   timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline > gpurun_out/${tag}_c5k.json 2> gpurun_out/${tag}_c5k.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/${tag}_c5k.json'));print(d['value'],d['ms_per_step'],d['pass_phases_rank0'])" ;;
 esac
+case "$1" in
+relax)  # k_build's relaxation levels: parity (tiers, C3 full, deep, batched), then the C3 line relax on / off / on
+  timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_golden.py tests/test_gpu_deep.py > gpurun_out/${tag}_t.log 2>&1
+  rc=$?; tail -2 gpurun_out/${tag}_t.log; [ $rc -eq 0 ] || exit $rc
+  for v in 1 0 1; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --set build_relax=$v > gpurun_out/${tag}_c3_$v.json 2> gpurun_out/${tag}_c3_$v.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_c3_$v.json'));print('relax $v',d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'],d['roofline']['frac'])"
+  done ;;
+esac
