@@ -20,3 +20,12 @@ c)
   bash tools/prof_diff.sh r06final_dp || exit 1 ;;
 esac
 echo part $1 done
+case "$1" in
+z)  # after the last library change: the whole GPU suite, smoke, the driver's C3 line
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r06z_gputest.log 2>&1
+  rc=$?; tail -3 gpurun_out/r06z_gputest.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06z_smoke.log 2>&1 || exit 1
+  tail -1 gpurun_out/r06z_smoke.log
+  timeout -k 10 400 python -u bench.py > gpurun_out/r06z_bench.json 2> gpurun_out/r06z_bench.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/r06z_bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['e2e']['runs_per_s'] if d.get('e2e') else None)" ;;
+esac
