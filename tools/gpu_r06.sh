@@ -212,3 +212,10 @@ relax)  # k_build's relaxation levels: parity (tiers, C3 full, deep, batched), t
     python -c "import json;d=json.load(open('gpurun_out/${tag}_c3_$v.json'));print('relax $v',d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'],d['roofline']['frac'])"
   done ;;
 esac
+case "$1" in
+c5kab)  # C5 1k line: load_parts 8 and 125-run batches against the defaults
+  for args in "" "--set load_parts=8" "--batch-runs 125"; do
+    timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline $args > gpurun_out/${tag}_x.json 2> gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('[$args]',d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
+  done ;;
+esac
