@@ -82,7 +82,9 @@ def parse():
                     help="C5 at its configured size (BASELINE configs[4]: 1k runs): the runs in batches of "
                          "--batch-runs, each uploaded (H2D + CSR) on one of two contexts while the previous batch is "
                          "analysed on the other; value = runs/s of whole passes including the uploads")
-    ap.add_argument("--batch-runs", type=int, default=160)
+    ap.add_argument("--batch-runs", type=int, default=0,
+                    help="runs per batch of --runs-total (0: by the device's CUs, so that a batch's graphs, run 0's "
+                         "included, are at most one per CU)")
     ap.add_argument("--diff-reps", type=int, default=5,
                     help="per_run differential-provenance leg after the timed steps (roofline_diff): this many "
                          "nemo_diffprov(failed, NEMO_DIFF_PER_RUN) calls over the resident corpus (0: off)")
@@ -455,7 +457,15 @@ def runs_total_main(args, cfg, gen, threads, world, rank, local, torch, dist):
     mode = DIFF_PER_RUN if args.diff_mode == "per_run" else DIFF_REFERENCE
     R = args.runs_total // world
     base = rank * R
-    sizes = split_even(R, args.batch_runs)
+    # the deep graphs' per-graph kernels (k_topo_deep, k_glob_prep / k_chains_glob) run one workgroup per
+    # graph and are latency-bound: a batch of at most one graph per CU gives each its own CU (1000 runs:
+    # eight batches of 125 + run 0 = 252 graphs on 256 CUs, 447.5 runs/s, against seven of 143 + run 0 =
+    # 288 graphs, 408.7, on one box, gpurun_out r06ab)
+    batch = args.batch_runs
+    if batch <= 0:
+        n_cu = torch.cuda.get_device_properties(local).multi_processor_count
+        batch = max(1, n_cu // 2 - 1)
+    sizes = split_even(R, batch)
     t0 = time.time()
     batches, a = [], 0
     for n in sizes:
