@@ -219,3 +219,10 @@ c5kab)  # C5 1k line: load_parts 8 and 125-run batches against the defaults
     python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('[$args]',d['value'],d['ms_per_step'],d['pass_phases_rank0'])"
   done ;;
 esac
+case "$1" in
+c5kbs)  # C5 1k line: smaller batches
+  for b in 112 100 84; do
+    timeout -k 10 500 python -u bench.py --config c5 --runs-total 1000 --steps 2 --warmup 1 --e2e-runs 0 --no-cpu-baseline --batch-runs $b > gpurun_out/${tag}_x.json 2> gpurun_out/${tag}_x.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('[$b]',d['value'],d['ms_per_step'],d['config']['batch_sizes'][:2],d['pass_phases_rank0']['load_s'][:3],d['pass_phases_rank0']['analyse_s'][:3])"
+  done ;;
+esac
