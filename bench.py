@@ -76,6 +76,9 @@ def parse():
                          "sweeps overlap another's bandwidth-bound passes (default: the config's)")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="a libnemohip option (nemo_set_option) before the load, e.g. chains_glob_block=512")
+    ap.add_argument("--diff-at", choices=("mark", "protos"), default="mark",
+                    help="where the step issues the diff: after mark (its kernels beside the simplification) or "
+                         "after the protos, as main.go:146-160 orders CreatePrototypes and CreateNaiveDiffProv")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="--runs-total passes: no load of the next pass's first batch beside the last analysis")
     ap.add_argument("--runs-total", type=int, default=None,
@@ -228,18 +231,25 @@ def main():
         # every device phase is enqueued first; host-side retrieval (which syncs) comes last
         eng.rebuild()
         eng.mark()
+
         # CreateNaiveDiffProv reads only the raw run-0 graph and the label source
-        # (differential-provenance.go:22-98): issued here, its kernels run on the library's second
-        # stream beside the simplification; pull(2) and the mask views wait for them
-        if label_bcast:
-            if rank == lab_owner:
-                eng.goal_labels(f0, 1, d_lab.data_ptr(), lab_cap)
-            dist.broadcast(d_lab, lab_owner)
-            eng.diffprov_labels(failed, d_lab.data_ptr(), lab_cap)
-        else:
-            eng.diffprov(failed, mode)
+        # (differential-provenance.go:22-98): its kernels run on the library's second stream from the
+        # point of the call on (beside the simplification, or beside the protos and pulls);
+        # pull(2) and the mask views wait for them
+        def diff():
+            if label_bcast:
+                if rank == lab_owner:
+                    eng.goal_labels(f0, 1, d_lab.data_ptr(), lab_cap)
+                dist.broadcast(d_lab, lab_owner)
+                eng.diffprov_labels(failed, d_lab.data_ptr(), lab_cap)
+            else:
+                eng.diffprov(failed, mode)
+        if args.diff_at == "mark":
+            diff()
         eng.simplify()
         eng.protos_partial(success, d_red.data_ptr())
+        if args.diff_at == "protos":
+            diff()
         # flags + chain pairs -> pinned host on the copy stream, overlapping the pulls (queued
         # after k_proto_lds, the LDS-heaviest kernel, which a concurrent PCIe blit slows most)
         eng.stage_simplified()

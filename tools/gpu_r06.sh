@@ -226,3 +226,12 @@ c5kbs)  # C5 1k line: smaller batches
     python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('[$b]',d['value'],d['ms_per_step'],d['config']['batch_sizes'][:2],d['pass_phases_rank0']['load_s'][:3],d['pass_phases_rank0']['analyse_s'][:3])"
   done ;;
 esac
+case "$1" in
+diffat)  # where the step issues the diff: after mark / after the protos, both diff modes
+  for m in reference per_run; do
+    for at in mark protos mark protos; do
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --e2e-runs 0 --diff-reps 0 --diff-mode $m --diff-at $at > gpurun_out/${tag}_x.json 2> gpurun_out/${tag}_x.err || exit 1
+      python -c "import json;d=json.load(open('gpurun_out/${tag}_x.json'));print('$m $at',d['value'],d['ms_per_step'])"
+    done
+  done ;;
+esac
